@@ -1,0 +1,159 @@
+#!/usr/bin/env python
+"""Headline benchmark: image-pairs/s, fwd+bwd training step of ResNet-101 +
+NC-Net (5,5,5 / 16,16,1) at 400x400, bf16, synthetic pairs, random init
+(BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--impl hip|reference]
+
+One process per GPU (torchrun env for N > 1; RCCL all-reduce of gradients).
+A step is exactly what train.py does per batch: zero_grad, backbone on the
+pair images, correlation of positive and rolled-negative pairs, MutualMatching,
+symmetric NeighConsensus, MutualMatching, weak loss, backward, gradient
+all-reduce, Adam step.  K steps are timed between barrier+synchronize fences
+and the max over ranks is reported.  ``value`` is whole-job pairs/s.
+
+``--impl reference`` times the reference ALGORITHM in plain PyTorch-ROCm
+(4 backbone images per pair, bmm correlation, per-slice conv3d Conv4d), which
+is the measured baseline of BASELINE.md (no published numbers exist).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Measured reference-algorithm baseline on one MI355X (pairs/s), see BASELINE.md.
+BASELINE_PAIRS_PER_S = None
+_BASELINE_FILE = os.path.join(ROOT, "profiles", "baseline_reference.json")
+
+
+def _baseline():
+    if BASELINE_PAIRS_PER_S is not None:
+        return BASELINE_PAIRS_PER_S
+    try:
+        with open(_BASELINE_FILE) as f:
+            return float(json.load(f)["pairs_per_s_per_gpu"])
+    except Exception:
+        return None
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="pairs per GPU (train.py default 16)")
+    ap.add_argument("--image-size", type=int, default=400)
+    ap.add_argument("--impl", choices=["hip", "reference"], default="hip")
+    ap.add_argument("--ref-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--profile", type=str, default="", help="write a torch.profiler trace to this dir")
+    args = ap.parse_args(argv)
+
+    from ncnet_amd.engine.trainer import weak_loss
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.parallel.dist import (GradBucket, all_reduce_max_float, barrier, broadcast_parameters,
+                                         init_distributed)
+
+    ctx = init_distributed()
+    if ctx.world_size != args.gpus and ctx.is_main:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}", file=sys.stderr)
+    torch.manual_seed(1)
+    torch.backends.cudnn.benchmark = True
+    dev = ctx.device
+    model = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1], dtype="bf16").to(dev)
+    model.train()
+    params = [p for p in model.parameters() if p.requires_grad]
+    broadcast_parameters(params, ctx)
+    opt = torch.optim.Adam(params, lr=5e-4)
+    bucket = GradBucket(params, ctx)
+
+    # a small pool of synthetic batches (random normalised images), generated on device
+    gen = torch.Generator(device=dev).manual_seed(1234 + ctx.rank)
+    s = args.image_size
+    pool = [{"source_image": torch.randn(args.batch, 3, s, s, device=dev, generator=gen),
+             "target_image": torch.randn(args.batch, 3, s, s, device=dev, generator=gen)} for _ in range(2)]
+
+    if args.impl == "hip":
+        def step(batch):
+            opt.zero_grad(set_to_none=True)
+            loss = weak_loss(model, batch)
+            loss.backward()
+            bucket.allreduce()
+            opt.step()
+            return loss
+    else:
+        from ncnet_amd.engine.reference_impl import ReferenceAlgorithm, reference_weak_loss
+        alg = ReferenceAlgorithm(model, torch.float32 if args.ref_dtype == "fp32" else torch.bfloat16)
+
+        def step(batch):
+            opt.zero_grad(set_to_none=True)
+            loss = reference_weak_loss(alg, batch)
+            loss.backward()
+            bucket.allreduce()
+            opt.step()
+            return loss
+
+    for w in range(args.warmup):
+        loss = step(pool[w % len(pool)])
+    torch.cuda.synchronize(dev)
+    barrier(ctx)
+    torch.cuda.synchronize(dev)
+
+    prof = None
+    if args.profile and ctx.is_main:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+        prof.__enter__()
+    t0 = time.perf_counter()
+    for it in range(args.steps):
+        loss = step(pool[it % len(pool)])
+    torch.cuda.synchronize(dev)
+    barrier(ctx)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(args.profile, exist_ok=True)
+        with open(os.path.join(args.profile, "torch_profile.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+    elapsed = all_reduce_max_float(elapsed, ctx)
+
+    ms_per_step = 1000.0 * elapsed / args.steps
+    pairs_per_s = args.batch * ctx.world_size * args.steps / elapsed
+    base = _baseline()
+    vs = None
+    if base:
+        vs = pairs_per_s / (base * ctx.world_size)
+    if ctx.is_main:
+        rec = {
+            "metric": "image-pairs/sec fwd+bwd, ResNet-101+NC-Net(5,5,5) 400x400 bf16",
+            "value": round(pairs_per_s, 3),
+            "unit": "image-pairs/s",
+            "n_gpus": ctx.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if vs is None else round(vs, 3),
+            "dtype": "bf16" if args.impl == "hip" or args.ref_dtype == "bf16" else "fp32",
+            "data": "synthetic (random normalised 400x400 pairs, random-init weights)",
+            "config": {"model": "ResNet-101(layer3)+NC-Net ncons 5,5,5/16,16,1", "global_batch": args.batch * ctx.world_size,
+                       "per_gpu_batch": args.batch, "seq_len": None, "image_size": s,
+                       "parallelism": f"dp{ctx.world_size}", "impl": args.impl,
+                       "final_loss": float(loss)},
+        }
+        print(json.dumps(rec), flush=True)
+    from ncnet_amd.parallel.dist import destroy
+    destroy(ctx)
+
+
+if __name__ == "__main__":
+    main()

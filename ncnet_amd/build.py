@@ -1,0 +1,111 @@
+"""In-tree build of the gfx950 HIP extension ``ncnet_amd/_C.so``.
+
+Each ``csrc/*.hip`` file is compiled by hipcc for gfx950 only (no torch
+headers, so kernels rebuild in seconds); ``bindings.cpp`` is the only
+translation unit that includes torch.  Objects are relinked into one shared
+library that lives next to the package, so it travels to the GPU box with the
+repository snapshot.  Rebuilds are incremental (mtime based).
+
+    python -m ncnet_amd.build [--force] [-j N]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+BUILD = PKG / "_build"
+TARGET = PKG / "_C.so"
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+ARCH = os.environ.get("NCNET_OFFLOAD_ARCH", "gfx950")
+
+HIP_FLAGS = [
+    "-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-mcode-object-version=5",
+    "-ffp-contract=fast", "-Wno-unused-result", "-Wno-unused-variable",
+]
+
+
+def _torch_paths():
+    import torch
+    import torch.utils.cpp_extension as ce
+
+    inc = ce.include_paths()
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, libdir, abi
+
+
+def _newer(src: Path, dst: Path, deps=()) -> bool:
+    if not dst.exists():
+        return True
+    t = dst.stat().st_mtime
+    return src.stat().st_mtime > t or any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build step failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    headers = sorted(CSRC.glob("*.h"))
+    hip_srcs = sorted(CSRC.glob("*.hip"))
+    inc, libdir, abi = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+
+    steps = []
+    objs = []
+    for src in hip_srcs:
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _newer(src, obj, headers):
+            steps.append([HIPCC, *HIP_FLAGS, "-I", str(CSRC), "-c", str(src), "-o", str(obj)])
+    bsrc = CSRC / "bindings.cpp"
+    bobj = BUILD / "bindings.o"
+    objs.append(bobj)
+    if force or _newer(bsrc, bobj):
+        cmd = ["g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+               "-DTORCH_EXTENSION_NAME=_C", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I", py_inc,
+               "-I", os.path.join(ROCM, "include"), "-Wno-deprecated-declarations"]
+        for p in inc:
+            cmd += ["-I", p]
+        cmd += ["-c", str(bsrc), "-o", str(bobj)]
+        steps.append(cmd)
+
+    if steps:
+        jobs = jobs or min(len(steps), max(1, (os.cpu_count() or 4) // 2), 16)
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            for out in ex.map(_run, steps):
+                if verbose and out.strip():
+                    print(out)
+    if force or steps or not TARGET.exists() or any(o.stat().st_mtime > TARGET.stat().st_mtime for o in objs):
+        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(TARGET) + ".tmp",
+                "-L", libdir, "-Wl,-rpath," + libdir, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
+                "-ltorch_hip", "-ltorch_python", "-L", os.path.join(ROCM, "lib"), "-lamdhip64"]
+        _run(link)
+        os.replace(str(TARGET) + ".tmp", TARGET)
+    return TARGET
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("-v", action="store_true")
+    a = ap.parse_args(argv)
+    out = build(force=a.force, jobs=a.j, verbose=a.v)
+    print(f"built {out}")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,312 @@
+// Python bindings for the gfx950 NC-Net kernels.
+//
+// Every entry point validates device, dtype, contiguity and the exact shapes
+// the kernel's grid assumes BEFORE launching: a malformed call raises a Python
+// exception instead of faulting the GPU.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv1in_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv1out_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_wgrad1(const void*, const void*, float*, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, hipStream_t);
+int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
+int ncnet_corr_gemm(const void*, const void*, void*, const int*, const int*, int, int, int, int, long long, long long,
+                    long long, int, hipStream_t);
+int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, int, int, int, int, long long, long long,
+                          hipStream_t);
+int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, hipStream_t);
+int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, hipStream_t);
+int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, hipStream_t);
+int ncnet_mm_bwd(const float*, const float*, const float*, const int*, const float*, const int*, float*, float*, float*,
+                 int, int, int, float, hipStream_t);
+int ncnet_combine_fwd(const float*, float*, int, int, int, hipStream_t);
+int ncnet_combine_bwd(const float*, const float*, void*, int, int, int, hipStream_t);
+int ncnet_softmax_max_bwd(const float*, const float*, const int*, const float*, const float*, const int*, const float*,
+                          const float*, const float*, float*, int, int, int, hipStream_t);
+int ncnet_maxpool4d(const void*, int, float*, uint8_t*, int, int, int, int, int, int, hipStream_t);
+int ncnet_transpose(const void*, void*, int, int, int, int, hipStream_t);
+}
+
+namespace {
+
+using torch::Tensor;
+
+hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+void check(const Tensor& t, const char* name, c10::ScalarType dt) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+void check_shape(const Tensor& t, const char* name, std::vector<int64_t> shape) {
+  TORCH_CHECK(t.sizes().vec() == shape, name, " has shape ", t.sizes(), ", expected ", c10::IntArrayRef(shape));
+}
+void ok(int rc, const char* what) { TORCH_CHECK(rc == 0, what, " launch failed (code ", rc, ")"); }
+template <typename T>
+const T* opt_ptr(const c10::optional<Tensor>& t) { return t.has_value() && t->defined() ? (const T*)t->data_ptr() : nullptr; }
+
+int conv_pairs16(int ks) { return (ks * ks + 1) / 2; }
+int conv_m1(int ks) { return (ks + 3) / 4; }
+int conv_pairs1o(int ks) { return ((ks + 3) * (ks + 3) + 1) / 2; }
+
+// X [V,I,J,K,L,16] bf16 -> Y [V,I,J,K,L,16] bf16
+void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi) {
+  const c10::hip::HIPGuard guard(X.device());
+  check(X, "X", at::kBFloat16); check(Y, "Y", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
+  TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
+  check_shape(Y, "Y", X.sizes().vec());
+  check_shape(Wp, "Wp", {ks * ks, conv_pairs16(ks), 64, 8});
+  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
+  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", X.sizes().vec()); }
+  ok(ncnet_conv16_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), X.size(0),
+                      X.size(1), X.size(2), X.size(3), X.size(4), ks, epi, cur_stream(X)), "conv16_fwd");
+}
+
+// X [V,I,J,K,L] bf16 -> Y [V,I,J,K,L,16] bf16
+void conv1in_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi) {
+  const c10::hip::HIPGuard guard(X.device());
+  check(X, "X", at::kBFloat16); check(Y, "Y", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
+  TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
+  auto ys = X.sizes().vec(); ys.push_back(16);
+  check_shape(Y, "Y", ys);
+  check_shape(Wp, "Wp", {ks * ks, conv_m1(ks), 64, 8});
+  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
+  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", ys); }
+  ok(ncnet_conv1in_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), X.size(0),
+                       X.size(1), X.size(2), X.size(3), X.size(4), ks, epi, cur_stream(X)), "conv1in_fwd");
+}
+
+// X [V,I,J,K,L,16] bf16 -> Y [V,I,J,K,L] fp32
+void conv1out_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t epi) {
+  const c10::hip::HIPGuard guard(X.device());
+  check(X, "X", at::kBFloat16); check(Y, "Y", at::kFloat); check(Wp, "Wp", at::kBFloat16);
+  TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
+  check_shape(Y, "Y", {X.size(0), X.size(1), X.size(2), X.size(3), X.size(4)});
+  check_shape(Wp, "Wp", {ks * ks, conv_pairs1o(ks), 64, 8});
+  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
+  TORCH_CHECK(epi == 0 || epi == 1, "conv1out supports epi none / bias_relu");
+  ok(ncnet_conv1out_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), (float*)Y.data_ptr(), X.size(0), X.size(1),
+                        X.size(2), X.size(3), X.size(4), ks, epi, cur_stream(X)), "conv1out_fwd");
+}
+
+void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t ngroups) {
+  const c10::hip::HIPGuard guard(X.device());
+  check(X, "X", at::kBFloat16); check(G, "G", at::kBFloat16); check(part, "part", at::kFloat); check(partb, "partb", at::kFloat);
+  TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
+  check_shape(G, "G", X.sizes().vec());
+  check_shape(part, "part", {ngroups, ks * ks, ks * ks, 16, 16});
+  check_shape(partb, "partb", {ngroups, 16});
+  ok(ncnet_wgrad16(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(0), X.size(1),
+                   X.size(2), X.size(3), X.size(4), ks, ngroups, cur_stream(X)), "wgrad16");
+}
+
+void wgrad1(Tensor S16, Tensor P1, Tensor part, int64_t ks, int64_t mode, int64_t ngroups) {
+  const c10::hip::HIPGuard guard(S16.device());
+  check(S16, "S16", at::kBFloat16); check(P1, "P1", at::kBFloat16); check(part, "part", at::kFloat);
+  TORCH_CHECK(S16.dim() == 6 && S16.size(5) == 16, "S16 must be [V,I,J,K,L,16]");
+  check_shape(P1, "P1", {S16.size(0), S16.size(1), S16.size(2), S16.size(3), S16.size(4)});
+  check_shape(part, "part", {ngroups, ks * ks, ks * ks, 16});
+  TORCH_CHECK(mode == 0 || mode == 1);
+  ok(ncnet_wgrad1(S16.data_ptr(), P1.data_ptr(), (float*)part.data_ptr(), S16.size(0), S16.size(1), S16.size(2),
+                  S16.size(3), S16.size(4), ks, mode, ngroups, cur_stream(S16)), "wgrad1");
+}
+
+void l2norm_rows(Tensor x, Tensor y, c10::optional<Tensor> inv) {
+  const c10::hip::HIPGuard guard(x.device());
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous());
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat);
+  check(y, "y", at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2 && y.sizes() == x.sizes(), "x,y must be [rows, C]");
+  if (inv.has_value()) { check(*inv, "inv", at::kFloat); check_shape(*inv, "inv", {x.size(0)}); }
+  ok(ncnet_l2norm_rows(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(),
+                       inv.has_value() ? (float*)inv->data_ptr() : nullptr, x.size(0), x.size(1), cur_stream(x)), "l2norm");
+}
+
+void l2norm_rows_bwd(Tensor x, Tensor g, Tensor inv, Tensor gx) {
+  const c10::hip::HIPGuard guard(x.device());
+  check(x, "x", at::kFloat); check(g, "g", at::kFloat); check(inv, "inv", at::kFloat); check(gx, "gx", at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && g.sizes() == x.sizes() && gx.sizes() == x.sizes());
+  check_shape(inv, "inv", {x.size(0)});
+  ok(ncnet_l2norm_rows_bwd((float*)x.data_ptr(), (float*)g.data_ptr(), (float*)inv.data_ptr(), (float*)gx.data_ptr(),
+                           x.size(0), x.size(1), cur_stream(x)), "l2norm_bwd");
+}
+
+// A [Ba, M, K], B [Bb, N, K] bf16; C [batch, M, N] fp32/bf16
+void corr_gemm(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> amap, c10::optional<Tensor> bmap) {
+  const c10::hip::HIPGuard guard(A.device());
+  check(A, "A", at::kBFloat16); check(B, "B", at::kBFloat16);
+  TORCH_CHECK(C.is_cuda() && C.is_contiguous() && (C.scalar_type() == at::kFloat || C.scalar_type() == at::kBFloat16));
+  TORCH_CHECK(A.dim() == 3 && B.dim() == 3 && C.dim() == 3);
+  TORCH_CHECK(A.size(2) == B.size(2), "K mismatch");
+  TORCH_CHECK(A.size(2) % 8 == 0, "K must be a multiple of 8");
+  const int64_t batch = C.size(0);
+  TORCH_CHECK(C.size(1) == A.size(1) && C.size(2) == B.size(1), "C shape mismatch");
+  if (amap.has_value()) {
+    // maps are built by ncnet_amd.ops.correlation from arange/roll (in range by
+    // construction); no device->host read here, the call stays async.
+    check(*amap, "amap", at::kInt); check_shape(*amap, "amap", {batch});
+  } else TORCH_CHECK(A.size(0) == batch);
+  if (bmap.has_value()) {
+    check(*bmap, "bmap", at::kInt); check_shape(*bmap, "bmap", {batch});
+  } else TORCH_CHECK(B.size(0) == batch);
+  ok(ncnet_corr_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), opt_ptr<int>(amap), opt_ptr<int>(bmap), batch, A.size(1),
+                     B.size(1), A.size(2), A.size(1) * A.size(2), B.size(1) * B.size(2), C.size(1) * C.size(2),
+                     C.scalar_type() == at::kBFloat16, cur_stream(A)), "corr_gemm");
+}
+
+void corr_gemm_pool2(Tensor A, Tensor B, Tensor val, Tensor idx, int64_t hA, int64_t wA, int64_t hB, int64_t wB) {
+  const c10::hip::HIPGuard guard(A.device());
+  check(A, "A", at::kBFloat16); check(B, "B", at::kBFloat16); check(val, "val", at::kFloat); check(idx, "idx", at::kByte);
+  TORCH_CHECK(A.dim() == 3 && B.dim() == 3 && A.size(0) == B.size(0));
+  TORCH_CHECK(A.size(1) == hA * wA && B.size(1) == hB * wB && A.size(2) == B.size(2));
+  TORCH_CHECK(hA % 2 == 0 && wA % 2 == 0 && hB % 2 == 0 && wB % 2 == 0, "pooling needs even feature sizes");
+  TORCH_CHECK(A.size(2) % 8 == 0);
+  check_shape(val, "val", {A.size(0), hA / 2, wA / 2, hB / 2, wB / 2});
+  check_shape(idx, "idx", {A.size(0), hA / 2, wA / 2, hB / 2, wB / 2});
+  ok(ncnet_corr_gemm_pool2(A.data_ptr(), B.data_ptr(), (float*)val.data_ptr(), (uint8_t*)idx.data_ptr(), A.size(0), hA,
+                           wA, hB, wB, A.size(2), A.size(1) * A.size(2), B.size(1) * B.size(2), cur_stream(A)),
+     "corr_gemm_pool2");
+}
+
+// x [V,R,C] fp32 -> per-row (dim 2) stats [V,R]
+void stats_rows(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Tensor> se) {
+  const c10::hip::HIPGuard guard(x.device());
+  check(x, "x", at::kFloat); check(mx, "mx", at::kFloat);
+  TORCH_CHECK(x.dim() == 3);
+  check_shape(mx, "mx", {x.size(0), x.size(1)});
+  if (arg.has_value()) { check(*arg, "arg", at::kInt); check_shape(*arg, "arg", {x.size(0), x.size(1)}); }
+  if (se.has_value()) { check(*se, "se", at::kFloat); check_shape(*se, "se", {x.size(0), x.size(1)}); }
+  ok(ncnet_stats_rows((float*)x.data_ptr(), (float*)mx.data_ptr(), arg.has_value() ? (int*)arg->data_ptr() : nullptr,
+                      se.has_value() ? (float*)se->data_ptr() : nullptr, x.size(0) * x.size(1), x.size(2), cur_stream(x)),
+     "stats_rows");
+}
+
+// x [V,R,C] fp32 -> per-column (dim 1) stats [V,C]
+void stats_cols(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Tensor> se) {
+  const c10::hip::HIPGuard guard(x.device());
+  check(x, "x", at::kFloat); check(mx, "mx", at::kFloat);
+  TORCH_CHECK(x.dim() == 3);
+  check_shape(mx, "mx", {x.size(0), x.size(2)});
+  if (arg.has_value()) { check(*arg, "arg", at::kInt); check_shape(*arg, "arg", {x.size(0), x.size(2)}); }
+  if (se.has_value()) { check(*se, "se", at::kFloat); check_shape(*se, "se", {x.size(0), x.size(2)}); }
+  ok(ncnet_stats_cols((float*)x.data_ptr(), (float*)mx.data_ptr(), arg.has_value() ? (int*)arg->data_ptr() : nullptr,
+                      se.has_value() ? (float*)se->data_ptr() : nullptr, x.size(0), x.size(1), x.size(2), cur_stream(x)),
+     "stats_cols");
+}
+
+void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10::optional<Tensor> out_x,
+              c10::optional<Tensor> out_xt, double eps) {
+  const c10::hip::HIPGuard guard(c.device());
+  check(c, "c", at::kFloat); check(rmax, "rmax", at::kFloat); check(cmax, "cmax", at::kFloat);
+  TORCH_CHECK(c.dim() == 3);
+  const int64_t V = c.size(0), R = c.size(1), C = c.size(2);
+  check_shape(rmax, "rmax", {V, R}); check_shape(cmax, "cmax", {V, C});
+  if (out.has_value()) { check(*out, "out", at::kFloat); check_shape(*out, "out", {V, R, C}); }
+  if (out_x.has_value()) { check(*out_x, "out_x", at::kBFloat16); check_shape(*out_x, "out_x", {V, R, C}); }
+  if (out_xt.has_value()) { check(*out_xt, "out_xt", at::kBFloat16); check_shape(*out_xt, "out_xt", {V, C, R}); }
+  ok(ncnet_mm_apply((float*)c.data_ptr(), (float*)rmax.data_ptr(), (float*)cmax.data_ptr(),
+                    out.has_value() ? (float*)out->data_ptr() : nullptr, out_x.has_value() ? out_x->data_ptr() : nullptr,
+                    out_xt.has_value() ? out_xt->data_ptr() : nullptr, V, R, C, (float)eps, cur_stream(c)), "mm_apply");
+}
+
+void mm_bwd(Tensor c, Tensor g, Tensor rmax, Tensor rarg, Tensor cmax, Tensor carg, Tensor gc, double eps) {
+  const c10::hip::HIPGuard guard(c.device());
+  check(c, "c", at::kFloat); check(g, "g", at::kFloat); check(gc, "gc", at::kFloat);
+  check(rmax, "rmax", at::kFloat); check(cmax, "cmax", at::kFloat); check(rarg, "rarg", at::kInt); check(carg, "carg", at::kInt);
+  TORCH_CHECK(c.dim() == 3 && g.sizes() == c.sizes() && gc.sizes() == c.sizes());
+  const int64_t V = c.size(0), R = c.size(1), C = c.size(2);
+  check_shape(rmax, "rmax", {V, R}); check_shape(rarg, "rarg", {V, R});
+  check_shape(cmax, "cmax", {V, C}); check_shape(carg, "carg", {V, C});
+  auto rsum = torch::empty({V, R}, c.options());
+  auto csum = torch::empty({V, C}, c.options());
+  ok(ncnet_mm_bwd((float*)c.data_ptr(), (float*)g.data_ptr(), (float*)rmax.data_ptr(), (int*)rarg.data_ptr(),
+                  (float*)cmax.data_ptr(), (int*)carg.data_ptr(), (float*)rsum.data_ptr(), (float*)csum.data_ptr(),
+                  (float*)gc.data_ptr(), V, R, C, (float)eps, cur_stream(c)), "mm_bwd");
+}
+
+// z [2*Vh, R, C] (second half stored as [C, R]) -> y [Vh, R, C]
+void combine_fwd(Tensor z, Tensor y, int64_t R, int64_t C) {
+  const c10::hip::HIPGuard guard(z.device());
+  check(z, "z", at::kFloat); check(y, "y", at::kFloat);
+  TORCH_CHECK(z.numel() % (2 * R * C) == 0);
+  const int64_t Vh = z.numel() / (2 * R * C);
+  TORCH_CHECK(y.numel() == Vh * R * C);
+  ok(ncnet_combine_fwd((float*)z.data_ptr(), (float*)y.data_ptr(), Vh, R, C, cur_stream(z)), "combine_fwd");
+}
+
+void combine_bwd(Tensor g, Tensor z, Tensor gz, int64_t R, int64_t C) {
+  const c10::hip::HIPGuard guard(z.device());
+  check(g, "g", at::kFloat); check(z, "z", at::kFloat); check(gz, "gz", at::kBFloat16);
+  TORCH_CHECK(z.numel() % (2 * R * C) == 0);
+  const int64_t Vh = z.numel() / (2 * R * C);
+  TORCH_CHECK(g.numel() == Vh * R * C && gz.numel() == z.numel());
+  ok(ncnet_combine_bwd((float*)g.data_ptr(), (float*)z.data_ptr(), gz.data_ptr(), Vh, R, C, cur_stream(z)), "combine_bwd");
+}
+
+void softmax_max_bwd(Tensor x, Tensor rmax, Tensor rarg, Tensor rse, Tensor cmax, Tensor carg, Tensor cse, Tensor wr,
+                     Tensor wc, Tensor gx) {
+  const c10::hip::HIPGuard guard(x.device());
+  check(x, "x", at::kFloat); check(gx, "gx", at::kFloat);
+  TORCH_CHECK(x.dim() == 3 && gx.sizes() == x.sizes());
+  const int64_t V = x.size(0), R = x.size(1), C = x.size(2);
+  check(rmax, "rmax", at::kFloat); check(rse, "rse", at::kFloat); check(rarg, "rarg", at::kInt);
+  check(cmax, "cmax", at::kFloat); check(cse, "cse", at::kFloat); check(carg, "carg", at::kInt);
+  check(wr, "wr", at::kFloat); check(wc, "wc", at::kFloat);
+  check_shape(rmax, "rmax", {V, R}); check_shape(rse, "rse", {V, R}); check_shape(rarg, "rarg", {V, R});
+  check_shape(cmax, "cmax", {V, C}); check_shape(cse, "cse", {V, C}); check_shape(carg, "carg", {V, C});
+  check_shape(wr, "wr", {V}); check_shape(wc, "wc", {V});
+  ok(ncnet_softmax_max_bwd((float*)x.data_ptr(), (float*)rmax.data_ptr(), (int*)rarg.data_ptr(), (float*)rse.data_ptr(),
+                           (float*)cmax.data_ptr(), (int*)carg.data_ptr(), (float*)cse.data_ptr(), (float*)wr.data_ptr(),
+                           (float*)wc.data_ptr(), (float*)gx.data_ptr(), V, R, C, cur_stream(x)), "softmax_max_bwd");
+}
+
+void maxpool4d(Tensor x, Tensor y, Tensor code, int64_t ks) {
+  const c10::hip::HIPGuard guard(x.device());
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16));
+  TORCH_CHECK(x.dim() == 5, "x must be [V,I,J,K,L]");
+  TORCH_CHECK(ks >= 1 && ks <= 4);
+  for (int d = 1; d < 5; ++d) TORCH_CHECK(x.size(d) % ks == 0, "volume dims must be divisible by k_size");
+  std::vector<int64_t> os = {x.size(0), x.size(1) / ks, x.size(2) / ks, x.size(3) / ks, x.size(4) / ks};
+  check(y, "y", at::kFloat); check(code, "code", at::kByte);
+  check_shape(y, "y", os); check_shape(code, "code", os);
+  ok(ncnet_maxpool4d(x.data_ptr(), x.scalar_type() == at::kBFloat16, (float*)y.data_ptr(), (uint8_t*)code.data_ptr(),
+                     x.size(0), x.size(1), x.size(2), x.size(3), x.size(4), ks, cur_stream(x)), "maxpool4d");
+}
+
+void transpose(Tensor x, Tensor y) {
+  const c10::hip::HIPGuard guard(x.device());
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && y.is_contiguous() && x.scalar_type() == y.scalar_type());
+  TORCH_CHECK(x.dim() == 3 && y.dim() == 3 && y.size(0) == x.size(0) && y.size(1) == x.size(2) && y.size(2) == x.size(1));
+  ok(ncnet_transpose(x.data_ptr(), y.data_ptr(), x.element_size(), x.size(0), x.size(1), x.size(2), cur_stream(x)),
+     "transpose");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels for ncnet_amd";
+  m.def("conv16_fwd", &conv16_fwd);
+  m.def("conv1in_fwd", &conv1in_fwd);
+  m.def("conv1out_fwd", &conv1out_fwd);
+  m.def("wgrad16", &wgrad16);
+  m.def("wgrad1", &wgrad1);
+  m.def("l2norm_rows", &l2norm_rows);
+  m.def("l2norm_rows_bwd", &l2norm_rows_bwd);
+  m.def("corr_gemm", &corr_gemm);
+  m.def("corr_gemm_pool2", &corr_gemm_pool2);
+  m.def("stats_rows", &stats_rows);
+  m.def("stats_cols", &stats_cols);
+  m.def("mm_apply", &mm_apply);
+  m.def("mm_bwd", &mm_bwd);
+  m.def("combine_fwd", &combine_fwd);
+  m.def("combine_bwd", &combine_bwd);
+  m.def("softmax_max_bwd", &softmax_max_bwd);
+  m.def("maxpool4d", &maxpool4d);
+  m.def("transpose", &transpose);
+}

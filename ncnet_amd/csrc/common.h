@@ -1,0 +1,73 @@
+// Shared definitions for the gfx950 (CDNA4 / MI355X) NC-Net kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave64; blocks are multiples of 64 lanes.
+//  * bf16 operands are moved as 16-byte vectors (8 x bf16) everywhere the
+//    layout allows it (global -> registers -> LDS -> MFMA fragments).
+//  * MFMA shape is v_mfma_f32_16x16x32_bf16: lane l holds A[row l&15][k 8(l>>4)+j]
+//    and B[k 8(l>>4)+j][col l&15], j = 0..7; D[row 4(l>>4)+r][col l&15], r = 0..3.
+//  * Volumes are channels-last: [V, I, J, K, L, C] (C = 16 for the hidden
+//    Conv4d activations, C = 1 for correlation volumes, which are then just
+//    the matrix [V, I*J, K*L]).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16: 16-lane group reads a [4 rows x 16 cols] bf16 block;
+// lane 4q+p supplies the address of row q, columns 4p..4p+3 (8-byte aligned);
+// lane i of the group receives column i of the 4 rows.
+__device__ __forceinline__ bf16x4 lds_read_tr16(const char* lds_base, uint32_t byte_off) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds_base + byte_off));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+__device__ __forceinline__ bf16x8 cat8(const bf16x4& lo, const bf16x4& hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+__device__ __forceinline__ bf16x8 lds_read16(const char* lds_base, uint32_t byte_off) {
+  return *(const bf16x8*)(lds_base + byte_off);
+}
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Bijective XCD-aware remap of a linear block id: consecutive logical ids land
+// on the same XCD (blocks are dealt round-robin over the 8 XCDs), so
+// neighbouring output tiles that share input planes share an L2.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblocks) {
+  const uint32_t nx = 8;
+  if (nblocks < nx) return bid;
+  uint32_t q = nblocks / nx, r = nblocks % nx;
+  uint32_t x = bid % nx, k = bid / nx;
+  uint32_t start = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return start + k;
+}
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -1,0 +1,607 @@
+// Conv4d forward (and transposed-conv data gradient) on gfx950 MFMA.
+//
+// Semantics: "same"-padded stride-1 4D cross-correlation (lib/conv4d.py:11-51)
+//   Y[v,i,j,k,l,co] = sum_{di,dj,dk,dl,ci} X[v,i+di-P,j+dj-P,k+dk-P,l+dl-P,ci] W[co,ci,di,dj,dk,dl]
+// computed as an implicit GEMM: M = output voxels, N = Cout, K = taps x Cin.
+//
+// Work decomposition (all three kernels): one workgroup owns one output tile
+// (v, i, j, k0:k0+TK, l0:l0+TL) and streams the KS*KS input planes
+// (i+di-P, j+dj-P, :, :) through a single LDS plane buffer, zero-padded by the
+// halo, while the next plane is prefetched into registers (the reference's
+// Python slice loop, lib/conv4d.py:39-48, moved inside one kernel).  Planes
+// that fall outside the volume are skipped.  Bias + ReLU (forward) or the
+// ReLU-mask of the previous layer (data-gradient) are fused in the epilogue.
+//
+//   conv16_fwd   Cin=16 -> Cout=16 : MFMA D[co][voxel], K = 2 taps x 16 ci.
+//   conv1in_fwd  Cin=1  -> Cout=16 : K = 4 kernel rows x 8-wide l-windows built
+//                                    in LDS (16-byte aligned operand reads).
+//   conv1out_fwd Cin=16 -> Cout=1  : the 16 MFMA columns are 4x4 (k,l) output
+//                                    shifts of an anchor grid (weights shifted
+//                                    on the host), so N=1 still uses the MFMA.
+#include "common.h"
+
+namespace ncnet {
+
+enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2 };
+
+struct ConvGeom {
+  int V, I, J, K, L;  // volume dims
+  int TK, TL;         // output tile along k, l
+  int nkt, nlt;       // tiles along k, l
+  int PR, RS;         // staged plane rows / row stride (voxels)
+};
+
+// Decode the workgroup's output tile.
+struct TileId { int v, i, j, k0, l0; };
+__device__ __forceinline__ TileId decode_tile(const ConvGeom& g) {
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  TileId t;
+  int lt = bid % g.nlt; bid /= g.nlt;
+  int kt = bid % g.nkt; bid /= g.nkt;
+  t.j = bid % g.J; bid /= g.J;
+  t.i = bid % g.I; t.v = bid / g.I;
+  t.k0 = kt * g.TK; t.l0 = lt * g.TL;
+  return t;
+}
+
+// ---------------------------------------------------------------------------
+// Plane staging for 16-channel volumes: a (PR x RS) window of voxels whose
+// (0,0) corner sits at volume (kb, lb); out-of-volume voxels are zero.
+// Each 16-byte chunk is half a voxel (8 channels).
+template <int MAXCH>
+struct Stage16 {
+  u32x4 r[MAXCH];
+  __device__ __forceinline__ void load(const bf16* __restrict__ plane_ptr, const ConvGeom& g, int kb, int lb, int nchunk) {
+#pragma unroll
+    for (int m = 0; m < MAXCH; ++m) {
+      int c = threadIdx.x + m * 256;
+      u32x4 val = {0u, 0u, 0u, 0u};
+      if (c < nchunk) {
+        int pos = c >> 1, h = c & 1;
+        int row = pos / g.RS, col = pos - row * g.RS;
+        int kg = kb + row, lg = lb + col;
+        if (kg >= 0 && kg < g.K && lg >= 0 && lg < g.L)
+          val = *(const u32x4*)(plane_ptr + ((size_t)(kg * g.L + lg) * 16 + h * 8));
+      }
+      r[m] = val;
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int nchunk) {
+#pragma unroll
+    for (int m = 0; m < MAXCH; ++m) {
+      int c = threadIdx.x + m * 256;
+      if (c < nchunk) *(u32x4*)(lds + c * 16) = r[m];
+    }
+  }
+};
+
+template <int MAXW>
+struct StageW {
+  u32x4 r[MAXW];
+  __device__ __forceinline__ void load(const u32x4* __restrict__ src, int n) {
+#pragma unroll
+    for (int m = 0; m < MAXW; ++m) {
+      int c = threadIdx.x + m * 256;
+      r[m] = (c < n) ? src[c] : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int n) {
+#pragma unroll
+    for (int m = 0; m < MAXW; ++m) {
+      int c = threadIdx.x + m * 256;
+      if (c < n) *(u32x4*)(lds + c * 16) = r[m];
+    }
+  }
+};
+
+__device__ __forceinline__ size_t plane_offset(const ConvGeom& g, int v, int i, int j, int C) {
+  return ((((size_t)v * g.I + i) * g.J + j) * (size_t)g.K * g.L) * C;
+}
+
+// Epilogue for a [16 co x 16 voxel] accumulator tile: lane holds co = 4(l>>4)+r
+// of voxel (l & 15).
+template <int EPI>
+__device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
+                                        const float* __restrict__ bias, size_t vox_index, int co0) {
+  float o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float x = acc[r];
+    if (EPI == EPI_BIAS_RELU) x = fmaxf(x + bias[co0 + r], 0.f);
+    o[r] = x;
+  }
+  if (EPI == EPI_MASK) {
+    bf16x4 m = *(const bf16x4*)(M + vox_index * 16 + co0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = ((float)m[r] > 0.f) ? o[r] : 0.f;
+  }
+  bf16x4 out;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) out[r] = f2bf(o[r]);
+  *(bf16x4*)(Y + vox_index * 16 + co0) = out;
+}
+
+// ===========================================================================
+// conv16_fwd: Cin = 16, Cout = 16.
+// Wp: [KS*KS planes][NQ pairs][64 lanes] x 16 B fragments where lane l of pair
+// q holds W[co=l&15][ci=8((l>>4)&1)+0..7] of tap 2q+(l>>5) (zero past KS*KS).
+// ===========================================================================
+template <int KS, int EPI>
+__global__ __launch_bounds__(256, 2) void conv16_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
+                                                            const float* __restrict__ bias,
+                                                            const bf16* __restrict__ M, bf16* __restrict__ Y,
+                                                            ConvGeom g) {
+  constexpr int P = KS / 2;
+  constexpr int NT = KS * KS;
+  constexpr int NQ = (NT + 1) / 2;
+  constexpr int MAXT = 10;       // 16-voxel tiles per wave (TK*TL <= 640)
+  constexpr int MAXCH = 8;       // PR*RS*2 <= 2048 chunks
+  constexpr int WCH = NQ * 64;
+  constexpr int MAXW = (WCH + 255) / 256;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* plane = smem;
+  char* wlds = smem + g.PR * g.RS * 32;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const TileId t = decode_tile(g);
+  const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
+  const int dj_lo = max(0, P - t.j), dj_hi = min(KS, g.J + P - t.j);
+  const int ndj = dj_hi - dj_lo;
+  const int nplanes = (di_hi - di_lo) * ndj;
+  const int nchunk = g.PR * g.RS * 2;
+  const int nvox = g.TK * g.TL;
+  const int ntile = (nvox + 15) >> 4;
+
+  // Per-lane operand addresses.
+  uint32_t vbase[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int vi = (wave + 4 * tt) * 16 + (lane & 15);
+    if (vi >= nvox) vi = 0;
+    int kk = vi / g.TL, ll = vi - kk * g.TL;
+    vbase[tt] = (uint32_t)((kk * g.RS + ll) * 32 + ((lane >> 4) & 1) * 16);
+  }
+  uint32_t toff[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    int tap = 2 * q + (lane >> 5);
+    if (tap >= NT) tap = NT - 1;
+    int dk = tap / KS, dl = tap - dk * KS;
+    toff[q] = (uint32_t)((dk * g.RS + dl) * 32);
+  }
+
+  f32x4 acc[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage16<MAXCH> sx;
+  StageW<MAXW> sw;
+  auto plane_src = [&](int s, const bf16*& xp, const u32x4*& wp) {
+    int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
+    xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
+    wp = Wp + (size_t)(di * KS + dj) * WCH;
+  };
+  if (nplanes > 0) {
+    const bf16* xp; const u32x4* wp;
+    plane_src(0, xp, wp);
+    sx.load(xp, g, t.k0 - P, t.l0 - P, nchunk);
+    sw.load(wp, WCH);
+    sx.store(plane, nchunk);
+    sw.store(wlds, WCH);
+  }
+  __syncthreads();
+
+  for (int s = 0; s < nplanes; ++s) {
+    bf16x8 wf[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) wf[q] = lds_read16(wlds, (q * 64 + lane) * 16);
+    const bool more = (s + 1) < nplanes;
+    if (more) {
+      const bf16* xp; const u32x4* wp;
+      plane_src(s + 1, xp, wp);
+      sx.load(xp, g, t.k0 - P, t.l0 - P, nchunk);
+      sw.load(wp, WCH);
+    }
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      if (wave + 4 * tt < ntile) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          bf16x8 xf = lds_read16(plane, vbase[tt] + toff[q]);
+          acc[tt] = mfma16(wf[q], xf, acc[tt]);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      sx.store(plane, nchunk);
+      sw.store(wlds, WCH);
+    }
+    __syncthreads();
+  }
+
+  // Epilogue.
+  const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);  // voxel index of (k=0,l=0)
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int tile = wave + 4 * tt;
+    if (tile < ntile) {
+      int vi = tile * 16 + (lane & 15);
+      int kk = vi / g.TL, ll = vi - kk * g.TL;
+      int kg = t.k0 + kk, lg = t.l0 + ll;
+      if (vi < nvox && kg < g.K && lg < g.L)
+        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4));
+    }
+  }
+}
+
+// ===========================================================================
+// conv1in_fwd: Cin = 1, Cout = 16.
+// The staged plane is expanded in LDS into 8-wide l-windows
+// win[r][c] = plane[r][c .. c+7] so every MFMA operand read is one aligned
+// 16-byte ds_read.  K per MFMA = 4 kernel rows (dk) x 8 window taps (dl).
+// Wp: [KS*KS planes][NM][64 lanes] x 16 B, lane l of MFMA m holds
+// W[co=l&15][di][dj][dk=4m+(l>>4)][dl=0..7] (zero for dk,dl >= KS).
+// ===========================================================================
+template <int KS, int EPI>
+__global__ __launch_bounds__(256, 2) void conv1in_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
+                                                             const float* __restrict__ bias,
+                                                             const bf16* __restrict__ M, bf16* __restrict__ Y,
+                                                             ConvGeom g) {
+  constexpr int P = KS / 2;
+  constexpr int NM = (KS + 3) / 4;
+  constexpr int MAXT = 10;
+  constexpr int WCH = NM * 64;
+  constexpr int MAXE = 8;  // raw plane elements per thread (PR*RW <= 2048)
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int RW = g.TL + KS - 1 + 8;              // raw row width (elements), room for windows
+  char* win = smem;                              // PR * TL windows x 16 B
+  char* raw = smem + g.PR * g.TL * 16;           // PR * RW bf16
+  char* wlds = raw + ((g.PR * RW * 2 + 15) & ~15);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const TileId t = decode_tile(g);
+  const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
+  const int dj_lo = max(0, P - t.j), dj_hi = min(KS, g.J + P - t.j);
+  const int ndj = dj_hi - dj_lo;
+  const int nplanes = (di_hi - di_lo) * ndj;
+  const int nraw = g.PR * RW;
+  const int nwin = g.PR * g.TL;
+  const int nvox = g.TK * g.TL;
+  const int ntile = (nvox + 15) >> 4;
+
+  uint32_t vbase[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int vi = (wave + 4 * tt) * 16 + (lane & 15);
+    if (vi >= nvox) vi = 0;
+    int kk = vi / g.TL, ll = vi - kk * g.TL;
+    vbase[tt] = (uint32_t)((kk * g.TL + ll) * 16);
+  }
+  uint32_t roff[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    int dk = 4 * m + (lane >> 4);
+    if (dk >= KS) dk = KS - 1;
+    roff[m] = (uint32_t)(dk * g.TL * 16);
+  }
+
+  f32x4 acc[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16 rr[MAXE];
+  u32x4 wr = {0u, 0u, 0u, 0u};
+  auto load_plane = [&](int s) {
+    int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
+    const bf16* xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 1);
+    const int kb = t.k0 - P, lb = t.l0 - P;
+#pragma unroll
+    for (int m = 0; m < MAXE; ++m) {
+      int e = threadIdx.x + m * 256;
+      bf16 val = f2bf(0.f);
+      if (e < nraw) {
+        int row = e / RW, col = e - row * RW;
+        int kg = kb + row, lg = lb + col;
+        if (col < g.TL + KS - 1 && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L) val = xp[(size_t)kg * g.L + lg];
+      }
+      rr[m] = val;
+    }
+    const u32x4* wp = Wp + (size_t)(di * KS + dj) * WCH;
+    if (threadIdx.x < WCH) wr = wp[threadIdx.x];
+  };
+  auto store_raw = [&]() {
+#pragma unroll
+    for (int m = 0; m < MAXE; ++m) {
+      int e = threadIdx.x + m * 256;
+      if (e < nraw) ((bf16*)raw)[e] = rr[m];
+    }
+    if (threadIdx.x < WCH) *(u32x4*)(wlds + threadIdx.x * 16) = wr;
+  };
+  auto build_windows = [&]() {
+    for (int w = threadIdx.x; w < nwin; w += 256) {
+      int row = w / g.TL, c = w - row * g.TL;
+      const bf16* src = (const bf16*)raw + row * RW + c;
+      bf16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = src[q];
+      *(bf16x8*)(win + w * 16) = o;
+    }
+  };
+
+  if (nplanes > 0) {
+    load_plane(0);
+    store_raw();
+  }
+  __syncthreads();
+  if (nplanes > 0) build_windows();
+  __syncthreads();
+
+  for (int s = 0; s < nplanes; ++s) {
+    bf16x8 wf[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) wf[m] = lds_read16(wlds, (m * 64 + lane) * 16);
+    const bool more = (s + 1) < nplanes;
+    if (more) load_plane(s + 1);
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      if (wave + 4 * tt < ntile) {
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          bf16x8 xf = lds_read16(win, vbase[tt] + roff[m]);
+          acc[tt] = mfma16(wf[m], xf, acc[tt]);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) store_raw();
+    __syncthreads();
+    if (more) build_windows();
+    __syncthreads();
+  }
+
+  const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int tile = wave + 4 * tt;
+    if (tile < ntile) {
+      int vi = tile * 16 + (lane & 15);
+      int kk = vi / g.TL, ll = vi - kk * g.TL;
+      int kg = t.k0 + kk, lg = t.l0 + ll;
+      if (vi < nvox && kg < g.K && lg < g.L)
+        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4));
+    }
+  }
+}
+
+// ===========================================================================
+// conv1out_fwd: Cin = 16, Cout = 1 (fp32 output).
+// Anchors a = (4ak, 4al) cover the tile; MFMA column s = (sk, sl) in 4x4 is the
+// output voxel a + s.  With tau = s + d in [0, KS+3)^2:
+//   Y[a + s] = sum_tau Xpad[a + tau] . W'[tau][s],  W'[tau][s] = W[tau - s]
+// A operand = W' (rows s, K = 2 taus x 16 ci), B operand = X at the anchors.
+// The waves split the tau pairs (K-split) and reduce through LDS at the end.
+// Wp: [KS*KS planes][NPAIR][64 lanes] x 16 B.
+// ===========================================================================
+template <int KS, int EPI>
+__global__ __launch_bounds__(256, 2) void conv1out_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
+                                                              const float* __restrict__ bias,
+                                                              float* __restrict__ Y, ConvGeom g) {
+  constexpr int P = KS / 2;
+  constexpr int TS = KS + 3;                 // tau extent per dim
+  constexpr int NPAIR = (TS * TS + 1) / 2;
+  constexpr int PPW = (NPAIR + 3) / 4;       // pairs per wave
+  constexpr int MAXA = 4;                    // anchor tiles (na*nb <= 64)
+  constexpr int MAXCH = 8;                   // PR*RS*2 <= 2048 (PR, RS <= 32)
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* plane = smem;  // PR x RS x 32 B, reused for the cross-wave reduction
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const TileId t = decode_tile(g);
+  const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
+  const int dj_lo = max(0, P - t.j), dj_hi = min(KS, g.J + P - t.j);
+  const int ndj = dj_hi - dj_lo;
+  const int nplanes = (di_hi - di_lo) * ndj;
+  const int nchunk = g.PR * g.RS * 2;
+  const int na = (g.TK + 3) >> 2, nb = (g.TL + 3) >> 2;
+  const int nanch = na * nb;
+  const int natile = (nanch + 15) >> 4;
+
+  uint32_t abase[MAXA];
+#pragma unroll
+  for (int at = 0; at < MAXA; ++at) {
+    int ai = at * 16 + (lane & 15);
+    if (ai >= nanch) ai = 0;
+    int ak = ai / nb, al = ai - ak * nb;
+    abase[at] = (uint32_t)(((4 * ak) * g.RS + 4 * al) * 32 + ((lane >> 4) & 1) * 16);
+  }
+  uint32_t toff[PPW];
+#pragma unroll
+  for (int q = 0; q < PPW; ++q) {
+    int pr = wave * PPW + q;
+    int tau = 2 * pr + (lane >> 5);
+    if (tau >= TS * TS) tau = TS * TS - 1;
+    int tk = tau / TS, tl = tau - tk * TS;
+    toff[q] = (uint32_t)((tk * g.RS + tl) * 32);
+  }
+
+  f32x4 acc[MAXA];
+#pragma unroll
+  for (int at = 0; at < MAXA; ++at) acc[at] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage16<MAXCH> sx;
+  auto plane_ptr = [&](int s) {
+    int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
+    return X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
+  };
+  auto wptr = [&](int s) {
+    int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
+    return Wp + (size_t)(di * KS + dj) * NPAIR * 64;
+  };
+  bf16x8 wcur[PPW], wnext[PPW];
+  if (nplanes > 0) {
+    sx.load(plane_ptr(0), g, t.k0 - P, t.l0 - P, nchunk);
+    const u32x4* wp = wptr(0);
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      int pr = min(wave * PPW + q, NPAIR - 1);
+      wcur[q] = __builtin_bit_cast(bf16x8, wp[pr * 64 + lane]);
+    }
+    sx.store(plane, nchunk);
+  }
+  __syncthreads();
+
+  for (int s = 0; s < nplanes; ++s) {
+    const bool more = (s + 1) < nplanes;
+    if (more) {
+      sx.load(plane_ptr(s + 1), g, t.k0 - P, t.l0 - P, nchunk);
+      const u32x4* wp = wptr(s + 1);
+#pragma unroll
+      for (int q = 0; q < PPW; ++q) {
+        int pr = min(wave * PPW + q, NPAIR - 1);
+        wnext[q] = __builtin_bit_cast(bf16x8, wp[pr * 64 + lane]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      if (wave * PPW + q < NPAIR) {
+#pragma unroll
+        for (int at = 0; at < MAXA; ++at) {
+          if (at < natile) {
+            bf16x8 xf = lds_read16(plane, abase[at] + toff[q]);
+            acc[at] = mfma16(wcur[q], xf, acc[at]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      sx.store(plane, nchunk);
+#pragma unroll
+      for (int q = 0; q < PPW; ++q) wcur[q] = wnext[q];
+    }
+    __syncthreads();
+  }
+
+  // Cross-wave K reduction: red[wave][at][r][lane].
+  float* red = (float*)smem;
+#pragma unroll
+  for (int at = 0; at < MAXA; ++at)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[((wave * MAXA + at) * 4 + r) * 64 + lane] = acc[at][r];
+  __syncthreads();
+  const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);
+  const float b0 = (EPI == EPI_BIAS_RELU) ? bias[0] : 0.f;
+  for (int e = threadIdx.x; e < MAXA * 4 * 64; e += 256) {
+    int at = e / 256, r = (e >> 6) & 3, ln = e & 63;
+    if (at >= natile) continue;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) sum += red[((w * MAXA + at) * 4 + r) * 64 + ln];
+    int sidx = 4 * (ln >> 4) + r;
+    int ai = at * 16 + (ln & 15);
+    if (ai >= nanch) continue;
+    int ak = ai / nb, al = ai - ak * nb;
+    int kk = 4 * ak + (sidx >> 2), ll = 4 * al + (sidx & 3);
+    int kg = t.k0 + kk, lg = t.l0 + ll;
+    if (kk < g.TK && ll < g.TL && kg < g.K && lg < g.L) {
+      float x = sum;
+      if (EPI == EPI_BIAS_RELU) x = fmaxf(x + b0, 0.f);
+      Y[vbase_out + (size_t)kg * g.L + lg] = x;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers.
+// ---------------------------------------------------------------------------
+static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int tl, int extra_rows, int extra_cols) {
+  ConvGeom g;
+  g.V = V; g.I = I; g.J = J; g.K = K; g.L = L;
+  g.TK = tk; g.TL = tl;
+  g.nkt = cdiv(K, tk); g.nlt = cdiv(L, tl);
+  g.PR = tk + KS - 1 + extra_rows;
+  g.RS = tl + KS - 1 + extra_cols;
+  return g;
+}
+
+}  // namespace ncnet
+
+using namespace ncnet;
+
+// Tile choice: the whole (k,l) plane when it fits (<= 25 x 25 output), else
+// 25 x 25 tiles (InLoc-size planes).
+static void pick_tile(int K, int L, int& tk, int& tl) {
+  tk = K <= 25 ? K : 25;
+  tl = L <= 25 ? L : 25;
+  // keep TK*TL <= 640 (MAXT * 4 waves * 16 voxels)
+  while (tk * tl > 640) { if (tl > tk) --tl; else --tk; }
+}
+
+extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias, const void* M, void* Y,
+                                int V, int I, int J, int K, int L, int KS, int epi, hipStream_t stream) {
+  int tk, tl;
+  pick_tile(K, L, tk, tl);
+  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, 0, 0);
+  if (g.PR * g.RS * 2 > 8 * 256) return -1;
+  int nq = (KS * KS + 1) / 2;
+  size_t lds = (size_t)g.PR * g.RS * 32 + (size_t)nq * 64 * 16;
+  dim3 grid((unsigned)(V * I * J * g.nkt * g.nlt)), block(256);
+  const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
+#define L16(KSV, EPIV) hipLaunchKernelGGL((conv16_fwd_kernel<KSV, EPIV>), grid, block, lds, stream, x, w, bias, m, y, g)
+  if (KS == 5) {
+    if (epi == EPI_BIAS_RELU) L16(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16(5, EPI_MASK); else L16(5, EPI_NONE);
+  } else if (KS == 3) {
+    if (epi == EPI_BIAS_RELU) L16(3, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16(3, EPI_MASK); else L16(3, EPI_NONE);
+  } else return -2;
+#undef L16
+  return (int)hipGetLastError();
+}
+
+extern "C" int ncnet_conv1in_fwd(const void* X, const void* Wp, const float* bias, const void* M, void* Y,
+                                 int V, int I, int J, int K, int L, int KS, int epi, hipStream_t stream) {
+  int tk, tl;
+  pick_tile(K, L, tk, tl);
+  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, 0, 0);
+  int RW = tl + KS - 1 + 8;
+  if (g.PR * RW > 8 * 256) return -1;
+  int nm = (KS + 3) / 4;
+  size_t lds = (size_t)g.PR * tl * 16 + (((size_t)g.PR * RW * 2 + 15) & ~(size_t)15) + (size_t)nm * 64 * 16;
+  dim3 grid((unsigned)(V * I * J * g.nkt * g.nlt)), block(256);
+  const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
+#define L1(KSV, EPIV) hipLaunchKernelGGL((conv1in_fwd_kernel<KSV, EPIV>), grid, block, lds, stream, x, w, bias, m, y, g)
+  if (KS == 5) {
+    if (epi == EPI_BIAS_RELU) L1(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L1(5, EPI_MASK); else L1(5, EPI_NONE);
+  } else if (KS == 3) {
+    if (epi == EPI_BIAS_RELU) L1(3, EPI_BIAS_RELU); else if (epi == EPI_MASK) L1(3, EPI_MASK); else L1(3, EPI_NONE);
+  } else return -2;
+#undef L1
+  return (int)hipGetLastError();
+}
+
+extern "C" int ncnet_conv1out_fwd(const void* X, const void* Wp, const float* bias, float* Y,
+                                  int V, int I, int J, int K, int L, int KS, int epi, hipStream_t stream) {
+  int tk, tl;
+  pick_tile(K, L, tk, tl);
+  // anchors on a 4-grid: stage 4*ceil(T/4) + KS - 1 rows/cols
+  int pr = 4 * cdiv(tk, 4) + KS - 1, rs = 4 * cdiv(tl, 4) + KS - 1;
+  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, pr - (tk + KS - 1), rs - (tl + KS - 1));
+  if (g.PR * g.RS * 2 > 8 * 256) return -1;
+  if (cdiv(tk, 4) * cdiv(tl, 4) > 64) return -1;
+  size_t lds = (size_t)g.PR * g.RS * 32;
+  size_t red = (size_t)4 * 4 * 4 * 64 * 4;
+  if (lds < red) lds = red;
+  dim3 grid((unsigned)(V * I * J * g.nkt * g.nlt)), block(256);
+  const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp;
+#define LO(KSV, EPIV) hipLaunchKernelGGL((conv1out_fwd_kernel<KSV, EPIV>), grid, block, lds, stream, x, w, bias, Y, g)
+  if (KS == 5) {
+    if (epi == EPI_BIAS_RELU) LO(5, EPI_BIAS_RELU); else LO(5, EPI_NONE);
+  } else if (KS == 3) {
+    if (epi == EPI_BIAS_RELU) LO(3, EPI_BIAS_RELU); else LO(3, EPI_NONE);
+  } else return -2;
+#undef LO
+  return (int)hipGetLastError();
+}

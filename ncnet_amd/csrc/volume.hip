@@ -1,0 +1,406 @@
+// Volume-level kernels on 1-channel correlation volumes, viewed as matrices
+// [V, R = I*J (A positions), C = K*L (B positions)] of fp32.
+//
+//  * stats_rows / stats_cols: max, first-argmax and (optionally) sum exp(x-max)
+//    per row / column in one pass (online softmax).  Used by MutualMatching
+//    (lib/model.py:163-166), the weak loss (train.py:125-134) and
+//    corr_to_matches (lib/point_tnf.py:32-57).
+//  * mm_apply: MutualMatching output c*((c/(maxB+eps))*(c/(maxA+eps))); can
+//    also emit the bf16 NC input for BOTH symmetric branches (x and its A<->B
+//    swap, lib/model.py:147) so no permuted copy is ever made.
+//  * mm_bwd: gradient of MutualMatching including the max-routed terms.
+//  * combine: y = z1 + z2^T (the symmetric-branch un-swap + add) and its
+//    backward fused with the last Conv4d's ReLU mask.
+//  * softmax_max_bwd: backward of the weak-loss score (closed form).
+//  * maxpool4d: stride = kernel = ks 4D max pool + packed 2-bit offsets.
+#include "common.h"
+
+namespace ncnet {
+
+struct Stat { float m; float s; int idx; };
+
+__device__ __forceinline__ Stat stat_merge(Stat a, Stat b, bool want_sum) {
+  Stat r;
+  bool take_b = (b.m > a.m) || (b.m == a.m && b.idx < a.idx);
+  r.m = take_b ? b.m : a.m;
+  r.idx = take_b ? b.idx : a.idx;
+  if (want_sum) {
+    float sa = (a.s == 0.f) ? 0.f : a.s * __expf(a.m - r.m);
+    float sb = (b.s == 0.f) ? 0.f : b.s * __expf(b.m - r.m);
+    r.s = sa + sb;
+  } else r.s = 0.f;
+  return r;
+}
+
+__device__ __forceinline__ Stat stat_push(Stat a, float x, int idx, bool want_sum) {
+  if (x > a.m) {
+    if (want_sum) a.s = a.s * __expf(a.m - x) + 1.f;
+    a.m = x; a.idx = idx;
+  } else if (want_sum) {
+    a.s += __expf(x - a.m);
+  }
+  return a;
+}
+
+// One wave per row.
+__global__ __launch_bounds__(256) void stats_rows_kernel(const float* __restrict__ x, float* __restrict__ mx,
+                                                         int* __restrict__ arg, float* __restrict__ se,
+                                                         long long rows, int C) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * C;
+  const bool ws = se != nullptr;
+  Stat st{-INFINITY, 0.f, 0x7fffffff};
+  for (int c = lane; c < C; c += 64) st = stat_push(st, xr[c], c, ws);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Stat ot;
+    ot.m = __shfl_xor(st.m, o, 64);
+    ot.s = __shfl_xor(st.s, o, 64);
+    ot.idx = __shfl_xor(st.idx, o, 64);
+    st = stat_merge(st, ot, ws);
+  }
+  if (lane == 0) {
+    mx[row] = st.m;
+    if (arg) arg[row] = st.idx;
+    if (ws) se[row] = st.s;
+  }
+}
+
+// Block = 64 columns x 4 row-phases.
+__global__ __launch_bounds__(256) void stats_cols_kernel(const float* __restrict__ x, float* __restrict__ mx,
+                                                         int* __restrict__ arg, float* __restrict__ se,
+                                                         int R, int C) {
+  __shared__ float sm[4][64], ss[4][64];
+  __shared__ int si[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ncb = (C + 63) / 64;
+  const int v = blockIdx.x / ncb, cb = blockIdx.x % ncb;
+  const int c = cb * 64 + lane;
+  const bool ws = se != nullptr;
+  Stat st{-INFINITY, 0.f, 0x7fffffff};
+  if (c < C) {
+    const float* xv = x + (size_t)v * R * C + c;
+    for (int r = wave; r < R; r += 4) st = stat_push(st, xv[(size_t)r * C], r, ws);
+  }
+  sm[wave][lane] = st.m; ss[wave][lane] = st.s; si[wave][lane] = st.idx;
+  __syncthreads();
+  if (wave == 0 && c < C) {
+    Stat a{sm[0][lane], ss[0][lane], si[0][lane]};
+#pragma unroll
+    for (int w = 1; w < 4; ++w) a = stat_merge(a, Stat{sm[w][lane], ss[w][lane], si[w][lane]}, ws);
+    size_t o = (size_t)v * C + c;
+    mx[o] = a.m;
+    if (arg) arg[o] = a.idx;
+    if (ws) se[o] = a.s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MutualMatching apply, 64x64 tiles.  rmax: [V,R] (max over B for each A row),
+// cmax: [V,C] (max over A for each B column).
+//   out_f32 [V,R,C] (optional), out_x bf16 [V,R,C] at volume slot v (optional),
+//   out_xt bf16 [V,C,R] at volume slot v (optional; A<->B swapped copy).
+__global__ __launch_bounds__(256) void mm_apply_kernel(const float* __restrict__ c, const float* __restrict__ rmax,
+                                                       const float* __restrict__ cmax, float* __restrict__ out_f32,
+                                                       bf16* __restrict__ out_x, bf16* __restrict__ out_xt,
+                                                       int R, int C, float eps) {
+  __shared__ float tile[64][65];
+  const int ntr = (R + 63) / 64, ntc = (C + 63) / 64;
+  int b = blockIdx.x;
+  const int tc = b % ntc; b /= ntc;
+  const int tr = b % ntr; const int v = b / ntr;
+  const int r0 = tr * 64, c0 = tc * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const size_t vb = (size_t)v * R * C;
+  const int cc = c0 + tx;
+  const float cm = (cc < C) ? cmax[(size_t)v * C + cc] + eps : 1.f;
+  for (int rr = ty; rr < 64; rr += 4) {
+    int r = r0 + rr;
+    float o = 0.f;
+    if (r < R && cc < C) {
+      float x = c[vb + (size_t)r * C + cc];
+      float ra = rmax[(size_t)v * R + r] + eps;
+      o = x * ((x / ra) * (x / cm));
+      if (out_f32) out_f32[vb + (size_t)r * C + cc] = o;
+      if (out_x) out_x[vb + (size_t)r * C + cc] = f2bf(o);
+    }
+    tile[rr][tx] = o;
+  }
+  if (out_xt) {
+    __syncthreads();
+    // write transposed: row = c, col = r
+    const int rw = r0 + tx;
+    for (int cl = ty; cl < 64; cl += 4) {
+      int ccol = c0 + cl;
+      if (ccol < C && rw < R) out_xt[vb + (size_t)ccol * R + rw] = f2bf(tile[tx][cl]);
+    }
+  }
+}
+
+// Row / column sums of g * out for the MutualMatching backward (out recomputed).
+__global__ __launch_bounds__(256) void mm_bwd_rowsum_kernel(const float* __restrict__ c, const float* __restrict__ g,
+                                                            const float* __restrict__ rmax, const float* __restrict__ cmax,
+                                                            float* __restrict__ rsum, long long rows, int R, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int v = (int)(row / R);
+  const float ra = rmax[row] + eps;
+  const float* cr = c + row * C;
+  const float* gr = g + row * C;
+  const float* cmv = cmax + (size_t)v * C;
+  float s = 0.f;
+  for (int k = lane; k < C; k += 64) {
+    float x = cr[k];
+    s += gr[k] * (x * ((x / ra) * (x / (cmv[k] + eps))));
+  }
+  s = wave_sum(s);
+  if (lane == 0) rsum[row] = s;
+}
+
+__global__ __launch_bounds__(256) void mm_bwd_colsum_kernel(const float* __restrict__ c, const float* __restrict__ g,
+                                                            const float* __restrict__ rmax, const float* __restrict__ cmax,
+                                                            float* __restrict__ csum, int R, int C, float eps) {
+  __shared__ float sh[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ncb = (C + 63) / 64;
+  const int v = blockIdx.x / ncb, cb = blockIdx.x % ncb;
+  const int k = cb * 64 + lane;
+  float s = 0.f;
+  if (k < C) {
+    const float cm = cmax[(size_t)v * C + k] + eps;
+    const size_t vb = (size_t)v * R * C;
+    for (int r = wave; r < R; r += 4) {
+      float x = c[vb + (size_t)r * C + k];
+      float ra = rmax[(size_t)v * R + r] + eps;
+      s += g[vb + (size_t)r * C + k] * (x * ((x / ra) * (x / cm)));
+    }
+  }
+  sh[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && k < C) csum[(size_t)v * C + k] = sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane];
+}
+
+__global__ __launch_bounds__(256) void mm_bwd_apply_kernel(const float* __restrict__ c, const float* __restrict__ g,
+                                                           const float* __restrict__ rmax, const int* __restrict__ rarg,
+                                                           const float* __restrict__ rsum,
+                                                           const float* __restrict__ cmax, const int* __restrict__ carg,
+                                                           const float* __restrict__ csum, float* __restrict__ gc,
+                                                           long long total, int R, int C, float eps) {
+  long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int k = (int)(e % C);
+  const long long row = e / C;     // v*R + r
+  const int r = (int)(row % R);
+  const int v = (int)(row / R);
+  const float x = c[e];
+  const float ra = rmax[row] + eps;
+  const float cb = cmax[(size_t)v * C + k] + eps;
+  float gr = g[e] * (3.f * x * x / (ra * cb));
+  if (rarg[row] == k) gr -= rsum[row] / ra;
+  if (carg[(size_t)v * C + k] == r) gr -= csum[(size_t)v * C + k] / cb;
+  gc[e] = gr;
+}
+
+// ---------------------------------------------------------------------------
+// combine: y[v] = z[v] + z[v+Vh]^T  (z second half stored as [C, R])
+__global__ __launch_bounds__(256) void combine_fwd_kernel(const float* __restrict__ z, float* __restrict__ y,
+                                                          int Vh, int R, int C) {
+  __shared__ float tile[64][65];
+  const int ntr = (R + 63) / 64, ntc = (C + 63) / 64;
+  int b = blockIdx.x;
+  const int tc = b % ntc; b /= ntc;
+  const int tr = b % ntr; const int v = b / ntr;
+  const int r0 = tr * 64, c0 = tc * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const float* z2 = z + (size_t)(v + Vh) * R * C;   // [C][R]
+  // load z2 tile rows c0.., cols r0.. coalesced
+  for (int cl = ty; cl < 64; cl += 4) {
+    int cc = c0 + cl, rr = r0 + tx;
+    tile[cl][tx] = (cc < C && rr < R) ? z2[(size_t)cc * R + rr] : 0.f;
+  }
+  __syncthreads();
+  const float* z1 = z + (size_t)v * R * C;
+  float* yv = y + (size_t)v * R * C;
+  for (int rl = ty; rl < 64; rl += 4) {
+    int rr = r0 + rl, cc = c0 + tx;
+    if (rr < R && cc < C) yv[(size_t)rr * C + cc] = z1[(size_t)rr * C + cc] + tile[tx][rl];
+  }
+}
+
+// gz[v] = g[v] * (z[v] > 0), gz[v+Vh] = g[v]^T * (z[v+Vh] > 0) as bf16.
+__global__ __launch_bounds__(256) void combine_bwd_kernel(const float* __restrict__ g, const float* __restrict__ z,
+                                                          bf16* __restrict__ gz, int Vh, int R, int C) {
+  __shared__ float tile[64][65];
+  const int ntr = (R + 63) / 64, ntc = (C + 63) / 64;
+  int b = blockIdx.x;
+  const int tc = b % ntc; b /= ntc;
+  const int tr = b % ntr; const int v = b / ntr;
+  const int r0 = tr * 64, c0 = tc * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const size_t vb1 = (size_t)v * R * C, vb2 = (size_t)(v + Vh) * R * C;
+  for (int rl = ty; rl < 64; rl += 4) {
+    int rr = r0 + rl, cc = c0 + tx;
+    float gv = 0.f;
+    if (rr < R && cc < C) {
+      gv = g[vb1 + (size_t)rr * C + cc];
+      gz[vb1 + (size_t)rr * C + cc] = f2bf(z[vb1 + (size_t)rr * C + cc] > 0.f ? gv : 0.f);
+    }
+    tile[rl][tx] = gv;
+  }
+  __syncthreads();
+  for (int cl = ty; cl < 64; cl += 4) {
+    int cc = c0 + cl, rr = r0 + tx;
+    if (cc < C && rr < R) {
+      size_t o = vb2 + (size_t)cc * R + rr;
+      gz[o] = f2bf(z[o] > 0.f ? tile[tx][cl] : 0.f);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weak-loss score backward (softmax normalisation):
+//   s = max softmax = 1/sumexp; ds/dx_j = s (delta_{j,argmax} - softmax_j)
+// g = wr[v] * ds_row/dx + wc[v] * ds_col/dx
+__global__ __launch_bounds__(256) void softmax_max_bwd_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ rmax, const int* __restrict__ rarg,
+                                                              const float* __restrict__ rse,
+                                                              const float* __restrict__ cmax, const int* __restrict__ carg,
+                                                              const float* __restrict__ cse,
+                                                              const float* __restrict__ wr, const float* __restrict__ wc,
+                                                              float* __restrict__ gx, long long total, int R, int C) {
+  long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int k = (int)(e % C);
+  const long long row = e / C;
+  const int r = (int)(row % R);
+  const int v = (int)(row / R);
+  const float xv = x[e];
+  const float sr = 1.f / rse[row];
+  const size_t ci = (size_t)v * C + k;
+  const float sc = 1.f / cse[ci];
+  const float pr = __expf(xv - rmax[row]) * sr;
+  const float pc = __expf(xv - cmax[ci]) * sc;
+  float gr = wr[v] * sr * (((rarg[row] == k) ? 1.f : 0.f) - pr);
+  gr += wc[v] * sc * (((carg[ci] == r) ? 1.f : 0.f) - pc);
+  gx[e] = gr;
+}
+
+// ---------------------------------------------------------------------------
+// 4D max pool, stride = kernel = ks (<= 4).  idx code: di<<6 | dj<<4 | dk<<2 | dl
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool4d_kernel(const T* __restrict__ x, float* __restrict__ y,
+                                                        uint8_t* __restrict__ code, int V, int I, int J, int K,
+                                                        int L, int ks) {
+  const int Io = I / ks, Jo = J / ks, Ko = K / ks, Lo = L / ks;
+  long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  long long total = (long long)V * Io * Jo * Ko * Lo;
+  if (e >= total) return;
+  long long t = e;
+  const int lo = (int)(t % Lo); t /= Lo;
+  const int ko = (int)(t % Ko); t /= Ko;
+  const int jo = (int)(t % Jo); t /= Jo;
+  const int io = (int)(t % Io); const int v = (int)(t / Io);
+  float best = -INFINITY;
+  int bc = 0;
+  for (int a = 0; a < ks; ++a)
+    for (int b = 0; b < ks; ++b)
+      for (int c = 0; c < ks; ++c)
+        for (int d = 0; d < ks; ++d) {
+          size_t o = ((((size_t)v * I + io * ks + a) * J + jo * ks + b) * K + ko * ks + c) * (size_t)L + lo * ks + d;
+          float val = (float)x[o];
+          if (val > best) { best = val; bc = (a << 6) | (b << 4) | (c << 2) | d; }
+        }
+  y[e] = best;
+  code[e] = (uint8_t)bc;
+}
+
+// [V,R,C] -> [V,C,R] (bf16 or fp32), 64x64 tiles
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ x, T* __restrict__ y, int R, int C) {
+  __shared__ T tile[64][65];
+  const int ntr = (R + 63) / 64, ntc = (C + 63) / 64;
+  int b = blockIdx.x;
+  const int tc = b % ntc; b /= ntc;
+  const int tr = b % ntr; const int v = b / ntr;
+  const int r0 = tr * 64, c0 = tc * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const size_t vb = (size_t)v * R * C;
+  for (int rl = ty; rl < 64; rl += 4) {
+    int rr = r0 + rl, cc = c0 + tx;
+    if (rr < R && cc < C) tile[rl][tx] = x[vb + (size_t)rr * C + cc];
+  }
+  __syncthreads();
+  for (int cl = ty; cl < 64; cl += 4) {
+    int cc = c0 + cl, rr = r0 + tx;
+    if (cc < C && rr < R) y[vb + (size_t)cc * R + rr] = tile[tx][cl];
+  }
+}
+
+}  // namespace ncnet
+
+using namespace ncnet;
+
+static unsigned tiles64(int V, int R, int C) { return (unsigned)((long long)V * cdiv(R, 64) * cdiv(C, 64)); }
+
+extern "C" int ncnet_stats_rows(const float* x, float* mx, int* arg, float* se, long long rows, int C, hipStream_t s) {
+  hipLaunchKernelGGL(stats_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, mx, arg, se, rows, C);
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_stats_cols(const float* x, float* mx, int* arg, float* se, int V, int R, int C, hipStream_t s) {
+  hipLaunchKernelGGL(stats_cols_kernel, dim3((unsigned)(V * cdiv(C, 64))), dim3(256), 0, s, x, mx, arg, se, R, C);
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_mm_apply(const float* c, const float* rmax, const float* cmax, float* out_f32, void* out_x,
+                              void* out_xt, int V, int R, int C, float eps, hipStream_t s) {
+  hipLaunchKernelGGL(mm_apply_kernel, dim3(tiles64(V, R, C)), dim3(256), 0, s, c, rmax, cmax, out_f32, (bf16*)out_x,
+                     (bf16*)out_xt, R, C, eps);
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_mm_bwd(const float* c, const float* g, const float* rmax, const int* rarg, const float* cmax,
+                            const int* carg, float* rsum, float* csum, float* gc, int V, int R, int C, float eps,
+                            hipStream_t s) {
+  long long rows = (long long)V * R;
+  hipLaunchKernelGGL(mm_bwd_rowsum_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, c, g, rmax, cmax, rsum,
+                     rows, R, C, eps);
+  hipLaunchKernelGGL(mm_bwd_colsum_kernel, dim3((unsigned)(V * cdiv(C, 64))), dim3(256), 0, s, c, g, rmax, cmax, csum,
+                     R, C, eps);
+  long long total = rows * C;
+  hipLaunchKernelGGL(mm_bwd_apply_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, c, g, rmax, rarg,
+                     rsum, cmax, carg, csum, gc, total, R, C, eps);
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_combine_fwd(const float* z, float* y, int Vh, int R, int C, hipStream_t s) {
+  hipLaunchKernelGGL(combine_fwd_kernel, dim3(tiles64(Vh, R, C)), dim3(256), 0, s, z, y, Vh, R, C);
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_combine_bwd(const float* g, const float* z, void* gz, int Vh, int R, int C, hipStream_t s) {
+  hipLaunchKernelGGL(combine_bwd_kernel, dim3(tiles64(Vh, R, C)), dim3(256), 0, s, g, z, (bf16*)gz, Vh, R, C);
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_softmax_max_bwd(const float* x, const float* rmax, const int* rarg, const float* rse,
+                                     const float* cmax, const int* carg, const float* cse, const float* wr,
+                                     const float* wc, float* gx, int V, int R, int C, hipStream_t s) {
+  long long total = (long long)V * R * C;
+  hipLaunchKernelGGL(softmax_max_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, rmax, rarg, rse,
+                     cmax, carg, cse, wr, wc, gx, total, R, C);
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_maxpool4d(const void* x, int x_is_bf16, float* y, uint8_t* code, int V, int I, int J, int K,
+                               int L, int ks, hipStream_t s) {
+  if (ks > 4 || ks < 1) return -1;
+  long long total = (long long)V * (I / ks) * (J / ks) * (K / ks) * (L / ks);
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (x_is_bf16) hipLaunchKernelGGL((maxpool4d_kernel<bf16>), grid, dim3(256), 0, s, (const bf16*)x, y, code, V, I, J, K, L, ks);
+  else hipLaunchKernelGGL((maxpool4d_kernel<float>), grid, dim3(256), 0, s, (const float*)x, y, code, V, I, J, K, L, ks);
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_transpose(const void* x, void* y, int elem_bytes, int V, int R, int C, hipStream_t s) {
+  dim3 grid(tiles64(V, R, C));
+  if (elem_bytes == 2) hipLaunchKernelGGL((transpose_kernel<bf16>), grid, dim3(256), 0, s, (const bf16*)x, (bf16*)y, R, C);
+  else if (elem_bytes == 4) hipLaunchKernelGGL((transpose_kernel<float>), grid, dim3(256), 0, s, (const float*)x, (float*)y, R, C);
+  else return -1;
+  return (int)hipGetLastError();
+}

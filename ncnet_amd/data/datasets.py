@@ -1,0 +1,158 @@
+"""Pair datasets (lib/im_pair_dataset.py, lib/pf_dataset.py) and synthetic pairs.
+
+CSV formats:
+* train / val: ``source_image,target_image,class,flip``
+* PF-Pascal test: ``source_image,target_image,class,XA,YA,XB,YB`` with ``;``
+  separated point lists.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pandas as pd
+import torch
+from torch.utils.data import Dataset
+
+from .transforms import read_image, resize_bilinear, to_chw_float
+
+PF_CATEGORIES = ["aeroplane", "bicycle", "bird", "boat", "bottle", "bus", "car", "cat", "chair", "cow",
+                 "diningtable", "dog", "horse", "motorbike", "person", "pottedplant", "sheep", "sofa", "train",
+                 "tvmonitor"]
+
+
+class ImagePairDataset(Dataset):
+    """Weakly supervised image pairs (lib/im_pair_dataset.py:11-93)."""
+
+    def __init__(self, dataset_csv_path, dataset_csv_file, dataset_image_path, dataset_size=0,
+                 output_size=(240, 240), transform=None, random_crop=False):
+        self.random_crop = random_crop
+        self.out_h, self.out_w = output_size
+        data = pd.read_csv(os.path.join(dataset_csv_path, dataset_csv_file))
+        if dataset_size:
+            data = data.iloc[: min(dataset_size, len(data))]
+        self.img_A_names = data.iloc[:, 0].tolist()
+        self.img_B_names = data.iloc[:, 1].tolist()
+        self.set = data.iloc[:, 2].to_numpy()
+        self.flip = data.iloc[:, 3].to_numpy().astype("int")
+        self.dataset_image_path = dataset_image_path
+        self.transform = transform
+
+    def __len__(self):
+        return len(self.img_A_names)
+
+    def get_image(self, name, flip):
+        image = read_image(os.path.join(self.dataset_image_path, name))
+        if self.random_crop:
+            h, w, _ = image.shape
+            top = np.random.randint(h // 4)
+            bottom = int(3 * h / 4 + np.random.randint(h // 4))
+            left = np.random.randint(w // 4)
+            right = int(3 * w / 4 + np.random.randint(w // 4))
+            image = image[top:bottom, left:right, :]
+        if flip:
+            image = np.flip(image, 1)
+        im_size = torch.tensor(image.shape, dtype=torch.float32)
+        img = resize_bilinear(to_chw_float(image), self.out_h, self.out_w)
+        return img, im_size
+
+    def __getitem__(self, idx):
+        a, sa = self.get_image(self.img_A_names[idx], self.flip[idx])
+        b, sb = self.get_image(self.img_B_names[idx], self.flip[idx])
+        sample = {"source_image": a, "target_image": b, "source_im_size": sa, "target_im_size": sb,
+                  "set": int(self.set[idx])}
+        if self.transform:
+            sample = self.transform(sample)
+        return sample
+
+
+class PFPascalDataset(Dataset):
+    """PF-Pascal keypoint pairs (lib/pf_dataset.py:11-112)."""
+
+    def __init__(self, csv_file, dataset_path, output_size=(240, 240), transform=None, category=None,
+                 pck_procedure="pf"):
+        self.category_names = PF_CATEGORIES
+        self.out_h, self.out_w = output_size
+        pairs = pd.read_csv(csv_file)
+        self.category = pairs.iloc[:, 2].to_numpy().astype("float")
+        if category is not None:
+            keep = np.nonzero(self.category == category)[0]
+            self.category = self.category[keep]
+            pairs = pairs.iloc[keep, :]
+        self.pairs = pairs
+        self.img_A_names = pairs.iloc[:, 0].tolist()
+        self.img_B_names = pairs.iloc[:, 1].tolist()
+        self.point_A_coords = pairs.iloc[:, 3:5]
+        self.point_B_coords = pairs.iloc[:, 5:]
+        self.dataset_path = dataset_path
+        self.transform = transform
+        self.pck_procedure = pck_procedure
+
+    def __len__(self):
+        return len(self.pairs)
+
+    def get_image(self, name):
+        image = read_image(os.path.join(self.dataset_path, name))
+        im_size = torch.tensor(image.shape, dtype=torch.float32)
+        return resize_bilinear(to_chw_float(image), self.out_h, self.out_w), im_size
+
+    @staticmethod
+    def parse_points(xs: str, ys: str, n: int = 20) -> torch.Tensor:
+        x = np.array([float(v) for v in str(xs).split(";") if v != ""])
+        y = np.array([float(v) for v in str(ys).split(";") if v != ""])
+        out = -np.ones((2, n))
+        out[0, : len(x)] = x
+        out[1, : len(x)] = y
+        return torch.tensor(out, dtype=torch.float32)
+
+    def __getitem__(self, idx):
+        image_a, size_a = self.get_image(self.img_A_names[idx])
+        image_b, size_b = self.get_image(self.img_B_names[idx])
+        pa = self.parse_points(self.point_A_coords.iloc[idx, 0], self.point_A_coords.iloc[idx, 1])
+        pb = self.parse_points(self.point_B_coords.iloc[idx, 0], self.point_B_coords.iloc[idx, 1])
+        n_pts = int(torch.sum(pa[0] != -1))
+        if self.pck_procedure == "pf":
+            l_pck = torch.tensor([float(torch.max(pa[:, :n_pts].max(1)[0] - pa[:, :n_pts].min(1)[0]))])
+        elif self.pck_procedure == "scnet":
+            pa[0, :n_pts] *= 224 / size_a[1]
+            pa[1, :n_pts] *= 224 / size_a[0]
+            pb[0, :n_pts] *= 224 / size_b[1]
+            pb[1, :n_pts] *= 224 / size_b[0]
+            size_a[0:2] = torch.tensor([224.0, 224.0])
+            size_b[0:2] = torch.tensor([224.0, 224.0])
+            l_pck = torch.tensor([224.0])
+        else:
+            raise ValueError(self.pck_procedure)
+        sample = {"source_image": image_a, "target_image": image_b, "source_im_size": size_a,
+                  "target_im_size": size_b, "source_points": pa, "target_points": pb, "L_pck": l_pck}
+        if self.transform:
+            sample = self.transform(sample)
+        return sample
+
+
+class SyntheticPairDataset(Dataset):
+    """Random normalised image pairs of a fixed size (benchmarks, smoke tests)."""
+
+    def __init__(self, length: int = 64, image_size=(400, 400), seed: int = 0):
+        self.length = length
+        self.h, self.w = image_size
+        self.seed = seed
+
+    def __len__(self):
+        return self.length
+
+    def __getitem__(self, idx):
+        g = torch.Generator().manual_seed(self.seed * 100003 + idx)
+        a = torch.randn(3, self.h, self.w, generator=g)
+        b = torch.randn(3, self.h, self.w, generator=g)
+        size = torch.tensor([self.h, self.w, 3], dtype=torch.float32)
+        return {"source_image": a, "target_image": b, "source_im_size": size, "target_im_size": size, "set": 0}
+
+
+def synthetic_batch(batch: int, image_size=(400, 400), device="cpu", seed: int = 0):
+    """One batch of random normalised pairs generated directly on ``device``."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    h, w = image_size
+    src = torch.randn(batch, 3, h, w, generator=g, device=device)
+    tgt = torch.randn(batch, 3, h, w, generator=g, device=device)
+    return {"source_image": src, "target_image": tgt}

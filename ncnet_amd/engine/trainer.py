@@ -1,0 +1,101 @@
+"""Weakly-supervised training loop (train.py:110-205), DP-aware.
+
+Differences from the reference, all semantics-preserving:
+* the negative pass reuses the positive-pass backbone features rolled by one
+  (exact: the backbone is in eval mode and per-sample);
+* the loss is read back to the host only every ``log_interval`` steps;
+* evaluation (``mode='test'``) runs under ``torch.inference_mode`` (the
+  reference builds graphs it never uses, train.py:170-174);
+* gradients are averaged over ranks with one bucketed RCCL all-reduce;
+* optional NaN/Inf guard skips a step whose loss is not finite.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..ops.loss import weak_loss_from_corr
+from ..parallel.dist import DistContext, GradBucket, all_reduce_mean
+
+
+def weak_loss(model, batch, normalization: str | None = "softmax", alpha: float = 30) -> torch.Tensor:
+    """score_neg - score_pos (train.py:110-156). ``alpha`` is unused, as in the reference."""
+    src, tgt = batch["source_image"], batch["target_image"]
+    vols = model.weak_loss_volumes(src, tgt)
+    return weak_loss_from_corr(vols, src.shape[0], normalization)
+
+
+class Trainer:
+    def __init__(self, model, optimizer, ctx: DistContext, normalization="softmax", nan_guard=True,
+                 metrics_path: str | None = None, fault_step: int | None = None):
+        self.model = model
+        self.opt = optimizer
+        self.ctx = ctx
+        self.normalization = normalization
+        self.nan_guard = nan_guard
+        params = [p for p in model.parameters() if p.requires_grad]
+        self.bucket = GradBucket(params, ctx)
+        self.metrics_path = metrics_path if ctx.is_main else None
+        self.global_step = 0
+        self.fault_step = fault_step if fault_step is not None else int(os.environ.get("NCNET_FAULT_STEP", "-1"))
+
+    def to_device(self, batch):
+        dev = self.ctx.device
+        return {k: (v.to(dev, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()}
+
+    def train_step(self, batch) -> torch.Tensor:
+        if self.fault_step >= 0 and self.global_step == self.fault_step:
+            raise RuntimeError(f"injected fault at step {self.global_step} (NCNET_FAULT_STEP)")
+        self.opt.zero_grad(set_to_none=True)
+        loss = weak_loss(self.model, batch, self.normalization)
+        loss.backward()
+        self.bucket.allreduce()
+        if self.nan_guard:
+            finite = torch.isfinite(loss)
+            # stay asynchronous: zero the grads of a non-finite step instead of branching on the host
+            for p in self.bucket.params:
+                if p.grad is not None:
+                    p.grad.mul_(finite.to(p.grad.dtype))
+        self.opt.step()
+        self.global_step += 1
+        return loss.detach()
+
+    @torch.inference_mode()
+    def eval_step(self, batch) -> torch.Tensor:
+        return weak_loss(self.model, batch, self.normalization).detach()
+
+    def _log(self, rec: dict):
+        if self.metrics_path:
+            with open(self.metrics_path, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+
+    def process_epoch(self, mode: str, epoch: int, loader, log_interval: int = 1) -> float:
+        """Returns the epoch's mean loss (averaged over ranks)."""
+        is_train = mode == "train"
+        self.model.train(is_train)
+        total = torch.zeros((), device=self.ctx.device)
+        n = 0
+        t0 = time.perf_counter()
+        nb = len(loader)
+        for batch_idx, batch in enumerate(loader):
+            batch = self.to_device(batch)
+            loss = self.train_step(batch) if is_train else self.eval_step(batch)
+            total += loss.float()
+            n += 1
+            if log_interval and batch_idx % log_interval == 0:
+                lv = float(all_reduce_mean(loss, self.ctx))
+                dt = time.perf_counter() - t0
+                if self.ctx.is_main:
+                    print(f"{mode.capitalize()} Epoch: {epoch} [{batch_idx}/{nb} ({100.0 * batch_idx / max(nb, 1):.0f}%)]"
+                          f"\t\tLoss: {lv:.6f}", flush=True)
+                self._log({"mode": mode, "epoch": epoch, "step": batch_idx, "loss": lv, "elapsed_s": dt,
+                           "pairs": n * batch["source_image"].shape[0] * self.ctx.world_size})
+        mean = float(all_reduce_mean(total / max(n, 1), self.ctx))
+        if self.ctx.is_main:
+            print(f"{mode.capitalize()} set: Average loss: {mean:.4f}", flush=True)
+        return mean

@@ -1,0 +1,239 @@
+"""Feature-extraction backbones, written in-repo (torchvision is not available).
+
+Module names and ``nn.Sequential`` indices reproduce torchvision's, so the
+state-dict keys match the reference checkpoints exactly:
+``FeatureExtraction.model.{0,1,4,5,6}.*`` for the ResNet trunk that the
+reference builds as ``Sequential([conv1, bn1, relu, maxpool, layer1, layer2,
+layer3])`` (lib/model.py:37-44), VGG16 ``features[:pool4]`` (lib/model.py:24-35)
+and DenseNet-201 ``features[:-4]`` (lib/model.py:69-74).
+
+Weights are random-initialised (there is no network to fetch ImageNet weights);
+a local state-dict can be loaded with ``load_state_dict``.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _kaiming(m: nn.Module):
+    if isinstance(m, nn.Conv2d):
+        nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        if m.bias is not None:
+            nn.init.zeros_(m.bias)
+    elif isinstance(m, nn.BatchNorm2d):
+        nn.init.ones_(m.weight)
+        nn.init.zeros_(m.bias)
+
+
+class Bottleneck(nn.Module):
+    """torchvision-v1.5 bottleneck (stride on the 3x3 conv)."""
+    expansion = 4
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return self.relu(out + identity)
+
+
+class ResNet(nn.Module):
+    """ResNet with torchvision attribute names (conv1, bn1, relu, maxpool, layer1..4)."""
+
+    def __init__(self, layers=(3, 4, 23, 3)):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, layers[0])
+        self.layer2 = self._make_layer(128, layers[1], stride=2)
+        self.layer3 = self._make_layer(256, layers[2], stride=2)
+        self.layer4 = self._make_layer(512, layers[3], stride=2)
+        self.apply(_kaiming)
+
+    def _make_layer(self, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * 4:
+            downsample = nn.Sequential(
+                nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
+                nn.BatchNorm2d(planes * 4),
+            )
+        mods = [Bottleneck(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * 4
+        for _ in range(1, blocks):
+            mods.append(Bottleneck(self.inplanes, planes))
+        return nn.Sequential(*mods)
+
+
+RESNET_LAYERS = ["conv1", "bn1", "relu", "maxpool", "layer1", "layer2", "layer3", "layer4"]
+RESNET_DEPTHS = {"resnet18": None, "resnet50": (3, 4, 6, 3), "resnet101": (3, 4, 23, 3), "resnet152": (3, 8, 36, 3)}
+
+
+def resnet_trunk(arch: str = "resnet101", last_layer: str = "") -> nn.Sequential:
+    """Sequential trunk up to ``last_layer`` (default layer3: stride 16, 1024 ch)."""
+    depths = RESNET_DEPTHS.get(arch)
+    if depths is None:
+        raise ValueError(f"unsupported resnet variant {arch!r}")
+    net = ResNet(depths)
+    last = last_layer or "layer3"
+    idx = RESNET_LAYERS.index(last)
+    return nn.Sequential(*[getattr(net, n) for n in RESNET_LAYERS[: idx + 1]])
+
+
+VGG16_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
+VGG_LAYER_NAMES = ["conv1_1", "relu1_1", "conv1_2", "relu1_2", "pool1", "conv2_1", "relu2_1", "conv2_2",
+                   "relu2_2", "pool2", "conv3_1", "relu3_1", "conv3_2", "relu3_2", "conv3_3", "relu3_3",
+                   "pool3", "conv4_1", "relu4_1", "conv4_2", "relu4_2", "conv4_3", "relu4_3", "pool4",
+                   "conv5_1", "relu5_1", "conv5_2", "relu5_2", "conv5_3", "relu5_3", "pool5"]
+
+
+def vgg16_trunk(last_layer: str = "") -> nn.Sequential:
+    """torchvision vgg16().features[: last_layer] (default pool4, stride 16, 512 ch)."""
+    mods, c = [], 3
+    for v in VGG16_CFG:
+        if v == "M":
+            mods.append(nn.MaxPool2d(2, 2))
+        else:
+            mods += [nn.Conv2d(c, v, 3, padding=1), nn.ReLU(inplace=True)]
+            c = v
+    last = last_layer or "pool4"
+    idx = VGG_LAYER_NAMES.index(last)
+    seq = nn.Sequential(*mods[: idx + 1])
+    seq.apply(_kaiming)
+    return seq
+
+
+class _DenseLayer(nn.Module):
+    def __init__(self, cin, growth, bn_size):
+        super().__init__()
+        self.norm1 = nn.BatchNorm2d(cin)
+        self.relu1 = nn.ReLU(inplace=True)
+        self.conv1 = nn.Conv2d(cin, bn_size * growth, 1, bias=False)
+        self.norm2 = nn.BatchNorm2d(bn_size * growth)
+        self.relu2 = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(bn_size * growth, growth, 3, padding=1, bias=False)
+
+    def forward(self, feats):
+        x = torch.cat(feats, 1) if isinstance(feats, (list, tuple)) else feats
+        out = self.conv1(self.relu1(self.norm1(x)))
+        return self.conv2(self.relu2(self.norm2(out)))
+
+
+class _DenseBlock(nn.ModuleDict):
+    def __init__(self, n, cin, growth, bn_size):
+        super().__init__()
+        for i in range(n):
+            self.add_module("denselayer%d" % (i + 1), _DenseLayer(cin + i * growth, growth, bn_size))
+
+    def forward(self, x):
+        feats = [x]
+        for layer in self.values():
+            feats.append(layer(feats))
+        return torch.cat(feats, 1)
+
+
+class _Transition(nn.Sequential):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.add_module("norm", nn.BatchNorm2d(cin))
+        self.add_module("relu", nn.ReLU(inplace=True))
+        self.add_module("conv", nn.Conv2d(cin, cout, 1, bias=False))
+        self.add_module("pool", nn.AvgPool2d(2, 2))
+
+
+def densenet201_trunk() -> nn.Sequential:
+    """torchvision densenet201().features[:-4] (up to transition2, 256 ch, stride 16)."""
+    growth, bn_size, blocks, c = 32, 4, (6, 12, 48, 32), 64
+    feats = OrderedDict([
+        ("conv0", nn.Conv2d(3, c, 7, stride=2, padding=3, bias=False)),
+        ("norm0", nn.BatchNorm2d(c)),
+        ("relu0", nn.ReLU(inplace=True)),
+        ("pool0", nn.MaxPool2d(3, stride=2, padding=1)),
+    ])
+    for i, n in enumerate(blocks):
+        feats["denseblock%d" % (i + 1)] = _DenseBlock(n, c, growth, bn_size)
+        c = c + n * growth
+        if i != len(blocks) - 1:
+            feats["transition%d" % (i + 1)] = _Transition(c, c // 2)
+            c = c // 2
+    feats["norm5"] = nn.BatchNorm2d(c)
+    full = nn.Sequential(feats)
+    seq = nn.Sequential(*list(full.children())[:-4])
+    seq.apply(_kaiming)
+    return seq
+
+
+def build_trunk(cnn: str = "resnet101", last_layer: str = "") -> tuple[nn.Sequential, int, int]:
+    """Returns (trunk, out_channels, stride)."""
+    if cnn == "vgg":
+        return vgg16_trunk(last_layer), 512, 16
+    if cnn.startswith("resnet") and not cnn.endswith("fpn"):
+        last = last_layer or "layer3"
+        ch = {"layer1": 256, "layer2": 512, "layer3": 1024, "layer4": 2048}.get(last, 64)
+        stride = {"layer1": 4, "layer2": 8, "layer3": 16, "layer4": 32}.get(last, 4)
+        return resnet_trunk(cnn, last), ch, stride
+    if cnn == "densenet201":
+        return densenet201_trunk(), 256, 16
+    if cnn == "resnet101fpn":
+        # lib/model.py:46-67 references an undefined fpn_body: unsupported there too.
+        raise NotImplementedError("resnet101fpn is broken in the reference (undefined fpn_body, lib/model.py:61)")
+    raise ValueError(f"unknown feature_extraction_cnn {cnn!r}")
+
+
+@torch.no_grad()
+def fold_frozen_bn(trunk: nn.Module) -> nn.Module:
+    """Return a copy of an eval-mode trunk in which every Conv2d->BatchNorm2d
+    pair is folded into a single biased conv (frozen BN is an affine map), so
+    the frozen backbone issues one MIOpen conv per layer and no BN kernels."""
+    import copy
+
+    t = copy.deepcopy(trunk).eval()
+
+    def fold(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> nn.Conv2d:
+        scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+        fused = nn.Conv2d(conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride,
+                          conv.padding, conv.dilation, conv.groups, bias=True).to(conv.weight.device)
+        fused.weight.copy_(conv.weight * scale.view(-1, 1, 1, 1))
+        b = conv.bias if conv.bias is not None else torch.zeros_like(bn.running_mean)
+        fused.bias.copy_((b - bn.running_mean) * scale + bn.bias)
+        return fused
+
+    def walk(m: nn.Module):
+        if isinstance(m, Bottleneck):
+            m.conv1, m.bn1 = fold(m.conv1, m.bn1), nn.Identity()
+            m.conv2, m.bn2 = fold(m.conv2, m.bn2), nn.Identity()
+            m.conv3, m.bn3 = fold(m.conv3, m.bn3), nn.Identity()
+            if m.downsample is not None:
+                m.downsample = nn.Sequential(fold(m.downsample[0], m.downsample[1]))
+            return
+        if isinstance(m, nn.Sequential):
+            kids = list(m._modules.items())
+            for idx in range(len(kids) - 1):
+                (na, a), (nb, b) = kids[idx], kids[idx + 1]
+                if isinstance(a, nn.Conv2d) and isinstance(b, nn.BatchNorm2d):
+                    m._modules[na] = fold(a, b)
+                    m._modules[nb] = nn.Identity()
+        for c in m.children():
+            walk(c)
+
+    walk(t)
+    return t

@@ -1,0 +1,255 @@
+"""ImMatchNet (NC-Net) with the reference's constructor and forward API.
+
+Reference: lib/model.py:19-282.  Module names (``FeatureExtraction.model``,
+``NeighConsensus.conv.{0,2,4}``) and parameter shapes match the reference so
+``.pth.tar`` checkpoints load unchanged.
+
+Compute policy (MI355X):
+* the frozen backbone runs in eval mode under ``no_grad``, bf16, channels-last
+  (MIOpen); frozen BN is optionally folded into the convs;
+* L2-norm + operand packing, correlation GEMM, MutualMatching, the Conv4d
+  stack and the loss reductions run on the hand-written HIP kernels;
+* ``half_precision`` is kept for API parity: the NC path always runs bf16
+  operands with fp32 accumulation on GPU.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import reference as ref
+from ..ops.conv4d import Conv4d
+from ..ops.correlation import correlation, correlation_pool2, l2norm_pack, maxpool4d as _maxpool4d
+from ..ops.mutual import mutual_matching
+from ..ops.neigh_consensus import neigh_consensus
+from .backbones import build_trunk, fold_frozen_bn
+
+
+def featureL2Norm(feature: torch.Tensor) -> torch.Tensor:  # noqa: N802 (reference name)
+    return ref.feature_l2norm(feature)
+
+
+def MutualMatching(corr4d: torch.Tensor) -> torch.Tensor:  # noqa: N802 (reference name)
+    return mutual_matching(corr4d)
+
+
+def maxpool4d(corr4d_hres: torch.Tensor, k_size: int = 4):
+    """Returns (corr4d, max_i, max_j, max_k, max_l) like lib/model.py:177-191,
+    but batch-correct and with integer offsets."""
+    vals, (di, dj, dk, dl) = _maxpool4d(corr4d_hres, k_size)
+    return vals, di, dj, dk, dl
+
+
+class FeatureExtraction(nn.Module):
+    def __init__(self, train_fe: bool = False, feature_extraction_cnn: str = "resnet101",
+                 feature_extraction_model_file: str = "", normalization: bool = True, last_layer: str = "",
+                 use_cuda: bool = True):
+        super().__init__()
+        self.normalization = normalization
+        self.feature_extraction_cnn = feature_extraction_cnn
+        self.model, self.out_channels, self.stride = build_trunk(feature_extraction_cnn, last_layer)
+        if feature_extraction_model_file:
+            sd = torch.load(feature_extraction_model_file, map_location="cpu", weights_only=True)
+            self.model.load_state_dict(sd, strict=False)
+        if not train_fe:
+            for p in self.model.parameters():
+                p.requires_grad = False
+        if use_cuda and torch.cuda.is_available():
+            self.model = self.model.cuda()
+        self._folded = None
+        self._folded_version = None
+
+    def trunk_forward(self, images: torch.Tensor, dtype: torch.dtype | None = None) -> torch.Tensor:
+        """Raw (un-normalised) trunk features, channels-last on GPU."""
+        frozen = not any(p.requires_grad for p in self.model.parameters())
+        x = images
+        if x.is_cuda:
+            x = x.contiguous(memory_format=torch.channels_last)
+        if frozen and not self.training and x.is_cuda and self.feature_extraction_cnn.startswith("resnet"):
+            net = self._folded_trunk()
+        else:
+            net = self.model
+        use_amp = x.is_cuda and dtype in (torch.bfloat16, torch.float16)
+        with torch.autocast("cuda", dtype=dtype, enabled=use_amp):
+            with torch.set_grad_enabled(torch.is_grad_enabled() and not frozen):
+                return net(x)
+
+    def _folded_trunk(self):
+        ver = sum(p._version for p in self.model.parameters()) + sum(b._version for b in self.model.buffers())
+        if self._folded is None or self._folded_version != ver:
+            self._folded = fold_frozen_bn(self.model).to(memory_format=torch.channels_last)
+            self._folded_version = ver
+        return self._folded
+
+    def forward(self, image_batch: torch.Tensor) -> torch.Tensor:
+        features = self.trunk_forward(image_batch)
+        if self.normalization:
+            features = featureL2Norm(features.float())
+        return features
+
+
+class FeatureCorrelation(nn.Module):
+    """'4D' (used by ImMatchNet) and legacy '3D' correlation (lib/model.py:89-120)."""
+
+    def __init__(self, shape: str = "3D", normalization: bool = True):
+        super().__init__()
+        self.normalization = normalization
+        self.shape = shape
+        self.ReLU = nn.ReLU()
+
+    def forward(self, feature_A, feature_B):  # noqa: N803
+        if self.shape == "3D":
+            corr = ref.correlation_3d(feature_A, feature_B)
+        else:
+            b, c, ha, wa = feature_A.shape
+            _, _, hb, wb = feature_B.shape
+            fa = feature_A.permute(0, 2, 3, 1).reshape(b, ha * wa, c)
+            fb = feature_B.permute(0, 2, 3, 1).reshape(b, hb * wb, c)
+            corr = correlation(fa, fb).view(b, 1, ha, wa, hb, wb)
+        if self.normalization:
+            corr = featureL2Norm(self.ReLU(corr))
+        return corr
+
+
+class NeighConsensus(nn.Module):
+    def __init__(self, use_cuda: bool = True, kernel_sizes=(3, 3, 3), channels=(10, 10, 1),
+                 symmetric_mode: bool = True):
+        super().__init__()
+        self.symmetric_mode = symmetric_mode
+        self.kernel_sizes = list(kernel_sizes)
+        self.channels = list(channels)
+        mods = []
+        for i, (k, c) in enumerate(zip(kernel_sizes, channels)):
+            cin = 1 if i == 0 else channels[i - 1]
+            mods.append(Conv4d(in_channels=cin, out_channels=c, kernel_size=k, bias=True))
+            mods.append(nn.ReLU(inplace=True))
+        self.conv = nn.Sequential(*mods)
+        if use_cuda and torch.cuda.is_available():
+            self.conv.cuda()
+
+    def conv_layers(self):
+        return [m for m in self.conv if isinstance(m, Conv4d)]
+
+    def forward(self, x):
+        layers = self.conv_layers()
+        ws = [m.weight_ref() for m in layers]
+        bs = [m.bias if m.bias is not None else torch.zeros(m.out_channels, device=x.device) for m in layers]
+        return neigh_consensus(x, ws, bs, self.channels, symmetric=self.symmetric_mode)
+
+
+def _load_reference_checkpoint(path: str):
+    from ..engine.checkpoint import load_checkpoint
+
+    ck = load_checkpoint(path)
+    ck["state_dict"] = OrderedDict((k.replace("vgg", "model"), v) for k, v in ck["state_dict"].items())
+    return ck
+
+
+class ImMatchNet(nn.Module):
+    def __init__(self, feature_extraction_cnn: str = "resnet101", feature_extraction_last_layer: str = "",
+                 feature_extraction_model_file: str | None = None, return_correlation: bool = False,
+                 ncons_kernel_sizes=(3, 3, 3), ncons_channels=(10, 10, 1), normalize_features: bool = True,
+                 train_fe: bool = False, use_cuda: bool = True, relocalization_k_size: int = 0,
+                 half_precision: bool = False, checkpoint: str | None = None, dtype: str = "bf16",
+                 fold_bn: bool = True):
+        super().__init__()
+        ck = None
+        if checkpoint:
+            ck = _load_reference_checkpoint(checkpoint)
+            args = ck.get("args")
+            if args is not None:
+                ncons_channels = getattr(args, "ncons_channels", ncons_channels)
+                ncons_kernel_sizes = getattr(args, "ncons_kernel_sizes", ncons_kernel_sizes)
+        self.use_cuda = use_cuda and torch.cuda.is_available()
+        self.normalize_features = normalize_features
+        self.return_correlation = return_correlation
+        self.relocalization_k_size = relocalization_k_size
+        self.half_precision = half_precision
+        self.compute_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype]
+        self.fold_bn = fold_bn
+        self.FeatureExtraction = FeatureExtraction(train_fe=train_fe, feature_extraction_cnn=feature_extraction_cnn,
+                                                   feature_extraction_model_file=feature_extraction_model_file or "",
+                                                   last_layer=feature_extraction_last_layer,
+                                                   normalization=normalize_features, use_cuda=self.use_cuda)
+        self.FeatureCorrelation = FeatureCorrelation(shape="4D", normalization=False)
+        self.NeighConsensus = NeighConsensus(use_cuda=self.use_cuda, kernel_sizes=list(ncons_kernel_sizes),
+                                             channels=list(ncons_channels))
+        if ck is not None:
+            sd = ck["state_dict"]
+            fe_sd = self.FeatureExtraction.state_dict()
+            for name in fe_sd:
+                if "num_batches_tracked" in name:
+                    continue
+                fe_sd[name].copy_(sd["FeatureExtraction." + name])
+            for name, t in self.NeighConsensus.state_dict().items():
+                t.copy_(sd["NeighConsensus." + name])
+        self.FeatureExtraction.eval()
+
+    # -- training-mode control: the backbone stays in eval (BN frozen), as in
+    #    lib/model.py:251 and train.py:188.
+    def train(self, mode: bool = True):
+        super().train(mode)
+        self.FeatureExtraction.eval()
+        return self
+
+    def _fe_dtype(self, x):
+        return self.compute_dtype if x.is_cuda else None
+
+    def extract(self, images: torch.Tensor) -> torch.Tensor:
+        """images [N,3,H,W] -> L2-normalised packed features [N, H*W, C] (+ grid size)."""
+        f = self.FeatureExtraction.trunk_forward(images, self._fe_dtype(images))
+        if not self.FeatureExtraction.normalization:
+            n, c, h, w = f.shape
+            return f.permute(0, 2, 3, 1).reshape(n, h * w, c), (h, w)
+        return l2norm_pack(f), tuple(f.shape[-2:])
+
+    def process_correlation(self, corr4d: torch.Tensor) -> torch.Tensor:
+        """MutualMatching -> NeighConsensus -> MutualMatching (lib/model.py:274-276)."""
+        corr4d = MutualMatching(corr4d)
+        corr4d = self.NeighConsensus(corr4d)
+        return MutualMatching(corr4d)
+
+    def forward(self, tnf_batch):
+        src, tgt = tnf_batch["source_image"], tnf_batch["target_image"]
+        b = src.shape[0]
+        if src.shape == tgt.shape:
+            f, (h, w) = self.extract(torch.cat((src, tgt), 0))
+            fa, fb = f[:b], f[b:]
+            ha, wa, hb, wb = h, w, h, w
+        else:
+            fa, (ha, wa) = self.extract(src)
+            fb, (hb, wb) = self.extract(tgt)
+        k = self.relocalization_k_size
+        if k > 1:
+            if k == 2 and ha % 2 == 0 and wa % 2 == 0 and hb % 2 == 0 and wb % 2 == 0:
+                corr4d, delta = correlation_pool2(fa, fb, ha, wa, hb, wb)
+            else:
+                corr4d = correlation(fa, fb).view(b, 1, ha, wa, hb, wb)
+                corr4d, *delta = maxpool4d(corr4d, k)
+                delta = tuple(delta)
+        else:
+            corr4d = correlation(fa, fb).view(b, 1, ha, wa, hb, wb)
+        corr4d = self.process_correlation(corr4d)
+        if k > 1:
+            return corr4d, delta
+        return corr4d
+
+    def weak_loss_volumes(self, src: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
+        """Positive and rolled-negative volumes [2B,1,h,w,h,w] for the weak loss.
+
+        The negative pass of train.py:137 rolls the *source images* by -1; the
+        backbone is in eval mode and acts per sample, so this equals rolling
+        the source *features* -- the backbone runs once on 2B images instead
+        of 4B."""
+        b = src.shape[0]
+        f, (h, w) = self.extract(torch.cat((src, tgt), 0))
+        fa, fb = f[:b], f[b:]
+        dev = f.device
+        ar = torch.arange(b, device=dev, dtype=torch.int32)
+        amap = torch.cat((ar, torch.roll(ar, -1)))
+        bmap = torch.cat((ar, ar))
+        corr = correlation(fa, fb, amap, bmap).view(2 * b, 1, h, w, h, w)
+        return self.process_correlation(corr)

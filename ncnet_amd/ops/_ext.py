@@ -1,0 +1,61 @@
+"""Loader for the in-tree HIP extension (``ncnet_amd/_C.so``).
+
+Dispatch policy (used by every op in ``ncnet_amd.ops``):
+
+* GPU tensors run the hand-written gfx950 kernels.  If the extension cannot be
+  imported on a machine with a GPU the op raises -- there is no silent eager
+  fallback (set ``NCNET_ALLOW_TORCH_FALLBACK=1`` to opt into the PyTorch
+  oracle path explicitly, e.g. for A/B debugging).
+* CPU tensors run the pure-PyTorch oracles in ``ncnet_amd.ops.reference``.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+_C = None
+_ERR: Exception | None = None
+
+
+def load():
+    global _C, _ERR
+    if _C is not None or _ERR is not None:
+        return _C
+    try:
+        from ncnet_amd import _C as mod  # noqa: N813
+
+        _C = mod
+    except Exception as e:  # pragma: no cover - depends on the build state
+        _ERR = e
+    return _C
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def fallback_allowed() -> bool:
+    return os.environ.get("NCNET_ALLOW_TORCH_FALLBACK", "0") == "1"
+
+
+def use_hip(t: torch.Tensor) -> bool:
+    """True when ``t`` must go through the HIP kernels."""
+    if not t.is_cuda:
+        return False
+    if fallback_allowed() and os.environ.get("NCNET_FORCE_TORCH", "0") == "1":
+        return False
+    if load() is None:
+        if fallback_allowed():
+            return False
+        raise RuntimeError(
+            "ncnet_amd HIP extension (_C.so) is not built/importable on a GPU machine; "
+            f"run `python -m ncnet_amd.build` (import error: {_ERR!r})")
+    return True
+
+
+def ext():
+    m = load()
+    if m is None:
+        raise RuntimeError(f"ncnet_amd HIP extension unavailable: {_ERR!r}")
+    return m

@@ -1,0 +1,153 @@
+"""FeatureL2Norm + 4D FeatureCorrelation on the HIP kernels.
+
+* ``l2norm_pack``: L2-normalise channels (lib/model.py:14-17) and emit the
+  correlation GEMM operand ``[N, H*W, C]`` bf16 in one pass.  A channels-last
+  backbone output is already ``[N, H, W, C]`` in memory, so no transpose copy.
+* ``correlation``: batched MFMA GEMM ``A[amap[v]] . B[bmap[v]]^T`` with fp32
+  output (lib/model.py:106-115).  ``amap``/``bmap`` express the weak loss's
+  rolled negative pairs (train.py:137) without copying features.
+* ``correlation_pool2``: the InLoc relocalization path; GEMM with a fused
+  2x2x2x2 max-pool epilogue (lib/model.py:177-191) -- only the pooled volume
+  and packed argmax offsets are written.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ext
+from . import reference as ref
+
+
+class L2NormPackFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feat):
+        n, c, h, w = feat.shape
+        x = feat.permute(0, 2, 3, 1)
+        if not x.is_contiguous():
+            x = x.contiguous()
+        if x.dtype not in (torch.bfloat16, torch.float32):
+            x = x.float()
+        x2 = x.reshape(n * h * w, c)
+        y = torch.empty((n * h * w, c), dtype=torch.bfloat16, device=feat.device)
+        inv = torch.empty((n * h * w,), dtype=torch.float32, device=feat.device)
+        _ext.ext().l2norm_rows(x2, y, inv)
+        ctx.save_for_backward(x2, inv)
+        ctx.shape = (n, c, h, w)
+        ctx.in_dtype = feat.dtype
+        return y.reshape(n, h * w, c)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, inv = ctx.saved_tensors
+        n, c, h, w = ctx.shape
+        gx = torch.empty(x2.shape, dtype=torch.float32, device=gy.device)
+        _ext.ext().l2norm_rows_bwd(x2.float().contiguous(), gy.reshape(x2.shape).float().contiguous(), inv, gx)
+        return gx.reshape(n, h, w, c).permute(0, 3, 1, 2).to(ctx.in_dtype)
+
+
+def l2norm_pack(feat: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] -> L2-normalised [N, H*W, C] (bf16 on GPU)."""
+    if _ext.use_hip(feat):
+        return L2NormPackFn.apply(feat)
+    n, c, h, w = feat.shape
+    return ref.feature_l2norm(feat.float()).reshape(n, c, h * w).transpose(1, 2)
+
+
+def pack_rows(feat: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] -> [N, H*W, C] (no normalisation)."""
+    n, c, h, w = feat.shape
+    return feat.permute(0, 2, 3, 1).reshape(n, h * w, c)
+
+
+class CorrelationFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fa, fb, amap, bmap):
+        V = amap.numel()
+        out = torch.empty((V, fa.shape[1], fb.shape[1]), dtype=torch.float32, device=fa.device)
+        a = fa.to(torch.bfloat16).contiguous()
+        b = fb.to(torch.bfloat16).contiguous()
+        _ext.ext().corr_gemm(a, b, out, amap, bmap)
+        ctx.save_for_backward(a, b, amap, bmap)
+        ctx.dtypes = (fa.dtype, fb.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, amap, bmap = ctx.saved_tensors
+        am, bm = amap.long(), bmap.long()
+        ga = gb = None
+        g = g.float()
+        if ctx.needs_input_grad[0]:
+            ga = torch.zeros(a.shape, dtype=torch.float32, device=g.device)
+            ga.index_add_(0, am, torch.bmm(g, b.float()[bm]))
+            ga = ga.to(ctx.dtypes[0])
+        if ctx.needs_input_grad[1]:
+            gb = torch.zeros(b.shape, dtype=torch.float32, device=g.device)
+            gb.index_add_(0, bm, torch.bmm(g.transpose(1, 2), a.float()[am]))
+            gb = gb.to(ctx.dtypes[1])
+        return ga, gb, None, None
+
+
+def correlation(fa: torch.Tensor, fb: torch.Tensor, amap: torch.Tensor | None = None,
+                bmap: torch.Tensor | None = None) -> torch.Tensor:
+    """fa [Na, M, C], fb [Nb, N, C] -> [V, M, N] fp32 with V = len(amap)."""
+    if amap is None:
+        amap = torch.arange(fa.shape[0], device=fa.device, dtype=torch.int32)
+    if bmap is None:
+        bmap = torch.arange(fb.shape[0], device=fb.device, dtype=torch.int32)
+    if _ext.use_hip(fa):
+        return CorrelationFn.apply(fa, fb, amap.to(torch.int32), bmap.to(torch.int32))
+    return torch.bmm(fa.float()[amap.long()], fb.float()[bmap.long()].transpose(1, 2))
+
+
+def block_order_index(h: int, w: int, k: int, device) -> torch.Tensor:
+    """Permutation putting each k x k spatial block's rows next to each other
+    (row = (k*k)*blk + (k*dy + dx), blk row-major over the pooled grid)."""
+    ii = torch.arange(h, device=device).view(h, 1)
+    jj = torch.arange(w, device=device).view(1, w)
+    blk = (ii // k) * (w // k) + (jj // k)
+    sub = (ii % k) * k + (jj % k)
+    key = (blk * k * k + sub).reshape(-1)
+    perm = torch.empty_like(key)
+    perm[key] = torch.arange(h * w, device=device)
+    return perm  # new row r takes old row perm[r]
+
+
+def correlation_pool2(fa: torch.Tensor, fb: torch.Tensor, hA: int, wA: int, hB: int, wB: int):
+    """Fused correlation + maxpool4d(k=2). fa [V, hA*wA, C], fb [V, hB*wB, C]
+    (natural row order).  Returns (pooled [V,1,hA/2,wA/2,hB/2,wB/2] fp32,
+    (di, dj, dk, dl) int64 offsets of the same shape)."""
+    V = fa.shape[0]
+    if not _ext.use_hip(fa):
+        corr = torch.bmm(fa.float(), fb.float().transpose(1, 2)).view(V, 1, hA, wA, hB, wB)
+        return ref.maxpool4d(corr, 2)
+    pa = block_order_index(hA, wA, 2, fa.device)
+    pb = block_order_index(hB, wB, 2, fb.device)
+    a = fa.to(torch.bfloat16)[:, pa].contiguous()
+    b = fb.to(torch.bfloat16)[:, pb].contiguous()
+    shape = (V, hA // 2, wA // 2, hB // 2, wB // 2)
+    val = torch.empty(shape, dtype=torch.float32, device=fa.device)
+    code = torch.empty(shape, dtype=torch.uint8, device=fa.device)
+    _ext.ext().corr_gemm_pool2(a, b, val, code, hA, wA, hB, wB)
+    return val.unsqueeze(1), decode_offsets(code.unsqueeze(1))
+
+
+def decode_offsets(code: torch.Tensor):
+    c = code.long()
+    return ((c >> 6) & 3, (c >> 4) & 3, (c >> 2) & 3, c & 3)
+
+
+def maxpool4d(corr4d: torch.Tensor, k_size: int):
+    """Batch-correct 4D max-pool with integer offsets (lib/model.py:177-191)."""
+    if _ext.use_hip(corr4d) and 1 <= k_size <= 4:
+        b, ch, i, j, k, l = corr4d.shape
+        x = corr4d.reshape(b, i, j, k, l)
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        x = x.contiguous()
+        shape = (b, i // k_size, j // k_size, k // k_size, l // k_size)
+        val = torch.empty(shape, dtype=torch.float32, device=x.device)
+        code = torch.empty(shape, dtype=torch.uint8, device=x.device)
+        _ext.ext().maxpool4d(x, val, code, k_size)
+        return val.unsqueeze(1), decode_offsets(code.unsqueeze(1))
+    return ref.maxpool4d(corr4d, k_size)

@@ -1,0 +1,59 @@
+"""MutualMatching (lib/model.py:155-175) with a HIP forward and backward.
+
+Forward: one pass of row statistics (max over B for each A cell), one of
+column statistics (max over A for each B cell), and an elementwise apply
+``c * ((c / (maxA + eps)) * (c / (maxB + eps)))`` in the reference's order.
+
+Backward: ``d/dc`` of ``c^3 / (A B)`` plus the max-routed terms: the row
+(column) sum of ``-g * out / A`` (``/ B``) is added to the row's (column's)
+argmax element, which is exactly where autograd's ``max(dim)`` backward
+routes it.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ext
+from . import reference as ref
+
+EPS = ref.MUTUAL_EPS
+
+
+def _stats(c3: torch.Tensor):
+    C = _ext.ext()
+    V, R, Cc = c3.shape
+    rmax = torch.empty((V, R), dtype=torch.float32, device=c3.device)
+    rarg = torch.empty((V, R), dtype=torch.int32, device=c3.device)
+    cmax = torch.empty((V, Cc), dtype=torch.float32, device=c3.device)
+    carg = torch.empty((V, Cc), dtype=torch.int32, device=c3.device)
+    C.stats_rows(c3, rmax, rarg, None)
+    C.stats_cols(c3, cmax, carg, None)
+    return rmax, rarg, cmax, carg
+
+
+class MutualMatchingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, corr4d):
+        V, ch, I, J, K, L = corr4d.shape
+        assert ch == 1
+        c3 = corr4d.reshape(V, I * J, K * L).float().contiguous()
+        rmax, rarg, cmax, carg = _stats(c3)
+        out = torch.empty_like(c3)
+        _ext.ext().mm_apply(c3, rmax, cmax, out, None, None, EPS)
+        ctx.save_for_backward(c3, rmax, rarg, cmax, carg)
+        ctx.shape = corr4d.shape
+        return out.reshape(corr4d.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        c3, rmax, rarg, cmax, carg = ctx.saved_tensors
+        g3 = g.reshape(c3.shape).float().contiguous()
+        gc = torch.empty_like(c3)
+        _ext.ext().mm_bwd(c3, g3, rmax, rarg, cmax, carg, gc, EPS)
+        return gc.reshape(ctx.shape)
+
+
+def mutual_matching(corr4d: torch.Tensor) -> torch.Tensor:
+    if _ext.use_hip(corr4d):
+        return MutualMatchingFn.apply(corr4d)
+    return ref.mutual_matching(corr4d)

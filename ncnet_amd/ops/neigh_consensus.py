@@ -1,0 +1,271 @@
+"""Symmetric NeighConsensus (stack of Conv4d + ReLU) as one autograd Function.
+
+Reference semantics (lib/model.py:122-153): ``y = conv(x) + swap(conv(swap(x)))``
+where ``conv`` is the Conv4d+ReLU stack and ``swap`` exchanges the A and B
+axes of the correlation volume.  Because of the ReLUs this is not equivalent
+to symmetrised filters, so both branches are computed.
+
+MI355X design:
+* both branches (and, in training, the positive and negative pairs) are one
+  batch of volumes for every Conv4d launch: the swapped branch is built once
+  as a bf16 transposed copy of the 1-channel input (0.8 MB per volume) instead
+  of permuting the 16-channel activations;
+* hidden activations are channels-last bf16 ``[V, I, J, K, L, 16]``; channel
+  counts below 16 are zero-padded (zero weights and bias keep them at 0);
+* bias + ReLU are fused into each conv's epilogue; the backward runs the
+  data-gradient convs with the previous layer's ReLU mask fused into their
+  epilogue, and the weight gradients with the MFMA wgrad kernels;
+* ``y = z1 + z2^T`` (the branch un-swap) and, in backward, its transpose plus
+  the last layer's ReLU mask are single tiled kernels.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ext
+from . import reference as ref
+from .packing import pack_w16, pack_w1in, pack_w1out, transpose_for_dgrad
+
+HIP_KS = (3, 5)
+
+
+def layer_kinds(channels, kernel_sizes):
+    """Kernel family per layer or None if the stack needs the torch path."""
+    kinds = []
+    cin = 1
+    for idx, (c, k) in enumerate(zip(channels, kernel_sizes)):
+        if k not in HIP_KS or c > 16 or cin > 16:
+            return None
+        if cin == 1 and (c == 1 or idx > 0):
+            return None
+        if cin == 1:
+            kinds.append("1in")
+        elif c == 1:
+            kinds.append("1out")
+        else:
+            kinds.append("16")
+        cin = c
+    if not kinds or kinds[-1] != "1out":
+        return None
+    return kinds
+
+
+def wgrad_groups(ks: int, nitems: int) -> int:
+    """Number of K-split groups of the wgrad kernels: about one resident wave of
+    workgroups (2 per CU on 256 CUs) for KS*KS (di,dj) offsets."""
+    target = 512 // (ks * ks)
+    return max(1, min(target, nitems))
+
+
+def _std(w_ref: torch.Tensor) -> torch.Tensor:
+    return ref.conv4d_weight_to_std(w_ref).float()
+
+
+def _pad_bias(b: torch.Tensor, n: int) -> torch.Tensor:
+    b = b.float()
+    if b.numel() == n:
+        return b.contiguous()
+    out = b.new_zeros(n)
+    out[: b.numel()] = b
+    return out
+
+
+def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
+    """x0: [V,I,J,K,L] bf16 -> z fp32 [V,I,J,K,L]; appends layer inputs to save."""
+    C = _ext.ext()
+    h = x0
+    V, I, J, K, L = x0.shape
+    for li, (w_ref, b, kind) in enumerate(zip(ws, bs, kinds)):
+        ks = w_ref.shape[0]
+        w = _std(w_ref)
+        save.append(h)
+        last = li == len(kinds) - 1
+        if kind == "1in":
+            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
+            C.conv1in_fwd(h, pack_w1in(w), _pad_bias(b, 16), None, y, ks, 1)
+        elif kind == "16":
+            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
+            C.conv16_fwd(h, pack_w16(w), _pad_bias(b, 16), None, y, ks, 1)
+        else:
+            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
+            C.conv1out_fwd(h, pack_w1out(w), _pad_bias(b, 1), y, ks, 1)
+            if not last:
+                y = y.to(torch.bfloat16)
+        h = y
+    return h
+
+
+def _reduce_wgrad16(part: torch.Tensor, ks: int, cout: int, cin: int) -> torch.Tensor:
+    # part [G, dd, tap, ci, co] -> std [co, ci, di, dj, dk, dl]
+    s = part.sum(0).permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks, ks)
+    return s[:cout, :cin]
+
+
+def _reduce_wgrad1(part: torch.Tensor, ks: int, mode: int, c16: int) -> torch.Tensor:
+    s = part.sum(0)  # [dd, tap, c16]
+    if mode == 0:    # -> [co, 1, di, dj, dk, dl]
+        return s.permute(2, 0, 1).reshape(16, 1, ks, ks, ks, ks)[:c16]
+    # mode 1: tap index is flipped per (dk, dl): -> [1, ci, di, dj, dk, dl]
+    s = s.reshape(ks, ks, ks, ks, 16).flip(2, 3)
+    return s.permute(4, 0, 1, 2, 3).reshape(1, 16, ks, ks, ks, ks)[:, :c16]
+
+
+def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool):
+    """g_last: grad w.r.t. the last conv's PRE-activation (bf16, 1ch).
+    Returns (dW list in checkpoint layout, db list, g_x0 fp32 or None)."""
+    C = _ext.ext()
+    nl = len(kinds)
+    dws, dbs = [None] * nl, [None] * nl
+    g = g_last
+    gx0 = None
+    for li in range(nl - 1, -1, -1):
+        kind, w_ref, h = kinds[li], ws[li], saved[li]
+        ks = w_ref.shape[0]
+        cout = channels[li]
+        cin = 1 if li == 0 else channels[li - 1]
+        w = _std(w_ref)
+        V, I, J, K, L = h.shape[:5]
+        nitems = V * I * J * ((K + 24) // 25) * ((L + 24) // 25)
+        ng = wgrad_groups(ks, nitems)
+        mask_prev = h if li > 0 else None   # ReLU output of the previous layer
+        if kind == "1out":
+            if g.dim() == 6:
+                raise RuntimeError("internal: 1out layer expects a 1-channel gradient")
+            part = torch.empty((ng, ks * ks, ks * ks, 16), dtype=torch.float32, device=h.device)
+            C.wgrad1(h, g, part, ks, 1, ng)
+            dw = _reduce_wgrad1(part, ks, 1, cin)
+            db = g.float().sum().reshape(1)
+            if li > 0 or need_dx0:
+                gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
+                wt = transpose_for_dgrad(w)  # [16(ci as out), 1, k^4]
+                C.conv1in_fwd(g, pack_w1in(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0)
+                g = gi
+        elif kind == "16":
+            part = torch.empty((ng, ks * ks, ks * ks, 16, 16), dtype=torch.float32, device=h.device)
+            partb = torch.empty((ng, 16), dtype=torch.float32, device=h.device)
+            C.wgrad16(h, g, part, partb, ks, ng)
+            dw = _reduce_wgrad16(part, ks, cout, cin)
+            db = partb.sum(0)[:cout]
+            if li > 0 or need_dx0:
+                gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
+                wt = transpose_for_dgrad(w)
+                C.conv16_fwd(g, pack_w16(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0)
+                g = gi
+        else:  # "1in": h is the 1-channel input
+            part = torch.empty((ng, ks * ks, ks * ks, 16), dtype=torch.float32, device=h.device)
+            C.wgrad1(g, h, part, ks, 0, ng)
+            dw = _reduce_wgrad1(part, ks, 0, cout)
+            db = g.float().sum(dim=(0, 1, 2, 3, 4))[:cout]
+            if li > 0:
+                raise RuntimeError("internal: 1in layer must be first")
+            if need_dx0:
+                gi = torch.empty(h.shape, dtype=torch.float32, device=h.device)
+                wt = transpose_for_dgrad(w)  # [1, 16, k^4]
+                C.conv1out_fwd(g, pack_w1out(wt), None, gi, ks, 0)
+                gx0 = gi
+        dws[li] = ref.conv4d_weight_from_std(dw)
+        dbs[li] = db
+    return dws, dbs, gx0
+
+
+def _swap_flat(x: torch.Tensor, shape_ab):
+    """[V, I*J, K*L] -> [V, K*L, I*J] via the HIP tiled transpose."""
+    C = _ext.ext()
+    V = x.shape[0]
+    i, j, k, l = shape_ab
+    out = torch.empty((V, k * l, i * j), dtype=x.dtype, device=x.device)
+    C.transpose(x.reshape(V, i * j, k * l), out)
+    return out
+
+
+class NeighConsensusFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, symmetric, kinds, channels, *params):
+        ws, bs = params[0::2], params[1::2]
+        V, _, I, J, K, L = x.shape
+        R, Cc = I * J, K * L
+        xb = x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous()
+        saved_layers = []
+        if symmetric:
+            xt = _swap_flat(xb.reshape(V, R, Cc), (I, J, K, L)).reshape(V, K, L, I, J)
+            if (I, J) == (K, L):
+                x0 = torch.cat((xb, xt), 0)
+                z = _stack_fwd(x0, ws, bs, kinds, saved_layers)
+                branches = [saved_layers]
+            else:
+                s1, s2 = [], []
+                z1 = _stack_fwd(xb, ws, bs, kinds, s1)
+                z2 = _stack_fwd(xt, ws, bs, kinds, s2)
+                z = torch.cat((z1.reshape(-1), z2.reshape(-1)))
+                branches = [s1, s2]
+            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x.device)
+            _ext.ext().combine_fwd(z, y, R, Cc)
+        else:
+            z = _stack_fwd(xb, ws, bs, kinds, saved_layers)
+            branches = [saved_layers]
+            y = z
+        ctx.symmetric = symmetric
+        ctx.kinds = kinds
+        ctx.channels = channels
+        ctx.dims = (V, I, J, K, L)
+        ctx.nbranch = len(branches)
+        flat = [t for br in branches for t in br]
+        ctx.nper = len(branches[0])
+        ctx.save_for_backward(z, *params, *flat)
+        return y.reshape(V, 1, I, J, K, L)
+
+    @staticmethod
+    def backward(ctx, gy):
+        z, *rest = ctx.saved_tensors
+        nparam = 2 * len(ctx.kinds)
+        params, flat = rest[:nparam], rest[nparam:]
+        ws = params[0::2]
+        V, I, J, K, L = ctx.dims
+        R, Cc = I * J, K * L
+        need_dx0 = ctx.needs_input_grad[0]
+        gy = gy.reshape(V, R, Cc).float().contiguous()
+        if ctx.symmetric:
+            gz = torch.empty(z.numel(), dtype=torch.bfloat16, device=gy.device)
+            _ext.ext().combine_bwd(gy, z, gz, R, Cc)
+        else:
+            gz = (gy.reshape(-1) * (z.reshape(-1) > 0)).to(torch.bfloat16)
+        branches = [list(flat[b * ctx.nper:(b + 1) * ctx.nper]) for b in range(ctx.nbranch)]
+        if ctx.nbranch == 1:
+            nv = 2 * V if ctx.symmetric else V
+            g_last = gz.reshape(nv, *((I, J, K, L)))
+            dws, dbs, gx0 = _stack_bwd(g_last, branches[0], ws, ctx.kinds, ctx.channels, need_dx0)
+        else:
+            n1 = V * R * Cc
+            g1 = gz[:n1].reshape(V, I, J, K, L)
+            g2 = gz[n1:].reshape(V, K, L, I, J)
+            dws1, dbs1, gxa = _stack_bwd(g1, branches[0], ws, ctx.kinds, ctx.channels, need_dx0)
+            dws2, dbs2, gxb = _stack_bwd(g2, branches[1], ws, ctx.kinds, ctx.channels, need_dx0)
+            dws = [a + b for a, b in zip(dws1, dws2)]
+            dbs = [a + b for a, b in zip(dbs1, dbs2)]
+            gx0 = None if gxa is None else torch.cat((gxa.reshape(-1), gxb.reshape(-1)))
+        gx = None
+        if need_dx0 and gx0 is not None:
+            gx0 = gx0.reshape(-1)
+            if ctx.symmetric:
+                n1 = V * R * Cc
+                ga = gx0[:n1].reshape(V, R, Cc)
+                gb = _swap_flat(gx0[n1:].reshape(V, Cc, R), (K, L, I, J))
+                gx = (ga + gb).reshape(V, 1, I, J, K, L)
+            else:
+                gx = gx0.reshape(V, 1, I, J, K, L)
+        grads = []
+        for dw, db in zip(dws, dbs):
+            grads += [dw, db]
+        return (gx, None, None, None, *grads)
+
+
+def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool = True) -> torch.Tensor:
+    """x: [V,1,I,J,K,L] fp32; weights in checkpoint layout [k, out, in, k, k, k]."""
+    kernel_sizes = [w.shape[0] for w in weights]
+    kinds = layer_kinds(channels, kernel_sizes)
+    if _ext.use_hip(x) and kinds is not None:
+        params = []
+        for w, b in zip(weights, biases):
+            params += [w, b]
+        return NeighConsensusFn.apply(x.float().contiguous(), symmetric, tuple(kinds), tuple(channels), *params)
+    return ref.neigh_consensus(x.float(), [w.float() for w in weights], [b.float() for b in biases], symmetric)

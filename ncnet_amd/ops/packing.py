@@ -1,0 +1,113 @@
+"""Repack Conv4d weights into the MFMA fragment order each HIP kernel reads.
+
+Weights arrive in the standard layout ``[Cout, Cin, k, k, k, k]`` (see
+``reference.conv4d_weight_to_std`` for the checkpoint's pre-permuted layout).
+Packing is a single gather with cached index tensors, done once per forward
+(the tensors are <= 320 KB), in bf16.
+
+* ``pack_w16``   Cin=16, Cout=16 -> [k*k, ceil(k*k/2), 64, 8]
+                 lane l of pair q: W[co=l&15, ci=8((l>>4)&1)+j, di, dj, tap=2q+(l>>5)]
+* ``pack_w1in``  Cin=1,  Cout=16 -> [k*k, ceil(k/4), 64, 8]
+                 lane l of MFMA m: W[co=l&15, 0, di, dj, dk=4m+(l>>4), dl=j]
+* ``pack_w1out`` Cin=16, Cout=1  -> [k*k, ceil((k+3)^2/2), 64, 8]
+                 lane l of pair p: W'[tau=2p+(l>>5), s=l&15] for ci=8((l>>4)&1)+j
+                 with W'[tau, s] = W[0, ci, di, dj, tau - s] (4x4 shift grid)
+
+``transpose_for_dgrad`` gives the weights of the data-gradient convolution
+(swap in/out channels, flip all four kernel axes).
+"""
+from __future__ import annotations
+
+import functools
+
+import torch
+
+
+def transpose_for_dgrad(w_std: torch.Tensor) -> torch.Tensor:
+    return w_std.transpose(0, 1).flip(2, 3, 4, 5)
+
+
+@functools.lru_cache(maxsize=None)
+def _idx16(ks: int):
+    nt = ks * ks
+    nq = (nt + 1) // 2
+    q = torch.arange(nq).view(nq, 1, 1)
+    lane = torch.arange(64).view(1, 64, 1)
+    j = torch.arange(8).view(1, 1, 8)
+    tap = 2 * q + (lane >> 5)
+    co = (lane & 15).expand(nq, 64, 8)
+    ci = (8 * ((lane >> 4) & 1) + j).expand(nq, 64, 8)
+    valid = (tap < nt).expand(nq, 64, 8)
+    tap = torch.clamp(tap, max=nt - 1).expand(nq, 64, 8)
+    return co, ci, tap, valid
+
+
+@functools.lru_cache(maxsize=None)
+def _idx1in(ks: int):
+    nm = (ks + 3) // 4
+    m = torch.arange(nm).view(nm, 1, 1)
+    lane = torch.arange(64).view(1, 64, 1)
+    j = torch.arange(8).view(1, 1, 8)
+    dk = 4 * m + (lane >> 4)
+    dl = j
+    valid = ((dk < ks) & (dl < ks)).expand(nm, 64, 8)
+    tap = (torch.clamp(dk, max=ks - 1) * ks + torch.clamp(dl, max=ks - 1)).expand(nm, 64, 8)
+    co = (lane & 15).expand(nm, 64, 8)
+    return co, tap, valid
+
+
+@functools.lru_cache(maxsize=None)
+def _idx1out(ks: int):
+    ts = ks + 3
+    npair = (ts * ts + 1) // 2
+    p = torch.arange(npair).view(npair, 1, 1)
+    lane = torch.arange(64).view(1, 64, 1)
+    j = torch.arange(8).view(1, 1, 8)
+    tau = 2 * p + (lane >> 5)
+    s = lane & 15
+    sk, sl = s // 4, s % 4
+    tk, tl = tau // ts, tau % ts
+    dk, dl = tk - sk, tl - sl
+    valid = ((tau < ts * ts) & (dk >= 0) & (dk < ks) & (dl >= 0) & (dl < ks)).expand(npair, 64, 8)
+    tap = (torch.clamp(dk, 0, ks - 1) * ks + torch.clamp(dl, 0, ks - 1)).expand(npair, 64, 8)
+    ci = (8 * ((lane >> 4) & 1) + j).expand(npair, 64, 8)
+    return ci, tap, valid
+
+
+def _as_std(w_std: torch.Tensor, cout: int, cin: int) -> torch.Tensor:
+    """Zero-pad [co, ci, k^4] channels up to (cout, cin)."""
+    co, ci = w_std.shape[:2]
+    if co == cout and ci == cin:
+        return w_std
+    out = w_std.new_zeros((cout, cin) + tuple(w_std.shape[2:]))
+    out[:co, :ci] = w_std
+    return out
+
+
+def pack_w16(w_std: torch.Tensor) -> torch.Tensor:
+    ks = w_std.shape[-1]
+    w = _as_std(w_std, 16, 16).reshape(16, 16, ks * ks, ks * ks)
+    co, ci, tap, valid = (t.to(w.device) for t in _idx16(ks))
+    vals = w[co, ci, :, tap]                      # [nq, 64, 8, k*k]
+    vals = vals * valid.unsqueeze(-1).to(vals.dtype)
+    return vals.permute(3, 0, 1, 2).contiguous().to(torch.bfloat16)
+
+
+def pack_w1in(w_std: torch.Tensor) -> torch.Tensor:
+    ks = w_std.shape[-1]
+    assert w_std.shape[1] == 1
+    w = _as_std(w_std, 16, 1).reshape(16, ks * ks, ks * ks)
+    co, tap, valid = (t.to(w.device) for t in _idx1in(ks))
+    vals = w[co, :, tap]                           # [nm, 64, 8, k*k]
+    vals = vals * valid.unsqueeze(-1).to(vals.dtype)
+    return vals.permute(3, 0, 1, 2).contiguous().to(torch.bfloat16)
+
+
+def pack_w1out(w_std: torch.Tensor) -> torch.Tensor:
+    ks = w_std.shape[-1]
+    assert w_std.shape[0] == 1
+    w = _as_std(w_std, 1, 16).reshape(16, ks * ks, ks * ks)
+    ci, tap, valid = (t.to(w.device) for t in _idx1out(ks))
+    vals = w[ci, :, tap]                           # [npair, 64, 8, k*k]
+    vals = vals * valid.unsqueeze(-1).to(vals.dtype)
+    return vals.permute(3, 0, 1, 2).contiguous().to(torch.bfloat16)

@@ -1,0 +1,165 @@
+"""Data parallelism over RCCL (``torch.distributed`` backend "nccl" on ROCm).
+
+One process per GPU (torchrun-style env: RANK / WORLD_SIZE / LOCAL_RANK /
+MASTER_ADDR / MASTER_PORT).  The reference has no distributed code at all
+(SURVEY.md section 2.5); this is the new DP-1 component:
+
+* every rank trains on its own shard of pairs, with its own negative roll;
+* trainable parameters are broadcast from rank 0 at start;
+* after backward, ALL trainable gradients are flattened into one persistent
+  fp32 bucket and averaged with a single all-reduce.  The NC-Net gradient is
+  720 KB (PF config) -- latency-bound on xGMI, so one bucket issued once is
+  the right shape; with ``--fe_finetune_params`` the bucket grows by ~4.5 MB
+  per un-frozen bottleneck, still one collective;
+* scalar metrics are averaged with a tiny all-reduce only when logged.
+
+On CPU (tests) the same code runs over the gloo backend.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def enabled(self) -> bool:
+        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+
+
+def init_distributed(device: str | None = None, timeout_s: int = 600) -> DistContext:
+    """Initialise from the environment; a no-op single-process context when
+    WORLD_SIZE is unset or 1."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = (device != "cpu") and torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    backend = "none"
+    if world > 1:
+        backend = "nccl" if use_gpu else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if not dist.is_initialized():
+            kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+            if use_gpu:
+                kw["device_id"] = dev
+            dist.init_process_group(**kw)
+    return DistContext(rank, world, local, dev, backend)
+
+
+def broadcast_parameters(params, ctx: DistContext, src: int = 0):
+    if not ctx.enabled:
+        return
+    with torch.no_grad():
+        for p in params:
+            dist.broadcast(p.data, src)
+
+
+class GradBucket:
+    """One flat fp32 gradient bucket for a fixed list of parameters."""
+
+    def __init__(self, params, ctx: DistContext):
+        self.params = [p for p in params if p.requires_grad]
+        self.ctx = ctx
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self._work = None
+
+    def start(self):
+        """Pack grads and launch the (async) all-reduce."""
+        if not self.ctx.enabled:
+            return
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            if p.grad is None:
+                self.flat[off:off + n].zero_()
+            else:
+                self.flat[off:off + n].copy_(p.grad.reshape(-1))
+            off += n
+        op = dist.ReduceOp.SUM
+        self._work = dist.all_reduce(self.flat, op=op, async_op=True)
+
+    def finish(self):
+        """Wait and scatter the averaged gradients back."""
+        if not self.ctx.enabled or self._work is None:
+            return
+        self._work.wait()
+        self._work = None
+        self.flat.div_(self.ctx.world_size)
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            g = self.flat[off:off + n].view_as(p)
+            if p.grad is None:
+                p.grad = g.clone().to(p.dtype)
+            else:
+                p.grad.copy_(g)
+            off += n
+
+    def allreduce(self):
+        self.start()
+        self.finish()
+
+
+def all_reduce_mean(value: torch.Tensor, ctx: DistContext) -> torch.Tensor:
+    if not ctx.enabled:
+        return value
+    v = value.detach().clone().float()
+    dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    return v / ctx.world_size
+
+
+def all_reduce_max_float(x: float, ctx: DistContext) -> float:
+    if not ctx.enabled:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(ctx: DistContext):
+    if ctx.enabled:
+        if ctx.backend == "nccl":
+            dist.barrier(device_ids=[ctx.device.index])
+        else:
+            dist.barrier()
+
+
+def shard_indices(n: int, ctx: DistContext, epoch: int = 0, shuffle: bool = True, seed: int = 1,
+                  drop_last: bool = True) -> list[int]:
+    """DistributedSampler-style disjoint per-rank shard of range(n)."""
+    if shuffle:
+        g = torch.Generator().manual_seed(seed + epoch)
+        order = torch.randperm(n, generator=g).tolist()
+    else:
+        order = list(range(n))
+    per = n // ctx.world_size if drop_last else -(-n // ctx.world_size)
+    if not drop_last:
+        order = order + order[: per * ctx.world_size - n]
+    return order[ctx.rank * per:(ctx.rank + 1) * per]
+
+
+def destroy(ctx: DistContext):
+    if ctx.enabled:
+        dist.destroy_process_group()
