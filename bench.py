@@ -58,8 +58,7 @@ def main(argv=None):
 
     from ncnet_amd.engine.trainer import weak_loss
     from ncnet_amd.models import ImMatchNet
-    from ncnet_amd.parallel.dist import (GradBucket, all_reduce_max_float, barrier, broadcast_parameters,
-                                         init_distributed)
+    from ncnet_amd.parallel.dist import GradBucket, all_reduce_max_float, barrier, broadcast_module, init_distributed
 
     ctx = init_distributed()
     if ctx.world_size != args.gpus and ctx.is_main:
@@ -70,7 +69,7 @@ def main(argv=None):
     model = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1], dtype="bf16").to(dev)
     model.train()
     params = [p for p in model.parameters() if p.requires_grad]
-    broadcast_parameters(params, ctx)
+    broadcast_module(model, ctx)
     opt = torch.optim.Adam(params, lr=5e-4)
     bucket = GradBucket(params, ctx)
 

@@ -4,8 +4,8 @@
 // the kernel's grid assumes BEFORE launching: a malformed call raises a Python
 // exception instead of faulting the GPU.
 #include <torch/extension.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
 extern "C" {
@@ -37,7 +37,10 @@ namespace {
 
 using torch::Tensor;
 
-hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+// PyTorch-ROCm exposes HIP devices as device type "cuda": use the masquerading guard/stream.
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
+}
 
 void check(const Tensor& t, const char* name, c10::ScalarType dt) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -57,7 +60,7 @@ int conv_pairs1o(int ks) { return ((ks + 3) * (ks + 3) + 1) / 2; }
 
 // X [V,I,J,K,L,16] bf16 -> Y [V,I,J,K,L,16] bf16
 void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi) {
-  const c10::hip::HIPGuard guard(X.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(Y, "Y", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
   TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
   check_shape(Y, "Y", X.sizes().vec());
@@ -70,7 +73,7 @@ void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<T
 
 // X [V,I,J,K,L] bf16 -> Y [V,I,J,K,L,16] bf16
 void conv1in_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi) {
-  const c10::hip::HIPGuard guard(X.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(Y, "Y", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
   TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
   auto ys = X.sizes().vec(); ys.push_back(16);
@@ -84,7 +87,7 @@ void conv1in_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<
 
 // X [V,I,J,K,L,16] bf16 -> Y [V,I,J,K,L] fp32
 void conv1out_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t epi) {
-  const c10::hip::HIPGuard guard(X.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(Y, "Y", at::kFloat); check(Wp, "Wp", at::kBFloat16);
   TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
   check_shape(Y, "Y", {X.size(0), X.size(1), X.size(2), X.size(3), X.size(4)});
@@ -96,7 +99,7 @@ void conv1out_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int
 }
 
 void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t ngroups) {
-  const c10::hip::HIPGuard guard(X.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(G, "G", at::kBFloat16); check(part, "part", at::kFloat); check(partb, "partb", at::kFloat);
   TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
   check_shape(G, "G", X.sizes().vec());
@@ -107,7 +110,7 @@ void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t 
 }
 
 void wgrad1(Tensor S16, Tensor P1, Tensor part, int64_t ks, int64_t mode, int64_t ngroups) {
-  const c10::hip::HIPGuard guard(S16.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S16.device());
   check(S16, "S16", at::kBFloat16); check(P1, "P1", at::kBFloat16); check(part, "part", at::kFloat);
   TORCH_CHECK(S16.dim() == 6 && S16.size(5) == 16, "S16 must be [V,I,J,K,L,16]");
   check_shape(P1, "P1", {S16.size(0), S16.size(1), S16.size(2), S16.size(3), S16.size(4)});
@@ -118,7 +121,7 @@ void wgrad1(Tensor S16, Tensor P1, Tensor part, int64_t ks, int64_t mode, int64_
 }
 
 void l2norm_rows(Tensor x, Tensor y, c10::optional<Tensor> inv) {
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.is_cuda() && x.is_contiguous());
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat);
   check(y, "y", at::kBFloat16);
@@ -129,7 +132,7 @@ void l2norm_rows(Tensor x, Tensor y, c10::optional<Tensor> inv) {
 }
 
 void l2norm_rows_bwd(Tensor x, Tensor g, Tensor inv, Tensor gx) {
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check(x, "x", at::kFloat); check(g, "g", at::kFloat); check(inv, "inv", at::kFloat); check(gx, "gx", at::kFloat);
   TORCH_CHECK(x.dim() == 2 && g.sizes() == x.sizes() && gx.sizes() == x.sizes());
   check_shape(inv, "inv", {x.size(0)});
@@ -139,7 +142,7 @@ void l2norm_rows_bwd(Tensor x, Tensor g, Tensor inv, Tensor gx) {
 
 // A [Ba, M, K], B [Bb, N, K] bf16; C [batch, M, N] fp32/bf16
 void corr_gemm(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> amap, c10::optional<Tensor> bmap) {
-  const c10::hip::HIPGuard guard(A.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
   check(A, "A", at::kBFloat16); check(B, "B", at::kBFloat16);
   TORCH_CHECK(C.is_cuda() && C.is_contiguous() && (C.scalar_type() == at::kFloat || C.scalar_type() == at::kBFloat16));
   TORCH_CHECK(A.dim() == 3 && B.dim() == 3 && C.dim() == 3);
@@ -161,7 +164,7 @@ void corr_gemm(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> amap, c10::op
 }
 
 void corr_gemm_pool2(Tensor A, Tensor B, Tensor val, Tensor idx, int64_t hA, int64_t wA, int64_t hB, int64_t wB) {
-  const c10::hip::HIPGuard guard(A.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
   check(A, "A", at::kBFloat16); check(B, "B", at::kBFloat16); check(val, "val", at::kFloat); check(idx, "idx", at::kByte);
   TORCH_CHECK(A.dim() == 3 && B.dim() == 3 && A.size(0) == B.size(0));
   TORCH_CHECK(A.size(1) == hA * wA && B.size(1) == hB * wB && A.size(2) == B.size(2));
@@ -176,7 +179,7 @@ void corr_gemm_pool2(Tensor A, Tensor B, Tensor val, Tensor idx, int64_t hA, int
 
 // x [V,R,C] fp32 -> per-row (dim 2) stats [V,R]
 void stats_rows(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Tensor> se) {
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check(x, "x", at::kFloat); check(mx, "mx", at::kFloat);
   TORCH_CHECK(x.dim() == 3);
   check_shape(mx, "mx", {x.size(0), x.size(1)});
@@ -189,7 +192,7 @@ void stats_rows(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Te
 
 // x [V,R,C] fp32 -> per-column (dim 1) stats [V,C]
 void stats_cols(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Tensor> se) {
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check(x, "x", at::kFloat); check(mx, "mx", at::kFloat);
   TORCH_CHECK(x.dim() == 3);
   check_shape(mx, "mx", {x.size(0), x.size(2)});
@@ -202,7 +205,7 @@ void stats_cols(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Te
 
 void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10::optional<Tensor> out_x,
               c10::optional<Tensor> out_xt, double eps) {
-  const c10::hip::HIPGuard guard(c.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
   check(c, "c", at::kFloat); check(rmax, "rmax", at::kFloat); check(cmax, "cmax", at::kFloat);
   TORCH_CHECK(c.dim() == 3);
   const int64_t V = c.size(0), R = c.size(1), C = c.size(2);
@@ -216,7 +219,7 @@ void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10
 }
 
 void mm_bwd(Tensor c, Tensor g, Tensor rmax, Tensor rarg, Tensor cmax, Tensor carg, Tensor gc, double eps) {
-  const c10::hip::HIPGuard guard(c.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
   check(c, "c", at::kFloat); check(g, "g", at::kFloat); check(gc, "gc", at::kFloat);
   check(rmax, "rmax", at::kFloat); check(cmax, "cmax", at::kFloat); check(rarg, "rarg", at::kInt); check(carg, "carg", at::kInt);
   TORCH_CHECK(c.dim() == 3 && g.sizes() == c.sizes() && gc.sizes() == c.sizes());
@@ -232,7 +235,7 @@ void mm_bwd(Tensor c, Tensor g, Tensor rmax, Tensor rarg, Tensor cmax, Tensor ca
 
 // z [2*Vh, R, C] (second half stored as [C, R]) -> y [Vh, R, C]
 void combine_fwd(Tensor z, Tensor y, int64_t R, int64_t C) {
-  const c10::hip::HIPGuard guard(z.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(z.device());
   check(z, "z", at::kFloat); check(y, "y", at::kFloat);
   TORCH_CHECK(z.numel() % (2 * R * C) == 0);
   const int64_t Vh = z.numel() / (2 * R * C);
@@ -241,7 +244,7 @@ void combine_fwd(Tensor z, Tensor y, int64_t R, int64_t C) {
 }
 
 void combine_bwd(Tensor g, Tensor z, Tensor gz, int64_t R, int64_t C) {
-  const c10::hip::HIPGuard guard(z.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(z.device());
   check(g, "g", at::kFloat); check(z, "z", at::kFloat); check(gz, "gz", at::kBFloat16);
   TORCH_CHECK(z.numel() % (2 * R * C) == 0);
   const int64_t Vh = z.numel() / (2 * R * C);
@@ -251,7 +254,7 @@ void combine_bwd(Tensor g, Tensor z, Tensor gz, int64_t R, int64_t C) {
 
 void softmax_max_bwd(Tensor x, Tensor rmax, Tensor rarg, Tensor rse, Tensor cmax, Tensor carg, Tensor cse, Tensor wr,
                      Tensor wc, Tensor gx) {
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check(x, "x", at::kFloat); check(gx, "gx", at::kFloat);
   TORCH_CHECK(x.dim() == 3 && gx.sizes() == x.sizes());
   const int64_t V = x.size(0), R = x.size(1), C = x.size(2);
@@ -267,7 +270,7 @@ void softmax_max_bwd(Tensor x, Tensor rmax, Tensor rarg, Tensor rse, Tensor cmax
 }
 
 void maxpool4d(Tensor x, Tensor y, Tensor code, int64_t ks) {
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16));
   TORCH_CHECK(x.dim() == 5, "x must be [V,I,J,K,L]");
   TORCH_CHECK(ks >= 1 && ks <= 4);
@@ -280,7 +283,7 @@ void maxpool4d(Tensor x, Tensor y, Tensor code, int64_t ks) {
 }
 
 void transpose(Tensor x, Tensor y) {
-  const c10::hip::HIPGuard guard(x.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && y.is_contiguous() && x.scalar_type() == y.scalar_type());
   TORCH_CHECK(x.dim() == 3 && y.dim() == 3 && y.size(0) == x.size(0) && y.size(1) == x.size(2) && y.size(2) == x.size(1));
   ok(ncnet_transpose(x.data_ptr(), y.data_ptr(), x.element_size(), x.size(0), x.size(1), x.size(2), cur_stream(x)),

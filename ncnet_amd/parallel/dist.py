@@ -67,11 +67,19 @@ def init_distributed(device: str | None = None, timeout_s: int = 600) -> DistCon
 
 
 def broadcast_parameters(params, ctx: DistContext, src: int = 0):
+    """Broadcast tensors (parameters, or a module's whole state) from ``src``.
+
+    Pass ``model.state_dict().values()`` (or use ``broadcast_module``) so the
+    frozen backbone and BN statistics are identical on every rank too."""
     if not ctx.enabled:
         return
     with torch.no_grad():
         for p in params:
-            dist.broadcast(p.data, src)
+            dist.broadcast(p.data if hasattr(p, "data") else p, src)
+
+
+def broadcast_module(module: torch.nn.Module, ctx: DistContext, src: int = 0):
+    broadcast_parameters(list(module.state_dict().values()), ctx, src)
 
 
 class GradBucket:

@@ -1,0 +1,73 @@
+"""Data-parallel correctness over gloo on CPU (world_size 2).
+
+DP semantics: each rank computes the weak loss on
+its own shard with its own negative roll; the averaged gradient must equal the
+mean of the per-shard gradients computed in a single process."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch(seed):
+    g = torch.Generator().manual_seed(seed)
+    return {"source_image": torch.randn(2, 3, 64, 64, generator=g), "target_image": torch.randn(2, 3, 64, 64, generator=g)}
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from ncnet_amd.engine.trainer import weak_loss
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.parallel.dist import GradBucket, broadcast_module, destroy, init_distributed, shard_indices
+    ctx = init_distributed(device="cpu")
+    assert ctx.backend == "gloo" and ctx.world_size == world
+    torch.manual_seed(100 + rank)  # different init on purpose: broadcast must fix it
+    m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], use_cuda=False)
+    params = [p for p in m.parameters() if p.requires_grad]
+    broadcast_module(m, ctx)
+    loss = weak_loss(m, _batch(rank))
+    loss.backward()
+    GradBucket(params, ctx).allreduce()
+    torch.save({"state": m.state_dict(), "params": [p.detach() for p in params], "grads": [p.grad for p in params],
+                "shard": shard_indices(10, ctx, epoch=0)}, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy(ctx)
+
+
+def test_dp_gradients_equal_mean_of_shards(tmp_path):
+    world = 2
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(str(tmp_path / f"r{r}.pt"), weights_only=True) for r in range(world)]
+    for a, b in zip(res[0]["params"], res[1]["params"]):
+        assert torch.equal(a, b)  # broadcast from rank 0
+    for a, b in zip(res[0]["grads"], res[1]["grads"]):
+        assert torch.allclose(a, b)
+    # single-process reference with rank 0's parameters
+    from ncnet_amd.engine.trainer import weak_loss
+    from ncnet_amd.models import ImMatchNet
+    m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], use_cuda=False)
+    m.load_state_dict(res[0]["state"])
+    params = [p for p in m.parameters() if p.requires_grad]
+    acc = [torch.zeros_like(p) for p in params]
+    for r in range(world):
+        m.zero_grad()
+        weak_loss(m, _batch(r)).backward()
+        for a, p in zip(acc, params):
+            a += p.grad / world
+    for a, g in zip(acc, res[0]["grads"]):
+        assert torch.allclose(a, g, rtol=1e-4, atol=1e-8)
+    # disjoint shards covering the data
+    s0, s1 = res[0]["shard"], res[1]["shard"]
+    assert not set(s0) & set(s1) and len(s0) == len(s1) == 5

@@ -1,0 +1,102 @@
+"""Stage-by-stage check of the fused NeighConsensus backward against a
+*quantized* fp64 oracle that rounds to bf16 at exactly the points where the
+HIP path stores bf16 (layer activations, layer gradients, packed weights).
+Any difference left is fp32-vs-fp64 accumulation order, so tolerances are
+tight and a mismatch localises a bug to one stage."""
+import pytest
+import torch
+
+from ncnet_amd.ops import _ext
+from ncnet_amd.ops import reference as ref
+from ncnet_amd.ops.neigh_consensus import _stack_bwd, _stack_fwd, layer_kinds
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def q(x):
+    return x.to(torch.bfloat16).double()
+
+
+def rl2(a, b):
+    a, b = a.detach().double(), b.detach().double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def conv_fwd(x, w_std):  # x [V,C,I,J,K,L] fp64
+    return ref.conv4d(x, ref.conv4d_weight_from_std(w_std))
+
+
+def grads(x, w_std, g):
+    x = x.detach().requires_grad_(True)
+    w = w_std.detach().requires_grad_(True)
+    (conv_fwd(x, w) * g).sum().backward()
+    return x.grad, w.grad
+
+
+@pytest.mark.parametrize("ks,ch", [((5, 5, 5), (16, 16, 1)), ((3, 3), (16, 1))])
+def test_stack_stages_vs_quantized_oracle(ks, ch):
+    torch.manual_seed(11)
+    V, I, J, K, L = 3, 9, 8, 10, 11
+    x0 = torch.rand(V, I, J, K, L, device=DEV).to(torch.bfloat16)
+    ws_ref, bs, ws_std = [], [], []
+    cin = 1
+    for k, c in zip(ks, ch):
+        w_std = q(torch.randn(c, cin, k, k, k, k, device=DEV) * 0.1)
+        ws_std.append(w_std)
+        ws_ref.append(ref.conv4d_weight_from_std(w_std).float())
+        bs.append(torch.rand(c, device=DEV) * 0.1)
+        cin = c
+    kinds = layer_kinds(list(ch), list(ks))
+    saved = []
+    z = _stack_fwd(x0.contiguous(), ws_ref, bs, kinds, saved)
+    # quantized oracle forward
+    hs = [x0.double().unsqueeze(1)]
+    for li, (w, b) in enumerate(zip(ws_std, bs)):
+        pre = conv_fwd(hs[-1], w) + b.double().view(1, -1, 1, 1, 1, 1)
+        act = torch.relu(pre)
+        hs.append(act if li == len(ks) - 1 else q(act))
+    errs = {"z": rl2(z, hs[-1][:, 0])}
+    for li in range(1, len(ks)):
+        errs[f"h{li}"] = rl2(saved[li].permute(0, 5, 1, 2, 3, 4)[:, :ch[li - 1]], hs[li])
+    # backward from a random gradient on z
+    gz = torch.randn_like(z)
+    g_last = (gz * (z > 0)).to(torch.bfloat16)
+    dws, dbs, gx0 = _stack_bwd(g_last, saved, ws_ref, kinds, list(ch), True)
+    g = q(gz.double() * (hs[-1][:, 0] > 0)).unsqueeze(1)
+    for li in range(len(ks) - 1, -1, -1):
+        gx, gw = grads(hs[li], ws_std[li], g)
+        errs[f"dw{li}"] = rl2(ref.conv4d_weight_to_std(dws[li]), gw)
+        errs[f"db{li}"] = rl2(dbs[li], g.sum(dim=(0, 2, 3, 4, 5)))
+        if li > 0:
+            g = q(gx * (hs[li] > 0))
+        else:
+            errs["gx0"] = rl2(gx0, gx[:, 0])
+    assert max(errs.values()) < 5e-3, errs
+
+
+def test_symmetric_vs_nonsymmetric_consistency():
+    """symmetric NC == stack(x) + swap(stack(swap(x))) computed with two
+    non-symmetric calls of the same HIP op (forward and all gradients)."""
+    from ncnet_amd.ops.neigh_consensus import neigh_consensus
+    torch.manual_seed(12)
+    x = torch.rand(2, 1, 6, 7, 6, 7, device=DEV).to(torch.bfloat16).float()
+    ws = [(torch.randn(3, 16, 1, 3, 3, 3, device=DEV) * 0.1).requires_grad_(True),
+          (torch.randn(3, 1, 16, 3, 3, 3, device=DEV) * 0.1).requires_grad_(True)]
+    bs = [(torch.rand(16, device=DEV) * 0.1).requires_grad_(True), (torch.rand(1, device=DEV) * 0.1).requires_grad_(True)]
+    xa = x.clone().requires_grad_(True)
+    y = neigh_consensus(xa, ws, bs, [16, 1], symmetric=True)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    gs = [w.grad.clone() for w in ws] + [b.grad.clone() for b in bs] + [xa.grad.clone()]
+    for t in ws + bs:
+        t.grad = None
+    xb = x.clone().requires_grad_(True)
+    y1 = neigh_consensus(xb, ws, bs, [16, 1], symmetric=False)
+    y2 = ref.swap_ab(neigh_consensus(ref.swap_ab(xb).contiguous(), ws, bs, [16, 1], symmetric=False))
+    ys = y1 + y2
+    (ys * g).sum().backward()
+    gn = [w.grad.clone() for w in ws] + [b.grad.clone() for b in bs] + [xb.grad.clone()]
+    errs = {"y": rl2(y, ys)}
+    errs.update({f"g{i}": rl2(a, b) for i, (a, b) in enumerate(zip(gs, gn))})
+    assert max(errs.values()) < 1e-5, errs
