@@ -9,10 +9,12 @@
 #include <hip/hip_runtime.h>
 
 extern "C" {
-int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv1in_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv1out_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_jpack(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_jsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad1(const void*, const void*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
@@ -58,17 +60,27 @@ int conv_pairs16(int ks) { return (ks * ks + 1) / 2; }
 int conv_m1(int ks) { return (ks + 3) / 4; }
 int conv_pairs1o(int ks) { return ((ks + 3) * (ks + 3) + 1) / 2; }
 
-// X [V,I,J,K,L,16] bf16 -> Y [V,I,J,K,L,16] bf16
-void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi) {
+// X [V,I,J,K,L,16] bf16 -> Y [V,I,J,K,L,16] bf16, or (epi 3) fp32 [V,I,J,K,L,8] raw channels 0..7.
+// dj_center: only the dj = P input planes (j-offset encoded in channels).
+void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi,
+                int64_t dj_center) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
-  check(X, "X", at::kBFloat16); check(Y, "Y", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
+  check(X, "X", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
   TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
-  check_shape(Y, "Y", X.sizes().vec());
+  TORCH_CHECK(epi >= 0 && epi <= 3);
+  if (epi == 3) {
+    check(Y, "Y", at::kFloat);
+    check_shape(Y, "Y", {X.size(0), X.size(1), X.size(2), X.size(3), X.size(4), 8});
+  } else {
+    check(Y, "Y", at::kBFloat16);
+    check_shape(Y, "Y", X.sizes().vec());
+  }
   check_shape(Wp, "Wp", {ks * ks, conv_pairs16(ks), 64, 8});
   if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
   if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", X.sizes().vec()); }
   ok(ncnet_conv16_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), X.size(0),
-                      X.size(1), X.size(2), X.size(3), X.size(4), ks, epi, cur_stream(X)), "conv16_fwd");
+                      X.size(1), X.size(2), X.size(3), X.size(4), ks, epi, dj_center ? 1 : 0, cur_stream(X)),
+     "conv16_fwd");
 }
 
 // X [V,I,J,K,L] bf16 -> Y [V,I,J,K,L,16] bf16
@@ -98,15 +110,39 @@ void conv1out_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int
                         X.size(2), X.size(3), X.size(4), ks, epi, cur_stream(X)), "conv1out_fwd");
 }
 
-void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t ngroups) {
+void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t ngroups, int64_t dj_center) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(G, "G", at::kBFloat16); check(part, "part", at::kFloat); check(partb, "partb", at::kFloat);
   TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
   check_shape(G, "G", X.sizes().vec());
-  check_shape(part, "part", {ngroups, ks * ks, ks * ks, 16, 16});
+  check_shape(part, "part", {ngroups, dj_center ? ks : ks * ks, ks * ks, 16, 16});
   check_shape(partb, "partb", {ngroups, 16});
   ok(ncnet_wgrad16(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(0), X.size(1),
-                   X.size(2), X.size(3), X.size(4), ks, ngroups, cur_stream(X)), "wgrad16");
+                   X.size(2), X.size(3), X.size(4), ks, ngroups, dj_center ? 1 : 0, cur_stream(X)), "wgrad16");
+}
+
+// X [V,I,J,K,L] (bf16/fp32) -> S [V,I,J,K,L,16] bf16, S[..,c] = X[v,i,j+sgn*(c-P),k,l] (c < ks)
+void jpack(Tensor X, Tensor S, int64_t ks, int64_t sgn) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  TORCH_CHECK(X.is_cuda() && X.is_contiguous() && (X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kFloat));
+  TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
+  check(S, "S", at::kBFloat16);
+  check_shape(S, "S", {X.size(0), X.size(1), X.size(2), X.size(3), X.size(4), 16});
+  TORCH_CHECK(ks >= 1 && ks <= 8 && (sgn == 1 || sgn == -1));
+  ok(ncnet_jpack(X.data_ptr(), X.scalar_type() == at::kBFloat16, S.data_ptr(), X.size(0), X.size(1), X.size(2),
+                 X.size(3), X.size(4), ks, sgn, cur_stream(X)), "jpack");
+}
+
+// Z8 [V,I,J,K,L,8] fp32 -> y [V,I,J,K,L] fp32, y = act(b + sum_{c<ks} Z8[v,i,j+c-P,k,l,c])
+void jsum(Tensor Z8, c10::optional<Tensor> bias, Tensor y, int64_t ks, int64_t relu, int64_t sgn) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(Z8.device());
+  check(Z8, "Z8", at::kFloat); check(y, "y", at::kFloat);
+  TORCH_CHECK(Z8.dim() == 6 && Z8.size(5) == 8);
+  check_shape(y, "y", {Z8.size(0), Z8.size(1), Z8.size(2), Z8.size(3), Z8.size(4)});
+  if (bias.has_value()) { check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
+  TORCH_CHECK(ks >= 1 && ks <= 8 && (sgn == 1 || sgn == -1));
+  ok(ncnet_jsum((float*)Z8.data_ptr(), opt_ptr<float>(bias), (float*)y.data_ptr(), Z8.size(0), Z8.size(1), Z8.size(2),
+                Z8.size(3), Z8.size(4), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z8)), "jsum");
 }
 
 void wgrad1(Tensor S16, Tensor P1, Tensor part, int64_t ks, int64_t mode, int64_t ngroups) {
@@ -299,6 +335,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1out_fwd", &conv1out_fwd);
   m.def("wgrad16", &wgrad16);
   m.def("wgrad1", &wgrad1);
+  m.def("jpack", &jpack);
+  m.def("jsum", &jsum);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("l2norm_rows_bwd", &l2norm_rows_bwd);
   m.def("corr_gemm", &corr_gemm);

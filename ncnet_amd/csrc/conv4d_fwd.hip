@@ -19,16 +19,20 @@
 //                                    shifts of an anchor grid (weights shifted
 //                                    on the host), so N=1 still uses the MFMA.
 #include "common.h"
+#include <stdlib.h>
 
 namespace ncnet {
 
-enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2 };
+// EPI_F32: raw fp32 accumulators of channels 0..7 into Y as float[..., 8]
+// (the j-shift-encoded 16 -> 1 layers, summed afterwards by jsum).
+enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32 = 3 };
 
 struct ConvGeom {
   int V, I, J, K, L;  // volume dims
   int TK, TL;         // output tile along k, l
   int nkt, nlt;       // tiles along k, l
   int PR, RS;         // staged plane rows / row stride (voxels)
+  int dj_center;      // 1: only the dj = P planes (j-offset encoded in channels)
 };
 
 // Decode the workgroup's output tile.
@@ -103,6 +107,10 @@ __device__ __forceinline__ size_t plane_offset(const ConvGeom& g, int v, int i, 
 template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
                                         const float* __restrict__ bias, size_t vox_index, int co0) {
+  if (EPI == EPI_F32) {
+    if (co0 < 8) *(f32x4*)((float*)Y + vox_index * 8 + co0) = acc;
+    return;
+  }
   float o[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(256, 2) void conv16_fwd_kernel(const bf16* __restri
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const TileId t = decode_tile(g);
   const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
-  const int dj_lo = max(0, P - t.j), dj_hi = min(KS, g.J + P - t.j);
+  const int dj_lo = g.dj_center ? P : max(0, P - t.j), dj_hi = g.dj_center ? P + 1 : min(KS, g.J + P - t.j);
   const int ndj = dj_hi - dj_lo;
   const int nplanes = (di_hi - di_lo) * ndj;
   const int nchunk = g.PR * g.RS * 2;
@@ -226,6 +234,118 @@ __global__ __launch_bounds__(256, 2) void conv16_fwd_kernel(const bf16* __restri
 #pragma unroll
   for (int tt = 0; tt < MAXT; ++tt) {
     int tile = wave + 4 * tt;
+    if (tile < ntile) {
+      int vi = tile * 16 + (lane & 15);
+      int kk = vi / g.TL, ll = vi - kk * g.TL;
+      int kg = t.k0 + kk, lg = t.l0 + ll;
+      if (vi < nvox && kg < g.K && lg < g.L)
+        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4));
+    }
+  }
+}
+
+// ===========================================================================
+// conv16v2_fwd: same math as conv16_fwd, restructured for occupancy and
+// copy/compute overlap:
+//  * 8 waves per workgroup, 5 voxel tiles per wave (20 accumulator VGPRs);
+//  * planes and weights arrive by LDS-DMA (global_load_lds_dwordx4): one
+//    wave-instruction per plane row (<= 32 voxels = 1 KiB), no staging VGPRs;
+//  * two LDS buffers: plane s+1 streams in while plane s is computed, one
+//    barrier per plane.  Halo/out-of-volume voxels are zeroed once (they are
+//    at fixed positions for the workgroup's tile) and never written again.
+// Requires RS = TL + KS - 1 <= 32.
+// ===========================================================================
+template <int KS, int EPI>
+__global__ __launch_bounds__(512, 1) void conv16v2_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
+                                                              const float* __restrict__ bias,
+                                                              const bf16* __restrict__ M, bf16* __restrict__ Y,
+                                                              ConvGeom g) {
+  constexpr int P = KS / 2;
+  constexpr int NT = KS * KS;
+  constexpr int NQ = (NT + 1) / 2;
+  constexpr int NW = 8;
+  constexpr int MAXT = 5;  // 16-voxel tiles per wave (TK*TL <= 640)
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int plane_bytes = g.PR * g.RS * 32;
+  const int buf_bytes = plane_bytes + NQ * 1024;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const TileId t = decode_tile(g);
+  const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
+  const int dj_lo = g.dj_center ? P : max(0, P - t.j), dj_hi = g.dj_center ? P + 1 : min(KS, g.J + P - t.j);
+  const int ndj = dj_hi - dj_lo;
+  const int nplanes = (di_hi - di_lo) * ndj;
+  const int nvox = g.TK * g.TL;
+  const int ntile = (nvox + 15) >> 4;
+
+  for (int o = threadIdx.x * 16; o < 2 * buf_bytes; o += NW * 64 * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
+
+  uint32_t vbase[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int vi = (wave + NW * tt) * 16 + (lane & 15);
+    if (vi >= nvox) vi = 0;
+    int kk = vi / g.TL, ll = vi - kk * g.TL;
+    vbase[tt] = (uint32_t)((kk * g.RS + ll) * 32 + ((lane >> 4) & 1) * 16);
+  }
+  uint32_t toff[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    int tap = 2 * q + (lane >> 5);
+    if (tap >= NT) tap = NT - 1;
+    int dk = tap / KS, dl = tap - dk * KS;
+    toff[q] = (uint32_t)((dk * g.RS + dl) * 32);
+  }
+  f32x4 acc[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // in-volume column span of the staged rows (same for every plane)
+  const int lstart = max(0, t.l0 - P), lend = min(g.L, t.l0 - P + g.RS);
+  const int nchunk = 2 * (lend - lstart);
+  const int col0 = lstart - (t.l0 - P);
+
+  auto issue = [&](int s, char* buf) {
+    const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
+    const bf16* xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
+    for (int r = wave; r < g.PR; r += NW) {
+      const int kg = t.k0 - P + r;
+      if (kg >= 0 && kg < g.K && lane < nchunk) {
+        const bf16* src = xp + ((size_t)kg * g.L + lstart) * 16 + lane * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(void, buf + (r * g.RS + col0) * 32), 16, 0, 0);
+      }
+    }
+    const u32x4* wp = Wp + (size_t)(di * KS + dj) * (NQ * 64);
+    for (int q = wave; q < NQ; q += NW)
+      __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, buf + plane_bytes + q * 1024), 16, 0, 0);
+  };
+
+  __syncthreads();  // zero-fill complete before any DMA lands
+  if (nplanes > 0) issue(0, smem);
+  for (int s = 0; s < nplanes; ++s) {
+    __syncthreads();  // drains this wave's DMA (vmcnt 0) and orders every wave's plane s
+    char* cur = smem + (s & 1) * buf_bytes;
+    if (s + 1 < nplanes) issue(s + 1, smem + ((s + 1) & 1) * buf_bytes);
+    bf16x8 wf[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) wf[q] = lds_read16(cur + plane_bytes, (q * 64 + lane) * 16);
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      if (wave + NW * tt < ntile) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          bf16x8 xf = lds_read16(cur, vbase[tt] + toff[q]);
+          acc[tt] = mfma16(wf[q], xf, acc[tt]);
+        }
+      }
+    }
+  }
+
+  const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int tile = wave + NW * tt;
     if (tile < ntile) {
       int vi = tile * 16 + (lane & 15);
       int kk = vi / g.TL, ll = vi - kk * g.TL;
@@ -525,6 +645,7 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.nkt = cdiv(K, tk); g.nlt = cdiv(L, tl);
   g.PR = tk + KS - 1 + extra_rows;
   g.RS = tl + KS - 1 + extra_cols;
+  g.dj_center = 0;
   return g;
 }
 
@@ -541,21 +662,47 @@ static void pick_tile(int K, int L, int& tk, int& tl) {
   while (tk * tl > 640) { if (tl > tk) --tl; else --tk; }
 }
 
+static int conv16_variant() {
+  static int v = [] {
+    const char* e = getenv("NCNET_CONV16_VARIANT");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias, const void* M, void* Y,
-                                int V, int I, int J, int K, int L, int KS, int epi, hipStream_t stream) {
+                                int V, int I, int J, int K, int L, int KS, int epi, int dj_center,
+                                hipStream_t stream) {
   int tk, tl;
   pick_tile(K, L, tk, tl);
   ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, 0, 0);
+  g.dj_center = dj_center;
   if (g.PR * g.RS * 2 > 8 * 256) return -1;
   int nq = (KS * KS + 1) / 2;
+  const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
+  if (conv16_variant() == 2 && g.RS <= 32) {
+    size_t buf = (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
+    dim3 grid2((unsigned)(V * I * J * g.nkt * g.nlt)), block2(512);
+#define L16V2(KSV, EPIV) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV>), grid2, block2, 2 * buf, stream, x, w, bias, m, y, g)
+    if (KS == 5) {
+      if (epi == EPI_BIAS_RELU) L16V2(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2(5, EPI_MASK);
+      else if (epi == EPI_F32) L16V2(5, EPI_F32); else L16V2(5, EPI_NONE);
+    } else if (KS == 3) {
+      if (epi == EPI_BIAS_RELU) L16V2(3, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2(3, EPI_MASK);
+      else if (epi == EPI_F32) L16V2(3, EPI_F32); else L16V2(3, EPI_NONE);
+    } else return -2;
+#undef L16V2
+    return (int)hipGetLastError();
+  }
   size_t lds = (size_t)g.PR * g.RS * 32 + (size_t)nq * 64 * 16;
   dim3 grid((unsigned)(V * I * J * g.nkt * g.nlt)), block(256);
-  const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
 #define L16(KSV, EPIV) hipLaunchKernelGGL((conv16_fwd_kernel<KSV, EPIV>), grid, block, lds, stream, x, w, bias, m, y, g)
   if (KS == 5) {
-    if (epi == EPI_BIAS_RELU) L16(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16(5, EPI_MASK); else L16(5, EPI_NONE);
+    if (epi == EPI_BIAS_RELU) L16(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16(5, EPI_MASK);
+    else if (epi == EPI_F32) L16(5, EPI_F32); else L16(5, EPI_NONE);
   } else if (KS == 3) {
-    if (epi == EPI_BIAS_RELU) L16(3, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16(3, EPI_MASK); else L16(3, EPI_NONE);
+    if (epi == EPI_BIAS_RELU) L16(3, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16(3, EPI_MASK);
+    else if (epi == EPI_F32) L16(3, EPI_F32); else L16(3, EPI_NONE);
   } else return -2;
 #undef L16
   return (int)hipGetLastError();

@@ -28,6 +28,7 @@ struct WGeom {
   int TK, TL, nkt, nlt;
   int PR, RS;          // staged X plane (wgrad16)
   int nitems, ipg;     // output tiles, tiles per group
+  int dj_center;       // 1: only the (di, dj = P) offsets (j-offset encoded in channels)
 };
 
 struct Item { int v, i, j, k0, l0; };
@@ -65,8 +66,9 @@ __global__ __launch_bounds__(256, 2) void wgrad16_kernel(const bf16* __restrict_
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int dd = lb % NT, grp = lb / NT;
-  const int di = dd / KS, dj = dd % KS;
+  const int NDD = g.dj_center ? KS : NT;   // plane offsets handled by the grid
+  const int dd = lb % NDD, grp = lb / NDD;
+  const int di = g.dj_center ? dd : dd / KS, dj = g.dj_center ? P : dd % KS;
   const bool center = (di == P && dj == P);
 
   for (int e = threadIdx.x; e < nv32; e += 256) {
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(256, 2) void wgrad16_kernel(const bf16* __restrict_
   }
 
   // D[row = ci = 4(l>>4)+r][col = co = l&15]
-  float* pout = part + ((size_t)grp * NT + dd) * NT * 256;
+  float* pout = part + ((size_t)grp * NDD + dd) * NT * 256;
 #pragma unroll
   for (int tt = 0; tt < TPW; ++tt) {
     int tap = wave + 4 * tt;
@@ -380,18 +382,20 @@ static WGeom make_wgeom(int V, int I, int J, int K, int L, int KS, int ngroups) 
   g.PR = g.TK + KS - 1; g.RS = g.TL + KS - 1;
   g.nitems = V * I * J * g.nkt * g.nlt;
   g.ipg = cdiv(g.nitems, ngroups);
+  g.dj_center = 0;
   return g;
 }
 
-// part: [ngroups][KS*KS][KS*KS][16 ci][16 co] fp32; partb: [ngroups][16]
+// part: [ngroups][KS*KS (or KS when dj_center)][KS*KS][16 ci][16 co] fp32; partb: [ngroups][16]
 extern "C" int ncnet_wgrad16(const void* X, const void* G, float* part, float* partb, int V, int I, int J, int K,
-                             int L, int KS, int ngroups, hipStream_t stream) {
+                             int L, int KS, int ngroups, int dj_center, hipStream_t stream) {
   WGeom g = make_wgeom(V, I, J, K, L, KS, ngroups);
+  g.dj_center = dj_center;
   if (g.PR * g.RS * 2 > 8 * 256) return -1;
   int nv32 = (g.TK * g.TL + 31) & ~31;
   if (nv32 * 2 > 5 * 256) return -1;
   size_t lds = (size_t)g.PR * g.RS * 32 + (size_t)nv32 * 32 + (size_t)nv32 * 4;
-  dim3 grid((unsigned)(KS * KS * ngroups)), block(256);
+  dim3 grid((unsigned)((dj_center ? KS : KS * KS) * ngroups)), block(256);
   if (KS == 5) hipLaunchKernelGGL((wgrad16_kernel<5>), grid, block, lds, stream, (const bf16*)X, (const bf16*)G, part, partb, g);
   else if (KS == 3) hipLaunchKernelGGL((wgrad16_kernel<3>), grid, block, lds, stream, (const bf16*)X, (const bf16*)G, part, partb, g);
   else return -2;

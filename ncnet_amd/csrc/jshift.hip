@@ -1,0 +1,85 @@
+// j-offset <-> channel re-encoding for the 1-channel NC-Net layers.
+//
+// A Conv4d with one input (or one output) channel wastes 15/16 of an MFMA.
+// Moving the kernel's j-offset (dj) into the channel axis turns it into a
+// 16 -> 16 convolution whose kernel is non-zero only on the dj = P planes:
+//
+//   Cin = 1 :  X0s[v,i,j,k,l,c] = X0[v,i,j+(c-P),k,l]        (jpack, sgn = +1)
+//              Y = conv16_{dj=P}(X0s, W1s),  W1s[co][c][di][P][dk][dl] = W1[co][0][di][c][dk][dl]
+//   Cout = 1:  Z = conv16_{dj=P}(X2, Wz),    Wz[c][ci][di][P][dk][dl]  = W3[0][ci][di][c][dk][dl]
+//              y[v,i,j,k,l] = sum_c Z[v,i,j+(c-P),k,l,c]      (jsum; its adjoint is jpack with sgn = -1)
+//
+// so forward, data-gradient and weight-gradient of those layers all run on the
+// conv16 / wgrad16 MFMA kernels over KS planes instead of KS*KS.
+#include "common.h"
+
+namespace ncnet {
+
+// S[v,i,j,k,l,c] = X[v,i,j+sgn*(c-P),k,l] for c < KS (zero outside the volume / for c >= KS).
+template <typename T>
+__global__ __launch_bounds__(256) void jpack_kernel(const T* __restrict__ X, bf16* __restrict__ S, long long nvox,
+                                                    int J, int KL, int KS, int sgn) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nvox) return;
+  const int P = KS / 2;
+  const long long plane = e / KL;          // (v*I + i)*J + j
+  const int j = (int)(plane % J);
+  const int kl = (int)(e - plane * KL);
+  bf16x8 lo, hi;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    int jj = j + sgn * (c - P);
+    float v = 0.f;
+    if (c < KS && jj >= 0 && jj < J) v = (float)X[(plane + (jj - j)) * KL + kl];
+    lo[c] = f2bf(v);
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) hi[c] = f2bf(0.f);
+  bf16x8* o = (bf16x8*)(S + e * 16);
+  o[0] = lo;
+  o[1] = hi;
+}
+
+// y[v,i,j,k,l] = act(bias + sum_{c<KS} Z8[v,i,j+sgn*(c-P),k,l,c]),  Z8 fp32 [..., 8]
+// (sgn = +1: the Cout=1 forward; sgn = -1: adjoint of jpack(+1), the Cin=1 data gradient)
+__global__ __launch_bounds__(256) void jsum_kernel(const float* __restrict__ Z8, const float* __restrict__ bias,
+                                                   float* __restrict__ y, long long nvox, int J, int KL, int KS,
+                                                   int relu, int sgn) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nvox) return;
+  const int P = KS / 2;
+  const long long plane = e / KL;
+  const int j = (int)(plane % J);
+  const int kl = (int)(e - plane * KL);
+  float s = bias ? bias[0] : 0.f;
+  for (int c = 0; c < KS; ++c) {
+    int jj = j + sgn * (c - P);
+    if (jj >= 0 && jj < J) s += Z8[((plane + (jj - j)) * KL + kl) * 8 + c];
+  }
+  y[e] = relu ? fmaxf(s, 0.f) : s;
+}
+
+}  // namespace ncnet
+
+using namespace ncnet;
+
+extern "C" int ncnet_jpack(const void* X, int x_is_bf16, void* S, int V, int I, int J, int K, int L, int KS, int sgn,
+                           hipStream_t stream) {
+  if (KS > 8 || KS < 1) return -1;
+  long long nvox = (long long)V * I * J * K * L;
+  dim3 grid((unsigned)((nvox + 255) / 256));
+  if (x_is_bf16)
+    hipLaunchKernelGGL((jpack_kernel<bf16>), grid, dim3(256), 0, stream, (const bf16*)X, (bf16*)S, nvox, J, K * L, KS, sgn);
+  else
+    hipLaunchKernelGGL((jpack_kernel<float>), grid, dim3(256), 0, stream, (const float*)X, (bf16*)S, nvox, J, K * L, KS, sgn);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ncnet_jsum(const float* Z8, const float* bias, float* y, int V, int I, int J, int K, int L, int KS,
+                          int relu, int sgn, hipStream_t stream) {
+  if (KS > 8 || KS < 1) return -1;
+  long long nvox = (long long)V * I * J * K * L;
+  hipLaunchKernelGGL(jsum_kernel, dim3((unsigned)((nvox + 255) / 256)), dim3(256), 0, stream, Z8, bias, y, nvox, J,
+                     K * L, KS, relu, sgn);
+  return (int)hipGetLastError();
+}

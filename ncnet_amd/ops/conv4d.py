@@ -55,7 +55,7 @@ def _conv_cl(xcl: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, mask=N
         C.conv1out_fwd(xcl, pack_w1out(w_std), None, y, ks, 0)
     else:
         y = torch.empty(tuple(shp) + (16,), dtype=torch.bfloat16, device=xcl.device)
-        C.conv16_fwd(xcl, pack_w16(w_std), None, mask, y, ks, 2 if mask is not None else 0)
+        C.conv16_fwd(xcl, pack_w16(w_std), None, mask, y, ks, 2 if mask is not None else 0, 0)
     return y
 
 
@@ -104,7 +104,7 @@ class Conv4dFn(torch.autograd.Function):
             else:
                 part = torch.empty((ng, ks * ks, ks * ks, 16, 16), dtype=torch.float32, device=g.device)
                 partb = torch.empty((ng, 16), dtype=torch.float32, device=g.device)
-                C.wgrad16(xcl, gcl, part, partb, ks, ng)
+                C.wgrad16(xcl, gcl, part, partb, ks, ng, 0)
                 dw = _reduce_wgrad16(part, ks, cout, cin)
             gw = ref.conv4d_weight_from_std(dw).to(w_ref.dtype)
         if has_bias and ctx.needs_input_grad[2]:

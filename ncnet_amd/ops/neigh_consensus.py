@@ -24,9 +24,16 @@ import torch
 
 from . import _ext
 from . import reference as ref
-from .packing import pack_w16, pack_w1in, pack_w1out, transpose_for_dgrad
+from .packing import (jc_in_grad, jc_in_weights, jc_out_grad, jc_out_weights, pack_w16, pack_w1in, pack_w1out,
+                      transpose_for_dgrad)
 
 HIP_KS = (3, 5)
+# 1-channel layers through the j-offset channel encoding (csrc/jshift.hip) on
+# the conv16 / wgrad16 kernels; NCNET_NC_JC=0 selects the dedicated
+# 1-channel kernels (conv1in / conv1out / wgrad1) instead.
+import os as _os
+
+USE_JC = _os.environ.get("NCNET_NC_JC", "1") == "1"
 
 
 def layer_kinds(channels, kernel_sizes):
@@ -51,9 +58,10 @@ def layer_kinds(channels, kernel_sizes):
 
 
 def wgrad_groups(ks: int, nitems: int) -> int:
-    """Number of K-split groups of the wgrad kernels: about one resident wave of
-    workgroups (2 per CU on 256 CUs) for KS*KS (di,dj) offsets."""
-    target = 512 // (ks * ks)
+    """Number of K-split groups of the wgrad kernels (~3000 workgroups for the
+    KS*KS plane offsets; measured on MI355X: 120 groups at KS=5 beat 20 by 1.4x)."""
+    env = _os.environ.get("NCNET_WGRAD_GROUPS")
+    target = int(env) if env else 3072 // (ks * ks)
     return max(1, min(target, nitems))
 
 
@@ -80,12 +88,26 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
         w = _std(w_ref)
         save.append(h)
         last = li == len(kinds) - 1
-        if kind == "1in":
+        if kind == "1in" and USE_JC:
+            xs = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
+            C.jpack(h, xs, ks, 1)
+            save[-1] = xs  # the backward needs the j-packed input
+            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
+            C.conv16_fwd(xs, pack_w16(jc_in_weights(w)), _pad_bias(b, 16), None, y, ks, 1, 1)
+        elif kind == "1in":
             y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
             C.conv1in_fwd(h, pack_w1in(w), _pad_bias(b, 16), None, y, ks, 1)
         elif kind == "16":
             y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
-            C.conv16_fwd(h, pack_w16(w), _pad_bias(b, 16), None, y, ks, 1)
+            C.conv16_fwd(h, pack_w16(w), _pad_bias(b, 16), None, y, ks, 1, 0)
+        elif USE_JC:
+            z8 = torch.empty((V, I, J, K, L, 8), dtype=torch.float32, device=x0.device)
+            C.conv16_fwd(h, pack_w16(jc_out_weights(w)), None, None, z8, ks, 3, 1)
+            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
+            C.jsum(z8, _pad_bias(b, 1), y, ks, 1, 1)
+            del z8
+            if not last:
+                y = y.to(torch.bfloat16)
         else:
             y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
             C.conv1out_fwd(h, pack_w1out(w), _pad_bias(b, 1), y, ks, 1)
@@ -99,6 +121,18 @@ def _reduce_wgrad16(part: torch.Tensor, ks: int, cout: int, cin: int) -> torch.T
     # part [G, dd, tap, ci, co] -> std [co, ci, di, dj, dk, dl]
     s = part.sum(0).permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks, ks)
     return s[:cout, :cin]
+
+
+def _reduce_wgrad16_center(part: torch.Tensor, ks: int) -> torch.Tensor:
+    # part [G, di, tap, ci, co] (dj = P only) -> [co, ci, di, dk, dl]
+    return part.sum(0).permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks)
+
+
+def _wgrad16_center(C, x16, g16, ks, ng) -> torch.Tensor:
+    part = torch.empty((ng, ks, ks * ks, 16, 16), dtype=torch.float32, device=x16.device)
+    partb = torch.empty((ng, 16), dtype=torch.float32, device=x16.device)
+    C.wgrad16(x16, g16, part, partb, ks, ng, 1)
+    return _reduce_wgrad16_center(part, ks)
 
 
 def _reduce_wgrad1(part: torch.Tensor, ks: int, mode: int, c16: int) -> torch.Tensor:
@@ -128,7 +162,29 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
         nitems = V * I * J * ((K + 24) // 25) * ((L + 24) // 25)
         ng = wgrad_groups(ks, nitems)
         mask_prev = h if li > 0 else None   # ReLU output of the previous layer
-        if kind == "1out":
+        if kind == "1out" and USE_JC:
+            gs = torch.empty(tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
+            C.jpack(g, gs, ks, -1)                   # adjoint of jsum
+            dw = jc_out_grad(_wgrad16_center(C, h, gs, ks, ng), cin)
+            db = g.float().sum().reshape(1)
+            if li > 0 or need_dx0:
+                gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
+                wt = transpose_for_dgrad(jc_out_weights(w))
+                C.conv16_fwd(gs, pack_w16(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0, 1)
+                g = gi
+            del gs
+        elif kind == "1in" and USE_JC:               # h is jpack(X0) (16ch)
+            dw = jc_in_grad(_wgrad16_center(C, h, g, ks, ng), cout)
+            db = g.float().sum(dim=(0, 1, 2, 3, 4))[:cout]
+            if li > 0:
+                raise RuntimeError("internal: 1in layer must be first")
+            if need_dx0:
+                z8 = torch.empty(tuple(h.shape[:5]) + (8,), dtype=torch.float32, device=h.device)
+                wt = transpose_for_dgrad(jc_in_weights(w))
+                C.conv16_fwd(g, pack_w16(wt), None, None, z8, ks, 3, 1)
+                gx0 = torch.empty(tuple(h.shape[:5]), dtype=torch.float32, device=h.device)
+                C.jsum(z8, None, gx0, ks, 0, -1)      # adjoint of jpack(+1)
+        elif kind == "1out":
             if g.dim() == 6:
                 raise RuntimeError("internal: 1out layer expects a 1-channel gradient")
             part = torch.empty((ng, ks * ks, ks * ks, 16), dtype=torch.float32, device=h.device)
@@ -143,13 +199,13 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
         elif kind == "16":
             part = torch.empty((ng, ks * ks, ks * ks, 16, 16), dtype=torch.float32, device=h.device)
             partb = torch.empty((ng, 16), dtype=torch.float32, device=h.device)
-            C.wgrad16(h, g, part, partb, ks, ng)
+            C.wgrad16(h, g, part, partb, ks, ng, 0)
             dw = _reduce_wgrad16(part, ks, cout, cin)
             db = partb.sum(0)[:cout]
             if li > 0 or need_dx0:
                 gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
                 wt = transpose_for_dgrad(w)
-                C.conv16_fwd(g, pack_w16(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0)
+                C.conv16_fwd(g, pack_w16(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0, 0)
                 g = gi
         else:  # "1in": h is the 1-channel input
             part = torch.empty((ng, ks * ks, ks * ks, 16), dtype=torch.float32, device=h.device)

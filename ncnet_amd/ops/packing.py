@@ -111,3 +111,37 @@ def pack_w1out(w_std: torch.Tensor) -> torch.Tensor:
     vals = w[ci, :, tap]                           # [npair, 64, 8, k*k]
     vals = vals * valid.unsqueeze(-1).to(vals.dtype)
     return vals.permute(3, 0, 1, 2).contiguous().to(torch.bfloat16)
+
+
+# ---------------------------------------------------------------------------
+# j-offset <-> channel encoding of the 1-channel layers (see csrc/jshift.hip).
+# A Cin=1 layer W1 [co,1,k^4] becomes a 16->16 conv over jpack(X0) whose kernel
+# lives on the dj=P plane only; a Cout=1 layer W3 [1,ci,k^4] becomes a 16->16
+# conv (channels = dj) followed by jsum.
+
+def jc_in_weights(w_std: torch.Tensor) -> torch.Tensor:
+    """[co, 1, k^4] -> [16, 16, k^4]: out[co][c][di][P][dk][dl] = w[co][0][di][c][dk][dl]."""
+    co, ks = w_std.shape[0], w_std.shape[-1]
+    out = w_std.new_zeros((16, 16) + (ks,) * 4)
+    out[:co, :ks, :, ks // 2] = w_std[:, 0].permute(0, 2, 1, 3, 4)
+    return out
+
+
+def jc_out_weights(w_std: torch.Tensor) -> torch.Tensor:
+    """[1, ci, k^4] -> [16, 16, k^4]: out[c][ci][di][P][dk][dl] = w[0][ci][di][c][dk][dl]."""
+    ci, ks = w_std.shape[1], w_std.shape[-1]
+    out = w_std.new_zeros((16, 16) + (ks,) * 4)
+    out[:ks, :ci, :, ks // 2] = w_std[0].permute(2, 0, 1, 3, 4)
+    return out
+
+
+def jc_in_grad(s5: torch.Tensor, cout: int) -> torch.Tensor:
+    """dW of the dj=P slice [co, c, di, dk, dl] -> [co, 1, di, dj=c, dk, dl]."""
+    ks = s5.shape[-1]
+    return s5[:cout, :ks].permute(0, 2, 1, 3, 4).unsqueeze(1).contiguous()
+
+
+def jc_out_grad(s5: torch.Tensor, cin: int) -> torch.Tensor:
+    """dW of the dj=P slice [c, ci, di, dk, dl] -> [1, ci, di, dj=c, dk, dl]."""
+    ks = s5.shape[-1]
+    return s5[:ks, :cin].permute(1, 2, 0, 3, 4).unsqueeze(0).contiguous()

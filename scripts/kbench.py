@@ -63,16 +63,23 @@ def main():
     part16 = torch.empty((ng, ks * ks, ks * ks, 16, 16), device=dev)
     partb = torch.empty((ng, 16), device=dev)
     part1 = torch.empty((ng, ks * ks, ks * ks, 16), device=dev)
+    part16c = torch.empty((ng, ks, ks * ks, 16, 16), device=dev)
+    z8 = torch.empty(shp + (8,), device=dev)
+    g16b = torch.empty_like(g16)
     taps = ks ** 4
     fl16 = 2.0 * nvox * taps * 256
     fl1 = 2.0 * nvox * taps * 16
     cases = {
-        "conv16_fwd": (lambda: C.conv16_fwd(x16, w16, b16, None, y16, ks, 1), fl16),
-        "conv16_dgrad_mask": (lambda: C.conv16_fwd(g16, w16, None, x16, y16, ks, 2), fl16),
+        "conv16_fwd": (lambda: C.conv16_fwd(x16, w16, b16, None, y16, ks, 1, 0), fl16),
+        "conv16_dgrad_mask": (lambda: C.conv16_fwd(g16, w16, None, x16, y16, ks, 2, 0), fl16),
+        "conv16_center_f32": (lambda: C.conv16_fwd(x16, w16, None, None, z8, ks, 3, 1), fl16 / ks),
+        "jpack": (lambda: C.jpack(x1, g16b, ks, 1), None),
+        "jsum": (lambda: C.jsum(z8, b1, y1, ks, 1, 1), None),
         "conv1in_fwd": (lambda: C.conv1in_fwd(x1, w1i, b16, None, y16, ks, 1), fl1),
         "conv1in_dgrad_mask": (lambda: C.conv1in_fwd(g1, w1i, None, x16, y16, ks, 2), fl1),
         "conv1out_fwd": (lambda: C.conv1out_fwd(x16, w1o, b1, y1, ks, 1), fl1),
-        "wgrad16": (lambda: C.wgrad16(x16, g16, part16, partb, ks, ng), fl16),
+        "wgrad16": (lambda: C.wgrad16(x16, g16, part16, partb, ks, ng, 0), fl16),
+        "wgrad16_center": (lambda: C.wgrad16(x16, g16, part16c, partb, ks, ng, 1), fl16 / ks),
         "wgrad1_mode0": (lambda: C.wgrad1(g16, x1, part1, ks, 0, ng), fl1),
         "wgrad1_mode1": (lambda: C.wgrad1(x16, g1, part1, ks, 1, ng), fl1),
     }
@@ -82,8 +89,9 @@ def main():
         if only and name not in only:
             continue
         ms = timeit(fn, a.reps)
-        res[name] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
-        print(f"{name:22s} {ms:9.3f} ms  {fl / ms / 1e9:8.1f} TFLOP/s (useful)", flush=True)
+        tf = round(fl / ms / 1e9, 1) if fl else None
+        res[name] = {"ms": round(ms, 4), "tflops": tf}
+        print(f"{name:22s} {ms:9.3f} ms  " + (f"{tf:8.1f} TFLOP/s" if tf else ""), flush=True)
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"vols": V, "size": S, "ks": ks, "groups": ng, "kernels": res}, f, indent=1)

@@ -46,7 +46,7 @@ def test_conv16_fwd(ks, shape):
     b = torch.randn(16, device=DEV) * 0.1
     xcl = x.permute(0, 2, 3, 4, 5, 1).contiguous().to(torch.bfloat16)
     y = torch.empty_like(xcl)
-    _ext.ext().conv16_fwd(xcl, pack_w16(w), b, None, y, ks, 1)
+    _ext.ext().conv16_fwd(xcl, pack_w16(w), b, None, y, ks, 1, 0)
     yr = torch.relu(ref.conv4d(bf(x), ref.conv4d_weight_from_std(bf(w)), b.double()))
     assert relerr(y.permute(0, 5, 1, 2, 3, 4), yr) < 1e-2
 

@@ -213,3 +213,73 @@ def test_dgrad_weights_are_flipped_transpose(ks):
     (y * g).sum().backward()
     gx = ref.conv4d(g, ref.conv4d_weight_from_std(transpose_for_dgrad(w)))
     assert torch.allclose(gx, x.grad, atol=1e-9)
+
+
+def _jpack(x, ks, sgn):
+    """torch emulation of csrc/jshift.hip jpack: x [V,I,J,K,L] -> [V,16,I,J,K,L] (channels-first)."""
+    V, I, J, K, L = x.shape
+    P = ks // 2
+    out = torch.zeros(V, 16, I, J, K, L, dtype=x.dtype)
+    for c in range(ks):
+        s = sgn * (c - P)
+        lo, hi = max(0, -s), min(J, J - s)
+        out[:, c, :, lo:hi] = x[:, :, lo + s:hi + s]
+    return out
+
+
+def _jsum(z, ks, sgn):
+    """emulation of jsum: z [V,16,I,J,K,L] -> [V,I,J,K,L], y[j] = sum_c z[c][j + sgn*(c-P)]."""
+    V, _, I, J, K, L = z.shape
+    P = ks // 2
+    y = torch.zeros(V, I, J, K, L, dtype=z.dtype)
+    for c in range(ks):
+        s = sgn * (c - P)
+        lo, hi = max(0, -s), min(J, J - s)
+        y[:, :, lo:hi] += z[:, c, :, lo + s:hi + s]
+    return y
+
+
+@pytest.mark.parametrize("ks", [3, 5])
+def test_jchannel_encoding_forward_and_grads(ks):
+    """1->16 layer == conv16_{dj=P}(jpack(x)) and 16->1 layer == jsum(conv16_{dj=P}(x)),
+    including the weight-gradient maps jc_in_grad / jc_out_grad."""
+    from ncnet_amd.ops.packing import jc_in_grad, jc_in_weights, jc_out_grad, jc_out_weights
+    torch.manual_seed(3)
+    V, I, J, K, L = 2, 4, 6, 5, 5
+    P = ks // 2
+    # Cin = 1
+    x0 = torch.randn(V, I, J, K, L, dtype=torch.float64)
+    w1 = _rand_w(16, 1, ks)
+    y_ref = ref.conv4d(x0.unsqueeze(1), ref.conv4d_weight_from_std(w1))
+    wj = jc_in_weights(w1)
+    assert torch.count_nonzero(wj[:, :, :, [d for d in range(ks) if d != P]]) == 0
+    xs = _jpack(x0, ks, 1)
+    y_j = ref.conv4d(xs, ref.conv4d_weight_from_std(wj))
+    assert torch.allclose(y_j, y_ref, atol=1e-9)
+    g = torch.randn_like(y_ref)
+    w_a = w1.clone().requires_grad_(True)
+    (ref.conv4d(x0.unsqueeze(1), ref.conv4d_weight_from_std(w_a)) * g).sum().backward()
+    wj_a = wj.clone().requires_grad_(True)
+    (ref.conv4d(xs, ref.conv4d_weight_from_std(wj_a)) * g).sum().backward()
+    s5 = wj_a.grad[:, :, :, P]  # [co, ci, di, dk, dl]
+    assert torch.allclose(jc_in_grad(s5, 16), w_a.grad, atol=1e-9)
+    # Cout = 1
+    x2 = torch.randn(V, 16, I, J, K, L, dtype=torch.float64)
+    w3 = _rand_w(1, 16, ks)
+    y3_ref = ref.conv4d(x2, ref.conv4d_weight_from_std(w3))[:, 0]
+    wz = jc_out_weights(w3)
+    z = ref.conv4d(x2, ref.conv4d_weight_from_std(wz))
+    assert torch.allclose(_jsum(z, ks, 1), y3_ref, atol=1e-9)
+    g3 = torch.randn_like(y3_ref)
+    # adjoint: jsum(+1)^T == jpack(-1)
+    assert torch.allclose((_jsum(z, ks, 1) * g3).sum(), (z * _jpack(g3, ks, -1)).sum())
+    w3_a = w3.clone().requires_grad_(True)
+    (ref.conv4d(x2, ref.conv4d_weight_from_std(w3_a))[:, 0] * g3).sum().backward()
+    wz_a = wz.clone().requires_grad_(True)
+    (ref.conv4d(x2, ref.conv4d_weight_from_std(wz_a)) * _jpack(g3, ks, -1)).sum().backward()
+    assert torch.allclose(jc_out_grad(wz_a.grad[:, :, :, P], 16), w3_a.grad, atol=1e-9)
+    # data gradient of the Cin=1 layer: jsum(-1) of the dj=P transposed conv
+    x0a = x0.clone().requires_grad_(True)
+    (ref.conv4d(x0a.unsqueeze(1), ref.conv4d_weight_from_std(w1)) * g).sum().backward()
+    dxs = ref.conv4d(g, ref.conv4d_weight_from_std(transpose_for_dgrad(wj)))
+    assert torch.allclose(_jsum(dxs, ks, -1), x0a.grad, atol=1e-9)
