@@ -1,0 +1,134 @@
+#!/usr/bin/env python
+"""InLoc dense-match export (reference CLI: eval_inloc.py:29-40).
+
+Writes ``matches/<folder>/<q+1>.mat`` with the reference's contract
+(``matches`` [1, n_panos, N, 5], ``query_fn``, ``pano_fn``) for the MATLAB
+localization pipeline.  Relocalization k=2 uses the fused correlation +
+max-pool kernel (the full-resolution volume is never written).  Queries are
+sharded over ranks (torchrun) and existing outputs are skipped (resume).
+
+Extras: --synthetic_queries N builds a fake shortlist and random images in a
+temp dir (smoke / benchmark without the dataset); --ncons_* for
+checkpoint-less runs; --output_dir (default matches/).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from ncnet_amd.data.transforms import read_image  # noqa: E402
+from ncnet_amd.engine.checkpoint import str_to_bool  # noqa: E402
+from ncnet_amd.eval.inloc import (load_shortlist, n_matches, output_folder, pair_matches, prepare_image,  # noqa: E402
+                                  save_query)
+from ncnet_amd.models import ImMatchNet  # noqa: E402
+from ncnet_amd.parallel.dist import barrier, destroy, init_distributed  # noqa: E402
+
+
+def make_synthetic_inloc(root: str, n_queries: int, n_panos: int, h: int = 768, w: int = 1024):
+    """Fake shortlist .mat + random JPEGs laid out like datasets/inloc."""
+    from PIL import Image
+    from scipy.io import savemat
+
+    qdir, pdir = os.path.join(root, "query"), os.path.join(root, "pano")
+    os.makedirs(qdir, exist_ok=True)
+    os.makedirs(pdir, exist_ok=True)
+    rng = np.random.default_rng(0)
+    recs = []
+    for q in range(n_queries):
+        qn = f"IMG_{q:04d}.JPG"
+        Image.fromarray(rng.integers(0, 255, (h, w, 3), dtype=np.uint8)).save(os.path.join(qdir, qn))
+        pn = []
+        for p in range(n_panos):
+            name = f"DUC1/pano_{q:03d}_{p:02d}.jpg"
+            os.makedirs(os.path.dirname(os.path.join(pdir, name)), exist_ok=True)
+            Image.fromarray(rng.integers(0, 255, (h, w, 3), dtype=np.uint8)).save(os.path.join(pdir, name))
+            pn.append(name)
+        recs.append((qn, np.array(pn, dtype=object).reshape(1, -1)))
+    arr = np.empty((1, n_queries), dtype=[("queryname", "O"), ("topNname", "O")])
+    for q, (qn, pn) in enumerate(recs):
+        arr[0, q] = (qn, pn)
+    path = os.path.join(root, "synthetic_shortlist.mat")
+    savemat(path, {"ImgList": arr})
+    return path, qdir + "/", pdir + "/"
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Compute InLoc matches")
+    ap.add_argument("--checkpoint", type=str, default="")
+    ap.add_argument("--inloc_shortlist", type=str, default="datasets/inloc/densePE_top100_shortlist_cvpr18.mat")
+    ap.add_argument("--k_size", type=int, default=2)
+    ap.add_argument("--image_size", type=int, default=3200)
+    ap.add_argument("--n_queries", type=int, default=356)
+    ap.add_argument("--n_panos", type=int, default=10)
+    ap.add_argument("--softmax", type=str_to_bool, default=True)
+    ap.add_argument("--matching_both_directions", type=str_to_bool, default=True)
+    ap.add_argument("--flip_matching_direction", type=str_to_bool, default=False)
+    ap.add_argument("--pano_path", type=str, default="datasets/inloc/pano/")
+    ap.add_argument("--query_path", type=str, default="datasets/inloc/query/iphone7/")
+    ap.add_argument("--output_dir", type=str, default="matches/")
+    ap.add_argument("--synthetic_queries", type=int, default=0)
+    ap.add_argument("--ncons_kernel_sizes", nargs="+", type=int, default=[3, 3])
+    ap.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 1])
+    args = ap.parse_args(argv)
+    ctx = init_distributed()
+
+    tmp = None
+    if args.synthetic_queries:
+        tmp = tempfile.mkdtemp(prefix="ncnet_inloc_")
+        args.inloc_shortlist, args.query_path, args.pano_path = make_synthetic_inloc(
+            tmp, args.synthetic_queries, args.n_panos)
+        args.n_queries = args.synthetic_queries
+    model = ImMatchNet(use_cuda=ctx.device.type == "cuda", checkpoint=args.checkpoint or None,
+                       ncons_kernel_sizes=args.ncons_kernel_sizes, ncons_channels=args.ncons_channels,
+                       half_precision=True, relocalization_k_size=args.k_size).to(ctx.device)
+    model.eval()
+    folder = output_folder(args.inloc_shortlist, args.image_size, args.k_size, args.matching_both_directions,
+                           args.flip_matching_direction, args.softmax, args.checkpoint)
+    out_dir = os.path.join(args.output_dir, folder)
+    os.makedirs(out_dir, exist_ok=True)
+    if ctx.is_main:
+        print("Output matches folder: " + folder)
+    queries, panos, pano_all = load_shortlist(args.inloc_shortlist)
+    N = n_matches(args.image_size, args.k_size, args.matching_both_directions)
+    nq = min(args.n_queries, len(queries))
+    t0 = time.perf_counter()
+    npairs = 0
+    with torch.inference_mode():
+        for q in range(ctx.rank, nq, ctx.world_size):
+            path = os.path.join(out_dir, f"{q + 1}.mat")
+            if os.path.exists(path):
+                continue
+            matches = np.zeros((1, args.n_panos, N, 5))
+            src = prepare_image(read_image(os.path.join(args.query_path, queries[q])), args.image_size, args.k_size,
+                                ctx.device)
+            for idx in range(min(args.n_panos, len(panos[q]))):
+                tgt = prepare_image(read_image(os.path.join(args.pano_path, panos[q][idx])), args.image_size,
+                                    args.k_size, ctx.device)
+                out = model({"source_image": src, "target_image": tgt})
+                corr4d, delta4d = out if args.k_size > 1 else (out, None)
+                m = pair_matches(corr4d, delta4d, args.k_size, args.softmax, args.matching_both_directions,
+                                 args.flip_matching_direction).double().cpu().numpy()
+                n = min(len(m), N)
+                matches[0, idx, :n] = m[:n]
+                npairs += 1
+            save_query(path, matches, queries[q], pano_all)
+            if ctx.is_main:
+                print(f"query {q + 1}/{nq} ({npairs} pairs, {npairs / (time.perf_counter() - t0):.2f} pairs/s/rank)",
+                      flush=True)
+    barrier(ctx)
+    if ctx.is_main:
+        print("Done: " + out_dir)
+    destroy(ctx)
+    return out_dir
+
+
+if __name__ == "__main__":
+    main()

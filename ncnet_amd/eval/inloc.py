@@ -1,0 +1,119 @@
+"""InLoc dense-match export (eval_inloc.py), with the same ``.mat`` contract.
+
+Per query: ``matches`` float64 ``[1, n_panos, N, 5]`` with columns
+``(xA, yA, xB, yB, score)`` in pixel-centre-normalised [0,1] coordinates,
+unused rows 0, plus ``query_fn`` and ``pano_fn`` (eval_inloc.py:126,197-221).
+
+Differences from the reference, output-preserving:
+* the bidirectional de-duplication (sort by score, ``np.unique`` on the CPU,
+  eval_inloc.py:160-173) runs on the GPU with integer keys: the kept match of
+  every (xA,yA,xB,yB) is the highest-scoring one and the rows come out in the
+  lexicographic (xA,yA,xB,yB) order that ``np.unique`` produces;
+* query files that already exist are skipped (resume by idempotence, the same
+  idea as the MATLAB stage caching), and queries can be sharded over ranks.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ..data.transforms import normalize_image, resize_bilinear
+from .point_tnf import corr_to_matches
+
+SCALE_FACTOR = 0.0625  # feature stride 1/16 (eval_inloc.py:77)
+
+
+def output_folder(shortlist: str, image_size: int, k_size: int, both_dirs: bool, flip: bool, softmax: bool,
+                  checkpoint: str = "") -> str:
+    """eval_inloc.py:60-71."""
+    name = os.path.basename(shortlist).split(".")[0] + "_SZ_NEW_" + str(image_size) + "_K_" + str(k_size)
+    if both_dirs:
+        name += "_BOTHDIRS"
+    elif flip:
+        name += "_AtoB"
+    else:
+        name += "_BtoA"
+    if softmax:
+        name += "_SOFTMAX"
+    if checkpoint:
+        name += "_CHECKPOINT_" + os.path.basename(checkpoint).split(".")[0]
+    return name
+
+
+def n_matches(image_size: int, k_size: int, both_dirs: bool) -> int:
+    """eval_inloc.py:116-118 (sized for 4:3 landscape images)."""
+    a = image_size * SCALE_FACTOR / k_size
+    n = int(a * np.floor(a * 3 / 4))
+    return 2 * n if both_dirs else n
+
+
+def target_size(h: int, w: int, image_size: int, k_size: int):
+    """Longest side -> image_size, floored to a multiple of k_size/0.0625 px
+    when relocalizing (eval_inloc.py:83-89)."""
+    r = max(h, w) / image_size
+    if k_size == 1:
+        return int(h / r), int(w / r)
+    unit = SCALE_FACTOR / k_size
+    return (int(np.floor(h / r * unit) / unit), int(np.floor(w / r * unit) / unit))
+
+
+def prepare_image(img_uint8_hwc: np.ndarray, image_size: int, k_size: int, device) -> torch.Tensor:
+    x = torch.from_numpy(np.ascontiguousarray(img_uint8_hwc.transpose(2, 0, 1))).to(device).float() / 255.0
+    x = normalize_image(x)
+    h, w = target_size(x.shape[1], x.shape[2], image_size, k_size)
+    return resize_bilinear(x, h, w).unsqueeze(0)
+
+
+def pair_matches(corr4d, delta4d, k_size: int, do_softmax: bool = True, both_dirs: bool = True,
+                 flip: bool = False):
+    """Bidirectional, de-duplicated, recentred matches of one pair -> [Npts, 5] tensor."""
+    b, _, fs1, fs2, fs3, fs4 = corr4d.shape
+    k = max(1, k_size)
+    kw = dict(scale="positive", do_softmax=do_softmax, delta4d=delta4d, k_size=k, return_indices=True)
+    if both_dirs:
+        r1 = corr_to_matches(corr4d, **kw)
+        r2 = corr_to_matches(corr4d, invert_matching_direction=True, **kw)
+        xA, yA, xB, yB, sc, iA, jA, iB, jB = (torch.cat((a.reshape(-1), c.reshape(-1))) for a, c in zip(r1, r2))
+        HA, WA, HB, WB = fs1 * k, fs2 * k, fs3 * k, fs4 * k
+        key = ((jA.long() * HA + iA.long()) * WB + jB.long()) * HB + iB.long()  # lexicographic (xA,yA,xB,yB)
+        order = torch.argsort(-sc, stable=True)
+        key_s = key[order]
+        order2 = torch.argsort(key_s, stable=True)
+        idx = order[order2]
+        ks_ = key[idx]
+        first = torch.ones_like(ks_, dtype=torch.bool)
+        first[1:] = ks_[1:] != ks_[:-1]
+        idx = idx[first]
+        xA, yA, xB, yB, sc = xA[idx], yA[idx], xB[idx], yB[idx], sc[idx]
+    else:
+        xA, yA, xB, yB, sc, *_ = corr_to_matches(corr4d, invert_matching_direction=flip, **kw)
+        xA, yA, xB, yB, sc = (t.reshape(-1) for t in (xA, yA, xB, yB, sc))
+    # recentre to pixel centres (eval_inloc.py:180-189)
+    n1, n2, n3, n4 = fs1 * k, fs2 * k, fs3 * k, fs4 * k
+    yA = yA * (n1 - 1) / n1 + 0.5 / n1
+    xA = xA * (n2 - 1) / n2 + 0.5 / n2
+    yB = yB * (n3 - 1) / n3 + 0.5 / n3
+    xB = xB * (n4 - 1) / n4 + 0.5 / n4
+    return torch.stack((xA, yA, xB, yB, sc.float()), dim=1)
+
+
+def save_query(path: str, matches: np.ndarray, query_fn, pano_fns):
+    from scipy.io import savemat
+
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    tmp = path + ".tmp.mat"
+    savemat(tmp, {"matches": matches, "query_fn": query_fn, "pano_fn": pano_fns}, do_compression=True)
+    os.replace(tmp, path)
+
+
+def load_shortlist(path: str):
+    """ImgList struct array -> (query names, [pano name lists])."""
+    from scipy.io import loadmat
+
+    db = loadmat(path)["ImgList"][0, :]
+    queries = [str(np.asarray(db[q][0]).item()) for q in range(len(db))]
+    panos = [[str(np.asarray(p).item()) for p in np.asarray(db[q][1]).ravel()] for q in range(len(db))]
+    pano_all = np.vstack(tuple(np.asarray(db[q][1]) for q in range(len(db))))
+    return queries, panos, pano_all

@@ -1,0 +1,53 @@
+"""End-to-end CLI runs on CPU at tiny sizes (train -> checkpoint -> resume ->
+PF-Pascal eval -> InLoc export with the .mat contract)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+
+@pytest.fixture(scope="module")
+def workdir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("cli")
+    old = os.getcwd()
+    os.chdir(d)
+    yield d
+    os.chdir(old)
+
+
+def test_train_resume_eval(workdir):
+    import eval_pf_pascal
+    import train
+    train.main(["--synthetic", "4", "--batch_size", "2", "--image_size", "64", "--ncons_kernel_sizes", "3", "3",
+                "--ncons_channels", "16", "1", "--num_epochs", "1", "--result-model-dir", "models"])
+    cks = sorted(glob.glob("models/2*_checkpoint_adam.pth.tar"))
+    assert cks and os.path.exists(os.path.join("models", "best_" + os.path.basename(cks[0])))
+    from ncnet_amd.engine.checkpoint import load_checkpoint
+    ck = load_checkpoint(cks[0])
+    assert ck["epoch"] == 1 and ck["args"].ncons_channels == [16, 1]
+    assert set(ck) >= {"epoch", "args", "state_dict", "best_test_loss", "optimizer", "train_loss", "test_loss"}
+    train.main(["--synthetic", "4", "--batch_size", "2", "--image_size", "64", "--num_epochs", "2", "--resume", cks[0]])
+    ck2 = load_checkpoint(cks[0])
+    assert ck2["epoch"] == 2
+    stats = eval_pf_pascal.main(["--synthetic", "2", "--image_size", "64", "--checkpoint", cks[0]])
+    assert stats["point_tnf"]["pck"].shape == (2, 1)
+
+
+def test_inloc_export_contract(workdir):
+    import eval_inloc
+    from scipy.io import loadmat
+    out = eval_inloc.main(["--synthetic_queries", "1", "--n_panos", "2", "--image_size", "256", "--k_size", "2",
+                           "--output_dir", "m"])
+    assert os.path.basename(out) == "synthetic_shortlist_SZ_NEW_256_K_2_BOTHDIRS_SOFTMAX"
+    d = loadmat(os.path.join(out, "1.mat"))
+    m = d["matches"]
+    n = 2 * int(256 * 0.0625 / 2 * np.floor(256 * 0.0625 / 2 * 0.75))
+    assert m.shape == (1, 2, n, 5) and m.dtype == np.float64
+    used = m[0, 0, :, 4] > 0
+    xy = m[0, 0, used, :4]
+    assert (xy > 0).all() and (xy < 1).all()
+    # de-duplicated and in lexicographic (xA, yA, xB, yB) order like np.unique
+    rows = [tuple(r) for r in xy]
+    assert rows == sorted(set(rows))

@@ -1,0 +1,192 @@
+#!/usr/bin/env python
+"""Weakly-supervised NC-Net training (reference CLI: train.py:34-47).
+
+Same flags and defaults as the reference, plus:
+  --synthetic N        train on N random pairs instead of a CSV dataset
+  --num_workers W      data-loader workers per rank (reference: 0 train / 4 test)
+  --log_interval L     loss readback interval (reference: 1)
+  --resume PATH        real resume: weights + optimizer + epoch + RNG state
+  --max_steps S        stop after S training steps (smoke / profiling)
+  --metrics PATH       JSONL metrics (rank 0)
+  --dtype bf16|fp32    backbone compute dtype (NC path is always bf16 MFMA on GPU)
+
+Multi-GPU: launch with torchrun (one process per GPU); gradients are averaged
+with one bucketed RCCL all-reduce, every rank trains on its own shard.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader, Subset
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from ncnet_amd.data import ImagePairDataset, NormalizeImageDict, SyntheticPairDataset  # noqa: E402
+from ncnet_amd.engine.checkpoint import capture_rng, load_checkpoint, restore_rng, save_checkpoint  # noqa: E402
+from ncnet_amd.engine.trainer import Trainer  # noqa: E402
+from ncnet_amd.models import ImMatchNet  # noqa: E402
+from ncnet_amd.parallel.dist import barrier, broadcast_module, destroy, init_distributed, shard_indices  # noqa: E402
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="NC-Net training (MI355X)")
+    p.add_argument("--checkpoint", type=str, default="")
+    p.add_argument("--image_size", type=int, default=400)
+    p.add_argument("--dataset_image_path", type=str, default="datasets/pf-pascal/", help="path to PF Pascal dataset")
+    p.add_argument("--dataset_csv_path", type=str, default="datasets/pf-pascal/image_pairs/",
+                   help="path to PF Pascal training csv")
+    p.add_argument("--num_epochs", type=int, default=5, help="number of training epochs")
+    p.add_argument("--batch_size", type=int, default=16, help="training batch size (per GPU)")
+    p.add_argument("--lr", type=float, default=0.0005, help="learning rate")
+    p.add_argument("--ncons_kernel_sizes", nargs="+", type=int, default=[5, 5, 5], help="kernels sizes in neigh. cons.")
+    p.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 16, 1], help="channels in neigh. cons")
+    p.add_argument("--result_model_fn", type=str, default="checkpoint_adam", help="trained model filename")
+    p.add_argument("--result-model-dir", type=str, default="trained_models", help="path to trained models folder")
+    p.add_argument("--fe_finetune_params", type=int, default=0, help="number of layers to finetune")
+    # extensions
+    p.add_argument("--synthetic", type=int, default=0)
+    p.add_argument("--num_workers", type=int, default=0)
+    p.add_argument("--log_interval", type=int, default=1)
+    p.add_argument("--resume", type=str, default="")
+    p.add_argument("--max_steps", type=int, default=0)
+    p.add_argument("--metrics", type=str, default="")
+    p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--seed", type=int, default=1)
+    return p
+
+
+class _Shard(torch.utils.data.Sampler):
+    """Per-rank, per-epoch reshuffled shard (DistributedSampler semantics)."""
+
+    def __init__(self, n, ctx, shuffle=True, seed=1):
+        self.n, self.ctx, self.shuffle, self.seed, self.epoch = n, ctx, shuffle, seed, 0
+
+    def set_epoch(self, e):
+        self.epoch = e
+
+    def __iter__(self):
+        return iter(shard_indices(self.n, self.ctx, self.epoch, self.shuffle, self.seed, drop_last=self.ctx.world_size > 1))
+
+    def __len__(self):
+        return self.n // self.ctx.world_size if self.ctx.world_size > 1 else self.n
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    ctx = init_distributed()
+    torch.manual_seed(args.seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed(args.seed)
+    np.random.seed(args.seed)
+    if ctx.is_main:
+        print("ImMatchNet training script (ncnet_amd)")
+        print(args)
+
+    # --resume rebuilds the NC architecture from the checkpoint's args, like --checkpoint
+    model = ImMatchNet(use_cuda=ctx.device.type == "cuda", checkpoint=(args.resume or args.checkpoint) or None,
+                       ncons_kernel_sizes=args.ncons_kernel_sizes, ncons_channels=args.ncons_channels,
+                       dtype=args.dtype).to(ctx.device)
+    # the saved Namespace must describe the architecture actually built
+    args.ncons_kernel_sizes = list(model.NeighConsensus.kernel_sizes)
+    args.ncons_channels = list(model.NeighConsensus.channels)
+    if args.fe_finetune_params > 0:  # train.py:60-63
+        for i in range(args.fe_finetune_params):
+            for p in model.FeatureExtraction.model[-1][-(i + 1)].parameters():
+                p.requires_grad = True
+    broadcast_module(model, ctx)
+    params = [p for p in model.parameters() if p.requires_grad]
+    if ctx.is_main:
+        print("Trainable parameters:")
+        for i, p in enumerate(params):
+            print(f"{i + 1}: {tuple(p.shape)}")
+    optimizer = torch.optim.Adam(params, lr=args.lr)
+
+    size = (args.image_size, args.image_size)
+    if args.synthetic:
+        train_set = SyntheticPairDataset(args.synthetic, size, seed=1)
+        test_set = SyntheticPairDataset(max(2 * args.batch_size, args.synthetic // 8), size, seed=2)
+    else:
+        norm = NormalizeImageDict(["source_image", "target_image"])
+        train_set = ImagePairDataset(args.dataset_csv_path, "train_pairs.csv", args.dataset_image_path,
+                                     output_size=size, transform=norm)
+        test_set = ImagePairDataset(args.dataset_csv_path, "val_pairs.csv", args.dataset_image_path,
+                                    output_size=size, transform=norm)
+    tr_sampler = _Shard(len(train_set), ctx, True, args.seed)
+    te_sampler = _Shard(len(test_set), ctx, True, args.seed + 7)
+    pin = ctx.device.type == "cuda"
+    train_loader = DataLoader(train_set, batch_size=args.batch_size, sampler=tr_sampler, num_workers=args.num_workers,
+                              pin_memory=pin, drop_last=True)
+    test_loader = DataLoader(test_set, batch_size=args.batch_size, sampler=te_sampler, num_workers=args.num_workers,
+                             pin_memory=pin, drop_last=True)
+
+    checkpoint_name = os.path.join(args.result_model_dir,
+                                   datetime.datetime.now().strftime("%Y-%m-%d_%H:%M") + "_" + args.result_model_fn +
+                                   ".pth.tar")
+    train_loss = np.zeros(args.num_epochs)
+    test_loss = np.zeros(args.num_epochs)
+    best_test_loss = float("inf")
+    start_epoch = 1
+    if args.resume:
+        ck = load_checkpoint(args.resume)
+        optimizer.load_state_dict(ck["optimizer"])
+        start_epoch = int(ck["epoch"]) + 1
+        best_test_loss = float(ck.get("best_test_loss", best_test_loss))
+        n = min(len(train_loss), len(ck["train_loss"]))
+        train_loss[:n] = ck["train_loss"][:n]
+        test_loss[:n] = ck["test_loss"][:n]
+        restore_rng(ck.get("rng"))
+        checkpoint_name = args.resume
+        if ctx.is_main:
+            print(f"Resumed from {args.resume} at epoch {start_epoch}")
+    if ctx.is_main:
+        print("Checkpoint name: " + checkpoint_name)
+
+    trainer = Trainer(model, optimizer, ctx, metrics_path=args.metrics or None)
+    if args.max_steps:
+        # bounded run (smoke / profiling)
+        model.train()
+        t0 = time.perf_counter()
+        steps = 0
+        while steps < args.max_steps:
+            for batch in train_loader:
+                loss = trainer.train_step(trainer.to_device(batch))
+                steps += 1
+                if ctx.is_main and (steps % max(1, args.log_interval) == 0):
+                    print(f"step {steps} loss {float(loss):.6f}", flush=True)
+                if steps >= args.max_steps:
+                    break
+        if ctx.device.type == "cuda":
+            torch.cuda.synchronize()
+        if ctx.is_main:
+            dt = time.perf_counter() - t0
+            print(f"{steps} steps in {dt:.2f}s ({steps * args.batch_size * ctx.world_size / dt:.1f} pairs/s)")
+        destroy(ctx)
+        return
+
+    if ctx.is_main:
+        print("Starting training...")
+    for epoch in range(start_epoch, args.num_epochs + 1):
+        tr_sampler.set_epoch(epoch)
+        train_loss[epoch - 1] = trainer.process_epoch("train", epoch, train_loader, args.log_interval)
+        test_loss[epoch - 1] = trainer.process_epoch("test", epoch, test_loader, args.log_interval)
+        is_best = test_loss[epoch - 1] < best_test_loss
+        best_test_loss = min(test_loss[epoch - 1], best_test_loss)
+        if ctx.is_main:
+            save_checkpoint({"epoch": epoch, "args": args, "state_dict": model.state_dict(),
+                             "best_test_loss": best_test_loss, "optimizer": optimizer.state_dict(),
+                             "train_loss": train_loss, "test_loss": test_loss, "rng": capture_rng()},
+                            is_best, checkpoint_name)
+        barrier(ctx)
+    if ctx.is_main:
+        print("Done!")
+    destroy(ctx)
+
+
+if __name__ == "__main__":
+    main()
