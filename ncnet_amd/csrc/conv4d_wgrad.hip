@@ -193,6 +193,129 @@ __global__ __launch_bounds__(256, 2) void wgrad16_kernel(const bf16* __restrict_
 }
 
 // ===========================================================================
+// wgrad16v2: same math as wgrad16, restructured like conv16v2:
+//  * 8 waves = 4 tap groups x 2 halves of the voxel K-chunks; each half writes
+//    its own partial row (part is [2*ngroups, ...]), so no in-kernel reduction;
+//  * X plane rows and G tile rows arrive by LDS-DMA (global_load_lds_dwordx4),
+//    one wave-instruction per row (RS, TL <= 32 voxels): no staging VGPRs,
+//    ~60 VGPRs, three workgroups per CU share the latency;
+//  * halo / out-of-volume chunks are zeroed per item with ds_write.
+// ===========================================================================
+template <int KS>
+__global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restrict__ X, const bf16* __restrict__ G,
+                                                           float* __restrict__ part, float* __restrict__ partb,
+                                                           WGeom g) {
+  constexpr int P = KS / 2;
+  constexpr int NT = KS * KS;
+  constexpr int TPW = (NT + 3) / 4;   // taps per tap-group
+  constexpr int NW = 8;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nvox = g.TK * g.TL;
+  const int nv32 = (nvox + 31) & ~31;
+  const int plane_bytes = g.PR * g.RS * 32;
+  char* plane = smem;
+  char* gt = smem + plane_bytes;
+  int* voff = (int*)(gt + nv32 * 32);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tg = wave & 3, half = wave >> 2;
+  const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int NDD = g.dj_center ? KS : NT;
+  const int dd = lb % NDD, grp = lb / NDD;
+  const int di = g.dj_center ? dd : dd / KS, dj = g.dj_center ? P : dd % KS;
+  const bool center = (di == P && dj == P);
+
+  for (int o = threadIdx.x * 16; o < plane_bytes + nv32 * 32; o += NW * 64 * 16)
+    *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};   // tile padding voxels stay zero
+  for (int e = threadIdx.x; e < nv32; e += NW * 64) {
+    int kk = e / g.TL, ll = e - kk * g.TL;
+    voff[e] = (e < nvox) ? (kk * g.RS + ll) * 32 : 0;
+  }
+
+  uint32_t toffw[TPW];
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) {
+    int tap = min(tg + 4 * tt, NT - 1);
+    int dk = tap / KS, dl = tap - dk * KS;
+    toffw[tt] = (uint32_t)((dk * g.RS + dl) * 32);
+  }
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ones[q] = f2bf(1.f);
+
+  const int it_lo = grp * g.ipg, it_hi = min(g.nitems, it_lo + g.ipg);
+  const int nchunk = nv32 >> 5;
+  const int c_lo = half ? (nchunk + 1) / 2 : 0, c_hi = half ? nchunk : (nchunk + 1) / 2;
+  const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+
+  __syncthreads();  // zero fill done before any DMA lands
+  for (int it = it_lo; it < it_hi; ++it) {
+    const Item r = decode_item(g, it);
+    const int ii = r.i + di - P, jj = r.j + dj - P;
+    if (ii < 0 || ii >= g.I || jj < 0 || jj >= g.J) continue;   // uniform over the block
+    // Stage X plane rows (corner (k0-P, l0-P)) and G tile rows (corner (k0, l0)):
+    // in-volume 16-byte chunks by LDS-DMA, everything else of the row zeroed
+    // with ds_write (tile positions differ per item, so no stale halo survives).
+    const bf16* xp = X + plane_off(g, r.v, ii, jj, 16);
+    const bf16* gp = G + plane_off(g, r.v, r.i, r.j, 16);
+    {
+      const int ls = max(0, r.l0 - P), le = min(g.L, r.l0 - P + g.RS);
+      const int c0 = 2 * (ls - (r.l0 - P)), c1 = c0 + 2 * (le - ls);
+      for (int row = wave; row < g.PR; row += NW) {
+        const int kg = r.k0 - P + row;
+        const bool in_k = kg >= 0 && kg < g.K;
+        if (in_k) {
+          if (lane < c1 - c0)
+            __builtin_amdgcn_global_load_lds((const void*)(xp + ((size_t)kg * g.L + ls) * 16 + lane * 8),
+                                             LDS_PTR(void, plane + row * g.RS * 32 + c0 * 16), 16, 0, 0);
+        }
+        if (lane < 2 * g.RS && (!in_k || lane < c0 || lane >= c1))
+          *(u32x4*)(plane + row * g.RS * 32 + lane * 16) = u32x4{0u, 0u, 0u, 0u};
+      }
+      const int tl = min(g.TL, g.L - r.l0), tk = min(g.TK, g.K - r.k0);
+      for (int row = wave; row < g.TK; row += NW) {
+        if (row < tk && lane < 2 * tl)
+          __builtin_amdgcn_global_load_lds((const void*)(gp + ((size_t)(r.k0 + row) * g.L + r.l0) * 16 + lane * 8),
+                                           LDS_PTR(void, gt + row * g.TL * 32), 16, 0, 0);
+        else if (lane < 2 * g.TL)
+          *(u32x4*)(gt + row * g.TL * 32 + lane * 16) = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+    __syncthreads();  // vmcnt(0) + barrier: plane and tile landed
+    for (int c = c_lo; c < c_hi; ++c) {
+      const int vb0 = c * 32 + gq * 8 + qq, vb1 = vb0 + 4;
+      bf16x8 bfr = cat8(lds_read_tr16(gt, vb0 * 32 + pp * 8), lds_read_tr16(gt, vb1 * 32 + pp * 8));
+      const uint32_t pa0 = voff[vb0] + pp * 8, pa1 = voff[vb1] + pp * 8;
+#pragma unroll
+      for (int tt = 0; tt < TPW; ++tt) {
+        if (tg + 4 * tt < NT) {
+          bf16x8 afr = cat8(lds_read_tr16(plane, pa0 + toffw[tt]), lds_read_tr16(plane, pa1 + toffw[tt]));
+          acc[tt] = mfma16(afr, bfr, acc[tt]);
+        }
+      }
+      if (center && tg == 0) accb = mfma16(ones, bfr, accb);
+    }
+    __syncthreads();  // all reads done before the next DMA overwrites
+  }
+
+  float* pout = part + ((size_t)(grp * 2 + half) * NDD + dd) * NT * 256;
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) {
+    int tap = tg + 4 * tt;
+    if (tap < NT) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pout[tap * 256 + (4 * (lane >> 4) + r) * 16 + (lane & 15)] = acc[tt][r];
+    }
+  }
+  if (center && tg == 0 && lane < 16) partb[(grp * 2 + half) * 16 + lane] = accb[0];
+}
+
+// ===========================================================================
 struct W1Geom {
   WGeom w;
   int mode;                 // 0: S = G (16ch tile), P = X (1ch plane); 1: S = X (16ch plane), P = G (1ch tile)
@@ -386,18 +509,29 @@ static WGeom make_wgeom(int V, int I, int J, int K, int L, int KS, int ngroups) 
   return g;
 }
 
-// part: [ngroups][KS*KS (or KS when dj_center)][KS*KS][16 ci][16 co] fp32; partb: [ngroups][16]
+// part: [R][KS*KS (or KS when dj_center)][KS*KS][16 ci][16 co] fp32; partb: [R][16]
+// R = ngroups (variant 1) or 2 * ngroups (variant 2: one row per voxel-chunk half).
 extern "C" int ncnet_wgrad16(const void* X, const void* G, float* part, float* partb, int V, int I, int J, int K,
-                             int L, int KS, int ngroups, int dj_center, hipStream_t stream) {
+                             int L, int KS, int ngroups, int dj_center, int variant, hipStream_t stream) {
   WGeom g = make_wgeom(V, I, J, K, L, KS, ngroups);
   g.dj_center = dj_center;
-  if (g.PR * g.RS * 2 > 8 * 256) return -1;
   int nv32 = (g.TK * g.TL + 31) & ~31;
-  if (nv32 * 2 > 5 * 256) return -1;
   size_t lds = (size_t)g.PR * g.RS * 32 + (size_t)nv32 * 32 + (size_t)nv32 * 4;
-  dim3 grid((unsigned)((dj_center ? KS : KS * KS) * ngroups)), block(256);
-  if (KS == 5) hipLaunchKernelGGL((wgrad16_kernel<5>), grid, block, lds, stream, (const bf16*)X, (const bf16*)G, part, partb, g);
-  else if (KS == 3) hipLaunchKernelGGL((wgrad16_kernel<3>), grid, block, lds, stream, (const bf16*)X, (const bf16*)G, part, partb, g);
+  dim3 grid((unsigned)((dj_center ? KS : KS * KS) * ngroups));
+  const bf16* x = (const bf16*)X; const bf16* gg = (const bf16*)G;
+  if (variant == 2) {
+    if (g.RS > 32 || g.TL > 32) return -1;   // one wave-instruction per staged row
+    dim3 block(512);
+    if (KS == 5) hipLaunchKernelGGL((wgrad16v2_kernel<5>), grid, block, lds, stream, x, gg, part, partb, g);
+    else if (KS == 3) hipLaunchKernelGGL((wgrad16v2_kernel<3>), grid, block, lds, stream, x, gg, part, partb, g);
+    else return -2;
+    return (int)hipGetLastError();
+  }
+  if (g.PR * g.RS * 2 > 8 * 256) return -1;
+  if (nv32 * 2 > 5 * 256) return -1;
+  dim3 block(256);
+  if (KS == 5) hipLaunchKernelGGL((wgrad16_kernel<5>), grid, block, lds, stream, x, gg, part, partb, g);
+  else if (KS == 3) hipLaunchKernelGGL((wgrad16_kernel<3>), grid, block, lds, stream, x, gg, part, partb, g);
   else return -2;
   return (int)hipGetLastError();
 }

@@ -237,3 +237,76 @@ def fold_frozen_bn(trunk: nn.Module) -> nn.Module:
 
     walk(t)
     return t
+
+
+class FrozenResNetPlan(nn.Module):
+    """Inference plan of a frozen (BN-folded) ResNet trunk in one compute dtype.
+
+    Built once from ``fold_frozen_bn(trunk)``: every conv weight is cast to
+    ``dtype`` and laid out channels-last up front, so a training step issues no
+    per-step weight casts (autocast re-casts ~100 fp32 weights per forward);
+    epilogues (ReLU, residual add) run in place.  MIOpen's fused
+    conv+ReLU / conv+add+ReLU entry points were measured 40x slower for bf16
+    channels-last on MI355X (no fused solver; naive fallback), so they are
+    not used.  Reference: the frozen trunk of lib/model.py:37-44.
+    """
+
+    def __init__(self, folded: nn.Sequential, dtype: torch.dtype = torch.bfloat16):
+        super().__init__()
+        self.dtype = dtype
+        self.steps = []  # (kind, params)
+        convs = []
+
+        def conv_params(c: nn.Conv2d):
+            w = c.weight.detach().to(dtype).contiguous(memory_format=torch.channels_last)
+            b = c.bias.detach().to(dtype) if c.bias is not None else None
+            convs.append(w)
+            return (w, b, c.stride, c.padding)
+
+        mods = list(folded.children())
+        idx = 0
+        while idx < len(mods):
+            m = mods[idx]
+            if isinstance(m, nn.Conv2d):
+                relu = idx + 1 < len(mods) and any(isinstance(n, nn.ReLU) for n in mods[idx + 1: idx + 3])
+                self.steps.append(("conv_relu" if relu else "conv", conv_params(m)))
+            elif isinstance(m, nn.MaxPool2d):
+                self.steps.append(("maxpool", (m.kernel_size, m.stride, m.padding)))
+            elif isinstance(m, nn.Sequential):
+                for blk in m:
+                    if not isinstance(blk, Bottleneck):
+                        raise TypeError("FrozenResNetPlan expects Bottleneck layers")
+                    down = conv_params(blk.downsample[0]) if blk.downsample is not None else None
+                    self.steps.append(("bottleneck", (conv_params(blk.conv1), conv_params(blk.conv2),
+                                                      conv_params(blk.conv3), down)))
+            elif isinstance(m, (nn.ReLU, nn.Identity)):
+                pass
+            else:
+                raise TypeError(f"FrozenResNetPlan: unsupported module {type(m).__name__}")
+            idx += 1
+        self._keep = convs  # keep tensors referenced
+
+    def _conv(self, x, p, relu: bool, z=None):
+        w, b, stride, pad = p
+        y = F.conv2d(x, w, b, stride, pad)
+        if z is not None:
+            y.add_(z)
+        return y.relu_() if (relu or z is not None) else y
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = x.to(self.dtype).contiguous(memory_format=torch.channels_last)
+        for kind, p in self.steps:
+            if kind == "conv_relu":
+                x = self._conv(x, p, True)
+            elif kind == "conv":
+                x = self._conv(x, p, False)
+            elif kind == "maxpool":
+                x = F.max_pool2d(x, *p)
+            else:
+                c1, c2, c3, down = p
+                idt = x if down is None else self._conv(x, down, False)
+                y = self._conv(x, c1, True)
+                y = self._conv(y, c2, True)
+                x = self._conv(y, c3, True, z=idt)
+        return x

@@ -14,6 +14,7 @@ Compute policy (MI355X):
 """
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 
 import torch
@@ -25,7 +26,10 @@ from ..ops.conv4d import Conv4d
 from ..ops.correlation import correlation, correlation_pool2, l2norm_pack, maxpool4d as _maxpool4d
 from ..ops.mutual import mutual_matching
 from ..ops.neigh_consensus import neigh_consensus
-from .backbones import build_trunk, fold_frozen_bn
+from .backbones import FrozenResNetPlan, build_trunk, fold_frozen_bn
+
+# Frozen bf16 trunk: pre-cast execution plan (default) or autocast (NCNET_TRUNK_PLAN=0).
+_TRUNK_PLAN = os.environ.get("NCNET_TRUNK_PLAN", "1") != "0"
 
 
 def featureL2Norm(feature: torch.Tensor) -> torch.Tensor:  # noqa: N802 (reference name)
@@ -69,6 +73,8 @@ class FeatureExtraction(nn.Module):
         if x.is_cuda:
             x = x.contiguous(memory_format=torch.channels_last)
         if frozen and not self.training and x.is_cuda and self.feature_extraction_cnn.startswith("resnet"):
+            if dtype in (torch.bfloat16, torch.float16) and _TRUNK_PLAN:
+                return self._plan(dtype)(x)
             net = self._folded_trunk()
         else:
             net = self.model
@@ -83,6 +89,14 @@ class FeatureExtraction(nn.Module):
             self._folded = fold_frozen_bn(self.model).to(memory_format=torch.channels_last)
             self._folded_version = ver
         return self._folded
+
+    def _plan(self, dtype):
+        ver = sum(p._version for p in self.model.parameters()) + sum(b._version for b in self.model.buffers())
+        key = (ver, dtype, _TRUNK_PLAN)
+        if getattr(self, "_plan_key", None) != key:
+            self._plan_obj = FrozenResNetPlan(self._folded_trunk(), dtype)
+            self._plan_key = key
+        return self._plan_obj
 
     def forward(self, image_batch: torch.Tensor) -> torch.Tensor:
         features = self.trunk_forward(image_batch)

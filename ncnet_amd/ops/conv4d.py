@@ -21,7 +21,7 @@ import torch.nn as nn
 
 from . import _ext
 from . import reference as ref
-from .neigh_consensus import _reduce_wgrad1, _reduce_wgrad16, wgrad_groups
+from .neigh_consensus import _reduce_wgrad1, _reduce_wgrad16, wgrad16_partials, wgrad_groups
 from .packing import pack_w16, pack_w1in, pack_w1out, transpose_for_dgrad
 
 
@@ -102,10 +102,8 @@ class Conv4dFn(torch.autograd.Function):
                 C.wgrad1(xcl, gcl, part, ks, 1, ng)
                 dw = _reduce_wgrad1(part, ks, 1, cin)
             else:
-                part = torch.empty((ng, ks * ks, ks * ks, 16, 16), dtype=torch.float32, device=g.device)
-                partb = torch.empty((ng, 16), dtype=torch.float32, device=g.device)
-                C.wgrad16(xcl, gcl, part, partb, ks, ng, 0)
-                dw = _reduce_wgrad16(part, ks, cout, cin)
+                sw, _ = wgrad16_partials(C, xcl, gcl, ks, ng, False)
+                dw = _reduce_wgrad16(sw, ks, cout, cin)
             gw = ref.conv4d_weight_from_std(dw).to(w_ref.dtype)
         if has_bias and ctx.needs_input_grad[2]:
             gb = g.float().sum(dim=(0, 2, 3, 4, 5))

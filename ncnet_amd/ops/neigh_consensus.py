@@ -34,6 +34,8 @@ HIP_KS = (3, 5)
 import os as _os
 
 USE_JC = _os.environ.get("NCNET_NC_JC", "1") == "1"
+# wgrad16 kernel: 2 = 8-wave LDS-DMA kernel (default), 1 = 4-wave register-staged
+WGRAD_VARIANT = int(_os.environ.get("NCNET_WGRAD_VARIANT", "2"))
 
 
 def layer_kinds(channels, kernel_sizes):
@@ -117,22 +119,29 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
     return h
 
 
-def _reduce_wgrad16(part: torch.Tensor, ks: int, cout: int, cin: int) -> torch.Tensor:
-    # part [G, dd, tap, ci, co] -> std [co, ci, di, dj, dk, dl]
-    s = part.sum(0).permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks, ks)
-    return s[:cout, :cin]
+def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, ng: int, dj_center: bool):
+    """Run the wgrad16 kernel and reduce its per-group partials.
+
+    Returns (s, sb): s [dd, tap, ci, co] with dd = (di, dj) or di only when
+    ``dj_center``, sb [16] = sum of g16 over all voxels (bias gradient, from
+    the kernel's ones-MFMA in the centre block).  Variant 2 (default, 8-wave
+    LDS-DMA kernel) writes two partial rows per group.
+    """
+    rows = ng * (2 if WGRAD_VARIANT == 2 else 1)
+    part = torch.empty((rows, ks if dj_center else ks * ks, ks * ks, 16, 16), dtype=torch.float32, device=x16.device)
+    partb = torch.empty((rows, 16), dtype=torch.float32, device=x16.device)
+    C.wgrad16(x16, g16, part, partb, ks, 1 if dj_center else 0, WGRAD_VARIANT)
+    return part.sum(0), partb.sum(0)
 
 
-def _reduce_wgrad16_center(part: torch.Tensor, ks: int) -> torch.Tensor:
-    # part [G, di, tap, ci, co] (dj = P only) -> [co, ci, di, dk, dl]
-    return part.sum(0).permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks)
+def _reduce_wgrad16(s: torch.Tensor, ks: int, cout: int, cin: int) -> torch.Tensor:
+    # s [dd, tap, ci, co] -> std [co, ci, di, dj, dk, dl]
+    return s.permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks, ks)[:cout, :cin]
 
 
-def _wgrad16_center(C, x16, g16, ks, ng) -> torch.Tensor:
-    part = torch.empty((ng, ks, ks * ks, 16, 16), dtype=torch.float32, device=x16.device)
-    partb = torch.empty((ng, 16), dtype=torch.float32, device=x16.device)
-    C.wgrad16(x16, g16, part, partb, ks, ng, 1)
-    return _reduce_wgrad16_center(part, ks)
+def _reduce_wgrad16_center(s: torch.Tensor, ks: int) -> torch.Tensor:
+    # s [di, tap, ci, co] (dj = P only) -> [co, ci, di, dk, dl]
+    return s.permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks)
 
 
 def _reduce_wgrad1(part: torch.Tensor, ks: int, mode: int, c16: int) -> torch.Tensor:
@@ -165,8 +174,9 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
         if kind == "1out" and USE_JC:
             gs = torch.empty(tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
             C.jpack(g, gs, ks, -1)                   # adjoint of jsum
-            dw = jc_out_grad(_wgrad16_center(C, h, gs, ks, ng), cin)
-            db = g.float().sum().reshape(1)
+            sw, sb = wgrad16_partials(C, h, gs, ks, ng, True)
+            dw = jc_out_grad(_reduce_wgrad16_center(sw, ks), cin)
+            db = sb[ks // 2].reshape(1)              # channel P of jpack(g, -1) is g itself
             if li > 0 or need_dx0:
                 gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
                 wt = transpose_for_dgrad(jc_out_weights(w))
@@ -174,8 +184,9 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
                 g = gi
             del gs
         elif kind == "1in" and USE_JC:               # h is jpack(X0) (16ch)
-            dw = jc_in_grad(_wgrad16_center(C, h, g, ks, ng), cout)
-            db = g.float().sum(dim=(0, 1, 2, 3, 4))[:cout]
+            sw, sb = wgrad16_partials(C, h, g, ks, ng, True)
+            dw = jc_in_grad(_reduce_wgrad16_center(sw, ks), cout)
+            db = sb[:cout]
             if li > 0:
                 raise RuntimeError("internal: 1in layer must be first")
             if need_dx0:
@@ -197,11 +208,9 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
                 C.conv1in_fwd(g, pack_w1in(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0)
                 g = gi
         elif kind == "16":
-            part = torch.empty((ng, ks * ks, ks * ks, 16, 16), dtype=torch.float32, device=h.device)
-            partb = torch.empty((ng, 16), dtype=torch.float32, device=h.device)
-            C.wgrad16(h, g, part, partb, ks, ng, 0)
-            dw = _reduce_wgrad16(part, ks, cout, cin)
-            db = partb.sum(0)[:cout]
+            sw, sb = wgrad16_partials(C, h, g, ks, ng, False)
+            dw = _reduce_wgrad16(sw, ks, cout, cin)
+            db = sb[:cout]
             if li > 0 or need_dx0:
                 gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
                 wt = transpose_for_dgrad(w)

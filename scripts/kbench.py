@@ -60,10 +60,10 @@ def main():
     w1i = pack_w1in(torch.randn(16, 1, ks, ks, ks, ks, device=dev) * 0.05)
     w1o = pack_w1out(torch.randn(1, 16, ks, ks, ks, ks, device=dev) * 0.05)
     ng = a.groups or wgrad_groups(ks, V * S * S)
-    part16 = torch.empty((ng, ks * ks, ks * ks, 16, 16), device=dev)
-    partb = torch.empty((ng, 16), device=dev)
+    part16 = torch.empty((2 * ng, ks * ks, ks * ks, 16, 16), device=dev)
+    partb = torch.empty((2 * ng, 16), device=dev)
     part1 = torch.empty((ng, ks * ks, ks * ks, 16), device=dev)
-    part16c = torch.empty((ng, ks, ks * ks, 16, 16), device=dev)
+    part16c = torch.empty((2 * ng, ks, ks * ks, 16, 16), device=dev)
     z8 = torch.empty(shp + (8,), device=dev)
     g16b = torch.empty_like(g16)
     taps = ks ** 4
@@ -78,8 +78,10 @@ def main():
         "conv1in_fwd": (lambda: C.conv1in_fwd(x1, w1i, b16, None, y16, ks, 1), fl1),
         "conv1in_dgrad_mask": (lambda: C.conv1in_fwd(g1, w1i, None, x16, y16, ks, 2), fl1),
         "conv1out_fwd": (lambda: C.conv1out_fwd(x16, w1o, b1, y1, ks, 1), fl1),
-        "wgrad16": (lambda: C.wgrad16(x16, g16, part16, partb, ks, ng, 0), fl16),
-        "wgrad16_center": (lambda: C.wgrad16(x16, g16, part16c, partb, ks, ng, 1), fl16 / ks),
+        "wgrad16": (lambda: C.wgrad16(x16, g16, part16[:ng], partb[:ng], ks, 0, 1), fl16),
+        "wgrad16_center": (lambda: C.wgrad16(x16, g16, part16c[:ng], partb[:ng], ks, 1, 1), fl16 / ks),
+        "wgrad16v2": (lambda: C.wgrad16(x16, g16, part16, partb, ks, 0, 2), fl16),
+        "wgrad16v2_center": (lambda: C.wgrad16(x16, g16, part16c, partb, ks, 1, 2), fl16 / ks),
         "wgrad1_mode0": (lambda: C.wgrad1(g16, x1, part1, ks, 0, ng), fl1),
         "wgrad1_mode1": (lambda: C.wgrad1(x16, g1, part1, ks, 1, ng), fl1),
     }

@@ -188,3 +188,21 @@ def test_fold_frozen_bn_equivalence():
     x = torch.randn(1, 3, 64, 64)
     with torch.no_grad():
         assert torch.allclose(t(x), f(x), rtol=1e-4, atol=1e-4)
+
+
+def test_frozen_resnet_plan_equivalence():
+    """Pre-cast execution plan of the folded trunk == eager trunk (fp32, CPU)."""
+    from ncnet_amd.models.backbones import FrozenResNetPlan, fold_frozen_bn, resnet_trunk
+    torch.manual_seed(0)
+    t = resnet_trunk("resnet101", "layer3").eval()
+    for m in t.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.5, 1.5)
+            m.weight.data.uniform_(0.5, 1.5)
+    plan = FrozenResNetPlan(fold_frozen_bn(t), torch.float32)
+    x = torch.randn(1, 3, 80, 64)
+    with torch.no_grad():
+        r, p = t(x), plan(x)
+    assert p.shape == r.shape
+    assert ((p - r).norm() / r.norm()).item() < 1e-5

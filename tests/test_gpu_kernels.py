@@ -240,3 +240,33 @@ def test_immatchnet_volumes_and_grads_match_reference_algorithm():
     # MutualMatching route their gradient to different elements, so the end-to-end
     # gradient agrees to ~10-20% here; every op is pinned tightly by its own test.
     assert max(errs) < 0.3, errs
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("ks,shape", [(5, (2, 6, 5, 25, 25)), (5, (1, 5, 4, 30, 27)), (3, (1, 4, 5, 9, 33))])
+def test_wgrad16_kernel(variant, ks, shape, monkeypatch):
+    """Weight / bias gradient of a 16->16 Conv4d straight from the wgrad16
+    kernel (both variants; multi-tile K, L exercise the per-item halo), full
+    and dj-centre modes, vs autograd of the fp64 oracle."""
+    import importlib
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    monkeypatch.setattr(nc, "WGRAD_VARIANT", variant)
+    C = _ext.ext()
+    torch.manual_seed(11)
+    V, I, J, K, L = shape
+    x = torch.rand(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
+    g = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
+    xr = x.double().permute(0, 5, 1, 2, 3, 4)
+    wr = torch.zeros(ks, 16, 16, ks, ks, ks, device=DEV, dtype=torch.float64, requires_grad=True)
+    yr = ref.conv4d(xr, wr, None)
+    (yr * g.double().permute(0, 5, 1, 2, 3, 4)).sum().backward()
+    dstd = ref.conv4d_weight_to_std(wr.grad)           # [co, ci, di, dj, dk, dl]
+    ng = nc.wgrad_groups(ks, V * I * J * ((K + 24) // 25) * ((L + 24) // 25))
+    s, sb = nc.wgrad16_partials(C, x, g, ks, ng, False)
+    dw = nc._reduce_wgrad16(s, ks, 16, 16)
+    assert relerr(dw, dstd) < 1e-3
+    assert relerr(sb, g.double().sum(dim=(0, 1, 2, 3, 4))) < 1e-3
+    sc, sbc = nc.wgrad16_partials(C, x, g, ks, ng, True)
+    dwc = nc._reduce_wgrad16_center(sc, ks)            # [co, ci, di, dk, dl]
+    assert relerr(dwc, dstd[:, :, :, ks // 2]) < 1e-3
+    assert relerr(sbc, sb) < 1e-5
