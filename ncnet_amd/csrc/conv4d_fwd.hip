@@ -32,6 +32,7 @@ struct ConvGeom {
   int TK, TL;         // output tile along k, l
   int nkt, nlt;       // tiles along k, l
   int PR, RS;         // staged plane rows / row stride (voxels)
+  int RW;             // staged row width (voxels, <= RS)
   int dj_center;      // 1: only the dj = P planes (j-offset encoded in channels)
 };
 
@@ -250,13 +251,19 @@ __global__ __launch_bounds__(256, 2) void conv16_fwd_kernel(const bf16* __restri
 //  * 8 waves per workgroup, 5 voxel tiles per wave (20 accumulator VGPRs);
 //  * planes and weights arrive by LDS-DMA (global_load_lds_dwordx4): one
 //    wave-instruction per plane row (<= 32 voxels = 1 KiB), no staging VGPRs;
-//  * two LDS buffers: plane s+1 streams in while plane s is computed, one
-//    barrier per plane.  Halo/out-of-volume voxels are zeroed once (they are
-//    at fixed positions for the workgroup's tile) and never written again.
-// Requires RS = TL + KS - 1 <= 32.
+//  * plane rows at stride RS = TL + 8 voxels: a 16-voxel tile that wraps to
+//    the next row jumps a whole 256-B bank period, so the ds_read_b128 lane
+//    groups stay conflict-free;
+//  * two plane buffers (plane s+1 streams in while plane s is computed) and
+//    ONE weight buffer: the weights of plane s go to registers at the top of
+//    the plane, a mid-plane s_barrier (no vmcnt drain, so the plane DMA keeps
+//    flying) releases the buffer and plane s+1's weights stream in behind the
+//    remaining tiles.  2 x 30.6 KB + 13 KB keeps two workgroups per CU.
+//  * halo/out-of-volume voxels are zeroed once (fixed positions for the tile).
+// Requires RW = TL + KS - 1 <= 32.
 // ===========================================================================
 template <int KS, int EPI>
-__global__ __launch_bounds__(512, 1) void conv16v2_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
+__global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
                                                               const float* __restrict__ bias,
                                                               const bf16* __restrict__ M, bf16* __restrict__ Y,
                                                               ConvGeom g) {
@@ -268,7 +275,7 @@ __global__ __launch_bounds__(512, 1) void conv16v2_fwd_kernel(const bf16* __rest
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int plane_bytes = g.PR * g.RS * 32;
-  const int buf_bytes = plane_bytes + NQ * 1024;
+  char* wbuf = smem + 2 * plane_bytes;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const TileId t = decode_tile(g);
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(512, 1) void conv16v2_fwd_kernel(const bf16* __rest
   const int nvox = g.TK * g.TL;
   const int ntile = (nvox + 15) >> 4;
 
-  for (int o = threadIdx.x * 16; o < 2 * buf_bytes; o += NW * 64 * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
+  for (int o = threadIdx.x * 16; o < 2 * plane_bytes; o += NW * 64 * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
 
   uint32_t vbase[MAXT];
 #pragma unroll
@@ -302,11 +309,11 @@ __global__ __launch_bounds__(512, 1) void conv16v2_fwd_kernel(const bf16* __rest
   for (int tt = 0; tt < MAXT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // in-volume column span of the staged rows (same for every plane)
-  const int lstart = max(0, t.l0 - P), lend = min(g.L, t.l0 - P + g.RS);
+  const int lstart = max(0, t.l0 - P), lend = min(g.L, t.l0 - P + g.RW);
   const int nchunk = 2 * (lend - lstart);
   const int col0 = lstart - (t.l0 - P);
 
-  auto issue = [&](int s, char* buf) {
+  auto issue_x = [&](int s, char* buf) {
     const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
     const bf16* xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
     for (int r = wave; r < g.PR; r += NW) {
@@ -316,20 +323,27 @@ __global__ __launch_bounds__(512, 1) void conv16v2_fwd_kernel(const bf16* __rest
         __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(void, buf + (r * g.RS + col0) * 32), 16, 0, 0);
       }
     }
+  };
+  auto issue_w = [&](int s) {
+    const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
     const u32x4* wp = Wp + (size_t)(di * KS + dj) * (NQ * 64);
     for (int q = wave; q < NQ; q += NW)
-      __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, buf + plane_bytes + q * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + q * 1024), 16, 0, 0);
   };
 
   __syncthreads();  // zero-fill complete before any DMA lands
-  if (nplanes > 0) issue(0, smem);
+  if (nplanes > 0) { issue_x(0, smem); issue_w(0); }
   for (int s = 0; s < nplanes; ++s) {
-    __syncthreads();  // drains this wave's DMA (vmcnt 0) and orders every wave's plane s
-    char* cur = smem + (s & 1) * buf_bytes;
-    if (s + 1 < nplanes) issue(s + 1, smem + ((s + 1) & 1) * buf_bytes);
+    __syncthreads();  // drains this wave's DMA (vmcnt 0) and orders every wave's plane s + weights s
+    char* cur = smem + (s & 1) * plane_bytes;
+    if (s + 1 < nplanes) issue_x(s + 1, smem + ((s + 1) & 1) * plane_bytes);
     bf16x8 wf[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) wf[q] = lds_read16(cur + plane_bytes, (q * 64 + lane) * 16);
+    for (int q = 0; q < NQ; ++q) wf[q] = lds_read16(wbuf, (q * 64 + lane) * 16);
+    // weights in registers in every wave -> release the weight buffer without
+    // draining the in-flight plane DMA (plain s_barrier, LDS counter only)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (s + 1 < nplanes) issue_w(s + 1);
 #pragma unroll
     for (int tt = 0; tt < MAXT; ++tt) {
       if (wave + NW * tt < ntile) {
@@ -645,6 +659,7 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.nkt = cdiv(K, tk); g.nlt = cdiv(L, tl);
   g.PR = tk + KS - 1 + extra_rows;
   g.RS = tl + KS - 1 + extra_cols;
+  g.RW = g.RS;
   g.dj_center = 0;
   return g;
 }
@@ -680,10 +695,14 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
   if (g.PR * g.RS * 2 > 8 * 256) return -1;
   int nq = (KS * KS + 1) / 2;
   const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
-  if (conv16_variant() == 2 && g.RS <= 32) {
-    size_t buf = (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
+  if (conv16_variant() == 2 && g.RW <= 32) {
+    // Row stride RS = TL + 8: a 16-voxel tile that wraps to the next row then
+    // jumps 256 B (the full 64-bank period), so every ds_read_b128 lane group
+    // stays conflict-free (a TL + KS - 1 stride cost ~1/3 extra LDS cycles).
+    g.RS = tl + ((KS - 1 + 7) / 8) * 8;
+    size_t lds2 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
     dim3 grid2((unsigned)(V * I * J * g.nkt * g.nlt)), block2(512);
-#define L16V2(KSV, EPIV) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV>), grid2, block2, 2 * buf, stream, x, w, bias, m, y, g)
+#define L16V2(KSV, EPIV) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV>), grid2, block2, lds2, stream, x, w, bias, m, y, g)
     if (KS == 5) {
       if (epi == EPI_BIAS_RELU) L16V2(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2(5, EPI_MASK);
       else if (epi == EPI_F32) L16V2(5, EPI_F32); else L16V2(5, EPI_NONE);

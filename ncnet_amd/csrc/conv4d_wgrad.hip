@@ -26,7 +26,8 @@ namespace ncnet {
 struct WGeom {
   int V, I, J, K, L;
   int TK, TL, nkt, nlt;
-  int PR, RS;          // staged X plane (wgrad16)
+  int PR, RS;          // staged X plane rows / row stride (wgrad16)
+  int RW;              // staged row width (voxels, <= RS)
   int nitems, ipg;     // output tiles, tiles per group
   int dj_center;       // 1: only the (di, dj = P) offsets (j-offset encoded in channels)
 };
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
   const int plane_bytes = g.PR * g.RS * 32;
   char* plane = smem;
   char* gt = smem + plane_bytes;
-  int* voff = (int*)(gt + nv32 * 32);
+  uint16_t* voff = (uint16_t*)(gt + nv32 * 32);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tg = wave & 3, half = wave >> 2;
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
     *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};   // tile padding voxels stay zero
   for (int e = threadIdx.x; e < nv32; e += NW * 64) {
     int kk = e / g.TL, ll = e - kk * g.TL;
-    voff[e] = (e < nvox) ? (kk * g.RS + ll) * 32 : 0;
+    voff[e] = (uint16_t)((e < nvox) ? (kk * g.RS + ll) * 32 : 0);
   }
 
   uint32_t toffw[TPW];
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
     const bf16* xp = X + plane_off(g, r.v, ii, jj, 16);
     const bf16* gp = G + plane_off(g, r.v, r.i, r.j, 16);
     {
-      const int ls = max(0, r.l0 - P), le = min(g.L, r.l0 - P + g.RS);
+      const int ls = max(0, r.l0 - P), le = min(g.L, r.l0 - P + g.RW);
       const int c0 = 2 * (ls - (r.l0 - P)), c1 = c0 + 2 * (le - ls);
       for (int row = wave; row < g.PR; row += NW) {
         const int kg = r.k0 - P + row;
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
             __builtin_amdgcn_global_load_lds((const void*)(xp + ((size_t)kg * g.L + ls) * 16 + lane * 8),
                                              LDS_PTR(void, plane + row * g.RS * 32 + c0 * 16), 16, 0, 0);
         }
-        if (lane < 2 * g.RS && (!in_k || lane < c0 || lane >= c1))
+        if (lane < 2 * g.RW && (!in_k || lane < c0 || lane >= c1))
           *(u32x4*)(plane + row * g.RS * 32 + lane * 16) = u32x4{0u, 0u, 0u, 0u};
       }
       const int tl = min(g.TL, g.L - r.l0), tk = min(g.TK, g.K - r.k0);
@@ -288,7 +289,9 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
     }
     __syncthreads();  // vmcnt(0) + barrier: plane and tile landed
     for (int c = c_lo; c < c_hi; ++c) {
-      const int vb0 = c * 32 + gq * 8 + qq, vb1 = vb0 + 4;
+      // k-slot -> voxel: each 32-lane half of a tr-read covers 8 consecutive
+      // voxels (256 B, all 64 banks once); A and B use the same permutation.
+      const int vb0 = c * 32 + gq * 4 + qq, vb1 = vb0 + 16;
       bf16x8 bfr = cat8(lds_read_tr16(gt, vb0 * 32 + pp * 8), lds_read_tr16(gt, vb1 * 32 + pp * 8));
       const uint32_t pa0 = voff[vb0] + pp * 8, pa1 = voff[vb1] + pp * 8;
 #pragma unroll
@@ -502,7 +505,7 @@ static WGeom make_wgeom(int V, int I, int J, int K, int L, int KS, int ngroups) 
   g.V = V; g.I = I; g.J = J; g.K = K; g.L = L;
   pick_tile_w(K, L, g.TK, g.TL);
   g.nkt = cdiv(K, g.TK); g.nlt = cdiv(L, g.TL);
-  g.PR = g.TK + KS - 1; g.RS = g.TL + KS - 1;
+  g.PR = g.TK + KS - 1; g.RS = g.TL + KS - 1; g.RW = g.RS;
   g.nitems = V * I * J * g.nkt * g.nlt;
   g.ipg = cdiv(g.nitems, ngroups);
   g.dj_center = 0;
@@ -520,7 +523,12 @@ extern "C" int ncnet_wgrad16(const void* X, const void* G, float* part, float* p
   dim3 grid((unsigned)((dj_center ? KS : KS * KS) * ngroups));
   const bf16* x = (const bf16*)X; const bf16* gg = (const bf16*)G;
   if (variant == 2) {
-    if (g.RS > 32 || g.TL > 32) return -1;   // one wave-instruction per staged row
+    if (g.RW > 32 || g.TL > 32) return -1;   // one wave-instruction per staged row
+    // row stride TL + 8: a row wrap inside an 8-voxel read group jumps 256 B
+    // (bank period), keeping the transposed reads conflict-free
+    g.RS = g.TL + ((KS - 1 + 7) / 8) * 8;
+    if (g.PR * g.RS * 32 > 65535) return -1;  // 16-bit voxel offset table
+    lds = (size_t)g.PR * g.RS * 32 + (size_t)nv32 * 32 + (size_t)nv32 * 2;
     dim3 block(512);
     if (KS == 5) hipLaunchKernelGGL((wgrad16v2_kernel<5>), grid, block, lds, stream, x, gg, part, partb, g);
     else if (KS == 3) hipLaunchKernelGGL((wgrad16v2_kernel<3>), grid, block, lds, stream, x, gg, part, partb, g);
