@@ -13,6 +13,7 @@ int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*,
 int ncnet_conv1in_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv1out_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_wgrad16v3(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_jpack(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_jsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad1(const void*, const void*, float*, int, int, int, int, int, int, int, int, hipStream_t);
@@ -110,17 +111,23 @@ void conv1out_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int
                         X.size(2), X.size(3), X.size(4), ks, epi, cur_stream(X)), "conv1out_fwd");
 }
 
-// part rows R: ngroups (variant 1) or 2 * ngroups (variant 2, one row per voxel-chunk half)
+// part rows R: ngroups (variant 1) or 2 * ngroups (variants 2/3, one row per voxel-chunk half)
 void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t dj_center, int64_t variant) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(G, "G", at::kBFloat16); check(part, "part", at::kFloat); check(partb, "partb", at::kFloat);
   TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
-  TORCH_CHECK(variant == 1 || variant == 2, "wgrad16 variant must be 1 or 2");
+  TORCH_CHECK(variant >= 1 && variant <= 3, "wgrad16 variant must be 1, 2 or 3");
   check_shape(G, "G", X.sizes().vec());
   const int64_t rows = part.size(0);
-  TORCH_CHECK(rows > 0 && (variant == 1 || rows % 2 == 0), "wgrad16 v2 needs an even number of partial rows");
+  TORCH_CHECK(rows > 0 && (variant == 1 || rows % 2 == 0), "wgrad16 v2/v3 need an even number of partial rows");
   check_shape(part, "part", {rows, dj_center ? ks : ks * ks, ks * ks, 16, 16});
   check_shape(partb, "partb", {rows, 16});
+  if (variant == 3) {
+    ok(ncnet_wgrad16v3(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(0),
+                       X.size(1), X.size(2), X.size(3), X.size(4), ks, rows / 2, dj_center ? 1 : 0, cur_stream(X)),
+       "wgrad16v3");
+    return;
+  }
   ok(ncnet_wgrad16(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(0), X.size(1),
                    X.size(2), X.size(3), X.size(4), ks, variant == 2 ? rows / 2 : rows, dj_center ? 1 : 0, variant,
                    cur_stream(X)), "wgrad16");

@@ -319,6 +319,264 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
 }
 
 // ===========================================================================
+// wgrad16v3: sliding-window wgrad.  A workgroup owns one plane offset dj (or
+// dj = P in dj-centre mode) and ALL KS offsets di, and walks X-plane columns
+// (v, jj, tile) along ii.  X plane ii pairs with the G planes gi = ii - di + P
+// (di = 0..KS-1), i.e. ii-P..ii+P: consecutive steps share KS-1 of them, so G
+// tiles live in a ring of KS+1 LDS slots (one new tile per step streams in
+// behind the compute) and each X-shift fragment read from LDS feeds KS MFMAs
+// (one per di) instead of one: ~3x less LDS traffic per MFMA and ~KSx less
+// global traffic than the per-(di,dj) kernels.
+//   tiles: a contiguous range of VT (multiple of 64) voxels of the flattened
+//   (k, l) plane, so every tile splits into an even number of 32-voxel chunks
+//   (balanced halves); the X plane is staged full-width (L + KS - 1 <= 32) for
+//   the rows the tile touches, at row stride RS = L + 8 (conflict-free wraps).
+//   waves: 4 tap groups x 2 halves of the chunks; group g owns taps g, g+4, ..
+//   for every di; the last tap NT-1 is split over groups 1..3 by di.
+//   LDS: 2 X buffers + (KS+1) G slots + 1 zero slot (~110 KB: 1 WG/CU, 8 waves,
+//   up to 256 VGPRs for the 6 x 5 accumulator tiles).
+// part: [2*ngroups][NDD][NT][16 ci][16 co] (v2 layout), partb [2*ngroups][16].
+// ===========================================================================
+struct W3Geom {
+  int V, I, J, K, L;
+  int VT, ntl;         // voxels per tile (multiple of 64), tiles per plane
+  int PR, RS, RW;      // staged X rows, row stride, row width (voxels)
+  int ncols, cpg;      // X-plane columns (v, jj, tile); columns per group
+  int dj_center;
+};
+
+struct Col { int v, jj, a, nv, kf; };
+__device__ __forceinline__ Col decode_col(const W3Geom& g, int c) {
+  Col r;
+  const int t = c % g.ntl; c /= g.ntl;
+  r.jj = c % g.J; r.v = c / g.J;
+  r.a = t * g.VT;
+  r.nv = min(g.VT, g.K * g.L - r.a);
+  r.kf = r.a / g.L;
+  return r;
+}
+
+template <int KS>
+__global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ G,
+                                                           float* __restrict__ part, float* __restrict__ partb,
+                                                           W3Geom g) {
+  constexpr int P = KS / 2;
+  constexpr int NT = KS * KS;
+  constexpr int NS = KS + 1;             // G ring slots (+1 zero slot)
+  constexpr int TPG = (NT - 1) / 4;      // regular taps per tap group
+  constexpr int EXP = (KS + 2) / 3;      // di values of the last tap per group 1..3
+  constexpr int NW = 8;
+  constexpr int MAXC = 6;                // voxel chunks per half (VT <= 384)
+  static_assert((NT - 1) % 4 == 0, "NT must be 1 mod 4");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int xbytes = g.PR * g.RS * 32, gbytes = g.VT * 32;
+  char* xbuf = smem;                      // [2][xbytes]
+  char* gbuf = smem + 2 * xbytes;         // [NS + 1][gbytes]; slot NS stays zero (G planes outside the volume)
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> scalar branches
+  const int tg = wave & 3, half = wave >> 2;
+  const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int NDJ = g.dj_center ? 1 : KS;
+  const int djx = lb % NDJ, grp = lb / NDJ;
+  const int dj = g.dj_center ? P : djx;
+  const bool center_blk = (dj == P);
+  const int NDD = g.dj_center ? KS : NT;
+
+  for (int o = threadIdx.x * 16; o < 2 * xbytes + (NS + 1) * gbytes; o += NW * 64 * 16)
+    *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
+  uint32_t toff[TPG + 1];
+#pragma unroll
+  for (int m = 0; m <= TPG; ++m) {
+    int tap = (m < TPG) ? tg + 4 * m : NT - 1;
+    int dk = tap / KS, dl = tap - dk * KS;
+    toff[m] = (uint32_t)((dk * g.RS + dl) * 32);
+  }
+  const int xdi_lo = tg == 0 ? KS : (tg - 1) * EXP, xdi_hi = tg == 0 ? KS : min(KS, tg * EXP);
+
+  f32x4 acc[TPG][KS];
+  f32x4 accx[EXP];
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < TPG; ++m)
+#pragma unroll
+    for (int d = 0; d < KS; ++d) acc[m][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < EXP; ++e) accx[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ones[q] = f2bf(1.f);
+
+  const int c_lo = grp * g.cpg, c_hi = min(g.ncols, c_lo + g.cpg);
+  const int nch = (g.VT >> 6);            // chunks per half (VT multiple of 64)
+  const int ch_lo = half * nch;
+  const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const uint32_t ga_base = (ch_lo * 32 + gq * 4 + qq) * 32 + pp * 8;   // + u*1024 (+512 for the 2nd read)
+  // per-lane X voxel addresses of this half's chunks for the current tile
+  // (k-slot -> voxel: each 32-lane half of a tr-read covers 8 consecutive
+  // voxels, i.e. 256 B or one 256-B jump across a row wrap: all banks once)
+  uint32_t pav0[MAXC], pav1[MAXC];
+  auto set_tile = [&](const Col& r) {
+#pragma unroll
+    for (int u = 0; u < MAXC; ++u) {
+      const int e0 = (ch_lo + u) * 32 + gq * 4 + qq, e1 = e0 + 16;
+      const int f0 = r.a + e0, f1 = r.a + e1;
+      const int k0 = f0 / g.L, k1 = f1 / g.L;
+      pav0[u] = (e0 < r.nv ? ((k0 - r.kf) * g.RS + f0 - k0 * g.L) * 32 : 0) + pp * 8;
+      pav1[u] = (e1 < r.nv ? ((k1 - r.kf) * g.RS + f1 - k1 * g.L) * 32 : 0) + pp * 8;
+    }
+  };
+
+  auto col_ok = [&](int c) {
+    if (c >= c_hi) return true;   // end sentinel
+    const int gj = decode_col(g, c).jj - dj + P;
+    return gj >= 0 && gj < g.J;
+  };
+  auto next_col = [&](int c) {
+    ++c;
+    while (c < c_hi && !col_ok(c)) ++c;
+    return c;
+  };
+
+  // Stage the X rows kf-P .. kf-P+PR-1 of plane (ii, jj), full width, col 0 <-> l = -P.
+  auto stage_x = [&](const Col& r, int ii, char* buf) {
+    const bf16* xp = X + ((((size_t)r.v * g.I + ii) * g.J + r.jj) * (size_t)g.K * g.L) * 16;
+    for (int row = wave; row < g.PR; row += NW) {
+      const int kg = r.kf - P + row;
+      const bool in_k = kg >= 0 && kg < g.K;
+      if (in_k && lane < 2 * g.L)
+        __builtin_amdgcn_global_load_lds((const void*)(xp + (size_t)kg * g.L * 16 + lane * 8),
+                                         LDS_PTR(void, buf + row * g.RS * 32 + P * 32), 16, 0, 0);
+      if (lane < 2 * g.RW && (!in_k || lane < 2 * P || lane >= 2 * P + 2 * g.L))
+        *(u32x4*)(buf + row * g.RS * 32 + lane * 16) = u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  // Stage the tile's nv contiguous G voxels of plane (gi, gj); zero the rest of the slot.
+  auto stage_g = [&](const Col& r, int gi, char* buf) {
+    const int gj = r.jj - dj + P;
+    const bf16* gp = G + ((((size_t)r.v * g.I + gi) * g.J + gj) * (size_t)g.K * g.L + r.a) * 16;
+    for (int q = wave; q * 64 < 2 * g.VT; q += NW) {
+      const int ci = q * 64 + lane;
+      if (ci < 2 * r.nv)
+        __builtin_amdgcn_global_load_lds((const void*)(gp + ci * 8), LDS_PTR(void, buf + q * 1024), 16, 0, 0);
+      else
+        *(u32x4*)(buf + ci * 16) = u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+
+  int col = c_lo;
+  while (col < c_hi && !col_ok(col)) col = next_col(col);
+  // loaders: X (one plane per step), G (sequence over valid columns x gi)
+  int xl_col = col, xl_ii = 0, xl_step = 0;
+  int gl_col = col, gl_gi = 0, gl_seq = 0;
+  auto load_x_next = [&]() {
+    if (xl_col >= c_hi) return;
+    stage_x(decode_col(g, xl_col), xl_ii, xbuf + (xl_step & 1) * xbytes);
+    ++xl_step;
+    if (++xl_ii == g.I) { xl_ii = 0; xl_col = next_col(xl_col); }
+  };
+  auto load_g_upto = [&](int seq_max) {
+    while (gl_col < c_hi && gl_seq <= seq_max) {
+      stage_g(decode_col(g, gl_col), gl_gi, gbuf + (gl_seq % NS) * gbytes);
+      ++gl_seq;
+      if (++gl_gi == g.I) { gl_gi = 0; gl_col = next_col(gl_col); }
+    }
+  };
+
+  __syncthreads();   // zero fill before any DMA lands
+  load_x_next();
+  load_g_upto(NS - 2);
+  int step = 0, base = 0;
+  for (; col < c_hi; col = next_col(col), base += g.I) {
+    set_tile(decode_col(g, col));
+    for (int ii = 0; ii < g.I; ++ii, ++step) {
+      __syncthreads();   // X[step] and the G tiles of this step landed; previous step's reads done
+      load_x_next();
+      load_g_upto(base + max(0, ii - P) + NS - 1);
+      const char* xc = xbuf + (step & 1) * xbytes;
+      // valid di: gi = ii - di + P in [0, I); invalid ones read the zero slot,
+      // so every MFMA is issued unconditionally (<5% zero work at the I edges)
+      const int di_lo = max(0, ii + P - g.I + 1), di_hi = min(KS - 1, ii + P);
+      uint32_t gslot[KS];
+#pragma unroll
+      for (int d = 0; d < KS; ++d)
+        gslot[d] = (uint32_t)((d >= di_lo && d <= di_hi) ? (base + ii - d + P) % NS : NS) * gbytes;
+      // software pipeline: the next chunk's G fragments and the next tap's X
+      // fragment are in flight while the current MFMAs run
+      bf16x8 bcur[KS], bnxt[KS];
+#pragma unroll
+      for (int d = 0; d < KS; ++d)
+        bcur[d] = cat8(lds_read_tr16(gbuf, gslot[d] + ga_base), lds_read_tr16(gbuf, gslot[d] + ga_base + 512));
+#pragma unroll
+      for (int u = 0; u < MAXC; ++u) {
+        if (u < nch) {
+          const uint32_t pa0 = pav0[u], pa1 = pav1[u];
+          bf16x8 afr = cat8(lds_read_tr16(xc, pa0 + toff[0]), lds_read_tr16(xc, pa1 + toff[0]));
+          if (u + 1 < nch) {
+            const uint32_t gn = ga_base + (u + 1) * 1024;
+#pragma unroll
+            for (int d = 0; d < KS; ++d)
+              bnxt[d] = cat8(lds_read_tr16(gbuf, gslot[d] + gn), lds_read_tr16(gbuf, gslot[d] + gn + 512));
+          }
+#pragma unroll
+          for (int m = 0; m < TPG; ++m) {
+            bf16x8 afn = afr;
+            if (m + 1 < TPG || tg > 0)
+              afn = cat8(lds_read_tr16(xc, pa0 + toff[m + 1]), lds_read_tr16(xc, pa1 + toff[m + 1]));
+#pragma unroll
+            for (int d = 0; d < KS; ++d) acc[m][d] = mfma16(afr, bcur[d], acc[m][d]);
+            afr = afn;
+          }
+          if (tg > 0) {   // last tap (afr), this group's di range (B re-read from LDS)
+            const uint32_t ga = ga_base + u * 1024;
+#pragma unroll
+            for (int e = 0; e < EXP; ++e) {
+              const int d = xdi_lo + e;
+              if (d < xdi_hi) {
+                const uint32_t gsx = (uint32_t)((d >= di_lo && d <= di_hi) ? (base + ii - d + P) % NS : NS) * gbytes;
+                bf16x8 bx = cat8(lds_read_tr16(gbuf, gsx + ga), lds_read_tr16(gbuf, gsx + ga + 512));
+                accx[e] = mfma16(afr, bx, accx[e]);
+              }
+            }
+          }
+          if (center_blk && tg == 0) accb = mfma16(ones, bcur[P], accb);
+          if (u + 1 < nch) {
+#pragma unroll
+            for (int d = 0; d < KS; ++d) bcur[d] = bnxt[d];
+          }
+        }
+      }
+    }
+  }
+
+  // D[row = ci = 4(l>>4)+r][col = co = l&15]
+  const int row = grp * 2 + half;
+#pragma unroll
+  for (int m = 0; m < TPG; ++m) {
+    const int tap = tg + 4 * m;
+#pragma unroll
+    for (int d = 0; d < KS; ++d) {
+      const int ddi = g.dj_center ? d : d * KS + dj;
+      float* pout = part + (((size_t)row * NDD + ddi) * NT + tap) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pout[(4 * (lane >> 4) + r) * 16 + (lane & 15)] = acc[m][d][r];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EXP; ++e) {
+    const int d = xdi_lo + e;
+    if (d < xdi_hi) {
+      const int ddi = g.dj_center ? d : d * KS + dj;
+      float* pout = part + (((size_t)row * NDD + ddi) * NT + (NT - 1)) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pout[(4 * (lane >> 4) + r) * 16 + (lane & 15)] = accx[e][r];
+    }
+  }
+  if (center_blk && tg == 0 && lane < 16) partb[row * 16 + lane] = accb[0];
+}
+
+// ===========================================================================
 struct W1Geom {
   WGeom w;
   int mode;                 // 0: S = G (16ch tile), P = X (1ch plane); 1: S = X (16ch plane), P = G (1ch tile)
@@ -540,6 +798,34 @@ extern "C" int ncnet_wgrad16(const void* X, const void* G, float* part, float* p
   dim3 block(256);
   if (KS == 5) hipLaunchKernelGGL((wgrad16_kernel<5>), grid, block, lds, stream, x, gg, part, partb, g);
   else if (KS == 3) hipLaunchKernelGGL((wgrad16_kernel<3>), grid, block, lds, stream, x, gg, part, partb, g);
+  else return -2;
+  return (int)hipGetLastError();
+}
+
+// v3: ngroups column groups per dj (grid = ngroups * (dj_center ? 1 : KS)).
+// Tile rule (mirrored in ops/neigh_consensus.py wgrad_v3_groups):
+// ntl = ceil(K*L / 320), VT = roundup(ceil(K*L / ntl), 64).
+extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float* partb, int V, int I, int J, int K,
+                               int L, int KS, int ngroups, int dj_center, hipStream_t stream) {
+  W3Geom g;
+  g.V = V; g.I = I; g.J = J; g.K = K; g.L = L;
+  const int KL = K * L;
+  g.ntl = cdiv(KL, 320);
+  g.VT = ((cdiv(KL, g.ntl) + 63) / 64) * 64;
+  g.RW = L + KS - 1;
+  g.RS = L + ((KS - 1 + 7) / 8) * 8;
+  g.PR = (g.VT - 1) / L + 2 + KS - 1;
+  g.ncols = V * J * g.ntl;
+  g.cpg = cdiv(g.ncols, ngroups);
+  g.dj_center = dj_center;
+  if (g.RW > 32) return -1;                 // one wave-instruction per staged row
+  if (g.VT > 384) return -1;                // <= 6 chunks per half
+  size_t lds = 2 * (size_t)g.PR * g.RS * 32 + (size_t)(KS + 2) * g.VT * 32;
+  if (lds > 160 * 1024) return -1;
+  dim3 grid((unsigned)((dj_center ? 1 : KS) * ngroups)), block(512);
+  const bf16* x = (const bf16*)X; const bf16* gg = (const bf16*)G;
+  if (KS == 5) hipLaunchKernelGGL((wgrad16v3_kernel<5>), grid, block, lds, stream, x, gg, part, partb, g);
+  else if (KS == 3) hipLaunchKernelGGL((wgrad16v3_kernel<3>), grid, block, lds, stream, x, gg, part, partb, g);
   else return -2;
   return (int)hipGetLastError();
 }

@@ -34,8 +34,9 @@ HIP_KS = (3, 5)
 import os as _os
 
 USE_JC = _os.environ.get("NCNET_NC_JC", "1") == "1"
-# wgrad16 kernel: 2 = 8-wave LDS-DMA kernel (default), 1 = 4-wave register-staged
-WGRAD_VARIANT = int(_os.environ.get("NCNET_WGRAD_VARIANT", "2"))
+# wgrad16 kernel: 3 = sliding G-plane ring (default), 2 = 8-wave LDS-DMA per
+# (di, dj) plane, 1 = 4-wave register-staged
+WGRAD_VARIANT = int(_os.environ.get("NCNET_WGRAD_VARIANT", "3"))
 
 
 def layer_kinds(channels, kernel_sizes):
@@ -119,6 +120,25 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
     return h
 
 
+def wgrad_v3_ok(shape, ks: int) -> bool:
+    """wgrad16v3 stages full-width X rows: L + ks - 1 <= 32."""
+    return shape[4] + ks - 1 <= 32
+
+
+def wgrad_v3_groups(shape, ks: int, dj_center: bool) -> int:
+    """Column groups per dj for wgrad16v3: ~2 workgroups per CU in full mode
+    (KS dj values), ~1 per CU in dj-centre mode, never more than the columns
+    (v, j, tile).  Tile rule mirrors ncnet_wgrad16v3."""
+    V, I, J, K, L = shape[:5]
+    ntl = -(-(K * L) // 320)
+    ncols = V * J * ntl
+    target = 256 if dj_center else max(1, 512 // ks)
+    env = _os.environ.get("NCNET_WGRAD_GROUPS")
+    if env:
+        target = int(env)
+    return max(1, min(target, ncols))
+
+
 def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, ng: int, dj_center: bool):
     """Run the wgrad16 kernel and reduce its per-group partials.
 
@@ -127,10 +147,15 @@ def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, ng: int, 
     the kernel's ones-MFMA in the centre block).  Variant 2 (default, 8-wave
     LDS-DMA kernel) writes two partial rows per group.
     """
-    rows = ng * (2 if WGRAD_VARIANT == 2 else 1)
+    variant = WGRAD_VARIANT
+    if variant == 3 and not wgrad_v3_ok(x16.shape, ks):
+        variant = 2
+    if variant == 3:
+        ng = wgrad_v3_groups(x16.shape, ks, dj_center)
+    rows = ng * (2 if variant >= 2 else 1)
     part = torch.empty((rows, ks if dj_center else ks * ks, ks * ks, 16, 16), dtype=torch.float32, device=x16.device)
     partb = torch.empty((rows, 16), dtype=torch.float32, device=x16.device)
-    C.wgrad16(x16, g16, part, partb, ks, 1 if dj_center else 0, WGRAD_VARIANT)
+    C.wgrad16(x16, g16, part, partb, ks, 1 if dj_center else 0, variant)
     return part.sum(0), partb.sum(0)
 
 

@@ -65,6 +65,12 @@ def main():
     part1 = torch.empty((ng, ks * ks, ks * ks, 16), device=dev)
     part16c = torch.empty((2 * ng, ks, ks * ks, 16, 16), device=dev)
     z8 = torch.empty(shp + (8,), device=dev)
+    from ncnet_amd.ops.neigh_consensus import wgrad_v3_groups
+    n3, n3c = wgrad_v3_groups(shp, ks, False), wgrad_v3_groups(shp, ks, True)
+    p3 = torch.empty((2 * n3, ks ** 2, ks ** 2, 16, 16), device=dev)
+    p3b = torch.empty((2 * n3, 16), device=dev)
+    p3c = torch.empty((2 * n3c, ks, ks ** 2, 16, 16), device=dev)
+    p3cb = torch.empty((2 * n3c, 16), device=dev)
     g16b = torch.empty_like(g16)
     taps = ks ** 4
     fl16 = 2.0 * nvox * taps * 256
@@ -82,6 +88,8 @@ def main():
         "wgrad16_center": (lambda: C.wgrad16(x16, g16, part16c[:ng], partb[:ng], ks, 1, 1), fl16 / ks),
         "wgrad16v2": (lambda: C.wgrad16(x16, g16, part16, partb, ks, 0, 2), fl16),
         "wgrad16v2_center": (lambda: C.wgrad16(x16, g16, part16c, partb, ks, 1, 2), fl16 / ks),
+        "wgrad16v3": (lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3), fl16),
+        "wgrad16v3_center": (lambda: C.wgrad16(x16, g16, p3c, p3cb, ks, 1, 3), fl16 / ks),
         "wgrad1_mode0": (lambda: C.wgrad1(g16, x1, part1, ks, 0, ng), fl1),
         "wgrad1_mode1": (lambda: C.wgrad1(x16, g1, part1, ks, 1, ng), fl1),
     }

@@ -242,8 +242,9 @@ def test_immatchnet_volumes_and_grads_match_reference_algorithm():
     assert max(errs) < 0.3, errs
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-@pytest.mark.parametrize("ks,shape", [(5, (2, 6, 5, 25, 25)), (5, (1, 5, 4, 30, 27)), (3, (1, 4, 5, 9, 33))])
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("ks,shape", [(5, (2, 6, 5, 25, 25)), (5, (1, 5, 4, 30, 27)), (3, (1, 4, 5, 9, 33)),
+                                      (5, (1, 2, 3, 7, 6))])
 def test_wgrad16_kernel(variant, ks, shape, monkeypatch):
     """Weight / bias gradient of a 16->16 Conv4d straight from the wgrad16
     kernel (both variants; multi-tile K, L exercise the per-item halo), full
