@@ -16,6 +16,7 @@ int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, 
 int ncnet_wgrad16v3(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_jpack(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_jsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_bias_act(void*, const float*, long long, int, int, hipStream_t);
 int ncnet_wgrad1(const void*, const void*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
@@ -340,6 +341,26 @@ void transpose(Tensor x, Tensor y) {
 
 }  // namespace
 
+// In place Y = act(Y + b) over the channel axis: Y bf16, either a contiguous
+// [rows, C] matrix or a channels-last [N, C, H, W] tensor; b fp32 [C].
+void bias_act_(Tensor Y, Tensor b, int64_t relu) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(Y.device());
+  TORCH_CHECK(Y.is_cuda() && Y.scalar_type() == at::kBFloat16, "bias_act_: Y must be a bf16 GPU tensor");
+  int64_t C;
+  if (Y.dim() == 4) {
+    TORCH_CHECK(Y.is_contiguous(at::MemoryFormat::ChannelsLast), "bias_act_: 4-D Y must be channels-last");
+    C = Y.size(1);
+  } else {
+    TORCH_CHECK(Y.dim() == 2 && Y.is_contiguous(), "bias_act_: Y must be [rows, C] contiguous");
+    C = Y.size(1);
+  }
+  check(b, "b", at::kFloat);
+  check_shape(b, "b", {C});
+  TORCH_CHECK(C % 8 == 0, "bias_act_: C must be a multiple of 8");
+  ok(ncnet_bias_act(Y.data_ptr(), (const float*)b.data_ptr(), Y.numel() / C, (int)C, relu ? 1 : 0, cur_stream(Y)),
+     "bias_act_");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for ncnet_amd";
   m.def("conv16_fwd", &conv16_fwd);
@@ -349,6 +370,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad1", &wgrad1);
   m.def("jpack", &jpack);
   m.def("jsum", &jsum);
+  m.def("bias_act_", &bias_act_);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("l2norm_rows_bwd", &l2norm_rows_bwd);
   m.def("corr_gemm", &corr_gemm);

@@ -1,0 +1,43 @@
+// Backbone epilogues for the frozen-trunk execution plan (models/backbones.py
+// FrozenResNetPlan).  MIOpen's bf16 NHWC convolutions add a bias in a separate
+// pass and PyTorch then runs ReLU / residual add as further passes (~7 full
+// activation round trips per bottleneck).  The plan routes 1x1 convolutions
+// to hipBLASLt GEMMs (bias + ReLU in the GEMM epilogue, residual as the C
+// operand) and finishes everything else with this single in-place pass:
+//
+//   Y[r, c] = act(Y[r, c] + b[c])          (bf16 rows of C channels, fp32 bias)
+#include "common.h"
+
+namespace ncnet {
+
+// 8 channels (16 B) per thread; C % 8 == 0.
+template <bool RELU>
+__global__ __launch_bounds__(256) void bias_act_kernel(bf16* __restrict__ Y, const float* __restrict__ b,
+                                                       long long n8, int C8) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n8) return;
+  const int c0 = (int)(e % C8) * 8;
+  bf16x8 v = *(const bf16x8*)(Y + e * 8);
+  const f32x4 b0 = *(const f32x4*)(b + c0), b1 = *(const f32x4*)(b + c0 + 4);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float x = bf2f(v[q]) + (q < 4 ? b0[q] : b1[q - 4]);
+    if (RELU) x = fmaxf(x, 0.f);
+    v[q] = f2bf(x);
+  }
+  *(bf16x8*)(Y + e * 8) = v;
+}
+
+}  // namespace ncnet
+
+using namespace ncnet;
+
+extern "C" int ncnet_bias_act(void* Y, const float* b, long long rows, int C, int relu, hipStream_t stream) {
+  if (C % 8) return -1;
+  const long long n8 = rows * (C / 8);
+  if (n8 == 0) return 0;
+  dim3 grid((unsigned)((n8 + 255) / 256)), block(256);
+  if (relu) hipLaunchKernelGGL((bias_act_kernel<true>), grid, block, 0, stream, (bf16*)Y, b, n8, C / 8);
+  else hipLaunchKernelGGL((bias_act_kernel<false>), grid, block, 0, stream, (bf16*)Y, b, n8, C / 8);
+  return (int)hipGetLastError();
+}

@@ -242,71 +242,111 @@ def fold_frozen_bn(trunk: nn.Module) -> nn.Module:
 class FrozenResNetPlan(nn.Module):
     """Inference plan of a frozen (BN-folded) ResNet trunk in one compute dtype.
 
-    Built once from ``fold_frozen_bn(trunk)``: every conv weight is cast to
-    ``dtype`` and laid out channels-last up front, so a training step issues no
-    per-step weight casts (autocast re-casts ~100 fp32 weights per forward);
-    epilogues (ReLU, residual add) run in place.  MIOpen's fused
-    conv+ReLU / conv+add+ReLU entry points were measured 40x slower for bf16
-    channels-last on MI355X (no fused solver; naive fallback), so they are
-    not used.  Reference: the frozen trunk of lib/model.py:37-44.
+    Built once from ``fold_frozen_bn(trunk)``; weights are cast and laid out up
+    front (no per-step autocast casts).  Activations stay NHWC (channels-last)
+    and each bottleneck runs as
+      conv1 (1x1)  -> GEMM with bias+ReLU in the hipBLASLt epilogue
+      conv2 (3x3)  -> MIOpen conv (no bias) + one fused bias+ReLU pass (HIP)
+      conv3 (1x1)  -> GEMM with the residual as C operand (+ the downsample
+                      GEMM/conv feeding it), then one fused bias+ReLU pass
+    i.e. 2 activation round trips besides the convolutions, instead of ~7
+    (MIOpen bias pass, ReLU, add, ReLU ...).  MIOpen's own fused
+    conv+ReLU / conv+add+ReLU entry points were measured ~40x slower for bf16
+    channels-last on MI355X (no fused solver), so they are not used.
+    Reference: the frozen trunk of lib/model.py:37-44.
     """
 
     def __init__(self, folded: nn.Sequential, dtype: torch.dtype = torch.bfloat16):
         super().__init__()
         self.dtype = dtype
-        self.steps = []  # (kind, params)
-        convs = []
+        self.steps = []
+        keep = []
 
-        def conv_params(c: nn.Conv2d):
+        def w4(c: nn.Conv2d):
             w = c.weight.detach().to(dtype).contiguous(memory_format=torch.channels_last)
-            b = c.bias.detach().to(dtype) if c.bias is not None else None
-            convs.append(w)
-            return (w, b, c.stride, c.padding)
+            keep.append(w)
+            return w
+
+        def wt(c: nn.Conv2d):  # 1x1 conv weight as the [Cin, Cout] GEMM operand (transposed view)
+            w = c.weight.detach().to(dtype).reshape(c.out_channels, c.in_channels).contiguous()
+            keep.append(w)
+            return w.t()
+
+        def bias(c: nn.Conv2d, dt):
+            b = c.bias.detach().float() if c.bias is not None else torch.zeros(c.out_channels,
+                                                                                 device=c.weight.device)
+            return b.to(dt).contiguous()
 
         mods = list(folded.children())
-        idx = 0
-        while idx < len(mods):
-            m = mods[idx]
+        for idx, m in enumerate(mods):
             if isinstance(m, nn.Conv2d):
-                relu = idx + 1 < len(mods) and any(isinstance(n, nn.ReLU) for n in mods[idx + 1: idx + 3])
-                self.steps.append(("conv_relu" if relu else "conv", conv_params(m)))
+                relu = any(isinstance(n, nn.ReLU) for n in mods[idx + 1: idx + 3])
+                self.steps.append(("conv", (w4(m), bias(m, torch.float32), m.stride, m.padding, relu)))
             elif isinstance(m, nn.MaxPool2d):
                 self.steps.append(("maxpool", (m.kernel_size, m.stride, m.padding)))
             elif isinstance(m, nn.Sequential):
                 for blk in m:
                     if not isinstance(blk, Bottleneck):
                         raise TypeError("FrozenResNetPlan expects Bottleneck layers")
-                    down = conv_params(blk.downsample[0]) if blk.downsample is not None else None
-                    self.steps.append(("bottleneck", (conv_params(blk.conv1), conv_params(blk.conv2),
-                                                      conv_params(blk.conv3), down)))
+                    b3 = bias(blk.conv3, torch.float32)
+                    down = None
+                    if blk.downsample is not None:
+                        dc = blk.downsample[0]
+                        b3 = b3 + bias(dc, torch.float32)   # relu(x W3 + b3 + (xs Wd + bd))
+                        down = (wt(dc), 1) if dc.stride == (1, 1) else (w4(dc), dc.stride)
+                    self.steps.append(("bottleneck", dict(
+                        w1t=wt(blk.conv1), b1=bias(blk.conv1, dtype), w2=w4(blk.conv2),
+                        b2=bias(blk.conv2, torch.float32), s2=blk.conv2.stride, w3t=wt(blk.conv3),
+                        b3=b3.contiguous(), down=down)))
             elif isinstance(m, (nn.ReLU, nn.Identity)):
                 pass
             else:
                 raise TypeError(f"FrozenResNetPlan: unsupported module {type(m).__name__}")
-            idx += 1
-        self._keep = convs  # keep tensors referenced
+        self._keep = keep
 
-    def _conv(self, x, p, relu: bool, z=None):
-        w, b, stride, pad = p
-        y = F.conv2d(x, w, b, stride, pad)
-        if z is not None:
-            y.add_(z)
-        return y.relu_() if (relu or z is not None) else y
+    @staticmethod
+    def _bias_act(y: torch.Tensor, b: torch.Tensor, relu: bool) -> torch.Tensor:
+        if y.is_cuda and y.dtype == torch.bfloat16:
+            from ..ops import _ext
+            if _ext.use_hip(y):
+                _ext.ext().bias_act_(y, b, 1 if relu else 0)
+                return y
+        shape = (1, -1, 1, 1) if y.dim() == 4 else (1, -1)
+        y.add_(b.to(y.dtype).view(shape))
+        return y.relu_() if relu else y
+
+    @staticmethod
+    def _rows(x: torch.Tensor) -> torch.Tensor:  # NCHW channels-last -> [N*H*W, C] view
+        return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
+
+    @staticmethod
+    def _nchw(y2d: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+        return y2d.view(n, h, w, -1).permute(0, 3, 1, 2)
 
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = x.to(self.dtype).contiguous(memory_format=torch.channels_last)
         for kind, p in self.steps:
-            if kind == "conv_relu":
-                x = self._conv(x, p, True)
-            elif kind == "conv":
-                x = self._conv(x, p, False)
+            if kind == "conv":
+                w, b, stride, pad, relu = p
+                x = self._bias_act(F.conv2d(x, w, None, stride, pad).contiguous(memory_format=torch.channels_last),
+                                   b, relu)
             elif kind == "maxpool":
-                x = F.max_pool2d(x, *p)
+                x = F.max_pool2d(x, *p).contiguous(memory_format=torch.channels_last)
             else:
-                c1, c2, c3, down = p
-                idt = x if down is None else self._conv(x, down, False)
-                y = self._conv(x, c1, True)
-                y = self._conv(y, c2, True)
-                x = self._conv(y, c3, True, z=idt)
+                n, _, h, w = x.shape
+                x2d = self._rows(x)
+                y1 = torch._addmm_activation(p["b1"], x2d, p["w1t"])            # relu(x W1 + b1)
+                y2 = F.conv2d(self._nchw(y1, n, h, w), p["w2"], None, p["s2"], 1)
+                y2 = self._bias_act(y2.contiguous(memory_format=torch.channels_last), p["b2"], True)
+                n2, _, h2, w2 = y2.shape
+                if p["down"] is None:
+                    idt = x2d
+                elif p["down"][1] == 1:
+                    idt = torch.mm(x2d, p["down"][0])
+                else:
+                    idt = self._rows(F.conv2d(x, p["down"][0], None, p["down"][1]).contiguous(
+                        memory_format=torch.channels_last))
+                out = torch.addmm(idt, self._rows(y2), p["w3t"])                # x W3 + identity
+                x = self._nchw(self._bias_act(out, p["b3"], True), n2, h2, w2)
         return x

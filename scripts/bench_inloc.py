@@ -1,0 +1,100 @@
+#!/usr/bin/env python
+"""InLoc dense-matching inference benchmark (BASELINE configs 4 and 5).
+
+One query/pano pair per forward, exactly the eval_inloc.py hot path
+(reference eval_inloc.py:124-189): backbone on both images, fused
+correlation + 2x2x2x2 max-pool (relocalization k=2), MutualMatching,
+NeighConsensus (3,3 / 16,1), MutualMatching, then bidirectional match
+extraction with GPU de-duplication.  Synthetic 4:3 images (random pixels,
+random-init weights); the images are resized exactly like eval_inloc
+(longest side -> --image-size, floored to a multiple of 32 px).
+
+Prints one JSON line with ms/pair and a per-stage breakdown (CUDA events).
+
+    python scripts/bench_inloc.py --image-size 1600 --pairs 5 --warmup 2
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+from ncnet_amd.eval.inloc import n_matches, pair_matches, target_size  # noqa: E402
+from ncnet_amd.models import ImMatchNet  # noqa: E402
+from ncnet_amd.ops.correlation import correlation, correlation_pool2  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--image-size", type=int, default=1600)
+    ap.add_argument("--k", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--ncons_kernel_sizes", nargs="+", type=int, default=[3, 3])
+    ap.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 1])
+    ap.add_argument("--src-hw", type=int, nargs=2, default=[3024, 4032], help="raw query size (iPhone7)")
+    ap.add_argument("--no-matches", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    model = ImMatchNet(use_cuda=True, ncons_kernel_sizes=a.ncons_kernel_sizes, ncons_channels=a.ncons_channels,
+                       half_precision=True, relocalization_k_size=a.k).to(dev).eval()
+    h, w = target_size(a.src_hw[0], a.src_hw[1], a.image_size, a.k)
+    src = torch.randn(1, 3, h, w, device=dev)
+    tgt = torch.randn(1, 3, h, w, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    stages = {"backbone": 0.0, "corr_pool": 0.0, "mm_nc_mm": 0.0, "matches": 0.0}
+    nmatch = 0
+
+    def one(timed: bool):
+        nonlocal nmatch
+        with torch.inference_mode():
+            ev[0].record()
+            f, (fh, fw) = model.extract(torch.cat((src, tgt), 0))
+            fa, fb = f[:1], f[1:]
+            ev[1].record()
+            if a.k == 2:
+                corr4d, delta = correlation_pool2(fa, fb, fh, fw, fh, fw)
+            else:
+                corr4d, delta = correlation(fa, fb).view(1, 1, fh, fw, fh, fw), None
+            ev[2].record()
+            corr4d = model.process_correlation(corr4d)
+            ev[3].record()
+            if not a.no_matches:
+                m = pair_matches(corr4d, delta, a.k, True, True)
+                nmatch = int(m.shape[0])
+            ev[4].record()
+        if timed:
+            torch.cuda.synchronize()
+            for i, k in enumerate(stages):
+                stages[k] += ev[i].elapsed_time(ev[i + 1])
+
+    for _ in range(a.warmup):
+        one(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.pairs):
+        one(True)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / a.pairs
+    fs = (h // 16 // a.k, w // 16 // a.k)
+    print(json.dumps({
+        "metric": "InLoc dense matching latency per pair (fwd, k=%d relocalization)" % a.k,
+        "value": round(ms, 3), "unit": "ms/pair", "higher_is_better": False,
+        "pairs_per_s": round(1e3 / ms, 3), "n_gpus": 1, "pairs": a.pairs, "warmup": a.warmup,
+        "dtype": "bf16", "data": "synthetic (random 4:3 images, random-init weights)",
+        "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,
+                   "ncons": [a.ncons_kernel_sizes, a.ncons_channels], "k": a.k},
+        "stages_ms": {k: round(v / a.pairs, 3) for k, v in stages.items()},
+        "matches": nmatch, "matches_contract": n_matches(a.image_size, a.k, True),
+    }))
+
+
+if __name__ == "__main__":
+    main()

@@ -271,3 +271,36 @@ def test_wgrad16_kernel(variant, ks, shape, monkeypatch):
     dwc = nc._reduce_wgrad16_center(sc, ks)            # [co, ci, di, dk, dl]
     assert relerr(dwc, dstd[:, :, :, ks // 2]) < 1e-3
     assert relerr(sbc, sb) < 1e-5
+
+
+def test_bias_act_kernel():
+    C = _ext.ext()
+    torch.manual_seed(5)
+    y = torch.randn(2, 64, 9, 7, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(64, device=DEV)
+    ref_ = torch.relu(y.float() + b.view(1, -1, 1, 1))
+    C.bias_act_(y, b, 1)
+    assert relerr(y, ref_) < 1e-2
+    z = torch.randn(33, 128, device=DEV).to(torch.bfloat16)
+    refz = z.float() + b.repeat(2)
+    C.bias_act_(z, b.repeat(2).contiguous(), 0)
+    assert relerr(z, refz) < 1e-2
+
+
+def test_frozen_trunk_plan_gpu():
+    """bf16 GEMM/epilogue execution plan of the frozen ResNet trunk vs the fp32 eager trunk."""
+    from ncnet_amd.models.backbones import FrozenResNetPlan, fold_frozen_bn, resnet_trunk
+    torch.manual_seed(0)
+    t = resnet_trunk("resnet101", "layer3").eval()
+    for m in t.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.5, 1.5)
+            m.weight.data.uniform_(0.5, 1.5)
+    t = t.to(DEV)
+    x = torch.randn(2, 3, 96, 128, device=DEV)
+    with torch.no_grad():
+        r = t(x)
+        p = FrozenResNetPlan(fold_frozen_bn(t), torch.bfloat16)(x)
+    assert p.shape == r.shape
+    assert rel_l2(p.float(), r) < 3e-2
