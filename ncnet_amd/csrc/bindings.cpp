@@ -18,12 +18,12 @@ int ncnet_jpack(const void*, int, void*, int, int, int, int, int, int, int, hipS
 int ncnet_jsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_bias_act(void*, const float*, long long, int, int, hipStream_t);
 int ncnet_wgrad1(const void*, const void*, float*, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, hipStream_t);
+int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
 int ncnet_corr_gemm(const void*, const void*, void*, const int*, const int*, int, int, int, int, long long, long long,
-                    long long, int, hipStream_t);
+                    long long, int, float, hipStream_t);
 int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, int, int, int, int, long long, long long,
-                          hipStream_t);
+                          float, hipStream_t);
 int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, hipStream_t);
 int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, hipStream_t);
 int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, hipStream_t);
@@ -169,15 +169,19 @@ void wgrad1(Tensor S16, Tensor P1, Tensor part, int64_t ks, int64_t mode, int64_
                   S16.size(3), S16.size(4), ks, mode, ngroups, cur_stream(S16)), "wgrad1");
 }
 
-void l2norm_rows(Tensor x, Tensor y, c10::optional<Tensor> inv) {
+// y: bf16, or OCP fp8 e4m3 holding fp8_scale * x / ||x|| (fp8_scale > 0)
+void l2norm_rows(Tensor x, Tensor y, c10::optional<Tensor> inv, double fp8_scale) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.is_cuda() && x.is_contiguous());
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat);
-  check(y, "y", at::kBFloat16);
+  const bool f8 = y.scalar_type() == at::kFloat8_e4m3fn;
+  check(y, "y", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
+  TORCH_CHECK(!f8 || fp8_scale > 0, "fp8 output needs fp8_scale > 0");
   TORCH_CHECK(x.dim() == 2 && y.sizes() == x.sizes(), "x,y must be [rows, C]");
   if (inv.has_value()) { check(*inv, "inv", at::kFloat); check_shape(*inv, "inv", {x.size(0)}); }
   ok(ncnet_l2norm_rows(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(),
-                       inv.has_value() ? (float*)inv->data_ptr() : nullptr, x.size(0), x.size(1), cur_stream(x)), "l2norm");
+                       inv.has_value() ? (float*)inv->data_ptr() : nullptr, x.size(0), x.size(1),
+                       f8 ? (float)fp8_scale : 0.f, cur_stream(x)), "l2norm");
 }
 
 void l2norm_rows_bwd(Tensor x, Tensor g, Tensor inv, Tensor gx) {
@@ -189,10 +193,13 @@ void l2norm_rows_bwd(Tensor x, Tensor g, Tensor inv, Tensor gx) {
                            x.size(0), x.size(1), cur_stream(x)), "l2norm_bwd");
 }
 
-// A [Ba, M, K], B [Bb, N, K] bf16; C [batch, M, N] fp32/bf16
-void corr_gemm(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> amap, c10::optional<Tensor> bmap) {
+// A [Ba, M, K], B [Bb, N, K] bf16 (or both OCP fp8 e4m3: C = out_scale * A.B^T); C [batch, M, N] fp32/bf16
+void corr_gemm(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> amap, c10::optional<Tensor> bmap,
+               double out_scale) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
-  check(A, "A", at::kBFloat16); check(B, "B", at::kBFloat16);
+  const bool f8 = A.scalar_type() == at::kFloat8_e4m3fn;
+  check(A, "A", f8 ? at::kFloat8_e4m3fn : at::kBFloat16); check(B, "B", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
+  TORCH_CHECK(!f8 || A.size(2) % 16 == 0, "fp8 K must be a multiple of 16");
   TORCH_CHECK(C.is_cuda() && C.is_contiguous() && (C.scalar_type() == at::kFloat || C.scalar_type() == at::kBFloat16));
   TORCH_CHECK(A.dim() == 3 && B.dim() == 3 && C.dim() == 3);
   TORCH_CHECK(A.size(2) == B.size(2), "K mismatch");
@@ -209,12 +216,16 @@ void corr_gemm(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> amap, c10::op
   } else TORCH_CHECK(B.size(0) == batch);
   ok(ncnet_corr_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), opt_ptr<int>(amap), opt_ptr<int>(bmap), batch, A.size(1),
                      B.size(1), A.size(2), A.size(1) * A.size(2), B.size(1) * B.size(2), C.size(1) * C.size(2),
-                     C.scalar_type() == at::kBFloat16, cur_stream(A)), "corr_gemm");
+                     C.scalar_type() == at::kBFloat16, f8 ? (float)out_scale : 0.f, cur_stream(A)), "corr_gemm");
 }
 
-void corr_gemm_pool2(Tensor A, Tensor B, Tensor val, Tensor idx, int64_t hA, int64_t wA, int64_t hB, int64_t wB) {
+void corr_gemm_pool2(Tensor A, Tensor B, Tensor val, Tensor idx, int64_t hA, int64_t wA, int64_t hB, int64_t wB,
+                     double out_scale) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
-  check(A, "A", at::kBFloat16); check(B, "B", at::kBFloat16); check(val, "val", at::kFloat); check(idx, "idx", at::kByte);
+  const bool f8 = A.scalar_type() == at::kFloat8_e4m3fn;
+  check(A, "A", f8 ? at::kFloat8_e4m3fn : at::kBFloat16); check(B, "B", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
+  check(val, "val", at::kFloat); check(idx, "idx", at::kByte);
+  TORCH_CHECK(!f8 || A.size(2) % 16 == 0, "fp8 K must be a multiple of 16");
   TORCH_CHECK(A.dim() == 3 && B.dim() == 3 && A.size(0) == B.size(0));
   TORCH_CHECK(A.size(1) == hA * wA && B.size(1) == hB * wB && A.size(2) == B.size(2));
   TORCH_CHECK(hA % 2 == 0 && wA % 2 == 0 && hB % 2 == 0 && wB % 2 == 0, "pooling needs even feature sizes");
@@ -222,7 +233,8 @@ void corr_gemm_pool2(Tensor A, Tensor B, Tensor val, Tensor idx, int64_t hA, int
   check_shape(val, "val", {A.size(0), hA / 2, wA / 2, hB / 2, wB / 2});
   check_shape(idx, "idx", {A.size(0), hA / 2, wA / 2, hB / 2, wB / 2});
   ok(ncnet_corr_gemm_pool2(A.data_ptr(), B.data_ptr(), (float*)val.data_ptr(), (uint8_t*)idx.data_ptr(), A.size(0), hA,
-                           wA, hB, wB, A.size(2), A.size(1) * A.size(2), B.size(1) * B.size(2), cur_stream(A)),
+                           wA, hB, wB, A.size(2), A.size(1) * A.size(2), B.size(1) * B.size(2),
+                           f8 ? (float)out_scale : 0.f, cur_stream(A)),
      "corr_gemm_pool2");
 }
 

@@ -26,6 +26,15 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// OCP fp8 e4m3 x fp8 e4m3 -> f32, 16x16x128, through the block-scaled MX form
+// (2x the bf16 MFMA rate) with unit E8M0 scales (127 = 2^0) on both operands.
+// Lane l holds A[row l&15][k = 32(l>>4) .. 32(l>>4)+31] (32 bytes, k in byte
+// order) and B[k same][col l&15]; C/D as the bf16 16x16 form.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma_fp8_k128(const i32x8& a, const i32x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
 // ds_read_b64_tr_b16: 16-lane group reads a [4 rows x 16 cols] bf16 block;
 // lane 4q+p supplies the address of row q, columns 4p..4p+3 (8-byte aligned);
 // lane i of the group receives column i of the 4 rows.

@@ -14,13 +14,15 @@
 //   lib/model.py:177-191) when the feature rows are ordered in ks x ks spatial
 //   blocks: the full-resolution volume is never written.
 #include "common.h"
+#include <hip/hip_fp8.h>
 
 namespace ncnet {
 
 // ---------------------------------------------------------------------------
-template <typename TIN>
-__global__ __launch_bounds__(256) void l2norm_rows_kernel(const TIN* __restrict__ x, bf16* __restrict__ y,
-                                                          float* __restrict__ inv_norm, int rows, int C) {
+template <typename TIN, bool FP8>
+__global__ __launch_bounds__(256) void l2norm_rows_kernel(const TIN* __restrict__ x, void* __restrict__ yv,
+                                                          float* __restrict__ inv_norm, int rows, int C,
+                                                          float out_scale) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -36,7 +38,31 @@ __global__ __launch_bounds__(256) void l2norm_rows_kernel(const TIN* __restrict_
   ss = wave_sum(ss);
   const float inv = 1.f / sqrtf(ss + 1e-6f);
   if (lane == 0 && inv_norm) inv_norm[row] = inv;
-  bf16* yr = y + (size_t)row * C;
+  if (FP8) {
+    // OCP e4m3, scaled by out_scale (unit rows have |y| <= 1: the scale moves
+    // the typical 1/sqrt(C) entries out of the subnormal range)
+    const float s = inv * out_scale;
+    uint8_t* yr = (uint8_t*)yv + (size_t)row * C;
+    for (int c = lane * 8; c < C; c += 512) {
+      if (c + 8 <= C) {
+        uint32_t w[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v |= (uint32_t)__hip_cvt_float_to_fp8((float)xr[c + 4 * h + e] * s, __HIP_SATFINITE, __HIP_E4M3) << (8 * e);
+          w[h] = v;
+        }
+        *(uint2*)(yr + c) = make_uint2(w[0], w[1]);
+      } else {
+        for (int e = 0; c + e < C; ++e)
+          yr[c + e] = (uint8_t)__hip_cvt_float_to_fp8((float)xr[c + e] * s, __HIP_SATFINITE, __HIP_E4M3);
+      }
+    }
+    return;
+  }
+  bf16* yr = (bf16*)yv + (size_t)row * C;
   for (int c = lane * 8; c < C; c += 512) {
     if (c + 8 <= C) {
       bf16x8 o;
@@ -69,15 +95,16 @@ __global__ __launch_bounds__(256) void l2norm_rows_bwd_kernel(const float* __res
 // ---------------------------------------------------------------------------
 constexpr int BM = 128, BN = 128, BK = 64;
 
-// LDS tile: [128 rows][64 k] bf16 = 128 B rows of 8 x 16-B chunks, chunk
-// position XOR-swizzled by (row & 7).
+// LDS tile: [128 rows][128 B] = 64 bf16 k (or 128 fp8 k) per row, 8 x 16-B
+// chunks, chunk position XOR-swizzled by (row & 7).
 __device__ __forceinline__ uint32_t tile_off(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ (row & 7)) << 4)); }
 
 struct GemmArgs {
-  const bf16* A; const bf16* B; void* C;
+  const void* A; const void* B; void* C;
   const int* amap; const int* bmap;
   int M, N, K;
   long long sA, sB, sC;   // batch strides (elements)
+  float out_scale;        // fp8: 1 / (scale_A * scale_B)
   int tiles_m, tiles_n;
   // fused max-pool epilogue
   int pool_ks;           // 0 = plain store
@@ -85,11 +112,13 @@ struct GemmArgs {
   int hA, wA, hB, wB;    // full-res feature grid (pooling only)
 };
 
-template <bool OUT_BF16, bool POOL>
+template <bool OUT_BF16, bool POOL, bool FP8>
 __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
+  constexpr int EB = FP8 ? 1 : 2;            // bytes per element
+  constexpr int KT = 128 / EB;               // k per 128-B LDS row
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* As = smem;                 // BM x BK
-  char* Bs = smem + BM * BK * 2;   // BN x BK
+  char* Bs = smem + BM * 128;      // BN x 128 B
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -98,8 +127,8 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
   const int tm = bid % p.tiles_m;
   const int b = bid / p.tiles_m;
   const int m0 = tm * BM, n0 = tn * BN;
-  const bf16* A = p.A + (size_t)(p.amap ? p.amap[b] : b) * p.sA;
-  const bf16* B = p.B + (size_t)(p.bmap ? p.bmap[b] : b) * p.sB;
+  const char* A = (const char*)p.A + (size_t)(p.amap ? p.amap[b] : b) * p.sA * EB;
+  const char* B = (const char*)p.B + (size_t)(p.bmap ? p.bmap[b] : b) * p.sB * EB;
 
   // staging: 1024 chunks per operand, 4 per thread
   u32x4 ra[4], rb[4];
@@ -108,9 +137,9 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
     for (int m = 0; m < 4; ++m) {
       int c = threadIdx.x + m * 256;
       int row = c >> 3, ch = c & 7;
-      int ga = m0 + row, gb = n0 + row, kk = k0 + ch * 8;
-      ra[m] = (ga < p.M && kk < p.K) ? *(const u32x4*)(A + (size_t)ga * p.K + kk) : u32x4{0u, 0u, 0u, 0u};
-      rb[m] = (gb < p.N && kk < p.K) ? *(const u32x4*)(B + (size_t)gb * p.K + kk) : u32x4{0u, 0u, 0u, 0u};
+      int ga = m0 + row, gb = n0 + row, kk = k0 + ch * (16 / EB);
+      ra[m] = (ga < p.M && kk < p.K) ? *(const u32x4*)(A + ((size_t)ga * p.K + kk) * EB) : u32x4{0u, 0u, 0u, 0u};
+      rb[m] = (gb < p.N && kk < p.K) ? *(const u32x4*)(B + ((size_t)gb * p.K + kk) * EB) : u32x4{0u, 0u, 0u, 0u};
     }
   };
   auto store = [&]() {
@@ -128,32 +157,62 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto finish = [&]() {
+    if (FP8) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = acc[i][j] * p.out_scale;
+    }
+  };
 
-  const int nk = (p.K + BK - 1) / BK;
+  const int nk = (p.K + KT - 1) / KT;
   load(0);
   store();
   __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
-    if (more) load((kt + 1) * BK);
+    if (more) load((kt + 1) * KT);
+    if (FP8) {
+      // one K=128 MX-fp8 MFMA per sub-tile: lane group fq owns bytes 32fq..32fq+31
+      i32x8 af[4], bfv[4];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfv[4];
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + fr;
+        u32x4 lo = *(const u32x4*)(As + tile_off(r, 2 * fq)), hi = *(const u32x4*)(As + tile_off(r, 2 * fq + 1));
+        af[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = lds_read16(As, tile_off(wm * 64 + i * 16 + fr, ks * 4 + fq));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfv[j] = lds_read16(Bs, tile_off(wn * 64 + j * 16 + fr, ks * 4 + fq));
+      for (int j = 0; j < 4; ++j) {
+        const int r = wn * 64 + j * 16 + fr;
+        u32x4 lo = *(const u32x4*)(Bs + tile_off(r, 2 * fq)), hi = *(const u32x4*)(Bs + tile_off(r, 2 * fq + 1));
+        bfv[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfv[j], acc[i][j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_fp8_k128(af[i], bfv[j], acc[i][j]);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[4], bfv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = lds_read16(As, tile_off(wm * 64 + i * 16 + fr, ks * 4 + fq));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfv[j] = lds_read16(Bs, tile_off(wn * 64 + j * 16 + fr, ks * 4 + fq));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfv[j], acc[i][j]);
+      }
     }
     __syncthreads();
     if (more) store();
     __syncthreads();
   }
 
+  finish();
   if (!POOL) {
     // D[row = 4fq + r][col = fr] of sub-tile (i,j)
 #pragma unroll
@@ -217,13 +276,18 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
 
 using namespace ncnet;
 
+// y dtype: bf16 (fp8_scale == 0) or OCP fp8 e4m3 scaled by fp8_scale.
 extern "C" int ncnet_l2norm_rows(const void* x, int x_is_bf16, void* y, float* inv_norm, int rows, int C,
-                                 hipStream_t stream) {
+                                 float fp8_scale, hipStream_t stream) {
   dim3 grid((unsigned)cdiv(rows, 4)), block(256);
-  if (x_is_bf16)
-    hipLaunchKernelGGL((l2norm_rows_kernel<bf16>), grid, block, 0, stream, (const bf16*)x, (bf16*)y, inv_norm, rows, C);
-  else
-    hipLaunchKernelGGL((l2norm_rows_kernel<float>), grid, block, 0, stream, (const float*)x, (bf16*)y, inv_norm, rows, C);
+  const bool f8 = fp8_scale != 0.f;
+  if (x_is_bf16) {
+    if (f8) hipLaunchKernelGGL((l2norm_rows_kernel<bf16, true>), grid, block, 0, stream, (const bf16*)x, y, inv_norm, rows, C, fp8_scale);
+    else hipLaunchKernelGGL((l2norm_rows_kernel<bf16, false>), grid, block, 0, stream, (const bf16*)x, y, inv_norm, rows, C, 1.f);
+  } else {
+    if (f8) hipLaunchKernelGGL((l2norm_rows_kernel<float, true>), grid, block, 0, stream, (const float*)x, y, inv_norm, rows, C, fp8_scale);
+    else hipLaunchKernelGGL((l2norm_rows_kernel<float, false>), grid, block, 0, stream, (const float*)x, y, inv_norm, rows, C, 1.f);
+  }
   return (int)hipGetLastError();
 }
 
@@ -235,18 +299,26 @@ extern "C" int ncnet_l2norm_rows_bwd(const float* x, const float* g, const float
 }
 
 // C[b] = A[amap[b]] . B[bmap[b]]^T ; out_bf16 selects the output dtype.
+// fp8_out_scale != 0: A, B are OCP fp8 e4m3 and C = fp8_out_scale * (A . B^T).
 extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int* amap, const int* bmap, int batch,
                                int M, int N, int K, long long sA, long long sB, long long sC, int out_bf16,
-                               hipStream_t stream) {
-  if (K % 8 != 0) return -1;
+                               float fp8_out_scale, hipStream_t stream) {
+  const bool f8 = fp8_out_scale != 0.f;
+  if (K % (f8 ? 16 : 8) != 0) return -1;
   GemmArgs p{};
-  p.A = (const bf16*)A; p.B = (const bf16*)B; p.C = C; p.amap = amap; p.bmap = bmap;
+  p.A = A; p.B = B; p.C = C; p.amap = amap; p.bmap = bmap;
   p.M = M; p.N = N; p.K = K; p.sA = sA; p.sB = sB; p.sC = sC;
+  p.out_scale = fp8_out_scale;
   p.tiles_m = cdiv(M, BM); p.tiles_n = cdiv(N, BN);
   dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(256);
-  size_t lds = (size_t)(BM + BN) * BK * 2;
-  if (out_bf16) hipLaunchKernelGGL((corr_gemm_kernel<true, false>), grid, block, lds, stream, p);
-  else hipLaunchKernelGGL((corr_gemm_kernel<false, false>), grid, block, lds, stream, p);
+  size_t lds = (size_t)(BM + BN) * 128;
+  if (f8) {
+    if (out_bf16) hipLaunchKernelGGL((corr_gemm_kernel<true, false, true>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((corr_gemm_kernel<false, false, true>), grid, block, lds, stream, p);
+  } else {
+    if (out_bf16) hipLaunchKernelGGL((corr_gemm_kernel<true, false, false>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((corr_gemm_kernel<false, false, false>), grid, block, lds, stream, p);
+  }
   return (int)hipGetLastError();
 }
 
@@ -254,16 +326,19 @@ extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int*
 // 2x2-block order (see ncnet_block_order_rows); hA, wA, hB, wB even.
 extern "C" int ncnet_corr_gemm_pool2(const void* A, const void* B, float* pool_val, uint8_t* pool_idx, int batch,
                                      int hA, int wA, int hB, int wB, int K, long long sA, long long sB,
-                                     hipStream_t stream) {
-  if (K % 8 != 0 || (hA & 1) || (wA & 1) || (hB & 1) || (wB & 1)) return -1;
+                                     float fp8_out_scale, hipStream_t stream) {
+  const bool f8 = fp8_out_scale != 0.f;
+  if (K % (f8 ? 16 : 8) != 0 || (hA & 1) || (wA & 1) || (hB & 1) || (wB & 1)) return -1;
   GemmArgs p{};
-  p.A = (const bf16*)A; p.B = (const bf16*)B; p.C = nullptr;
+  p.A = A; p.B = B; p.C = nullptr;
   p.M = hA * wA; p.N = hB * wB; p.K = K; p.sA = sA; p.sB = sB;
+  p.out_scale = fp8_out_scale;
   p.tiles_m = cdiv(p.M, BM); p.tiles_n = cdiv(p.N, BN);
   p.pool_ks = 2; p.pool_val = pool_val; p.pool_idx = pool_idx;
   p.hA = hA; p.wA = wA; p.hB = hB; p.wB = wB;
   dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(256);
-  size_t lds = (size_t)(BM + BN) * BK * 2;
-  hipLaunchKernelGGL((corr_gemm_kernel<false, true>), grid, block, lds, stream, p);
+  size_t lds = (size_t)(BM + BN) * 128;
+  if (f8) hipLaunchKernelGGL((corr_gemm_kernel<false, true, true>), grid, block, lds, stream, p);
+  else hipLaunchKernelGGL((corr_gemm_kernel<false, true, false>), grid, block, lds, stream, p);
   return (int)hipGetLastError();
 }

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from ..ops import reference as ref
 from ..ops.conv4d import Conv4d
-from ..ops.correlation import correlation, correlation_pool2, l2norm_pack, maxpool4d as _maxpool4d
+from ..ops.correlation import correlation, correlation_pool2, l2norm_pack, l2norm_pack_fp8, maxpool4d as _maxpool4d
 from ..ops.mutual import mutual_matching
 from ..ops.neigh_consensus import neigh_consensus
 from .backbones import FrozenResNetPlan, build_trunk, fold_frozen_bn
@@ -168,7 +168,7 @@ class ImMatchNet(nn.Module):
                  ncons_kernel_sizes=(3, 3, 3), ncons_channels=(10, 10, 1), normalize_features: bool = True,
                  train_fe: bool = False, use_cuda: bool = True, relocalization_k_size: int = 0,
                  half_precision: bool = False, checkpoint: str | None = None, dtype: str = "bf16",
-                 fold_bn: bool = True):
+                 fold_bn: bool = True, corr_dtype: str = "bf16"):
         super().__init__()
         ck = None
         if checkpoint:
@@ -184,6 +184,10 @@ class ImMatchNet(nn.Module):
         self.half_precision = half_precision
         self.compute_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype]
         self.fold_bn = fold_bn
+        if corr_dtype not in ("bf16", "fp8"):
+            raise ValueError("corr_dtype must be 'bf16' or 'fp8'")
+        # fp8: OCP e4m3 correlation operands on the MX-fp8 MFMA (inference only)
+        self.corr_dtype = corr_dtype
         self.FeatureExtraction = FeatureExtraction(train_fe=train_fe, feature_extraction_cnn=feature_extraction_cnn,
                                                    feature_extraction_model_file=feature_extraction_model_file or "",
                                                    last_layer=feature_extraction_last_layer,
@@ -218,6 +222,10 @@ class ImMatchNet(nn.Module):
         if not self.FeatureExtraction.normalization:
             n, c, h, w = f.shape
             return f.permute(0, 2, 3, 1).reshape(n, h * w, c), (h, w)
+        if self.corr_dtype == "fp8":
+            if torch.is_grad_enabled() and self.training:
+                raise RuntimeError("corr_dtype='fp8' is an inference path (no autograd)")
+            return l2norm_pack_fp8(f), tuple(f.shape[-2:])
         return l2norm_pack(f), tuple(f.shape[-2:])
 
     def process_correlation(self, corr4d: torch.Tensor) -> torch.Tensor:

@@ -9,6 +9,11 @@
 * ``correlation_pool2``: the InLoc relocalization path; GEMM with a fused
   2x2x2x2 max-pool epilogue (lib/model.py:177-191) -- only the pooled volume
   and packed argmax offsets are written.
+* fp8 inference path (BASELINE config 5): ``l2norm_pack_fp8`` writes OCP
+  e4m3 operands scaled by ``FP8_FEAT_SCALE`` (unit rows have entries ~1/sqrt(C),
+  the scale keeps them out of the e4m3 subnormals) and both correlation entry
+  points accept them, running the MX-scaled K=128 fp8 MFMA (2x the bf16 rate)
+  and undoing the scale in the epilogue.  No autograd (inference only).
 """
 from __future__ import annotations
 
@@ -30,7 +35,7 @@ class L2NormPackFn(torch.autograd.Function):
         x2 = x.reshape(n * h * w, c)
         y = torch.empty((n * h * w, c), dtype=torch.bfloat16, device=feat.device)
         inv = torch.empty((n * h * w,), dtype=torch.float32, device=feat.device)
-        _ext.ext().l2norm_rows(x2, y, inv)
+        _ext.ext().l2norm_rows(x2, y, inv, 0.0)
         ctx.save_for_backward(x2, inv)
         ctx.shape = (n, c, h, w)
         ctx.in_dtype = feat.dtype
@@ -53,6 +58,33 @@ def l2norm_pack(feat: torch.Tensor) -> torch.Tensor:
     return ref.feature_l2norm(feat.float()).reshape(n, c, h * w).transpose(1, 2)
 
 
+FP8_FEAT_SCALE = 16.0
+FP8 = torch.float8_e4m3fn
+
+
+def l2norm_pack_fp8(feat: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] -> FP8_FEAT_SCALE * L2-normalised [N, H*W, C] in OCP fp8
+    e4m3 (GPU, inference).  CPU: the same values through torch's fp8 cast."""
+    n, c, h, w = feat.shape
+    if not _ext.use_hip(feat):
+        y = ref.feature_l2norm(feat.float()).reshape(n, c, h * w).transpose(1, 2) * FP8_FEAT_SCALE
+        return y.contiguous().to(FP8)
+    x = feat.permute(0, 2, 3, 1)
+    if not x.is_contiguous():
+        x = x.contiguous()
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        x = x.float()
+    y = torch.empty((n * h * w, c), dtype=FP8, device=feat.device)
+    _ext.ext().l2norm_rows(x.reshape(n * h * w, c), y, None, FP8_FEAT_SCALE)
+    return y.reshape(n, h * w, c)
+
+
+def _fp8_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """Row gather of an fp8 tensor (through a uint8 view: fp8 indexing kernels
+    are not guaranteed on every backend)."""
+    return t.view(torch.uint8)[:, idx].contiguous().view(FP8)
+
+
 def pack_rows(feat: torch.Tensor) -> torch.Tensor:
     """[N, C, H, W] -> [N, H*W, C] (no normalisation)."""
     n, c, h, w = feat.shape
@@ -66,7 +98,7 @@ class CorrelationFn(torch.autograd.Function):
         out = torch.empty((V, fa.shape[1], fb.shape[1]), dtype=torch.float32, device=fa.device)
         a = fa.to(torch.bfloat16).contiguous()
         b = fb.to(torch.bfloat16).contiguous()
-        _ext.ext().corr_gemm(a, b, out, amap, bmap)
+        _ext.ext().corr_gemm(a, b, out, amap, bmap, 1.0)
         ctx.save_for_backward(a, b, amap, bmap)
         ctx.dtypes = (fa.dtype, fb.dtype)
         return out
@@ -95,6 +127,13 @@ def correlation(fa: torch.Tensor, fb: torch.Tensor, amap: torch.Tensor | None = 
         amap = torch.arange(fa.shape[0], device=fa.device, dtype=torch.int32)
     if bmap is None:
         bmap = torch.arange(fb.shape[0], device=fb.device, dtype=torch.int32)
+    if fa.dtype == FP8:
+        scale = 1.0 / (FP8_FEAT_SCALE * FP8_FEAT_SCALE)
+        if not _ext.use_hip(fa):
+            return torch.bmm(fa.float()[amap.long()], fb.float()[bmap.long()].transpose(1, 2)) * scale
+        out = torch.empty((amap.numel(), fa.shape[1], fb.shape[1]), dtype=torch.float32, device=fa.device)
+        _ext.ext().corr_gemm(fa.contiguous(), fb.contiguous(), out, amap.to(torch.int32), bmap.to(torch.int32), scale)
+        return out
     if _ext.use_hip(fa):
         return CorrelationFn.apply(fa, fb, amap.to(torch.int32), bmap.to(torch.int32))
     return torch.bmm(fa.float()[amap.long()], fb.float()[bmap.long()].transpose(1, 2))
@@ -118,17 +157,22 @@ def correlation_pool2(fa: torch.Tensor, fb: torch.Tensor, hA: int, wA: int, hB: 
     (natural row order).  Returns (pooled [V,1,hA/2,wA/2,hB/2,wB/2] fp32,
     (di, dj, dk, dl) int64 offsets of the same shape)."""
     V = fa.shape[0]
+    fp8 = fa.dtype == FP8
+    scale = 1.0 / (FP8_FEAT_SCALE * FP8_FEAT_SCALE) if fp8 else 1.0
     if not _ext.use_hip(fa):
-        corr = torch.bmm(fa.float(), fb.float().transpose(1, 2)).view(V, 1, hA, wA, hB, wB)
+        corr = torch.bmm(fa.float(), fb.float().transpose(1, 2)).view(V, 1, hA, wA, hB, wB) * scale
         return ref.maxpool4d(corr, 2)
     pa = block_order_index(hA, wA, 2, fa.device)
     pb = block_order_index(hB, wB, 2, fb.device)
-    a = fa.to(torch.bfloat16)[:, pa].contiguous()
-    b = fb.to(torch.bfloat16)[:, pb].contiguous()
+    if fp8:
+        a, b = _fp8_rows(fa, pa), _fp8_rows(fb, pb)
+    else:
+        a = fa.to(torch.bfloat16)[:, pa].contiguous()
+        b = fb.to(torch.bfloat16)[:, pb].contiguous()
     shape = (V, hA // 2, wA // 2, hB // 2, wB // 2)
     val = torch.empty(shape, dtype=torch.float32, device=fa.device)
     code = torch.empty(shape, dtype=torch.uint8, device=fa.device)
-    _ext.ext().corr_gemm_pool2(a, b, val, code, hA, wA, hB, wB)
+    _ext.ext().corr_gemm_pool2(a, b, val, code, hA, wA, hB, wB, scale)
     return val.unsqueeze(1), decode_offsets(code.unsqueeze(1))
 
 

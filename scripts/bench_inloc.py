@@ -40,11 +40,13 @@ def main():
     ap.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 1])
     ap.add_argument("--src-hw", type=int, nargs=2, default=[3024, 4032], help="raw query size (iPhone7)")
     ap.add_argument("--no-matches", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="OCP fp8 correlation operands (MX-fp8 MFMA)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
     model = ImMatchNet(use_cuda=True, ncons_kernel_sizes=a.ncons_kernel_sizes, ncons_channels=a.ncons_channels,
-                       half_precision=True, relocalization_k_size=a.k).to(dev).eval()
+                       half_precision=True, relocalization_k_size=a.k,
+                       corr_dtype="fp8" if a.fp8 else "bf16").to(dev).eval()
     h, w = target_size(a.src_hw[0], a.src_hw[1], a.image_size, a.k)
     src = torch.randn(1, 3, h, w, device=dev)
     tgt = torch.randn(1, 3, h, w, device=dev)
@@ -88,7 +90,7 @@ def main():
         "metric": "InLoc dense matching latency per pair (fwd, k=%d relocalization)" % a.k,
         "value": round(ms, 3), "unit": "ms/pair", "higher_is_better": False,
         "pairs_per_s": round(1e3 / ms, 3), "n_gpus": 1, "pairs": a.pairs, "warmup": a.warmup,
-        "dtype": "bf16", "data": "synthetic (random 4:3 images, random-init weights)",
+        "dtype": "fp8-corr/bf16" if a.fp8 else "bf16", "data": "synthetic (random 4:3 images, random-init weights)",
         "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,
                    "ncons": [a.ncons_kernel_sizes, a.ncons_channels], "k": a.k},
         "stages_ms": {k: round(v / a.pairs, 3) for k, v in stages.items()},

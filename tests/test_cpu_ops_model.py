@@ -206,3 +206,16 @@ def test_frozen_resnet_plan_equivalence():
         r, p = t(x), plan(x)
     assert p.shape == r.shape
     assert ((p - r).norm() / r.norm()).item() < 1e-5
+
+
+def test_fp8_correlation_cpu_path():
+    from ncnet_amd.ops.correlation import FP8, FP8_FEAT_SCALE, correlation, l2norm_pack_fp8
+    torch.manual_seed(0)
+    f = torch.randn(2, 64, 5, 4)
+    y = l2norm_pack_fp8(f)
+    assert y.dtype == FP8 and y.shape == (2, 20, 64)
+    c = correlation(y, y)
+    cb = correlation(ref.feature_l2norm(f).reshape(2, 64, 20).transpose(1, 2),
+                     ref.feature_l2norm(f).reshape(2, 64, 20).transpose(1, 2))
+    assert float((c - cb).abs().max()) < 0.08
+    assert abs(FP8_FEAT_SCALE - 16.0) < 1e-9

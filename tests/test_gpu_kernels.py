@@ -304,3 +304,48 @@ def test_frozen_trunk_plan_gpu():
         p = FrozenResNetPlan(fold_frozen_bn(t), torch.bfloat16)(x)
     assert p.shape == r.shape
     assert rel_l2(p.float(), r) < 3e-2
+
+
+def test_fp8_l2norm_and_correlation():
+    """fp8 (OCP e4m3) operands: pack kernel vs torch's e4m3 cast, MX-fp8 MFMA
+    GEMM (plain and fused 2x2x2x2 pool) vs fp64 math on the same fp8 values.
+    Rows are long enough (K = 1024 = 8 MFMA k-blocks) that a wrong lane->k map
+    in the K=128 fragments cannot cancel out."""
+    from ncnet_amd.ops.correlation import (FP8, FP8_FEAT_SCALE, correlation, correlation_pool2, l2norm_pack_fp8)
+    torch.manual_seed(7)
+    f = torch.randn(2, 1024, 12, 10, device=DEV).contiguous(memory_format=torch.channels_last)
+    y = l2norm_pack_fp8(f)
+    assert y.dtype == FP8 and y.shape == (2, 120, 1024)
+    yr = (ref.feature_l2norm(f.double()).reshape(2, 1024, 120).transpose(1, 2) * FP8_FEAT_SCALE).float().to(FP8)
+    mism = (y.view(torch.uint8) != yr.view(torch.uint8)).float().mean().item()
+    assert mism < 1e-3, mism
+    fa, fb = y, y.flip(0).contiguous()
+    c = correlation(fa, fb)
+    cr = torch.bmm(fa.double(), fb.double().transpose(1, 2)) / FP8_FEAT_SCALE ** 2
+    assert relerr(c, cr) < 1e-4   # fp32 accumulation order only
+    # asymmetric: A rows vs B rows of different images and sizes
+    g = torch.randn(1, 1024, 8, 6, device=DEV).contiguous(memory_format=torch.channels_last)
+    yb = l2norm_pack_fp8(g)
+    c2 = correlation(y[:1], yb)
+    cr2 = torch.bmm(y[:1].double(), yb.double().transpose(1, 2)) / FP8_FEAT_SCALE ** 2
+    assert relerr(c2, cr2) < 1e-4
+    val, (di, dj, dk, dl) = correlation_pool2(fa, fb, 12, 10, 12, 10)
+    full = cr.view(2, 1, 12, 10, 12, 10).float()
+    vr, *offs = ref.maxpool4d(full, 2)
+    assert relerr(val, vr) < 1e-4
+
+
+def test_immatchnet_fp8_correlation_path():
+    """corr_dtype='fp8' inference volumes vs the bf16 path (same weights)."""
+    from ncnet_amd.models import ImMatchNet
+    torch.manual_seed(0)
+    m = ImMatchNet(use_cuda=True, ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1],
+                   relocalization_k_size=2).to(DEV).eval()
+    batch = {"source_image": torch.randn(1, 3, 256, 320, device=DEV),
+             "target_image": torch.randn(1, 3, 256, 320, device=DEV)}
+    with torch.inference_mode():
+        c16, d16 = m(batch)
+        m.corr_dtype = "fp8"
+        c8, d8 = m(batch)
+    assert c8.shape == c16.shape
+    assert rel_l2(c8, c16) < 0.1
