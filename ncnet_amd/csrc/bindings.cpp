@@ -9,13 +9,15 @@
 #include <hip/hip_runtime.h>
 
 extern "C" {
-int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv1in_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv1out_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad16v3(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_jpack(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_jsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_ijpack(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_ijsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_bias_act(void*, const float*, long long, int, int, hipStream_t);
 int ncnet_wgrad1(const void*, const void*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, hipStream_t);
@@ -64,24 +66,31 @@ int conv_pairs1o(int ks) { return ((ks + 3) * (ks + 3) + 1) / 2; }
 
 // X [V,I,J,K,L,16] bf16 -> Y [V,I,J,K,L,16] bf16, or (epi 3) fp32 [V,I,J,K,L,8] raw channels 0..7.
 // dj_center: only the dj = P input planes (j-offset encoded in channels).
+// X [V,I,J,K,L,16] (planes (i+di-P, j+dj-P), dj_center: dj = P only) or
+// X [G,V,I,J,K,L,16] (group planes: G input groups at the (i, j) plane, Wp [G, ...]).
+// epi: 0 none, 1 bias+ReLU, 2 ReLU-mask M, 3 fp32 channels 0..7 [...,8], 4 fp32 channel-planar [16,V,I,J,K,L]
 void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi,
                 int64_t dj_center) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
-  TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
-  TORCH_CHECK(epi >= 0 && epi <= 3);
-  if (epi == 3) {
+  const bool grp = X.dim() == 7;
+  TORCH_CHECK((X.dim() == 6 || grp) && X.size(-1) == 16, "X must be [V,I,J,K,L,16] or [G,V,I,J,K,L,16]");
+  const int64_t npg = grp ? X.size(0) : 0;
+  std::vector<int64_t> vs(X.sizes().begin() + (grp ? 1 : 0), X.sizes().end());   // [V,I,J,K,L,16]
+  TORCH_CHECK(epi >= 0 && epi <= 4);
+  if (epi == 3 || epi == 4) {
     check(Y, "Y", at::kFloat);
-    check_shape(Y, "Y", {X.size(0), X.size(1), X.size(2), X.size(3), X.size(4), 8});
+    if (epi == 3) check_shape(Y, "Y", {vs[0], vs[1], vs[2], vs[3], vs[4], 8});
+    else check_shape(Y, "Y", {16, vs[0], vs[1], vs[2], vs[3], vs[4]});   // channel-planar
   } else {
     check(Y, "Y", at::kBFloat16);
-    check_shape(Y, "Y", X.sizes().vec());
+    check_shape(Y, "Y", vs);
   }
-  check_shape(Wp, "Wp", {ks * ks, conv_pairs16(ks), 64, 8});
+  check_shape(Wp, "Wp", {grp ? npg : ks * ks, conv_pairs16(ks), 64, 8});
   if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
-  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", X.sizes().vec()); }
-  ok(ncnet_conv16_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), X.size(0),
-                      X.size(1), X.size(2), X.size(3), X.size(4), ks, epi, dj_center ? 1 : 0, cur_stream(X)),
+  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", vs); }
+  ok(ncnet_conv16_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), vs[0],
+                      vs[1], vs[2], vs[3], vs[4], ks, epi, dj_center ? 1 : 0, (int)npg, cur_stream(X)),
      "conv16_fwd");
 }
 
@@ -121,7 +130,8 @@ void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t 
   check_shape(G, "G", X.sizes().vec());
   const int64_t rows = part.size(0);
   TORCH_CHECK(rows > 0 && (variant == 1 || rows % 2 == 0), "wgrad16 v2/v3 need an even number of partial rows");
-  check_shape(part, "part", {rows, dj_center ? ks : ks * ks, ks * ks, 16, 16});
+  TORCH_CHECK(dj_center >= 0 && dj_center <= 2 && (dj_center < 2 || variant == 2), "plane-only wgrad needs variant 2");
+  check_shape(part, "part", {rows, dj_center == 2 ? 1 : (dj_center ? ks : ks * ks), ks * ks, 16, 16});
   check_shape(partb, "partb", {rows, 16});
   if (variant == 3) {
     ok(ncnet_wgrad16v3(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(0),
@@ -130,7 +140,7 @@ void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t 
     return;
   }
   ok(ncnet_wgrad16(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(0), X.size(1),
-                   X.size(2), X.size(3), X.size(4), ks, variant == 2 ? rows / 2 : rows, dj_center ? 1 : 0, variant,
+                   X.size(2), X.size(3), X.size(4), ks, variant == 2 ? rows / 2 : rows, (int)dj_center, variant,
                    cur_stream(X)), "wgrad16");
 }
 
@@ -156,6 +166,30 @@ void jsum(Tensor Z8, c10::optional<Tensor> bias, Tensor y, int64_t ks, int64_t r
   TORCH_CHECK(ks >= 1 && ks <= 8 && (sgn == 1 || sgn == -1));
   ok(ncnet_jsum((float*)Z8.data_ptr(), opt_ptr<float>(bias), (float*)y.data_ptr(), Z8.size(0), Z8.size(1), Z8.size(2),
                 Z8.size(3), Z8.size(4), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z8)), "jsum");
+}
+
+// X [V,I,J,K,L] (bf16/fp32) -> S [G,V,I,J,K,L,16] bf16 (ij encoding, G = ceil(ks*ks/16))
+void ijpack(Tensor X, Tensor S, int64_t ks, int64_t sgn) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  TORCH_CHECK(X.is_cuda() && X.is_contiguous() && (X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kFloat));
+  TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
+  TORCH_CHECK(ks >= 1 && ks <= 5 && (sgn == 1 || sgn == -1));
+  check(S, "S", at::kBFloat16);
+  check_shape(S, "S", {(ks * ks + 15) / 16, X.size(0), X.size(1), X.size(2), X.size(3), X.size(4), 16});
+  ok(ncnet_ijpack(X.data_ptr(), X.scalar_type() == at::kBFloat16, S.data_ptr(), X.size(0), X.size(1), X.size(2),
+                  X.size(3), X.size(4), ks, sgn, cur_stream(X)), "ijpack");
+}
+
+// Z [G,16,V,I,J,K,L] fp32 (channel-planar) -> y [V,I,J,K,L] fp32 (ij encoding)
+void ijsum(Tensor Z, c10::optional<Tensor> bias, Tensor y, int64_t ks, int64_t relu, int64_t sgn) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(Z.device());
+  check(Z, "Z", at::kFloat); check(y, "y", at::kFloat);
+  TORCH_CHECK(ks >= 1 && ks <= 5 && (sgn == 1 || sgn == -1));
+  TORCH_CHECK(Z.dim() == 7 && Z.size(0) == (ks * ks + 15) / 16 && Z.size(1) == 16, "Z must be [G,16,V,I,J,K,L]");
+  check_shape(y, "y", {Z.size(2), Z.size(3), Z.size(4), Z.size(5), Z.size(6)});
+  if (bias.has_value()) { check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
+  ok(ncnet_ijsum((float*)Z.data_ptr(), opt_ptr<float>(bias), (float*)y.data_ptr(), Z.size(2), Z.size(3), Z.size(4),
+                 Z.size(5), Z.size(6), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z)), "ijsum");
 }
 
 void wgrad1(Tensor S16, Tensor P1, Tensor part, int64_t ks, int64_t mode, int64_t ngroups) {
@@ -382,6 +416,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad1", &wgrad1);
   m.def("jpack", &jpack);
   m.def("jsum", &jsum);
+  m.def("ijpack", &ijpack);
+  m.def("ijsum", &ijsum);
   m.def("bias_act_", &bias_act_);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("l2norm_rows_bwd", &l2norm_rows_bwd);

@@ -25,7 +25,7 @@ namespace ncnet {
 
 // EPI_F32: raw fp32 accumulators of channels 0..7 into Y as float[..., 8]
 // (the j-shift-encoded 16 -> 1 layers, summed afterwards by jsum).
-enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32 = 3 };
+enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32 = 3, EPI_F32X16 = 4 };
 
 struct ConvGeom {
   int V, I, J, K, L;  // volume dims
@@ -34,6 +34,8 @@ struct ConvGeom {
   int PR, RS;         // staged plane rows / row stride (voxels)
   int RW;             // staged row width (voxels, <= RS)
   int dj_center;      // 1: only the dj = P planes (j-offset encoded in channels)
+  int npg;            // > 0: "group planes" mode (v2 only): plane s is the (i, j)
+  long long gstride;  //   plane of input group s at X + s * gstride, weights plane s
 };
 
 // Decode the workgroup's output tile.
@@ -107,9 +109,14 @@ __device__ __forceinline__ size_t plane_offset(const ConvGeom& g, int v, int i, 
 // of voxel (l & 15).
 template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
-                                        const float* __restrict__ bias, size_t vox_index, int co0) {
+                                        const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0) {
   if (EPI == EPI_F32) {
     if (co0 < 8) *(f32x4*)((float*)Y + vox_index * 8 + co0) = acc;
+    return;
+  }
+  if (EPI == EPI_F32X16) {   // channel-planar fp32 [16][nvox_all]: 16 lanes write 16 consecutive voxels
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ((float*)Y)[(size_t)(co0 + r) * nvox_all + vox_index] = acc[r];
     return;
   }
   float o[4];
@@ -282,7 +289,7 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
   const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
   const int dj_lo = g.dj_center ? P : max(0, P - t.j), dj_hi = g.dj_center ? P + 1 : min(KS, g.J + P - t.j);
   const int ndj = dj_hi - dj_lo;
-  const int nplanes = (di_hi - di_lo) * ndj;
+  const int nplanes = g.npg > 0 ? g.npg : (di_hi - di_lo) * ndj;
   const int nvox = g.TK * g.TL;
   const int ntile = (nvox + 15) >> 4;
 
@@ -315,7 +322,8 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
 
   auto issue_x = [&](int s, char* buf) {
     const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-    const bf16* xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
+    const bf16* xp = g.npg > 0 ? X + s * g.gstride + plane_offset(g, t.v, t.i, t.j, 16)
+                               : X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
     for (int r = wave; r < g.PR; r += NW) {
       const int kg = t.k0 - P + r;
       if (kg >= 0 && kg < g.K && lane < nchunk) {
@@ -326,7 +334,7 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
   };
   auto issue_w = [&](int s) {
     const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-    const u32x4* wp = Wp + (size_t)(di * KS + dj) * (NQ * 64);
+    const u32x4* wp = Wp + (size_t)(g.npg > 0 ? s : di * KS + dj) * (NQ * 64);
     for (int q = wave; q < NQ; q += NW)
       __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + q * 1024), 16, 0, 0);
   };
@@ -365,7 +373,8 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
       int kk = vi / g.TL, ll = vi - kk * g.TL;
       int kg = t.k0 + kk, lg = t.l0 + ll;
       if (vi < nvox && kg < g.K && lg < g.L)
-        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4));
+        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4),
+                     (size_t)g.V * g.I * g.J * g.K * g.L);
     }
   }
 }
@@ -661,6 +670,7 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.RS = tl + KS - 1 + extra_cols;
   g.RW = g.RS;
   g.dj_center = 0;
+  g.npg = 0; g.gstride = 0;
   return g;
 }
 
@@ -685,13 +695,20 @@ static int conv16_variant() {
   return v;
 }
 
+// npg > 0: group-planes mode -- X holds npg input groups [npg][V,I,J,K,L,16]
+// and Y = sum_s conv_(dk,dl)(X[s] plane (i,j), Wp plane s): the (di, dj)
+// offsets live in the channels (ij encoding, csrc/jshift.hip).
 extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias, const void* M, void* Y,
-                                int V, int I, int J, int K, int L, int KS, int epi, int dj_center,
+                                int V, int I, int J, int K, int L, int KS, int epi, int dj_center, int npg,
                                 hipStream_t stream) {
   int tk, tl;
   pick_tile(K, L, tk, tl);
   ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, 0, 0);
   g.dj_center = dj_center;
+  g.npg = npg;
+  g.gstride = (long long)V * I * J * K * L * 16;
+  if (npg > 0 && !(conv16_variant() == 2 && g.RW <= 32)) return -3;   // v2 only
+  if (epi == EPI_F32X16 && !(conv16_variant() == 2 && g.RW <= 32)) return -3;
   if (g.PR * g.RS * 2 > 8 * 256) return -1;
   int nq = (KS * KS + 1) / 2;
   const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
@@ -705,10 +722,12 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
 #define L16V2(KSV, EPIV) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV>), grid2, block2, lds2, stream, x, w, bias, m, y, g)
     if (KS == 5) {
       if (epi == EPI_BIAS_RELU) L16V2(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2(5, EPI_MASK);
-      else if (epi == EPI_F32) L16V2(5, EPI_F32); else L16V2(5, EPI_NONE);
+      else if (epi == EPI_F32) L16V2(5, EPI_F32); else if (epi == EPI_F32X16) L16V2(5, EPI_F32X16);
+      else L16V2(5, EPI_NONE);
     } else if (KS == 3) {
       if (epi == EPI_BIAS_RELU) L16V2(3, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2(3, EPI_MASK);
-      else if (epi == EPI_F32) L16V2(3, EPI_F32); else L16V2(3, EPI_NONE);
+      else if (epi == EPI_F32) L16V2(3, EPI_F32); else if (epi == EPI_F32X16) L16V2(3, EPI_F32X16);
+      else L16V2(3, EPI_NONE);
     } else return -2;
 #undef L16V2
     return (int)hipGetLastError();

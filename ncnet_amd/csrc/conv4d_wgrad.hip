@@ -29,7 +29,8 @@ struct WGeom {
   int PR, RS;          // staged X plane rows / row stride (wgrad16)
   int RW;              // staged row width (voxels, <= RS)
   int nitems, ipg;     // output tiles, tiles per group
-  int dj_center;       // 1: only the (di, dj = P) offsets (j-offset encoded in channels)
+  int dj_center;       // 1: only the (di, dj = P) offsets (j-offset encoded in channels);
+                       // 2: only (P, P) (v2: ij encoding, both offsets in channels)
 };
 
 struct Item { int v, i, j, k0, l0; };
@@ -222,9 +223,9 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tg = wave & 3, half = wave >> 2;
   const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int NDD = g.dj_center ? KS : NT;
+  const int NDD = g.dj_center == 2 ? 1 : (g.dj_center ? KS : NT);
   const int dd = lb % NDD, grp = lb / NDD;
-  const int di = g.dj_center ? dd : dd / KS, dj = g.dj_center ? P : dd % KS;
+  const int di = g.dj_center == 2 ? P : (g.dj_center ? dd : dd / KS), dj = g.dj_center ? P : dd % KS;
   const bool center = (di == P && dj == P);
 
   for (int o = threadIdx.x * 16; o < plane_bytes + nv32 * 32; o += NW * 64 * 16)
@@ -778,8 +779,9 @@ extern "C" int ncnet_wgrad16(const void* X, const void* G, float* part, float* p
   g.dj_center = dj_center;
   int nv32 = (g.TK * g.TL + 31) & ~31;
   size_t lds = (size_t)g.PR * g.RS * 32 + (size_t)nv32 * 32 + (size_t)nv32 * 4;
-  dim3 grid((unsigned)((dj_center ? KS : KS * KS) * ngroups));
+  dim3 grid((unsigned)((dj_center == 2 ? 1 : (dj_center ? KS : KS * KS)) * ngroups));
   const bf16* x = (const bf16*)X; const bf16* gg = (const bf16*)G;
+  if (dj_center == 2 && variant != 2) return -3;   // plane-only mode: v2 kernel
   if (variant == 2) {
     if (g.RW > 32 || g.TL > 32) return -1;   // one wave-instruction per staged row
     // row stride TL + 8: a row wrap inside an 8-voxel read group jumps 256 B

@@ -11,6 +11,14 @@
 //
 // so forward, data-gradient and weight-gradient of those layers all run on the
 // conv16 / wgrad16 MFMA kernels over KS planes instead of KS*KS.
+//
+// ij encoding (ijpack / ijsum): BOTH plane offsets (di, dj) go into channels,
+// combo q = di*KS + dj, 16 combos per group, G = ceil(KS*KS/16) groups
+// (KS=3: 1 group, 9/16 channels used; KS=5: 2 groups, 25/32):
+//   S[g][v,i,j,k,l,c] = X[v, i+sgn*(di-P), j+sgn*(dj-P), k, l],  q = 16g + c
+//   y[v,i,j,k,l]      = act(b + sum_q Z[g][v, i+sgn*(di-P), j+sgn*(dj-P), k, l, c])
+// and the 1-channel layers become conv16 over G "group planes" with (dk, dl)
+// taps only: 2.5x (KS=5) / 3x (KS=3) fewer MFMAs than the j encoding.
 #include "common.h"
 
 namespace ncnet {
@@ -59,6 +67,59 @@ __global__ __launch_bounds__(256) void jsum_kernel(const float* __restrict__ Z8,
   y[e] = relu ? fmaxf(s, 0.f) : s;
 }
 
+// ---------------------------------------------------------------------------
+template <typename T, int KS>
+__global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, bf16* __restrict__ S, long long nvox,
+                                                     int I, int J, int KL, int sgn) {
+  constexpr int P = KS / 2, NQ = KS * KS, G = (NQ + 15) / 16;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nvox) return;
+  const long long plane = e / KL;           // (v*I + i)*J + j
+  const int j = (int)(plane % J);
+  const int i = (int)((plane / J) % I);
+  const int kl = (int)(e - plane * KL);
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    bf16x8 h[2];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      const int q = 16 * g + c;
+      float v = 0.f;
+      if (q < NQ) {
+        const int ii = i + sgn * (q / KS - P), jj = j + sgn * (q % KS - P);
+        if (ii >= 0 && ii < I && jj >= 0 && jj < J) v = (float)X[(plane + (long long)(ii - i) * J + (jj - j)) * KL + kl];
+      }
+      h[c >> 3][c & 7] = f2bf(v);
+    }
+    bf16x8* o = (bf16x8*)(S + ((long long)g * nvox + e) * 16);
+    o[0] = h[0];
+    o[1] = h[1];
+  }
+}
+
+// Z is channel-planar: Z[q >> 4][q & 15][voxel] (conv16 EPI_F32X16 layout).
+template <int KS>
+__global__ __launch_bounds__(256) void ijsum_kernel(const float* __restrict__ Z, const float* __restrict__ bias,
+                                                    float* __restrict__ y, long long nvox, int I, int J, int KL,
+                                                    int relu, int sgn) {
+  constexpr int P = KS / 2, NQ = KS * KS;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nvox) return;
+  const long long plane = e / KL;
+  const int j = (int)(plane % J);
+  const int i = (int)((plane / J) % I);
+  float s = bias ? bias[0] : 0.f;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int ii = i + sgn * (q / KS - P), jj = j + sgn * (q % KS - P);
+    if (ii >= 0 && ii < I && jj >= 0 && jj < J)
+      s += Z[(long long)q * nvox + e + ((long long)(ii - i) * J + (jj - j)) * KL];
+  }
+  y[e] = relu ? fmaxf(s, 0.f) : s;
+}
+
 }  // namespace ncnet
 
 using namespace ncnet;
@@ -81,5 +142,27 @@ extern "C" int ncnet_jsum(const float* Z8, const float* bias, float* y, int V, i
   long long nvox = (long long)V * I * J * K * L;
   hipLaunchKernelGGL(jsum_kernel, dim3((unsigned)((nvox + 255) / 256)), dim3(256), 0, stream, Z8, bias, y, nvox, J,
                      K * L, KS, relu, sgn);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ncnet_ijpack(const void* X, int x_is_bf16, void* S, int V, int I, int J, int K, int L, int KS, int sgn,
+                            hipStream_t stream) {
+  long long nvox = (long long)V * I * J * K * L;
+  dim3 grid((unsigned)((nvox + 255) / 256));
+#define IJP(T, KSV) hipLaunchKernelGGL((ijpack_kernel<T, KSV>), grid, dim3(256), 0, stream, (const T*)X, (bf16*)S, nvox, I, J, K * L, sgn)
+  if (KS == 5) { if (x_is_bf16) IJP(bf16, 5); else IJP(float, 5); }
+  else if (KS == 3) { if (x_is_bf16) IJP(bf16, 3); else IJP(float, 3); }
+  else return -1;
+#undef IJP
+  return (int)hipGetLastError();
+}
+
+extern "C" int ncnet_ijsum(const float* Z, const float* bias, float* y, int V, int I, int J, int K, int L, int KS,
+                           int relu, int sgn, hipStream_t stream) {
+  long long nvox = (long long)V * I * J * K * L;
+  dim3 grid((unsigned)((nvox + 255) / 256));
+  if (KS == 5) hipLaunchKernelGGL((ijsum_kernel<5>), grid, dim3(256), 0, stream, Z, bias, y, nvox, I, J, K * L, relu, sgn);
+  else if (KS == 3) hipLaunchKernelGGL((ijsum_kernel<3>), grid, dim3(256), 0, stream, Z, bias, y, nvox, I, J, K * L, relu, sgn);
+  else return -1;
   return (int)hipGetLastError();
 }

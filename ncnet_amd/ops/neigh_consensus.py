@@ -24,8 +24,9 @@ import torch
 
 from . import _ext
 from . import reference as ref
-from .packing import (jc_in_grad, jc_in_weights, jc_out_grad, jc_out_weights, pack_w16, pack_w1in, pack_w1out,
-                      transpose_for_dgrad)
+from .packing import (ij_groups, ij_in_grad, ij_in_weights, ij_out_grad, ij_out_weights, jc_in_grad, jc_in_weights,
+                      jc_out_grad, jc_out_weights, pack_w16, pack_w16_planes, pack_w1in, pack_w1out,
+                      plane_dgrad_weights, transpose_for_dgrad)
 
 HIP_KS = (3, 5)
 # 1-channel layers through the j-offset channel encoding (csrc/jshift.hip) on
@@ -33,7 +34,14 @@ HIP_KS = (3, 5)
 # 1-channel kernels (conv1in / conv1out / wgrad1) instead.
 import os as _os
 
-USE_JC = _os.environ.get("NCNET_NC_JC", "1") == "1"
+# Encoding of the 1-channel layers: "ij" (default: both plane offsets in
+# channels, conv16 group-plane mode), "jc" (dj only), "direct" (conv1in /
+# conv1out / wgrad1 kernels).  NCNET_NC_JC=0 is the legacy spelling of "direct".
+ENC = _os.environ.get("NCNET_NC_ENC", "ij")
+if _os.environ.get("NCNET_NC_JC") == "0":
+    ENC = "direct"
+USE_JC = ENC == "jc"
+USE_IJ = ENC == "ij"
 # wgrad16 kernel: 3 = sliding G-plane ring (default), 2 = 8-wave LDS-DMA per
 # (di, dj) plane, 1 = 4-wave register-staged
 WGRAD_VARIANT = int(_os.environ.get("NCNET_WGRAD_VARIANT", "3"))
@@ -91,7 +99,13 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
         w = _std(w_ref)
         save.append(h)
         last = li == len(kinds) - 1
-        if kind == "1in" and USE_JC:
+        if kind == "1in" and USE_IJ:
+            xs = torch.empty((ij_groups(ks), V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
+            C.ijpack(h, xs, ks, 1)
+            save[-1] = xs  # the backward needs the ij-packed input
+            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
+            C.conv16_fwd(xs, pack_w16_planes(ij_in_weights(w)), _pad_bias(b, 16), None, y, ks, 1, 0)
+        elif kind == "1in" and USE_JC:
             xs = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
             C.jpack(h, xs, ks, 1)
             save[-1] = xs  # the backward needs the j-packed input
@@ -103,6 +117,18 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
         elif kind == "16":
             y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
             C.conv16_fwd(h, pack_w16(w), _pad_bias(b, 16), None, y, ks, 1, 0)
+        elif USE_IJ:   # "1out"
+            G = ij_groups(ks)
+            wz = pack_w16_planes(ij_out_weights(w))
+            z = torch.empty((G, 16, V, I, J, K, L), dtype=torch.float32, device=x0.device)   # channel-planar
+            hx = h.unsqueeze(0)
+            for gi in range(G):
+                C.conv16_fwd(hx, wz[gi:gi + 1], None, None, z[gi], ks, 4, 0)
+            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
+            C.ijsum(z, _pad_bias(b, 1), y, ks, 1, 1)
+            del z
+            if not last:
+                y = y.to(torch.bfloat16)
         elif USE_JC:
             z8 = torch.empty((V, I, J, K, L, 8), dtype=torch.float32, device=x0.device)
             C.conv16_fwd(h, pack_w16(jc_out_weights(w)), None, None, z8, ks, 3, 1)
@@ -139,23 +165,36 @@ def wgrad_v3_groups(shape, ks: int, dj_center: bool) -> int:
     return max(1, min(target, ncols))
 
 
-def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, ng: int, dj_center: bool):
+def wgrad_plane_groups(nitems: int) -> int:
+    """Groups of the plane-only wgrad (grid = groups): ~3 workgroups per CU."""
+    env = _os.environ.get("NCNET_WGRAD_PLANE_GROUPS")
+    return max(1, min(int(env) if env else 768, nitems))
+
+
+def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, ng: int, dj_center):
     """Run the wgrad16 kernel and reduce its per-group partials.
 
-    Returns (s, sb): s [dd, tap, ci, co] with dd = (di, dj) or di only when
-    ``dj_center``, sb [16] = sum of g16 over all voxels (bias gradient, from
-    the kernel's ones-MFMA in the centre block).  Variant 2 (default, 8-wave
-    LDS-DMA kernel) writes two partial rows per group.
+    ``dj_center``: False/0 all (di, dj) plane offsets, True/1 dj = P only (j
+    encoding), 2 only (P, P) (ij encoding, plane-only).  Returns (s, sb): s
+    [dd, tap, ci, co], sb [16] = sum of g16 over all voxels (bias gradient,
+    from the kernel's ones-MFMA in the centre block).  Variant 3 (sliding G
+    ring) serves modes 0/1, variant 2 (8-wave LDS-DMA) mode 2 and volumes too
+    wide for v3.
     """
+    mode = int(dj_center)
     variant = WGRAD_VARIANT
-    if variant == 3 and not wgrad_v3_ok(x16.shape, ks):
+    if mode == 2 or (variant == 3 and not wgrad_v3_ok(x16.shape, ks)):
         variant = 2
-    if variant == 3:
-        ng = wgrad_v3_groups(x16.shape, ks, dj_center)
+    if mode == 2:
+        V, I, J, K, L = x16.shape[:5]
+        ng = wgrad_plane_groups(V * I * J * ((K + 24) // 25) * ((L + 24) // 25))
+    elif variant == 3:
+        ng = wgrad_v3_groups(x16.shape, ks, bool(mode))
     rows = ng * (2 if variant >= 2 else 1)
-    part = torch.empty((rows, ks if dj_center else ks * ks, ks * ks, 16, 16), dtype=torch.float32, device=x16.device)
+    ndd = 1 if mode == 2 else (ks if mode else ks * ks)
+    part = torch.empty((rows, ndd, ks * ks, 16, 16), dtype=torch.float32, device=x16.device)
     partb = torch.empty((rows, 16), dtype=torch.float32, device=x16.device)
-    C.wgrad16(x16, g16, part, partb, ks, 1 if dj_center else 0, variant)
+    C.wgrad16(x16, g16, part, partb, ks, mode, variant)
     return part.sum(0), partb.sum(0)
 
 
@@ -192,11 +231,40 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
         cout = channels[li]
         cin = 1 if li == 0 else channels[li - 1]
         w = _std(w_ref)
-        V, I, J, K, L = h.shape[:5]
+        V, I, J, K, L = h.shape[1:6] if h.dim() == 7 else h.shape[:5]
         nitems = V * I * J * ((K + 24) // 25) * ((L + 24) // 25)
         ng = wgrad_groups(ks, nitems)
         mask_prev = h if li > 0 else None   # ReLU output of the previous layer
-        if kind == "1out" and USE_JC:
+        if kind == "1out" and USE_IJ:
+            G = ij_groups(ks)
+            gs = torch.empty((G,) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
+            C.ijpack(g, gs, ks, -1)                  # adjoint of ijsum
+            parts = [wgrad16_partials(C, h, gs[gi], ks, ng, 2) for gi in range(G)]
+            dw = ij_out_grad(torch.stack([p[0][0] for p in parts]), cin)
+            qc = (ks // 2) * ks + ks // 2            # combo (P, P): its channel of ijpack(g, -1) is g itself
+            db = parts[qc // 16][1][qc % 16].reshape(1)
+            if li > 0 or need_dx0:
+                gi_ = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
+                wd = pack_w16_planes(plane_dgrad_weights(ij_out_weights(w)))
+                C.conv16_fwd(gs, wd, None, mask_prev, gi_, ks, 2 if mask_prev is not None else 0, 0)
+                g = gi_
+            del gs
+        elif kind == "1in" and USE_IJ:               # h is ijpack(X0) [G, ...]
+            G = h.shape[0]
+            parts = [wgrad16_partials(C, h[gi], g, ks, ng, 2) for gi in range(G)]
+            dw = ij_in_grad(torch.stack([p[0][0] for p in parts]), cout)
+            db = parts[0][1][:cout]
+            if li > 0:
+                raise RuntimeError("internal: 1in layer must be first")
+            if need_dx0:
+                wd = pack_w16_planes(plane_dgrad_weights(ij_in_weights(w)))
+                z = torch.empty((G, 16, V, I, J, K, L), dtype=torch.float32, device=h.device)
+                gx = g.unsqueeze(0)
+                for gi in range(G):
+                    C.conv16_fwd(gx, wd[gi:gi + 1], None, None, z[gi], ks, 4, 0)
+                gx0 = torch.empty((V, I, J, K, L), dtype=torch.float32, device=h.device)
+                C.ijsum(z, None, gx0, ks, 0, -1)      # adjoint of ijpack(+1)
+        elif kind == "1out" and USE_JC:
             gs = torch.empty(tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
             C.jpack(g, gs, ks, -1)                   # adjoint of jsum
             sw, sb = wgrad16_partials(C, h, gs, ks, ng, True)

@@ -145,3 +145,62 @@ def jc_out_grad(s5: torch.Tensor, cin: int) -> torch.Tensor:
     """dW of the dj=P slice [c, ci, di, dk, dl] -> [1, ci, di, dj=c, dk, dl]."""
     ks = s5.shape[-1]
     return s5[:ks, :cin].permute(1, 2, 0, 3, 4).unsqueeze(0).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# ij encoding (csrc/jshift.hip ijpack / ijsum): both plane offsets (di, dj) go
+# into channels, combo q = di*k + dj, 16 combos per group, G = ceil(k*k/16).
+# A Cin=1 layer becomes sum_g conv2d_(dk,dl)(ijpack(X0)[g], W_g) and a Cout=1
+# layer ijsum(conv2d_(dk,dl)(X, W_g) for each g), all on conv16's group-plane
+# mode; plane weights are [G, 16 out, 16 in, k, k].
+
+def ij_groups(ks: int) -> int:
+    return (ks * ks + 15) // 16
+
+
+def pack_w16_planes(wp: torch.Tensor) -> torch.Tensor:
+    """[NPL, 16 co, 16 ci, k, k] -> [NPL, ceil(k*k/2), 64, 8] (pack_w16 per plane)."""
+    npl, ks = wp.shape[0], wp.shape[-1]
+    w = wp.reshape(npl, 16, 16, ks * ks)
+    co, ci, tap, valid = (t.to(w.device) for t in _idx16(ks))
+    vals = w[:, co, ci, tap] * valid.to(w.dtype)      # [npl, nq, 64, 8]
+    return vals.contiguous().to(torch.bfloat16)
+
+
+def ij_in_weights(w_std: torch.Tensor) -> torch.Tensor:
+    """[co, 1, k^4] -> [G, 16 co, 16 c, k, k]: out[g][co][c] = w[co][0][di][dj] with 16g + c = di*k + dj."""
+    co, ks = w_std.shape[0], w_std.shape[-1]
+    G = ij_groups(ks)
+    tmp = w_std.new_zeros((16, G * 16, ks, ks))
+    tmp[:co, : ks * ks] = w_std[:, 0].reshape(co, ks * ks, ks, ks)
+    return tmp.view(16, G, 16, ks, ks).permute(1, 0, 2, 3, 4).contiguous()
+
+
+def ij_out_weights(w_std: torch.Tensor) -> torch.Tensor:
+    """[1, ci, k^4] -> [G, 16 c, 16 ci, k, k]: out[g][c][ci] = w[0][ci][di][dj] with 16g + c = di*k + dj."""
+    ci, ks = w_std.shape[1], w_std.shape[-1]
+    G = ij_groups(ks)
+    tmp = w_std.new_zeros((G * 16, 16, ks, ks))
+    tmp[: ks * ks, :ci] = w_std[0].reshape(ci, ks * ks, ks, ks).permute(1, 0, 2, 3)
+    return tmp.view(G, 16, 16, ks, ks).contiguous()
+
+
+def plane_dgrad_weights(wp: torch.Tensor) -> torch.Tensor:
+    """Data-gradient weights of a (dk, dl)-only plane conv: swap channels, flip taps."""
+    return wp.transpose(1, 2).flip(-2, -1)
+
+
+def ij_in_grad(s: torch.Tensor, cout: int) -> torch.Tensor:
+    """s [G, tap, c, co] (plane wgrad of X = ijpack(X0)[g], G = grad) -> dW [co, 1, k, k, k, k]."""
+    G, nt = s.shape[0], s.shape[1]
+    ks = int(round(nt ** 0.5))
+    d = s.permute(3, 0, 2, 1).reshape(16, G * 16, nt)[:cout, :nt]      # [co, q, tap]
+    return d.reshape(cout, 1, ks, ks, ks, ks).contiguous()
+
+
+def ij_out_grad(s: torch.Tensor, cin: int) -> torch.Tensor:
+    """s [G, tap, ci, c] (plane wgrad of X = layer input, G = ijpack(g, -1)[g]) -> dW [1, ci, k, k, k, k]."""
+    G, nt = s.shape[0], s.shape[1]
+    ks = int(round(nt ** 0.5))
+    d = s.permute(2, 0, 3, 1).reshape(16, G * 16, nt)[:cin, :nt]      # [ci, q, tap]
+    return d.reshape(1, cin, ks, ks, ks, ks).contiguous()

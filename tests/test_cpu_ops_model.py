@@ -219,3 +219,13 @@ def test_fp8_correlation_cpu_path():
                      ref.feature_l2norm(f).reshape(2, 64, 20).transpose(1, 2))
     assert float((c - cb).abs().max()) < 0.08
     assert abs(FP8_FEAT_SCALE - 16.0) < 1e-9
+
+
+def test_extension_imports_when_built():
+    """A built _C.so must import on CPU too (catches unresolved launcher symbols
+    before a GPU run)."""
+    from ncnet_amd.ops import _ext
+    so = os.path.join(os.path.dirname(_ext.__file__), "..", "_C.so")
+    if not os.path.exists(so):
+        pytest.skip("extension not built")
+    assert _ext.load() is not None
