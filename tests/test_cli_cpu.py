@@ -51,3 +51,10 @@ def test_inloc_export_contract(workdir):
     # de-duplicated and in lexicographic (xA, yA, xB, yB) order like np.unique
     rows = [tuple(r) for r in xy]
     assert rows == sorted(set(rows))
+
+
+def test_point_transfer_demo(workdir):
+    import point_transfer_demo
+    out = os.path.join(workdir, "demo.png")
+    acc = point_transfer_demo.main(["--synthetic", "--image_size", "160", "--out", out])
+    assert os.path.exists(out) and 0.0 <= acc <= 1.0

@@ -1,0 +1,43 @@
+import os
+
+import numpy as np
+import torch
+
+from ncnet_amd.data.transforms import normalize_image
+from ncnet_amd.utils.plot import denormalize_image, plot_image, save_plot
+from ncnet_amd.utils.torch_util import (BatchToDevice, collate_custom, create_file_path, expand_dim, softmax_1d,
+                                        str_to_bool)
+
+
+def test_collate_custom_keeps_lists():
+    b = [{"a": torch.ones(2), "pts": [1, 2]}, {"a": torch.zeros(2), "pts": [3]}]
+    out = collate_custom(b)
+    assert out["a"].shape == (2, 2)
+    assert out["pts"] == [[1, 2], [3]]
+
+
+def test_batch_to_device_softmax_expand(tmp_path):
+    out = BatchToDevice("cpu")({"x": torch.ones(3), "name": "q"})
+    assert out["name"] == "q" and out["x"].device.type == "cpu"
+    x = torch.randn(4, 5)
+    assert torch.allclose(softmax_1d(x, 1), torch.softmax(x, 1))
+    assert expand_dim(torch.ones(1, 3), 0, 4).shape == (4, 3)
+    p = tmp_path / "a" / "b" / "c.txt"
+    create_file_path(str(p))
+    assert os.path.isdir(p.parent)
+    assert str_to_bool("yes") and not str_to_bool("0")
+
+
+def test_plot_roundtrip(tmp_path):
+    img = torch.rand(3, 8, 10)
+    arr = plot_image(normalize_image(img), return_im=True)
+    assert arr.shape == (8, 10, 3) and arr.dtype == np.uint8
+    assert np.abs(arr.astype(float) - img.permute(1, 2, 0).numpy() * 255).max() <= 1.0
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    plt.figure()
+    plt.imshow(denormalize_image(normalize_image(img)))
+    save_plot(str(tmp_path / "x.png"))
+    plt.close("all")
+    assert (tmp_path / "x.png").exists()
