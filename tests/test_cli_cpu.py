@@ -58,3 +58,21 @@ def test_point_transfer_demo(workdir):
     out = os.path.join(workdir, "demo.png")
     acc = point_transfer_demo.main(["--synthetic", "--image_size", "160", "--out", out])
     assert os.path.exists(out) and 0.0 <= acc <= 1.0
+
+
+def test_inloc_localize_synthetic(workdir):
+    import inloc_localize
+    est, rate = inloc_localize.main(["--synthetic", "2", "--out", os.path.join(workdir, "poses.npz")])
+    assert len(est) == 2 and rate[-1] == 1.0
+    assert os.path.exists(os.path.join(workdir, "poses.npz"))
+
+
+def test_reference_refposes_parse():
+    """The reference's own GT pose file (MATLAB v5, read with scipy.io.loadmat)."""
+    import inloc_localize
+    path = "/root/reference/lib_matlab/DUC_refposes_all.mat"
+    if not os.path.exists(path):
+        pytest.skip("reference GT poses not present")
+    refs = inloc_localize.load_refposes(path)
+    assert len(refs) == 198 + 131
+    assert refs[0]["P"].shape == (3, 4) and refs[0]["floor"] == "DUC1"
