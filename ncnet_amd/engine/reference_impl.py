@@ -59,3 +59,25 @@ def reference_weak_loss(alg: ReferenceAlgorithm, batch) -> torch.Tensor:
     batch["source_image"] = batch["source_image"][np.roll(np.arange(b), -1)]
     neg = ref.match_score(alg(batch))
     return neg - pos
+
+
+def reference_inloc_forward(alg: ReferenceAlgorithm, src: torch.Tensor, tgt: torch.Tensor, k_size: int = 2,
+                            nc_dtype: torch.dtype = torch.float16):
+    """eval_inloc.py's forward as the reference executes it: fp32 (or alg.dtype)
+    backbone on both images, then ``.half()`` volume (lib/model.py:265-267),
+    torch.bmm correlation of the full-resolution volume, the k^4-slice
+    maxpool4d (lib/model.py:177-191, batch 1), MutualMatching, the per-slice
+    conv3d NeighConsensus and MutualMatching -- the InLoc baseline."""
+    fa = alg._fe(src).to(nc_dtype)
+    fb = alg._fe(tgt).to(nc_dtype)
+    corr = ref.correlation_4d(fa, fb)
+    delta = None
+    if k_size > 1:
+        corr, delta = ref.maxpool4d(corr, k_size)
+    corr = ref.mutual_matching(corr)
+    layers = alg.m.NeighConsensus.conv_layers()
+    ws = [l.weight_ref().to(nc_dtype) for l in layers]
+    bs = [l.bias.to(nc_dtype) for l in layers]
+    corr = ref.neigh_consensus(corr, ws, bs, symmetric=True, conv=ref.conv4d_sliced)
+    corr = ref.mutual_matching(corr)
+    return corr, delta

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--src-hw", type=int, nargs=2, default=[3024, 4032], help="raw query size (iPhone7)")
     ap.add_argument("--no-matches", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="OCP fp8 correlation operands (MX-fp8 MFMA)")
+    ap.add_argument("--impl", choices=["hip", "reference"], default="hip",
+                    help="reference: the reference algorithm in plain PyTorch-ROCm (fp32 backbone, fp16 volume)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -54,7 +56,28 @@ def main():
     stages = {"backbone": 0.0, "corr_pool": 0.0, "mm_nc_mm": 0.0, "matches": 0.0}
     nmatch = 0
 
+    if a.impl == "reference":
+        from ncnet_amd.engine.reference_impl import ReferenceAlgorithm, reference_inloc_forward
+        alg = ReferenceAlgorithm(model, torch.float32)
+
+    def one_ref(timed: bool):
+        nonlocal nmatch
+        with torch.inference_mode():
+            ev[0].record()
+            corr4d, delta = reference_inloc_forward(alg, src, tgt, a.k)
+            ev[3].record()
+            if not a.no_matches:
+                m = pair_matches(corr4d.float(), tuple(d.long() for d in delta) if delta else None, a.k, True, True)
+                nmatch = int(m.shape[0])
+            ev[4].record()
+        if timed:
+            torch.cuda.synchronize()
+            stages["mm_nc_mm"] += ev[0].elapsed_time(ev[3])
+            stages["matches"] += ev[3].elapsed_time(ev[4])
+
     def one(timed: bool):
+        if a.impl == "reference":
+            return one_ref(timed)
         nonlocal nmatch
         with torch.inference_mode():
             ev[0].record()
@@ -90,7 +113,9 @@ def main():
         "metric": "InLoc dense matching latency per pair (fwd, k=%d relocalization)" % a.k,
         "value": round(ms, 3), "unit": "ms/pair", "higher_is_better": False,
         "pairs_per_s": round(1e3 / ms, 3), "n_gpus": 1, "pairs": a.pairs, "warmup": a.warmup,
-        "dtype": "fp8-corr/bf16" if a.fp8 else "bf16", "data": "synthetic (random 4:3 images, random-init weights)",
+        "impl": a.impl,
+        "dtype": ("fp32-backbone/fp16-volume" if a.impl == "reference" else ("fp8-corr/bf16" if a.fp8 else "bf16")),
+        "data": "synthetic (random 4:3 images, random-init weights)",
         "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,
                    "ncons": [a.ncons_kernel_sizes, a.ncons_channels], "k": a.k},
         "stages_ms": {k: round(v / a.pairs, 3) for k, v in stages.items()},
