@@ -74,7 +74,7 @@ def main(argv=None):
     bucket = GradBucket(params, ctx)
 
     # a small pool of synthetic batches (random normalised images), generated on device
-    gen = torch.Generator(device=dev).manual_seed(1234 + ctx.rank)
+    gen = torch.Generator(device=dev).manual_seed(1234 + ctx.rank)   # (CPU: gloo smoke runs only)
     s = args.image_size
     pool = [{"source_image": torch.randn(args.batch, 3, s, s, device=dev, generator=gen),
              "target_image": torch.randn(args.batch, 3, s, s, device=dev, generator=gen)} for _ in range(2)]
@@ -99,11 +99,15 @@ def main(argv=None):
             opt.step()
             return loss
 
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
     for w in range(args.warmup):
         loss = step(pool[w % len(pool)])
-    torch.cuda.synchronize(dev)
+    sync()
     barrier(ctx)
-    torch.cuda.synchronize(dev)
+    sync()
 
     prof = None
     if args.profile and ctx.is_main:
@@ -113,9 +117,9 @@ def main(argv=None):
     t0 = time.perf_counter()
     for it in range(args.steps):
         loss = step(pool[it % len(pool)])
-    torch.cuda.synchronize(dev)
+    sync()
     barrier(ctx)
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
     if prof is not None:
         prof.__exit__(None, None, None)
@@ -127,9 +131,11 @@ def main(argv=None):
     ms_per_step = 1000.0 * elapsed / args.steps
     pairs_per_s = args.batch * ctx.world_size * args.steps / elapsed
     base = _baseline()
+    # vs_baseline = value / the BASELINE.md number (the reference algorithm
+    # measured on ONE MI355X); per-GPU ratio = vs_baseline / n_gpus.
     vs = None
     if base:
-        vs = pairs_per_s / (base * ctx.world_size)
+        vs = pairs_per_s / base
     if ctx.is_main:
         rec = {
             "metric": "image-pairs/sec fwd+bwd, ResNet-101+NC-Net(5,5,5) 400x400 bf16",
@@ -147,7 +153,7 @@ def main(argv=None):
             "config": {"model": "ResNet-101(layer3)+NC-Net ncons 5,5,5/16,16,1", "global_batch": args.batch * ctx.world_size,
                        "per_gpu_batch": args.batch, "seq_len": None, "image_size": s,
                        "parallelism": f"dp{ctx.world_size}", "impl": args.impl,
-                       "final_loss": float(loss)},
+                       "baseline_pairs_per_s_1gpu": base, "final_loss": float(loss.detach())},
         }
         print(json.dumps(rec), flush=True)
     from ncnet_amd.parallel.dist import destroy

@@ -71,3 +71,23 @@ def test_dp_gradients_equal_mean_of_shards(tmp_path):
     # disjoint shards covering the data
     s0, s1 = res[0]["shard"], res[1]["shard"]
     assert not set(s0) & set(s1) and len(s0) == len(s1) == 5
+
+
+def test_bench_torchrun_two_ranks_cpu(tmp_path):
+    """The driver's multi-GPU launch line, on CPU/gloo at a toy size: two ranks,
+    one JSON line from rank 0 with whole-job throughput and dp2."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2", NCNET_FORCE_TORCH="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29731", os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1",
+           "--warmup", "1", "--batch", "2", "--image-size", "64"]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 4
+    assert rec["value"] > 0 and rec["steps"] == 1 and rec["warmup"] == 1
