@@ -41,7 +41,13 @@ ENC = _os.environ.get("NCNET_NC_ENC", "ij")
 if _os.environ.get("NCNET_NC_JC") == "0":
     ENC = "direct"
 USE_JC = ENC == "jc"
-USE_IJ = ENC == "ij"
+USE_IJ = ENC in ("ij", "ijfull")
+# "ij" keeps the Cout=1 layer's forward and data gradient on the j encoding
+# (one conv pass with an 8-channel fp32 output beats two group-plane passes
+# with 16-channel planar outputs at 25^4: measured 1.97 vs 2.56 ms fwd) and
+# uses the ij encoding for its weight gradient (plane-only wgrad, 1.5 vs
+# 1.8 ms); "ijfull" runs that layer entirely on the ij encoding.
+OUT_IJ_FWD = ENC == "ijfull"
 # wgrad16 kernel: 3 = sliding G-plane ring (default), 2 = 8-wave LDS-DMA per
 # (di, dj) plane, 1 = 4-wave register-staged
 WGRAD_VARIANT = int(_os.environ.get("NCNET_WGRAD_VARIANT", "3"))
@@ -117,7 +123,7 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
         elif kind == "16":
             y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
             C.conv16_fwd(h, pack_w16(w), _pad_bias(b, 16), None, y, ks, 1, 0)
-        elif USE_IJ:   # "1out"
+        elif USE_IJ and OUT_IJ_FWD:   # "1out"
             G = ij_groups(ks)
             wz = pack_w16_planes(ij_out_weights(w))
             z = torch.empty((G, 16, V, I, J, K, L), dtype=torch.float32, device=x0.device)   # channel-planar
@@ -129,7 +135,7 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
             del z
             if not last:
                 y = y.to(torch.bfloat16)
-        elif USE_JC:
+        elif USE_JC or USE_IJ:
             z8 = torch.empty((V, I, J, K, L, 8), dtype=torch.float32, device=x0.device)
             C.conv16_fwd(h, pack_w16(jc_out_weights(w)), None, None, z8, ks, 3, 1)
             y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
@@ -243,12 +249,21 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
             dw = ij_out_grad(torch.stack([p[0][0] for p in parts]), cin)
             qc = (ks // 2) * ks + ks // 2            # combo (P, P): its channel of ijpack(g, -1) is g itself
             db = parts[qc // 16][1][qc % 16].reshape(1)
+            del gs
             if li > 0 or need_dx0:
                 gi_ = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
-                wd = pack_w16_planes(plane_dgrad_weights(ij_out_weights(w)))
-                C.conv16_fwd(gs, wd, None, mask_prev, gi_, ks, 2 if mask_prev is not None else 0, 0)
+                if OUT_IJ_FWD:
+                    gs = torch.empty((G,) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
+                    C.ijpack(g, gs, ks, -1)
+                    wd = pack_w16_planes(plane_dgrad_weights(ij_out_weights(w)))
+                    C.conv16_fwd(gs, wd, None, mask_prev, gi_, ks, 2 if mask_prev is not None else 0, 0)
+                else:                                # j encoding: 1 pass over the KS dj = P planes
+                    gs = torch.empty(tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
+                    C.jpack(g, gs, ks, -1)
+                    wt = transpose_for_dgrad(jc_out_weights(w))
+                    C.conv16_fwd(gs, pack_w16(wt), None, mask_prev, gi_, ks, 2 if mask_prev is not None else 0, 1)
                 g = gi_
-            del gs
+                del gs
         elif kind == "1in" and USE_IJ:               # h is ijpack(X0) [G, ...]
             G = h.shape[0]
             parts = [wgrad16_partials(C, h[gi], g, ks, ng, 2) for gi in range(G)]
