@@ -9,7 +9,7 @@
 #include <hip/hip_runtime.h>
 
 extern "C" {
-int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv1in_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv1out_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -27,7 +27,7 @@ int ncnet_corr_gemm(const void*, const void*, void*, const int*, const int*, int
 int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, int, int, int, int, long long, long long,
                           float, hipStream_t);
 int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, hipStream_t);
-int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, hipStream_t);
+int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, float*, int, hipStream_t);
 int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, hipStream_t);
 int ncnet_mm_bwd(const float*, const float*, const float*, const int*, const float*, const int*, float*, float*, float*,
                  int, int, int, float, hipStream_t);
@@ -68,7 +68,7 @@ int conv_pairs1o(int ks) { return ((ks + 3) * (ks + 3) + 1) / 2; }
 // dj_center: only the dj = P input planes (j-offset encoded in channels).
 // X [V,I,J,K,L,16] (planes (i+di-P, j+dj-P), dj_center: dj = P only) or
 // X [G,V,I,J,K,L,16] (group planes: G input groups at the (i, j) plane, Wp [G, ...]).
-// epi: 0 none, 1 bias+ReLU, 2 ReLU-mask M, 3 fp32 channels 0..7 [...,8], 4 fp32 channel-planar [16,V,I,J,K,L]
+// epi: 0 none, 1 bias+ReLU, 2 ReLU-mask M, 3/4 fp32 channel-planar [nco,V,I,J,K,L] (nco <= 8 / 16)
 void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi,
                 int64_t dj_center) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
@@ -78,10 +78,12 @@ void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<T
   const int64_t npg = grp ? X.size(0) : 0;
   std::vector<int64_t> vs(X.sizes().begin() + (grp ? 1 : 0), X.sizes().end());   // [V,I,J,K,L,16]
   TORCH_CHECK(epi >= 0 && epi <= 4);
-  if (epi == 3 || epi == 4) {
+  int64_t nco = 16;
+  if (epi == 3 || epi == 4) {   // channel-planar fp32 [nco, V,I,J,K,L]: the first nco output channels
     check(Y, "Y", at::kFloat);
-    if (epi == 3) check_shape(Y, "Y", {vs[0], vs[1], vs[2], vs[3], vs[4], 8});
-    else check_shape(Y, "Y", {16, vs[0], vs[1], vs[2], vs[3], vs[4]});   // channel-planar
+    nco = Y.size(0);
+    TORCH_CHECK(nco >= 1 && nco <= (epi == 3 ? 8 : 16), "planar output channels out of range");
+    check_shape(Y, "Y", {nco, vs[0], vs[1], vs[2], vs[3], vs[4]});
   } else {
     check(Y, "Y", at::kBFloat16);
     check_shape(Y, "Y", vs);
@@ -90,7 +92,7 @@ void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<T
   if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
   if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", vs); }
   ok(ncnet_conv16_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), vs[0],
-                      vs[1], vs[2], vs[3], vs[4], ks, epi, dj_center ? 1 : 0, (int)npg, cur_stream(X)),
+                      vs[1], vs[2], vs[3], vs[4], ks, epi, dj_center ? 1 : 0, (int)npg, (int)nco, cur_stream(X)),
      "conv16_fwd");
 }
 
@@ -156,16 +158,16 @@ void jpack(Tensor X, Tensor S, int64_t ks, int64_t sgn) {
                  X.size(3), X.size(4), ks, sgn, cur_stream(X)), "jpack");
 }
 
-// Z8 [V,I,J,K,L,8] fp32 -> y [V,I,J,K,L] fp32, y = act(b + sum_{c<ks} Z8[v,i,j+c-P,k,l,c])
+// Z8 [>=ks,V,I,J,K,L] fp32 (channel-planar) -> y [V,I,J,K,L] fp32, y = act(b + sum_{c<ks} Z8[c][v,i,j+sgn*(c-P),k,l])
 void jsum(Tensor Z8, c10::optional<Tensor> bias, Tensor y, int64_t ks, int64_t relu, int64_t sgn) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(Z8.device());
   check(Z8, "Z8", at::kFloat); check(y, "y", at::kFloat);
-  TORCH_CHECK(Z8.dim() == 6 && Z8.size(5) == 8);
-  check_shape(y, "y", {Z8.size(0), Z8.size(1), Z8.size(2), Z8.size(3), Z8.size(4)});
+  TORCH_CHECK(Z8.dim() == 6 && Z8.size(0) >= ks, "Z8 must be [>=ks,V,I,J,K,L]");
+  check_shape(y, "y", {Z8.size(1), Z8.size(2), Z8.size(3), Z8.size(4), Z8.size(5)});
   if (bias.has_value()) { check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
   TORCH_CHECK(ks >= 1 && ks <= 8 && (sgn == 1 || sgn == -1));
-  ok(ncnet_jsum((float*)Z8.data_ptr(), opt_ptr<float>(bias), (float*)y.data_ptr(), Z8.size(0), Z8.size(1), Z8.size(2),
-                Z8.size(3), Z8.size(4), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z8)), "jsum");
+  ok(ncnet_jsum((float*)Z8.data_ptr(), opt_ptr<float>(bias), (float*)y.data_ptr(), Z8.size(1), Z8.size(2), Z8.size(3),
+                Z8.size(4), Z8.size(5), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z8)), "jsum");
 }
 
 // X [V,I,J,K,L] (bf16/fp32) -> S [G,V,I,J,K,L,16] bf16 (ij encoding, G = ceil(ks*ks/16))
@@ -180,16 +182,16 @@ void ijpack(Tensor X, Tensor S, int64_t ks, int64_t sgn) {
                   X.size(3), X.size(4), ks, sgn, cur_stream(X)), "ijpack");
 }
 
-// Z [G,16,V,I,J,K,L] fp32 (channel-planar) -> y [V,I,J,K,L] fp32 (ij encoding)
+// Z [ks*ks,V,I,J,K,L] fp32 (channel-planar by combo q = di*ks + dj) -> y [V,I,J,K,L] fp32 (ij encoding)
 void ijsum(Tensor Z, c10::optional<Tensor> bias, Tensor y, int64_t ks, int64_t relu, int64_t sgn) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(Z.device());
   check(Z, "Z", at::kFloat); check(y, "y", at::kFloat);
   TORCH_CHECK(ks >= 1 && ks <= 5 && (sgn == 1 || sgn == -1));
-  TORCH_CHECK(Z.dim() == 7 && Z.size(0) == (ks * ks + 15) / 16 && Z.size(1) == 16, "Z must be [G,16,V,I,J,K,L]");
-  check_shape(y, "y", {Z.size(2), Z.size(3), Z.size(4), Z.size(5), Z.size(6)});
+  TORCH_CHECK(Z.dim() == 6 && Z.size(0) == ks * ks, "Z must be [ks*ks,V,I,J,K,L]");
+  check_shape(y, "y", {Z.size(1), Z.size(2), Z.size(3), Z.size(4), Z.size(5)});
   if (bias.has_value()) { check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
-  ok(ncnet_ijsum((float*)Z.data_ptr(), opt_ptr<float>(bias), (float*)y.data_ptr(), Z.size(2), Z.size(3), Z.size(4),
-                 Z.size(5), Z.size(6), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z)), "ijsum");
+  ok(ncnet_ijsum((float*)Z.data_ptr(), opt_ptr<float>(bias), (float*)y.data_ptr(), Z.size(1), Z.size(2), Z.size(3),
+                 Z.size(4), Z.size(5), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z)), "ijsum");
 }
 
 void wgrad1(Tensor S16, Tensor P1, Tensor part, int64_t ks, int64_t mode, int64_t ngroups) {
@@ -293,8 +295,16 @@ void stats_cols(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Te
   check_shape(mx, "mx", {x.size(0), x.size(2)});
   if (arg.has_value()) { check(*arg, "arg", at::kInt); check_shape(*arg, "arg", {x.size(0), x.size(2)}); }
   if (se.has_value()) { check(*se, "se", at::kFloat); check_shape(*se, "se", {x.size(0), x.size(2)}); }
+  // few wide columns (InLoc volumes): split the rows over chunks so the grid fills the chip
+  const int64_t V = x.size(0), R = x.size(1), C = x.size(2);
+  const int64_t blocks = V * ((C + 63) / 64);
+  int64_t nchunk = 1;
+  if (blocks < 1024) nchunk = std::min<int64_t>((2048 + blocks - 1) / blocks, (R + 63) / 64);
+  Tensor work;
+  if (nchunk > 1) work = at::empty({3 * V * nchunk * C}, x.options());
   ok(ncnet_stats_cols((float*)x.data_ptr(), (float*)mx.data_ptr(), arg.has_value() ? (int*)arg->data_ptr() : nullptr,
-                      se.has_value() ? (float*)se->data_ptr() : nullptr, x.size(0), x.size(1), x.size(2), cur_stream(x)),
+                      se.has_value() ? (float*)se->data_ptr() : nullptr, V, R, C,
+                      nchunk > 1 ? (float*)work.data_ptr() : nullptr, (int)nchunk, cur_stream(x)),
      "stats_cols");
 }
 

@@ -25,7 +25,7 @@ namespace ncnet {
 
 // EPI_F32: raw fp32 accumulators of channels 0..7 into Y as float[..., 8]
 // (the j-shift-encoded 16 -> 1 layers, summed afterwards by jsum).
-enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32 = 3, EPI_F32X16 = 4 };
+enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32 = 3, EPI_F32X16 = 4 };  // F32*: channel-planar fp32
 
 struct ConvGeom {
   int V, I, J, K, L;  // volume dims
@@ -34,6 +34,7 @@ struct ConvGeom {
   int PR, RS;         // staged plane rows / row stride (voxels)
   int RW;             // staged row width (voxels, <= RS)
   int dj_center;      // 1: only the dj = P planes (j-offset encoded in channels)
+  int nco;            // planar fp32 epilogues: output channels written (<= 8 / 16)
   int npg;            // > 0: "group planes" mode (v2 only): plane s is the (i, j)
   long long gstride;  //   plane of input group s at X + s * gstride, weights plane s
 };
@@ -109,14 +110,14 @@ __device__ __forceinline__ size_t plane_offset(const ConvGeom& g, int v, int i, 
 // of voxel (l & 15).
 template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
-                                        const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0) {
-  if (EPI == EPI_F32) {
-    if (co0 < 8) *(f32x4*)((float*)Y + vox_index * 8 + co0) = acc;
-    return;
-  }
-  if (EPI == EPI_F32X16) {   // channel-planar fp32 [16][nvox_all]: 16 lanes write 16 consecutive voxels
+                                        const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0,
+                                        int nco = 16) {
+  if (EPI == EPI_F32 || EPI == EPI_F32X16) {
+    // channel-planar fp32 [nco][nvox_all] (only the channels a consumer reads):
+    // 16 lanes write 16 consecutive voxels of one channel
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ((float*)Y)[(size_t)(co0 + r) * nvox_all + vox_index] = acc[r];
+    for (int r = 0; r < 4; ++r)
+      if (co0 + r < nco) ((float*)Y)[(size_t)(co0 + r) * nvox_all + vox_index] = acc[r];
     return;
   }
   float o[4];
@@ -247,7 +248,8 @@ __global__ __launch_bounds__(256, 2) void conv16_fwd_kernel(const bf16* __restri
       int kk = vi / g.TL, ll = vi - kk * g.TL;
       int kg = t.k0 + kk, lg = t.l0 + ll;
       if (vi < nvox && kg < g.K && lg < g.L)
-        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4));
+        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4),
+                     (size_t)g.V * g.I * g.J * g.K * g.L, g.nco);
     }
   }
 }
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
       int kg = t.k0 + kk, lg = t.l0 + ll;
       if (vi < nvox && kg < g.K && lg < g.L)
         store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4),
-                     (size_t)g.V * g.I * g.J * g.K * g.L);
+                     (size_t)g.V * g.I * g.J * g.K * g.L, g.nco);
     }
   }
 }
@@ -670,7 +672,7 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.RS = tl + KS - 1 + extra_cols;
   g.RW = g.RS;
   g.dj_center = 0;
-  g.npg = 0; g.gstride = 0;
+  g.npg = 0; g.gstride = 0; g.nco = 16;
   return g;
 }
 
@@ -700,13 +702,14 @@ static int conv16_variant() {
 // offsets live in the channels (ij encoding, csrc/jshift.hip).
 extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias, const void* M, void* Y,
                                 int V, int I, int J, int K, int L, int KS, int epi, int dj_center, int npg,
-                                hipStream_t stream) {
+                                int nco, hipStream_t stream) {
   int tk, tl;
   pick_tile(K, L, tk, tl);
   ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, 0, 0);
   g.dj_center = dj_center;
   g.npg = npg;
   g.gstride = (long long)V * I * J * K * L * 16;
+  g.nco = nco;
   if (npg > 0 && !(conv16_variant() == 2 && g.RW <= 32)) return -3;   // v2 only
   if (epi == EPI_F32X16 && !(conv16_variant() == 2 && g.RW <= 32)) return -3;
   if (g.PR * g.RS * 2 > 8 * 256) return -1;

@@ -27,12 +27,14 @@ namespace ncnet {
 template <typename T>
 __global__ __launch_bounds__(256) void jpack_kernel(const T* __restrict__ X, bf16* __restrict__ S, long long nvox,
                                                     int J, int KL, int KS, int sgn) {
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= nvox) return;
+  // grid (planes, ceil(KL/256)): the plane index is block-uniform, so its
+  // decomposition is scalar and no per-thread 64-bit division is needed
+  const int kl = blockIdx.y * 256 + threadIdx.x;
+  if (kl >= KL) return;
   const int P = KS / 2;
-  const long long plane = e / KL;          // (v*I + i)*J + j
-  const int j = (int)(plane % J);
-  const int kl = (int)(e - plane * KL);
+  const long long plane = blockIdx.x;      // (v*I + i)*J + j
+  const int j = (int)(blockIdx.x % J);
+  const long long e = plane * KL + kl;
   bf16x8 lo, hi;
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
@@ -48,21 +50,20 @@ __global__ __launch_bounds__(256) void jpack_kernel(const T* __restrict__ X, bf1
   o[1] = hi;
 }
 
-// y[v,i,j,k,l] = act(bias + sum_{c<KS} Z8[v,i,j+sgn*(c-P),k,l,c]),  Z8 fp32 [..., 8]
+// y[v,i,j,k,l] = act(bias + sum_{c<KS} Z8[c][v,i,j+sgn*(c-P),k,l]),  Z8 fp32 channel-planar [8][...]
 // (sgn = +1: the Cout=1 forward; sgn = -1: adjoint of jpack(+1), the Cin=1 data gradient)
 __global__ __launch_bounds__(256) void jsum_kernel(const float* __restrict__ Z8, const float* __restrict__ bias,
                                                    float* __restrict__ y, long long nvox, int J, int KL, int KS,
                                                    int relu, int sgn) {
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= nvox) return;
+  const int kl = blockIdx.y * 256 + threadIdx.x;
+  if (kl >= KL) return;
   const int P = KS / 2;
-  const long long plane = e / KL;
-  const int j = (int)(plane % J);
-  const int kl = (int)(e - plane * KL);
+  const int j = (int)(blockIdx.x % J);
+  const long long e = (long long)blockIdx.x * KL + kl;
   float s = bias ? bias[0] : 0.f;
   for (int c = 0; c < KS; ++c) {
     int jj = j + sgn * (c - P);
-    if (jj >= 0 && jj < J) s += Z8[((plane + (jj - j)) * KL + kl) * 8 + c];
+    if (jj >= 0 && jj < J) s += Z8[(long long)c * nvox + e + (long long)(jj - j) * KL];
   }
   y[e] = relu ? fmaxf(s, 0.f) : s;
 }
@@ -72,12 +73,12 @@ template <typename T, int KS>
 __global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, bf16* __restrict__ S, long long nvox,
                                                      int I, int J, int KL, int sgn) {
   constexpr int P = KS / 2, NQ = KS * KS, G = (NQ + 15) / 16;
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= nvox) return;
-  const long long plane = e / KL;           // (v*I + i)*J + j
-  const int j = (int)(plane % J);
-  const int i = (int)((plane / J) % I);
-  const int kl = (int)(e - plane * KL);
+  const int kl = blockIdx.y * 256 + threadIdx.x;
+  if (kl >= KL) return;
+  const long long plane = blockIdx.x;       // (v*I + i)*J + j, block-uniform
+  const int j = (int)(blockIdx.x % J);
+  const int i = (int)((blockIdx.x / J) % I);
+  const long long e = plane * KL + kl;
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     bf16x8 h[2];
@@ -99,17 +100,17 @@ __global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, bf
   }
 }
 
-// Z is channel-planar: Z[q >> 4][q & 15][voxel] (conv16 EPI_F32X16 layout).
+// Z is channel-planar by combo: Z[q][voxel] (conv16 planar fp32 epilogue).
 template <int KS>
 __global__ __launch_bounds__(256) void ijsum_kernel(const float* __restrict__ Z, const float* __restrict__ bias,
                                                     float* __restrict__ y, long long nvox, int I, int J, int KL,
                                                     int relu, int sgn) {
   constexpr int P = KS / 2, NQ = KS * KS;
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= nvox) return;
-  const long long plane = e / KL;
-  const int j = (int)(plane % J);
-  const int i = (int)((plane / J) % I);
+  const int kl = blockIdx.y * 256 + threadIdx.x;
+  if (kl >= KL) return;
+  const int j = (int)(blockIdx.x % J);
+  const int i = (int)((blockIdx.x / J) % I);
+  const long long e = (long long)blockIdx.x * KL + kl;
   float s = bias ? bias[0] : 0.f;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
@@ -128,7 +129,7 @@ extern "C" int ncnet_jpack(const void* X, int x_is_bf16, void* S, int V, int I, 
                            hipStream_t stream) {
   if (KS > 8 || KS < 1) return -1;
   long long nvox = (long long)V * I * J * K * L;
-  dim3 grid((unsigned)((nvox + 255) / 256));
+  dim3 grid((unsigned)(V * I * J), (unsigned)((K * L + 255) / 256));
   if (x_is_bf16)
     hipLaunchKernelGGL((jpack_kernel<bf16>), grid, dim3(256), 0, stream, (const bf16*)X, (bf16*)S, nvox, J, K * L, KS, sgn);
   else
@@ -140,15 +141,15 @@ extern "C" int ncnet_jsum(const float* Z8, const float* bias, float* y, int V, i
                           int relu, int sgn, hipStream_t stream) {
   if (KS > 8 || KS < 1) return -1;
   long long nvox = (long long)V * I * J * K * L;
-  hipLaunchKernelGGL(jsum_kernel, dim3((unsigned)((nvox + 255) / 256)), dim3(256), 0, stream, Z8, bias, y, nvox, J,
-                     K * L, KS, relu, sgn);
+  hipLaunchKernelGGL(jsum_kernel, dim3((unsigned)(V * I * J), (unsigned)((K * L + 255) / 256)), dim3(256), 0, stream,
+                     Z8, bias, y, nvox, J, K * L, KS, relu, sgn);
   return (int)hipGetLastError();
 }
 
 extern "C" int ncnet_ijpack(const void* X, int x_is_bf16, void* S, int V, int I, int J, int K, int L, int KS, int sgn,
                             hipStream_t stream) {
   long long nvox = (long long)V * I * J * K * L;
-  dim3 grid((unsigned)((nvox + 255) / 256));
+  dim3 grid((unsigned)(V * I * J), (unsigned)((K * L + 255) / 256));
 #define IJP(T, KSV) hipLaunchKernelGGL((ijpack_kernel<T, KSV>), grid, dim3(256), 0, stream, (const T*)X, (bf16*)S, nvox, I, J, K * L, sgn)
   if (KS == 5) { if (x_is_bf16) IJP(bf16, 5); else IJP(float, 5); }
   else if (KS == 3) { if (x_is_bf16) IJP(bf16, 3); else IJP(float, 3); }
@@ -160,7 +161,7 @@ extern "C" int ncnet_ijpack(const void* X, int x_is_bf16, void* S, int V, int I,
 extern "C" int ncnet_ijsum(const float* Z, const float* bias, float* y, int V, int I, int J, int K, int L, int KS,
                            int relu, int sgn, hipStream_t stream) {
   long long nvox = (long long)V * I * J * K * L;
-  dim3 grid((unsigned)((nvox + 255) / 256));
+  dim3 grid((unsigned)(V * I * J), (unsigned)((K * L + 255) / 256));
   if (KS == 5) hipLaunchKernelGGL((ijsum_kernel<5>), grid, dim3(256), 0, stream, Z, bias, y, nvox, I, J, K * L, relu, sgn);
   else if (KS == 3) hipLaunchKernelGGL((ijsum_kernel<3>), grid, dim3(256), 0, stream, Z, bias, y, nvox, I, J, K * L, relu, sgn);
   else return -1;

@@ -68,21 +68,26 @@ __global__ __launch_bounds__(256) void stats_rows_kernel(const float* __restrict
   }
 }
 
-// Block = 64 columns x 4 row-phases.
+// Block = 64 columns x 4 row-phases over the row range of chunk (blockIdx %
+// nchunk).  nchunk == 1 writes the final stats; otherwise per-chunk partials
+// (pm, pi, ps: [V][nchunk][C]) merged in row order by stats_cols_merge_kernel,
+// so a short-and-wide volume (InLoc: V = 1, C = 7500) still fills the chip.
 __global__ __launch_bounds__(256) void stats_cols_kernel(const float* __restrict__ x, float* __restrict__ mx,
                                                          int* __restrict__ arg, float* __restrict__ se,
-                                                         int R, int C) {
+                                                         int R, int C, int nchunk, int rpc) {
   __shared__ float sm[4][64], ss[4][64];
   __shared__ int si[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ncb = (C + 63) / 64;
-  const int v = blockIdx.x / ncb, cb = blockIdx.x % ncb;
+  const int chunk = blockIdx.x % nchunk, rest = blockIdx.x / nchunk;
+  const int v = rest / ncb, cb = rest % ncb;
   const int c = cb * 64 + lane;
   const bool ws = se != nullptr;
+  const int r0 = chunk * rpc, r1 = min(R, r0 + rpc);
   Stat st{-INFINITY, 0.f, 0x7fffffff};
   if (c < C) {
     const float* xv = x + (size_t)v * R * C + c;
-    for (int r = wave; r < R; r += 4) st = stat_push(st, xv[(size_t)r * C], r, ws);
+    for (int r = r0 + wave; r < r1; r += 4) st = stat_push(st, xv[(size_t)r * C], r, ws);
   }
   sm[wave][lane] = st.m; ss[wave][lane] = st.s; si[wave][lane] = st.idx;
   __syncthreads();
@@ -90,11 +95,29 @@ __global__ __launch_bounds__(256) void stats_cols_kernel(const float* __restrict
     Stat a{sm[0][lane], ss[0][lane], si[0][lane]};
 #pragma unroll
     for (int w = 1; w < 4; ++w) a = stat_merge(a, Stat{sm[w][lane], ss[w][lane], si[w][lane]}, ws);
-    size_t o = (size_t)v * C + c;
+    const size_t o = ((size_t)v * nchunk + chunk) * C + c;
     mx[o] = a.m;
     if (arg) arg[o] = a.idx;
     if (ws) se[o] = a.s;
   }
+}
+
+__global__ __launch_bounds__(256) void stats_cols_merge_kernel(const float* __restrict__ pm, const int* __restrict__ pi,
+                                                               const float* __restrict__ ps, float* __restrict__ mx,
+                                                               int* __restrict__ arg, float* __restrict__ se, int V,
+                                                               int C, int nchunk) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)V * C) return;
+  const int v = (int)(e / C), c = (int)(e % C);
+  const bool ws = se != nullptr;
+  Stat a{-INFINITY, 0.f, 0x7fffffff};
+  for (int k = 0; k < nchunk; ++k) {
+    const size_t o = ((size_t)v * nchunk + k) * C + c;
+    a = stat_merge(a, Stat{pm[o], ws ? ps[o] : 0.f, pi[o]}, ws);
+  }
+  mx[e] = a.m;
+  if (arg) arg[e] = a.idx;
+  if (ws) se[e] = a.s;
 }
 
 // ---------------------------------------------------------------------------
@@ -349,8 +372,20 @@ extern "C" int ncnet_stats_rows(const float* x, float* mx, int* arg, float* se, 
   hipLaunchKernelGGL(stats_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, mx, arg, se, rows, C);
   return (int)hipGetLastError();
 }
-extern "C" int ncnet_stats_cols(const float* x, float* mx, int* arg, float* se, int V, int R, int C, hipStream_t s) {
-  hipLaunchKernelGGL(stats_cols_kernel, dim3((unsigned)(V * cdiv(C, 64))), dim3(256), 0, s, x, mx, arg, se, R, C);
+// work: nullptr (nchunk = 1) or 3 * V * nchunk * C floats of partials.
+extern "C" int ncnet_stats_cols(const float* x, float* mx, int* arg, float* se, int V, int R, int C, float* work,
+                                int nchunk, hipStream_t s) {
+  if (nchunk <= 1 || work == nullptr) {
+    hipLaunchKernelGGL(stats_cols_kernel, dim3((unsigned)(V * cdiv(C, 64))), dim3(256), 0, s, x, mx, arg, se, R, C, 1, R);
+    return (int)hipGetLastError();
+  }
+  const size_t n = (size_t)V * nchunk * C;
+  float* pm = work; int* pi = (int*)(work + n); float* ps = work + 2 * n;
+  const int rpc = cdiv(R, nchunk);
+  hipLaunchKernelGGL(stats_cols_kernel, dim3((unsigned)(V * cdiv(C, 64) * nchunk)), dim3(256), 0, s, x, pm, pi,
+                     se ? ps : nullptr, R, C, nchunk, rpc);
+  hipLaunchKernelGGL(stats_cols_merge_kernel, dim3((unsigned)cdiv(V * C, 256)), dim3(256), 0, s, pm, pi,
+                     se ? ps : nullptr, mx, arg, se, V, C, nchunk);
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_mm_apply(const float* c, const float* rmax, const float* cmax, float* out_f32, void* out_x,

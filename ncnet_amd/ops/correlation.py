@@ -177,8 +177,9 @@ def correlation_pool2(fa: torch.Tensor, fb: torch.Tensor, hA: int, wA: int, hB: 
 
 
 def decode_offsets(code: torch.Tensor):
-    c = code.long()
-    return ((c >> 6) & 3, (c >> 4) & 3, (c >> 2) & 3, c & 3)
+    """Packed 2-bit offsets -> (di, dj, dk, dl) as uint8 volumes (8x less traffic
+    than int64 at InLoc size; they index / add like integers)."""
+    return ((code >> 6) & 3, (code >> 4) & 3, (code >> 2) & 3, code & 3)
 
 
 def maxpool4d(corr4d: torch.Tensor, k_size: int):

@@ -46,8 +46,13 @@ USE_IJ = ENC in ("ij", "ijfull")
 # (one conv pass with an 8-channel fp32 output beats two group-plane passes
 # with 16-channel planar outputs at 25^4: measured 1.97 vs 2.56 ms fwd) and
 # uses the ij encoding for its weight gradient (plane-only wgrad, 1.5 vs
-# 1.8 ms); "ijfull" runs that layer entirely on the ij encoding.
-OUT_IJ_FWD = ENC == "ijfull"
+# 1.8 ms); "ijfull" runs that layer entirely on the ij encoding.  At KS = 3
+# the ij encoding has a single group (one pass over one plane instead of 3
+# planes), so it is used there in all modes.
+
+
+def _out_ij_fwd(ks: int) -> bool:
+    return ENC == "ijfull" or (ENC == "ij" and ks * ks <= 16)
 # wgrad16 kernel: 3 = sliding G-plane ring (default), 2 = 8-wave LDS-DMA per
 # (di, dj) plane, 1 = 4-wave register-staged
 WGRAD_VARIANT = int(_os.environ.get("NCNET_WGRAD_VARIANT", "3"))
@@ -123,20 +128,21 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
         elif kind == "16":
             y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
             C.conv16_fwd(h, pack_w16(w), _pad_bias(b, 16), None, y, ks, 1, 0)
-        elif USE_IJ and OUT_IJ_FWD:   # "1out"
+        elif USE_IJ and _out_ij_fwd(ks):   # "1out"
             G = ij_groups(ks)
             wz = pack_w16_planes(ij_out_weights(w))
-            z = torch.empty((G, 16, V, I, J, K, L), dtype=torch.float32, device=x0.device)   # channel-planar
+            nq = ks * ks
+            z = torch.empty((nq, V, I, J, K, L), dtype=torch.float32, device=x0.device)   # planar by combo
             hx = h.unsqueeze(0)
             for gi in range(G):
-                C.conv16_fwd(hx, wz[gi:gi + 1], None, None, z[gi], ks, 4, 0)
+                C.conv16_fwd(hx, wz[gi:gi + 1], None, None, z[16 * gi:min(nq, 16 * gi + 16)], ks, 4, 0)
             y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
             C.ijsum(z, _pad_bias(b, 1), y, ks, 1, 1)
             del z
             if not last:
                 y = y.to(torch.bfloat16)
         elif USE_JC or USE_IJ:
-            z8 = torch.empty((V, I, J, K, L, 8), dtype=torch.float32, device=x0.device)
+            z8 = torch.empty((ks, V, I, J, K, L), dtype=torch.float32, device=x0.device)   # planar, dj = 0..ks-1
             C.conv16_fwd(h, pack_w16(jc_out_weights(w)), None, None, z8, ks, 3, 1)
             y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
             C.jsum(z8, _pad_bias(b, 1), y, ks, 1, 1)
@@ -252,7 +258,7 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
             del gs
             if li > 0 or need_dx0:
                 gi_ = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
-                if OUT_IJ_FWD:
+                if _out_ij_fwd(ks):
                     gs = torch.empty((G,) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
                     C.ijpack(g, gs, ks, -1)
                     wd = pack_w16_planes(plane_dgrad_weights(ij_out_weights(w)))
@@ -273,10 +279,11 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
                 raise RuntimeError("internal: 1in layer must be first")
             if need_dx0:
                 wd = pack_w16_planes(plane_dgrad_weights(ij_in_weights(w)))
-                z = torch.empty((G, 16, V, I, J, K, L), dtype=torch.float32, device=h.device)
+                nq = ks * ks
+                z = torch.empty((nq, V, I, J, K, L), dtype=torch.float32, device=h.device)
                 gx = g.unsqueeze(0)
                 for gi in range(G):
-                    C.conv16_fwd(gx, wd[gi:gi + 1], None, None, z[gi], ks, 4, 0)
+                    C.conv16_fwd(gx, wd[gi:gi + 1], None, None, z[16 * gi:min(nq, 16 * gi + 16)], ks, 4, 0)
                 gx0 = torch.empty((V, I, J, K, L), dtype=torch.float32, device=h.device)
                 C.ijsum(z, None, gx0, ks, 0, -1)      # adjoint of ijpack(+1)
         elif kind == "1out" and USE_JC:
@@ -298,7 +305,7 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
             if li > 0:
                 raise RuntimeError("internal: 1in layer must be first")
             if need_dx0:
-                z8 = torch.empty(tuple(h.shape[:5]) + (8,), dtype=torch.float32, device=h.device)
+                z8 = torch.empty((ks,) + tuple(h.shape[:5]), dtype=torch.float32, device=h.device)
                 wt = transpose_for_dgrad(jc_in_weights(w))
                 C.conv16_fwd(g, pack_w16(wt), None, None, z8, ks, 3, 1)
                 gx0 = torch.empty(tuple(h.shape[:5]), dtype=torch.float32, device=h.device)

@@ -64,7 +64,7 @@ def main():
     partb = torch.empty((2 * ng, 16), device=dev)
     part1 = torch.empty((ng, ks * ks, ks * ks, 16), device=dev)
     part16c = torch.empty((2 * ng, ks, ks * ks, 16, 16), device=dev)
-    z8 = torch.empty(shp + (8,), device=dev)
+    z8 = torch.empty((ks,) + shp, device=dev)
     from ncnet_amd.ops.neigh_consensus import wgrad_v3_groups
     n3, n3c = wgrad_v3_groups(shp, ks, False), wgrad_v3_groups(shp, ks, True)
     p3 = torch.empty((2 * n3, ks ** 2, ks ** 2, 16, 16), device=dev)

@@ -199,14 +199,14 @@ def test_maxpool4d_and_fused_pool():
     vr, offr = ref.maxpool4d(v.cpu(), 2)
     assert torch.equal(val.cpu(), vr)
     for a, b in zip(off, offr):
-        assert torch.equal(a.cpu(), b)
+        assert torch.equal(a.cpu().long(), b.long())
     fa = torch.randn(2, 6 * 8, 64, device=DEV).to(torch.bfloat16).float()
     fb = torch.randn(2, 4 * 10, 64, device=DEV).to(torch.bfloat16).float()
     pv, po = correlation_pool2(fa, fb, 6, 8, 4, 10)
     full = correlation(fa, fb).view(2, 1, 6, 8, 4, 10)
     rv, ro = ref.maxpool4d(full.cpu(), 2)
     assert relerr(pv, rv) < 1e-5
-    agree = sum(int(torch.equal(a.cpu(), b)) for a, b in zip(po, ro))
+    agree = sum(int(torch.equal(a.cpu().long(), b.long())) for a, b in zip(po, ro))
     assert agree == 4
 
 
