@@ -56,6 +56,7 @@ def main(argv=None):
     ap.add_argument("--profile", type=str, default="", help="write a torch.profiler trace to this dir")
     args = ap.parse_args(argv)
 
+    from ncnet_amd.config import RuntimeConfig
     from ncnet_amd.engine.trainer import weak_loss
     from ncnet_amd.models import ImMatchNet
     from ncnet_amd.parallel.dist import GradBucket, all_reduce_max_float, barrier, broadcast_module, init_distributed
@@ -153,7 +154,8 @@ def main(argv=None):
             "config": {"model": "ResNet-101(layer3)+NC-Net ncons 5,5,5/16,16,1", "global_batch": args.batch * ctx.world_size,
                        "per_gpu_batch": args.batch, "seq_len": None, "image_size": s,
                        "parallelism": f"dp{ctx.world_size}", "impl": args.impl,
-                       "baseline_pairs_per_s_1gpu": base, "final_loss": float(loss.detach())},
+                       "baseline_pairs_per_s_1gpu": base, "final_loss": float(loss.detach()),
+                       "runtime": RuntimeConfig.from_env().as_dict()},
         }
         print(json.dumps(rec), flush=True)
     from ncnet_amd.parallel.dist import destroy

@@ -1,0 +1,39 @@
+"""Typed view of the framework's runtime configuration.
+
+The CLIs keep the reference's argparse flags (Appendix A); the kernel and
+execution toggles are environment variables read at import time by the op
+modules.  ``RuntimeConfig.from_env()`` collects them in one dataclass so a
+run can log exactly which code paths it used (bench.py puts it in its JSON).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+
+
+@dataclasses.dataclass(frozen=True)
+class RuntimeConfig:
+    nc_encoding: str = "ij"          # NCNET_NC_ENC: ij | ijfull | jc | direct
+    wgrad_variant: int = 3           # NCNET_WGRAD_VARIANT
+    conv16_variant: int = 2          # NCNET_CONV16_VARIANT
+    trunk_plan: bool = True          # NCNET_TRUNK_PLAN
+    trunk_graph: bool = True         # NCNET_TRUNK_GRAPH
+    force_torch: bool = False        # NCNET_FORCE_TORCH
+    allow_torch_fallback: bool = False  # NCNET_ALLOW_TORCH_FALLBACK
+
+    @classmethod
+    def from_env(cls, env=None) -> "RuntimeConfig":
+        e = os.environ if env is None else env
+        enc = e.get("NCNET_NC_ENC", "ij")
+        if e.get("NCNET_NC_JC") == "0":
+            enc = "direct"
+        return cls(nc_encoding=enc,
+                   wgrad_variant=int(e.get("NCNET_WGRAD_VARIANT", "3")),
+                   conv16_variant=int(e.get("NCNET_CONV16_VARIANT", "2")),
+                   trunk_plan=e.get("NCNET_TRUNK_PLAN", "1") != "0",
+                   trunk_graph=e.get("NCNET_TRUNK_GRAPH", "1") != "0",
+                   force_torch=e.get("NCNET_FORCE_TORCH", "0") == "1",
+                   allow_torch_fallback=e.get("NCNET_ALLOW_TORCH_FALLBACK", "0") == "1")
+
+    def as_dict(self) -> dict:
+        return dataclasses.asdict(self)

@@ -16,9 +16,11 @@ int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, 
 int ncnet_wgrad16v3(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_jpack(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_jsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_ijpack(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_ijpack(const void*, int, void*, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv16f8_fwd(const void*, const void*, const float*, void*, int, int, int, int, int, int, int, int, int, int, float, hipStream_t);
 int ncnet_ijsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_bias_act(void*, const float*, long long, int, int, hipStream_t);
+int ncnet_conv2d_nhwc(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad1(const void*, const void*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
@@ -176,10 +178,11 @@ void ijpack(Tensor X, Tensor S, int64_t ks, int64_t sgn) {
   TORCH_CHECK(X.is_cuda() && X.is_contiguous() && (X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kFloat));
   TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
   TORCH_CHECK(ks >= 1 && ks <= 5 && (sgn == 1 || sgn == -1));
-  check(S, "S", at::kBFloat16);
+  const bool f8 = S.scalar_type() == at::kFloat8_e4m3fn;   // fp8 inference path
+  check(S, "S", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
   check_shape(S, "S", {(ks * ks + 15) / 16, X.size(0), X.size(1), X.size(2), X.size(3), X.size(4), 16});
   ok(ncnet_ijpack(X.data_ptr(), X.scalar_type() == at::kBFloat16, S.data_ptr(), X.size(0), X.size(1), X.size(2),
-                  X.size(3), X.size(4), ks, sgn, cur_stream(X)), "ijpack");
+                  X.size(3), X.size(4), ks, sgn, f8 ? 1 : 0, cur_stream(X)), "ijpack");
 }
 
 // Z [ks*ks,V,I,J,K,L] fp32 (channel-planar by combo q = di*ks + dj) -> y [V,I,J,K,L] fp32 (ij encoding)
@@ -417,6 +420,63 @@ void bias_act_(Tensor Y, Tensor b, int64_t relu) {
      "bias_act_");
 }
 
+// fp8 inference Conv4d 16->16: X fp8 [V,I,J,K,L,16] or [G,V,I,J,K,L,16] (group planes),
+// Wp fp8 [planes, ceil(ks*ks/2), 64, 8] (weights * wscale), oscale = 1 / wscale.
+// epi 1: Y fp8 [V,I,J,K,L,16] = relu(oscale * acc + bias); epi 4: Y fp32 planar [nco, V,I,J,K,L].
+void conv16f8_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t epi, int64_t dj_center,
+                  double oscale) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kFloat8_e4m3fn); check(Wp, "Wp", at::kFloat8_e4m3fn);
+  const bool grp = X.dim() == 7;
+  TORCH_CHECK((X.dim() == 6 || grp) && X.size(-1) == 16, "X must be [V,I,J,K,L,16] or [G,V,I,J,K,L,16]");
+  const int64_t npg = grp ? X.size(0) : 0;
+  std::vector<int64_t> vs(X.sizes().begin() + (grp ? 1 : 0), X.sizes().end());
+  TORCH_CHECK(epi == 1 || epi == 4, "fp8 conv supports epi 1 (bias+ReLU -> fp8) and 4 (planar fp32)");
+  int64_t nco = 16;
+  if (epi == 4) {
+    check(Y, "Y", at::kFloat);
+    nco = Y.size(0);
+    TORCH_CHECK(nco >= 1 && nco <= 16);
+    check_shape(Y, "Y", {nco, vs[0], vs[1], vs[2], vs[3], vs[4]});
+  } else {
+    check(Y, "Y", at::kFloat8_e4m3fn);
+    check_shape(Y, "Y", vs);
+    TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16});
+  }
+  check_shape(Wp, "Wp", {grp ? npg : ks * ks, conv_pairs16(ks), 64, 8});
+  ok(ncnet_conv16f8_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), Y.data_ptr(), vs[0], vs[1], vs[2], vs[3],
+                        vs[4], ks, epi, dj_center ? 1 : 0, (int)npg, (int)nco, (float)oscale, cur_stream(X)),
+     "conv16f8_fwd");
+}
+
+// NHWC implicit-GEMM conv with fused bias (+ residual) (+ ReLU).  X [N,Cin,H,W],
+// W [Cout,Cin,KH,KW], R / Y [N,Cout,Ho,Wo]: all bf16 channels-last; bias fp32 [Cout].
+void conv2d_nhwc(Tensor X, Tensor W, Tensor bias, c10::optional<Tensor> R, Tensor Y, int64_t stride, int64_t pad,
+                 int64_t relu) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  auto cl = at::MemoryFormat::ChannelsLast;
+  TORCH_CHECK(X.is_cuda() && X.scalar_type() == at::kBFloat16 && X.dim() == 4 && X.is_contiguous(cl),
+              "conv2d_nhwc: X must be bf16 channels-last [N,C,H,W]");
+  TORCH_CHECK(W.is_cuda() && W.scalar_type() == at::kBFloat16 && W.dim() == 4 && W.is_contiguous(cl),
+              "conv2d_nhwc: W must be bf16 channels-last [Cout,Cin,KH,KW]");
+  const int64_t N = X.size(0), Cin = X.size(1), H = X.size(2), Wd = X.size(3);
+  const int64_t Cout = W.size(0), KH = W.size(2), KW = W.size(3);
+  TORCH_CHECK(W.size(1) == Cin, "conv2d_nhwc: Cin mismatch");
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "conv2d_nhwc: channels must be multiples of 64");
+  const int64_t Ho = (H + 2 * pad - KH) / stride + 1, Wo = (Wd + 2 * pad - KW) / stride + 1;
+  check(bias, "bias", at::kFloat); check_shape(bias, "bias", {Cout});
+  TORCH_CHECK(Y.is_cuda() && Y.scalar_type() == at::kBFloat16 && Y.is_contiguous(cl), "conv2d_nhwc: Y must be bf16 channels-last");
+  check_shape(Y, "Y", {N, Cout, Ho, Wo});
+  if (R.has_value()) {
+    TORCH_CHECK(R->is_cuda() && R->scalar_type() == at::kBFloat16 && R->is_contiguous(cl), "conv2d_nhwc: R must be bf16 channels-last");
+    check_shape(*R, "R", {N, Cout, Ho, Wo});
+  }
+  TORCH_CHECK(N * Ho * Wo < (1LL << 31) && Cout * KH * KW * Cin < (1LL << 31), "conv2d_nhwc: sizes exceed int32");
+  ok(ncnet_conv2d_nhwc(X.data_ptr(), W.data_ptr(), (const float*)bias.data_ptr(), R.has_value() ? R->data_ptr() : nullptr,
+                       Y.data_ptr(), N, H, Wd, Cin, Cout, KH, KW, stride, pad, relu ? 1 : 0, cur_stream(X)),
+     "conv2d_nhwc");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for ncnet_amd";
   m.def("conv16_fwd", &conv16_fwd);
@@ -427,8 +487,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("jpack", &jpack);
   m.def("jsum", &jsum);
   m.def("ijpack", &ijpack);
+  m.def("conv16f8_fwd", &conv16f8_fwd);
   m.def("ijsum", &ijsum);
   m.def("bias_act_", &bias_act_);
+  m.def("conv2d_nhwc", &conv2d_nhwc);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("l2norm_rows_bwd", &l2norm_rows_bwd);
   m.def("corr_gemm", &corr_gemm);

@@ -1,0 +1,189 @@
+// NHWC implicit-GEMM 2D convolution with fused epilogues, for the frozen
+// ResNet trunk (models/backbones.py FrozenResNetPlan).
+//
+//   Y[p, co] = act( sum_{dh,dw,ci} X[n, ho*s+dh-pad, wo*s+dw-pad, ci] * W[co, dh, dw, ci]
+//                   + bias[co] (+ R[p, co]) ),      p = (n, ho, wo) row-major
+//
+// GEMM view: M = N*Ho*Wo pixels, N = Cout, K = KH*KW*Cin.  X, Y, R are
+// channels-last (NHWC) bf16, W is [Cout][KH][KW][Cin] (a channels-last conv
+// weight), bias fp32.  A k-step is one tap x 64 input channels, so the
+// im2col gather is one 128-B row load per pixel (zero outside the image) and
+// never materialised.  128 x BN output tile per 4-wave workgroup (BN = 128:
+// 2x2 waves of 64x64; BN = 64 for the 64-channel layers: 4x1 waves of 32x64),
+// v_mfma_f32_16x16x32_bf16, XOR-swizzled LDS rows, register double buffer,
+// XCD-aware tile order.  The epilogue fuses bias, the bottleneck residual and
+// ReLU, so a bottleneck is exactly four kernels and no elementwise passes
+// (MIOpen: conv + separate bias pass + PyTorch ReLU / add passes).
+// Requires Cin % 64 == 0 and Cout % 64 == 0 (every ResNet conv but the stem).
+#include "common.h"
+
+namespace ncnet {
+
+namespace cv {
+constexpr int BM = 128, BK = 64;
+__device__ __forceinline__ uint32_t toff(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ (row & 7)) << 4)); }
+}  // namespace cv
+
+struct Conv2dArgs {
+  const bf16* X; const bf16* W; const float* bias; const bf16* R; bf16* Y;
+  int N, H, Wd, Cin, Cout, KH, KW, stride, pad, Ho, Wo;
+  int M, tiles_m, tiles_n, relu;
+};
+
+template <int BN>
+__global__ __launch_bounds__(256, 2) void conv2d_nhwc_kernel(Conv2dArgs p) {
+  using namespace cv;
+  constexpr int WN = BN == 128 ? 2 : 1;          // waves along N
+  constexpr int WMW = 4 / WN;                    // waves along M
+  constexpr int TM = BM / WMW / 16;              // 16-row MFMA tiles per wave (4 or 2)
+  constexpr int TN = BN / WN / 16;               // 16-col MFMA tiles per wave (4)
+  constexpr int BCH = BN * 8 / 256;              // B chunks per thread (4 or 2)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* As = smem;
+  char* Bs = smem + BM * 128;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = bid % p.tiles_n, tm = bid / p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ch = threadIdx.x & 7;
+
+  // this thread's 4 A rows (pixels): image base offset and top-left input coordinate
+  int a_hi0[4], a_wi0[4];
+  size_t a_base[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int row = (threadIdx.x >> 3) + 32 * m;
+    const int pix = m0 + row;
+    if (pix < p.M) {
+      const int wo = pix % p.Wo, t = pix / p.Wo, ho = t % p.Ho, n = t / p.Ho;
+      a_hi0[m] = ho * p.stride - p.pad;
+      a_wi0[m] = wo * p.stride - p.pad;
+      a_base[m] = (size_t)n * p.H * p.Wd;
+    } else {
+      a_hi0[m] = -(1 << 28);   // never inside the image
+      a_wi0[m] = 0;
+      a_base[m] = 0;
+    }
+  }
+  const int K = p.KH * p.KW * p.Cin;
+  const int cpt = p.Cin / BK;                    // k-steps per tap
+  const int nk = p.KH * p.KW * cpt;
+
+  u32x4 ra[4], rb[BCH];
+  auto load = [&](int ks) {
+    const int tap = ks / cpt, c0 = (ks - tap * cpt) * BK;
+    const int dh = tap / p.KW, dw = tap - dh * p.KW;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int hi = a_hi0[m] + dh, wi = a_wi0[m] + dw;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.Wd)
+        v = *(const u32x4*)(p.X + (a_base[m] + (size_t)hi * p.Wd + wi) * p.Cin + c0 + ch * 8);
+      ra[m] = v;
+    }
+    const int kk = tap * p.Cin + c0 + ch * 8;
+#pragma unroll
+    for (int m = 0; m < BCH; ++m) {
+      const int row = (threadIdx.x >> 3) + 32 * m;
+      rb[m] = *(const u32x4*)(p.W + (size_t)(n0 + row) * K + kk);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) *(u32x4*)(As + toff((threadIdx.x >> 3) + 32 * m, ch)) = ra[m];
+#pragma unroll
+    for (int m = 0; m < BCH; ++m) *(u32x4*)(Bs + toff((threadIdx.x >> 3) + 32 * m, ch)) = rb[m];
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store();
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int ks = 0; ks < nk; ++ks) {
+    const bool more = ks + 1 < nk;
+    if (more) load(ks + 1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      bf16x8 af[TM], bfv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = lds_read16(As, toff(wm * TM * 16 + i * 16 + fr, kh * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfv[j] = lds_read16(Bs, toff(wn * TN * 16 + j * 16 + fr, kh * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfv[j], acc[i][j]);
+    }
+    __syncthreads();
+    if (more) store();
+    __syncthreads();
+  }
+
+  // epilogue, staged through LDS so the global writes (and the residual
+  // reads) are full 16-B-per-lane row segments: (acc + bias) -> bf16 tile
+  // [BM][BN] in LDS (row = pixel), then + residual, ReLU, store.
+  bf16* Ts = (bf16*)smem;                         // BM * BN * 2 <= (BM + BN) * 128 bytes
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wn * TN * 16 + j * 16 + fr;
+    const float b = p.bias[n0 + col];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ts[(wm * TM * 16 + i * 16 + 4 * fq + r) * BN + col] = f2bf(acc[i][j][r] + b);
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;                     // 16-B chunks per tile row
+#pragma unroll
+  for (int c = threadIdx.x; c < BM * CPR; c += 256) {
+    const int row = c / CPR, cc = c - row * CPR;
+    const int pix = m0 + row;
+    if (pix < p.M) {
+      bf16x8 v = *(const bf16x8*)(Ts + row * BN + cc * 8);
+      const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
+      if (p.R) {
+        const bf16x8 rr = *(const bf16x8*)(p.R + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[e]));
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf(bf2f(v[e]), 0.f));
+      }
+      *(bf16x8*)(p.Y + o) = v;
+    }
+  }
+}
+
+}  // namespace ncnet
+
+using namespace ncnet;
+
+extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias, const void* R, void* Y, int N, int H,
+                                 int Wd, int Cin, int Cout, int KH, int KW, int stride, int pad, int relu,
+                                 hipStream_t stream) {
+  if (Cin % 64 || Cout % 64 || stride < 1) return -1;
+  Conv2dArgs p;
+  p.X = (const bf16*)X; p.W = (const bf16*)W; p.bias = bias; p.R = (const bf16*)R; p.Y = (bf16*)Y;
+  p.N = N; p.H = H; p.Wd = Wd; p.Cin = Cin; p.Cout = Cout; p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad;
+  p.Ho = (H + 2 * pad - KH) / stride + 1;
+  p.Wo = (Wd + 2 * pad - KW) / stride + 1;
+  p.M = N * p.Ho * p.Wo;
+  p.relu = relu;
+  const int BN = (Cout % 128 == 0) ? 128 : 64;
+  p.tiles_m = cdiv(p.M, cv::BM);
+  p.tiles_n = Cout / BN;
+  dim3 grid((unsigned)(p.tiles_m * p.tiles_n)), block(256);
+  const size_t lds = (size_t)(cv::BM + BN) * 128;
+  if (BN == 128) hipLaunchKernelGGL((conv2d_nhwc_kernel<128>), grid, block, lds, stream, p);
+  else hipLaunchKernelGGL((conv2d_nhwc_kernel<64>), grid, block, lds, stream, p);
+  return (int)hipGetLastError();
+}

@@ -19,6 +19,7 @@
 //                                    shifts of an anchor grid (weights shifted
 //                                    on the host), so N=1 still uses the MFMA.
 #include "common.h"
+#include <hip/hip_fp8.h>
 #include <stdlib.h>
 
 namespace ncnet {
@@ -35,6 +36,7 @@ struct ConvGeom {
   int RW;             // staged row width (voxels, <= RS)
   int dj_center;      // 1: only the dj = P planes (j-offset encoded in channels)
   int nco;            // planar fp32 epilogues: output channels written (<= 8 / 16)
+  float oscale;       // fp8 kernel: accumulator scale (1 / weight scale)
   int npg;            // > 0: "group planes" mode (v2 only): plane s is the (i, j)
   long long gstride;  //   plane of input group s at X + s * gstride, weights plane s
 };
@@ -382,6 +384,141 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
 }
 
 // ===========================================================================
+// conv16f8_fwd: inference Conv4d 16 -> 16 on OCP fp8 e4m3 operands
+// (v_mfma_f32_16x16x32_fp8_fp8, BASELINE config 5).  Same structure as
+// conv16v2 (8 waves, LDS-DMA, double-buffered planes, single weight buffer with
+// a mid-plane s_barrier, group-plane mode) with 16-byte voxels: every LDS,
+// DMA and operand byte count halves (one ds_read_b64 per MFMA instead of a
+// b128) and the weight fragments take 26 instead of 52 VGPRs.  The plane row
+// stride is TL + 16 voxels so a wrapping 16-voxel tile still jumps one 256-B
+// bank period.  Weights are pre-scaled by 1/oscale into the e4m3 range.
+// Epilogues: EPI_BIAS_RELU -> fp8 [.., 16] (next layer's input),
+//            EPI_F32X16   -> channel-planar fp32 partials (ijsum input).
+// ===========================================================================
+template <int KS, int EPI>
+__global__ __launch_bounds__(512, 2) void conv16f8_fwd_kernel(const uint8_t* __restrict__ X,
+                                                              const uint8_t* __restrict__ Wp,
+                                                              const float* __restrict__ bias, void* __restrict__ Y,
+                                                              ConvGeom g) {
+  constexpr int P = KS / 2;
+  constexpr int NT = KS * KS;
+  constexpr int NQ = (NT + 1) / 2;
+  constexpr int NW = 8;
+  constexpr int MAXT = 5;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int plane_bytes = g.PR * g.RS * 16;
+  char* wbuf = smem + 2 * plane_bytes;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const TileId t = decode_tile(g);
+  const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
+  const int dj_lo = g.dj_center ? P : max(0, P - t.j), dj_hi = g.dj_center ? P + 1 : min(KS, g.J + P - t.j);
+  const int ndj = dj_hi - dj_lo;
+  const int nplanes = g.npg > 0 ? g.npg : (di_hi - di_lo) * ndj;
+  const int nvox = g.TK * g.TL;
+  const int ntile = (nvox + 15) >> 4;
+
+  for (int o = threadIdx.x * 16; o < 2 * plane_bytes; o += NW * 64 * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
+
+  uint32_t vbase[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int vi = (wave + NW * tt) * 16 + (lane & 15);
+    if (vi >= nvox) vi = 0;
+    int kk = vi / g.TL, ll = vi - kk * g.TL;
+    vbase[tt] = (uint32_t)((kk * g.RS + ll) * 16 + ((lane >> 4) & 1) * 8);
+  }
+  uint32_t toff[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    int tap = 2 * q + (lane >> 5);
+    if (tap >= NT) tap = NT - 1;
+    int dk = tap / KS, dl = tap - dk * KS;
+    toff[q] = (uint32_t)((dk * g.RS + dl) * 16);
+  }
+  f32x4 acc[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lstart = max(0, t.l0 - P), lend = min(g.L, t.l0 - P + g.RW);
+  const int nvx = lend - lstart;          // 16-byte voxels per staged row (<= 32)
+  const int col0 = lstart - (t.l0 - P);
+
+  auto issue_x = [&](int s, char* buf) {
+    const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
+    const uint8_t* xp = g.npg > 0 ? X + s * g.gstride + plane_offset(g, t.v, t.i, t.j, 16)
+                                  : X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
+    for (int r = wave; r < g.PR; r += NW) {
+      const int kg = t.k0 - P + r;
+      if (kg >= 0 && kg < g.K && lane < nvx)
+        __builtin_amdgcn_global_load_lds((const void*)(xp + ((size_t)kg * g.L + lstart + lane) * 16),
+                                         LDS_PTR(void, buf + (r * g.RS + col0) * 16), 16, 0, 0);
+    }
+  };
+  auto issue_w = [&](int s) {   // NQ * 512 B of fragments = NQ * 32 16-byte chunks
+    const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
+    const uint8_t* wp = Wp + (size_t)(g.npg > 0 ? s : di * KS + dj) * (NQ * 512);
+    for (int c = wave * 64; c < NQ * 32; c += NW * 64)
+      if (c + lane < NQ * 32)
+        __builtin_amdgcn_global_load_lds((const void*)(wp + (size_t)(c + lane) * 16), LDS_PTR(void, wbuf + c * 16),
+                                         16, 0, 0);
+  };
+
+  __syncthreads();
+  if (nplanes > 0) { issue_x(0, smem); issue_w(0); }
+  for (int s = 0; s < nplanes; ++s) {
+    __syncthreads();
+    char* cur = smem + (s & 1) * plane_bytes;
+    if (s + 1 < nplanes) issue_x(s + 1, smem + ((s + 1) & 1) * plane_bytes);
+    long wf[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) wf[q] = *(const long*)(wbuf + (q * 64 + lane) * 8);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (s + 1 < nplanes) issue_w(s + 1);
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      if (wave + NW * tt < ntile) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const long xf = *(const long*)(cur + vbase[tt] + toff[q]);
+          acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(wf[q], xf, acc[tt], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);
+  const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
+  const int co0 = 4 * (lane >> 4);
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int tile = wave + NW * tt;
+    if (tile < ntile) {
+      int vi = tile * 16 + (lane & 15);
+      int kk = vi / g.TL, ll = vi - kk * g.TL;
+      int kg = t.k0 + kk, lg = t.l0 + ll;
+      if (vi < nvox && kg < g.K && lg < g.L) {
+        const size_t vox = vbase_out + (size_t)kg * g.L + lg;
+        if (EPI == EPI_F32X16) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (co0 + r < g.nco) ((float*)Y)[(size_t)(co0 + r) * nvox_all + vox] = acc[tt][r] * g.oscale;
+        } else {
+          uint32_t packed = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = fmaxf(acc[tt][r] * g.oscale + bias[co0 + r], 0.f);
+            packed |= (uint32_t)__hip_cvt_float_to_fp8(x, __HIP_SATFINITE, __HIP_E4M3) << (8 * r);
+          }
+          *(uint32_t*)((uint8_t*)Y + vox * 16 + co0) = packed;
+        }
+      }
+    }
+  }
+}
+
+// ===========================================================================
 // conv1in_fwd: Cin = 1, Cout = 16.
 // The staged plane is expanded in LDS into 8-wide l-windows
 // win[r][c] = plane[r][c .. c+7] so every MFMA operand read is one aligned
@@ -672,7 +809,7 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.RS = tl + KS - 1 + extra_cols;
   g.RW = g.RS;
   g.dj_center = 0;
-  g.npg = 0; g.gstride = 0; g.nco = 16;
+  g.npg = 0; g.gstride = 0; g.nco = 16; g.oscale = 1.f;
   return g;
 }
 
@@ -746,6 +883,32 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
     else if (epi == EPI_F32) L16(3, EPI_F32); else L16(3, EPI_NONE);
   } else return -2;
 #undef L16
+  return (int)hipGetLastError();
+}
+
+// fp8 (OCP e4m3) inference Conv4d 16 -> 16; epi 1 (fp8 out) or 4 (planar fp32), oscale = 1 / weight scale.
+extern "C" int ncnet_conv16f8_fwd(const void* X, const void* Wp, const float* bias, void* Y, int V, int I, int J, int K,
+                                  int L, int KS, int epi, int dj_center, int npg, int nco, float oscale,
+                                  hipStream_t stream) {
+  int tk, tl;
+  pick_tile(K, L, tk, tl);
+  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, 0, 0);
+  g.dj_center = dj_center;
+  g.npg = npg;
+  g.gstride = (long long)V * I * J * K * L * 16;
+  g.nco = nco;
+  g.oscale = oscale;
+  if (g.RW > 32) return -1;
+  g.RS = tl + 16;                       // 16-byte voxels: a row wrap jumps 256 B
+  const int nq = (KS * KS + 1) / 2;
+  size_t lds = 2 * (size_t)g.PR * g.RS * 16 + (size_t)nq * 512;
+  dim3 grid((unsigned)(V * I * J * g.nkt * g.nlt)), block(512);
+  const uint8_t* x = (const uint8_t*)X; const uint8_t* w = (const uint8_t*)Wp;
+#define LF8(KSV, EPIV) hipLaunchKernelGGL((conv16f8_fwd_kernel<KSV, EPIV>), grid, block, lds, stream, x, w, bias, Y, g)
+  if (KS == 5) { if (epi == EPI_BIAS_RELU) LF8(5, EPI_BIAS_RELU); else if (epi == EPI_F32X16) LF8(5, EPI_F32X16); else return -2; }
+  else if (KS == 3) { if (epi == EPI_BIAS_RELU) LF8(3, EPI_BIAS_RELU); else if (epi == EPI_F32X16) LF8(3, EPI_F32X16); else return -2; }
+  else return -2;
+#undef LF8
   return (int)hipGetLastError();
 }
 

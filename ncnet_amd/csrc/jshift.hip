@@ -20,6 +20,7 @@
 // and the 1-channel layers become conv16 over G "group planes" with (dk, dl)
 // taps only: 2.5x (KS=5) / 3x (KS=3) fewer MFMAs than the j encoding.
 #include "common.h"
+#include <hip/hip_fp8.h>
 
 namespace ncnet {
 
@@ -69,8 +70,9 @@ __global__ __launch_bounds__(256) void jsum_kernel(const float* __restrict__ Z8,
 }
 
 // ---------------------------------------------------------------------------
-template <typename T, int KS>
-__global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, bf16* __restrict__ S, long long nvox,
+// F8OUT: S is OCP fp8 e4m3 [G][..][16] (inference path), else bf16.
+template <typename T, int KS, bool F8OUT>
+__global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, void* __restrict__ S, long long nvox,
                                                      int I, int J, int KL, int sgn) {
   constexpr int P = KS / 2, NQ = KS * KS, G = (NQ + 15) / 16;
   const int kl = blockIdx.y * 256 + threadIdx.x;
@@ -81,22 +83,36 @@ __global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, bf
   const long long e = plane * KL + kl;
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    bf16x8 h[2];
+    float vals[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-      constexpr int dummy = 0;
-      (void)dummy;
       const int q = 16 * g + c;
       float v = 0.f;
       if (q < NQ) {
         const int ii = i + sgn * (q / KS - P), jj = j + sgn * (q % KS - P);
         if (ii >= 0 && ii < I && jj >= 0 && jj < J) v = (float)X[(plane + (long long)(ii - i) * J + (jj - j)) * KL + kl];
       }
-      h[c >> 3][c & 7] = f2bf(v);
+      vals[c] = v;
     }
-    bf16x8* o = (bf16x8*)(S + ((long long)g * nvox + e) * 16);
-    o[0] = h[0];
-    o[1] = h[1];
+    if (F8OUT) {
+      u32x4 o;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        uint32_t p = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          p |= (uint32_t)__hip_cvt_float_to_fp8(vals[4 * w + b], __HIP_SATFINITE, __HIP_E4M3) << (8 * b);
+        o[w] = p;
+      }
+      *(u32x4*)((uint8_t*)S + ((long long)g * nvox + e) * 16) = o;
+    } else {
+      bf16x8 h[2];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) h[c >> 3][c & 7] = f2bf(vals[c]);
+      bf16x8* o = (bf16x8*)((bf16*)S + ((long long)g * nvox + e) * 16);
+      o[0] = h[0];
+      o[1] = h[1];
+    }
   }
 }
 
@@ -147,10 +163,11 @@ extern "C" int ncnet_jsum(const float* Z8, const float* bias, float* y, int V, i
 }
 
 extern "C" int ncnet_ijpack(const void* X, int x_is_bf16, void* S, int V, int I, int J, int K, int L, int KS, int sgn,
-                            hipStream_t stream) {
+                            int s_fp8, hipStream_t stream) {
   long long nvox = (long long)V * I * J * K * L;
   dim3 grid((unsigned)(V * I * J), (unsigned)((K * L + 255) / 256));
-#define IJP(T, KSV) hipLaunchKernelGGL((ijpack_kernel<T, KSV>), grid, dim3(256), 0, stream, (const T*)X, (bf16*)S, nvox, I, J, K * L, sgn)
+#define IJP(T, KSV) do { if (s_fp8) hipLaunchKernelGGL((ijpack_kernel<T, KSV, true>), grid, dim3(256), 0, stream, (const T*)X, S, nvox, I, J, K * L, sgn); \
+                         else hipLaunchKernelGGL((ijpack_kernel<T, KSV, false>), grid, dim3(256), 0, stream, (const T*)X, S, nvox, I, J, K * L, sgn); } while (0)
   if (KS == 5) { if (x_is_bf16) IJP(bf16, 5); else IJP(float, 5); }
   else if (KS == 3) { if (x_is_bf16) IJP(bf16, 3); else IJP(float, 3); }
   else return -1;

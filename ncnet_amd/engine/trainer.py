@@ -93,8 +93,12 @@ class Trainer:
                 if self.ctx.is_main:
                     print(f"{mode.capitalize()} Epoch: {epoch} [{batch_idx}/{nb} ({100.0 * batch_idx / max(nb, 1):.0f}%)]"
                           f"\t\tLoss: {lv:.6f}", flush=True)
-                self._log({"mode": mode, "epoch": epoch, "step": batch_idx, "loss": lv, "elapsed_s": dt,
-                           "pairs": n * batch["source_image"].shape[0] * self.ctx.world_size})
+                pairs = n * batch["source_image"].shape[0] * self.ctx.world_size
+                rec = {"mode": mode, "epoch": epoch, "step": batch_idx, "loss": lv, "elapsed_s": dt,
+                       "pairs": pairs, "pairs_per_s": pairs / max(dt, 1e-9)}
+                if self.ctx.device.type == "cuda":
+                    rec["hbm_peak_gb"] = torch.cuda.max_memory_allocated(self.ctx.device) / 2 ** 30
+                self._log(rec)
         mean = float(all_reduce_mean(total / max(n, 1), self.ctx))
         if self.ctx.is_main:
             print(f"{mode.capitalize()} set: Average loss: {mean:.4f}", flush=True)

@@ -294,15 +294,29 @@ class FrozenResNetPlan(nn.Module):
                         dc = blk.downsample[0]
                         b3 = b3 + bias(dc, torch.float32)   # relu(x W3 + b3 + (xs Wd + bd))
                         down = (wt(dc), 1) if dc.stride == (1, 1) else (w4(dc), dc.stride)
+                    dn = None
+                    if blk.downsample is not None:
+                        dc = blk.downsample[0]
+                        dn = (w4(dc), bias(dc, torch.float32), dc.stride[0], 0)
                     self.steps.append(("bottleneck", dict(
                         w1t=wt(blk.conv1), b1=bias(blk.conv1, dtype), w2=w4(blk.conv2),
                         b2=bias(blk.conv2, torch.float32), s2=blk.conv2.stride, w3t=wt(blk.conv3),
-                        b3=b3.contiguous(), down=down)))
+                        b3=b3.contiguous(), down=down,
+                        # native NHWC implicit-GEMM kernels (csrc/conv2d.hip): every conv with its own bias
+                        n1=(w4(blk.conv1), bias(blk.conv1, torch.float32), 1, 0),
+                        n2=(w4(blk.conv2), bias(blk.conv2, torch.float32), blk.conv2.stride[0], 1),
+                        n3=(w4(blk.conv3), bias(blk.conv3, torch.float32), 1, 0), nd=dn)))
             elif isinstance(m, (nn.ReLU, nn.Identity)):
                 pass
             else:
                 raise TypeError(f"FrozenResNetPlan: unsupported module {type(m).__name__}")
         self._keep = keep
+        import os
+        self.use_graphs = os.environ.get("NCNET_TRUNK_GRAPH", "1") != "0"
+        # "native": NHWC implicit-GEMM HIP kernels with fused bias/residual/ReLU
+        # (csrc/conv2d.hip); "blas": hipBLASLt 1x1 GEMMs + MIOpen 3x3 + bias_act
+        self.conv_mode = os.environ.get("NCNET_TRUNK_CONV", "native")
+        self._graphs = {}
 
     @staticmethod
     def _bias_act(y: torch.Tensor, b: torch.Tensor, relu: bool) -> torch.Tensor:
@@ -316,6 +330,17 @@ class FrozenResNetPlan(nn.Module):
         return y.relu_() if relu else y
 
     @staticmethod
+    def _nconv(x: torch.Tensor, p, relu: bool, res: torch.Tensor | None = None) -> torch.Tensor:
+        from ..ops import _ext
+        w, b, stride, pad = p
+        n, _, h, wd = x.shape
+        co, _, kh, kw = w.shape
+        ho, wo = (h + 2 * pad - kh) // stride + 1, (wd + 2 * pad - kw) // stride + 1
+        y = torch.empty((n, co, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        _ext.ext().conv2d_nhwc(x, w, b, res, y, stride, pad, 1 if relu else 0)
+        return y
+
+    @staticmethod
     def _rows(x: torch.Tensor) -> torch.Tensor:  # NCHW channels-last -> [N*H*W, C] view
         return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
 
@@ -325,6 +350,41 @@ class FrozenResNetPlan(nn.Module):
 
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """GPU: replays a HIP graph of the whole trunk per input shape (captured
+        after two eager warm-up runs, so MIOpen / hipBLASLt solver selection
+        happens outside the capture).  At InLoc size the ~150 per-layer
+        launches otherwise leave the GPU idle for a third of the trunk time."""
+        if x.is_cuda and self.use_graphs:
+            try:
+                return self._graph_forward(x)
+            except RuntimeError as err:          # capture unsupported -> stay eager
+                self.use_graphs = False
+                import warnings
+                warnings.warn(f"FrozenResNetPlan: HIP graph capture disabled ({err})")
+        return self._run(x)
+
+    def _graph_forward(self, x: torch.Tensor) -> torch.Tensor:
+        key = (tuple(x.shape), x.dtype, x.device)
+        ent = self._graphs.get(key)
+        if ent is None:
+            static_in = x.clone()
+            side = torch.cuda.Stream(device=x.device)
+            side.wait_stream(torch.cuda.current_stream(x.device))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self._run(static_in)
+            torch.cuda.current_stream(x.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static_out = self._run(static_in)
+            ent = (graph, static_in, static_out)
+            self._graphs[key] = ent
+        graph, static_in, static_out = ent
+        static_in.copy_(x)
+        graph.replay()
+        return static_out.clone(memory_format=torch.channels_last)
+
+    def _run(self, x: torch.Tensor) -> torch.Tensor:
         x = x.to(self.dtype).contiguous(memory_format=torch.channels_last)
         for kind, p in self.steps:
             if kind == "conv":
@@ -333,6 +393,11 @@ class FrozenResNetPlan(nn.Module):
                                    b, relu)
             elif kind == "maxpool":
                 x = F.max_pool2d(x, *p).contiguous(memory_format=torch.channels_last)
+            elif self.conv_mode == "native" and x.is_cuda and self.dtype == torch.bfloat16:
+                y1 = self._nconv(x, p["n1"], True)
+                y2 = self._nconv(y1, p["n2"], True)
+                idt = x if p["nd"] is None else self._nconv(x, p["nd"], False)
+                x = self._nconv(y2, p["n3"], True, idt)
             else:
                 n, _, h, w = x.shape
                 x2d = self._rows(x)

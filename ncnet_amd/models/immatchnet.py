@@ -151,7 +151,8 @@ class NeighConsensus(nn.Module):
         layers = self.conv_layers()
         ws = [m.weight_ref() for m in layers]
         bs = [m.bias if m.bias is not None else torch.zeros(m.out_channels, device=x.device) for m in layers]
-        return neigh_consensus(x, ws, bs, self.channels, symmetric=self.symmetric_mode)
+        return neigh_consensus(x, ws, bs, self.channels, symmetric=self.symmetric_mode,
+                               fp8=getattr(self, "fp8", False))
 
 
 def _load_reference_checkpoint(path: str):
@@ -186,7 +187,8 @@ class ImMatchNet(nn.Module):
         self.fold_bn = fold_bn
         if corr_dtype not in ("bf16", "fp8"):
             raise ValueError("corr_dtype must be 'bf16' or 'fp8'")
-        # fp8: OCP e4m3 correlation operands on the MX-fp8 MFMA (inference only)
+        # fp8: OCP e4m3 correlation operands on the MX-fp8 MFMA and fp8
+        # NeighConsensus (fp8 MFMA Conv4d) -- inference only
         self.corr_dtype = corr_dtype
         self.FeatureExtraction = FeatureExtraction(train_fe=train_fe, feature_extraction_cnn=feature_extraction_cnn,
                                                    feature_extraction_model_file=feature_extraction_model_file or "",
@@ -231,6 +233,7 @@ class ImMatchNet(nn.Module):
     def process_correlation(self, corr4d: torch.Tensor) -> torch.Tensor:
         """MutualMatching -> NeighConsensus -> MutualMatching (lib/model.py:274-276)."""
         corr4d = MutualMatching(corr4d)
+        self.NeighConsensus.fp8 = self.corr_dtype == "fp8"
         corr4d = self.NeighConsensus(corr4d)
         return MutualMatching(corr4d)
 

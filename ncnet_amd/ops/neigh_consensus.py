@@ -20,6 +20,7 @@ MI355X design:
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import _ext
@@ -439,11 +440,84 @@ class NeighConsensusFn(torch.autograd.Function):
         return (gx, None, None, None, *grads)
 
 
-def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool = True) -> torch.Tensor:
-    """x: [V,1,I,J,K,L] fp32; weights in checkpoint layout [k, out, in, k, k, k]."""
+# ---------------------------------------------------------------------------
+# fp8 inference path (BASELINE config 5): OCP e4m3 activations and weights on
+# the fp8 MFMA conv kernel, ij encoding for the 1-channel layers.
+
+FP8 = torch.float8_e4m3fn
+
+
+def _fp8_weights(packed_bf16: torch.Tensor):
+    """Packed bf16 fragments -> (fp8 fragments scaled into the e4m3 range, 1/scale)."""
+    amax = float(packed_bf16.abs().max())
+    e = 0 if amax == 0 else int(np.floor(np.log2(240.0 / amax)))
+    e = max(-8, min(12, e))
+    return (packed_bf16.float() * 2.0 ** e).to(FP8), 2.0 ** -e
+
+
+def _stack_fwd_fp8(x0: torch.Tensor, ws, bs, kinds) -> torch.Tensor:
+    """x0 [V,I,J,K,L] bf16 -> last layer output fp32 [V,I,J,K,L] (ReLU'd), fp8 inside."""
+    C = _ext.ext()
+    V, I, J, K, L = x0.shape
+    h = x0
+    for li, (w_ref, b, kind) in enumerate(zip(ws, bs, kinds)):
+        ks = w_ref.shape[0]
+        w = _std(w_ref)
+        if kind == "1in":
+            G = ij_groups(ks)
+            xs = torch.empty((G, V, I, J, K, L, 16), dtype=FP8, device=x0.device)
+            C.ijpack(h, xs, ks, 1)
+            wq, osc = _fp8_weights(pack_w16_planes(ij_in_weights(w)))
+            y = torch.empty((V, I, J, K, L, 16), dtype=FP8, device=x0.device)
+            C.conv16f8_fwd(xs, wq, _pad_bias(b, 16), y, ks, 1, 0, osc)
+        elif kind == "16":
+            wq, osc = _fp8_weights(pack_w16(w))
+            y = torch.empty((V, I, J, K, L, 16), dtype=FP8, device=x0.device)
+            C.conv16f8_fwd(h, wq, _pad_bias(b, 16), y, ks, 1, 0, osc)
+        else:  # "1out"
+            G, nq = ij_groups(ks), ks * ks
+            wq, osc = _fp8_weights(pack_w16_planes(ij_out_weights(w)))
+            z = torch.empty((nq, V, I, J, K, L), dtype=torch.float32, device=x0.device)
+            hx = h.unsqueeze(0)
+            for gi in range(G):
+                C.conv16f8_fwd(hx, wq[gi:gi + 1], None, z[16 * gi:min(nq, 16 * gi + 16)], ks, 4, 0, osc)
+            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
+            C.ijsum(z, _pad_bias(b, 1), y, ks, 1, 1)
+            del z
+            if li != len(kinds) - 1:
+                raise RuntimeError("fp8 NC path: the 1-channel output layer must be last")
+        h = y
+    return h
+
+
+def neigh_consensus_fp8(x: torch.Tensor, weights, biases, kinds, symmetric: bool = True) -> torch.Tensor:
+    """Inference-only NeighConsensus with fp8 operands (no autograd)."""
+    V, _, I, J, K, L = x.shape
+    R, Cc = I * J, K * L
+    xb = x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous()
+    if not symmetric:
+        return _stack_fwd_fp8(xb, weights, biases, kinds).reshape(V, 1, I, J, K, L)
+    xt = _swap_flat(xb.reshape(V, R, Cc), (I, J, K, L)).reshape(V, K, L, I, J)
+    if (I, J) == (K, L):
+        z = _stack_fwd_fp8(torch.cat((xb, xt), 0), weights, biases, kinds)
+    else:
+        z = torch.cat((_stack_fwd_fp8(xb, weights, biases, kinds).reshape(-1),
+                       _stack_fwd_fp8(xt, weights, biases, kinds).reshape(-1)))
+    y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x.device)
+    _ext.ext().combine_fwd(z, y, R, Cc)
+    return y.reshape(V, 1, I, J, K, L)
+
+
+def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool = True, fp8: bool = False) -> torch.Tensor:
+    """x: [V,1,I,J,K,L] fp32; weights in checkpoint layout [k, out, in, k, k, k].
+
+    ``fp8``: inference through the fp8 MFMA kernels (ignored when gradients
+    are required or the stack shape has no fp8 kernels)."""
     kernel_sizes = [w.shape[0] for w in weights]
     kinds = layer_kinds(channels, kernel_sizes)
     if _ext.use_hip(x) and kinds is not None:
+        if fp8 and not torch.is_grad_enabled() and kinds[0] == "1in" and kinds[-1] == "1out":
+            return neigh_consensus_fp8(x.float().contiguous(), weights, biases, kinds, symmetric)
         params = []
         for w, b in zip(weights, biases):
             params += [w, b]

@@ -349,3 +349,106 @@ def test_immatchnet_fp8_correlation_path():
         c8, d8 = m(batch)
     assert c8.shape == c16.shape
     assert rel_l2(c8, c16) < 0.1
+
+
+@pytest.mark.parametrize("ks,shape", [(5, (2, 25, 25, 25, 25)), (3, (1, 7, 9, 30, 27))])
+def test_conv16_fp8_kernel(ks, shape):
+    """fp8 (OCP e4m3) inference conv16 vs fp64 math on the same fp8 values:
+    bias+ReLU -> fp8 output and planar fp32 output, plain and group-plane mode."""
+    from ncnet_amd.ops.packing import pack_w16, pack_w16_planes
+    C = _ext.ext()
+    F8 = torch.float8_e4m3fn
+    torch.manual_seed(21)
+    V, I, J, K, L = shape
+    x = (torch.rand(V, I, J, K, L, 16, device=DEV) * 2).to(F8)
+    w = (torch.randn(16, 16, ks, ks, ks, ks, device=DEV) * 0.05).to(torch.bfloat16).float()
+    wsc = 64.0
+    wq = (pack_w16(w).float() * wsc).to(F8)
+    wr = (w * wsc).to(F8).double() / wsc          # the exact fp8 weight values used
+    b = torch.randn(16, device=DEV) * 0.1
+    xr = x.double().permute(0, 5, 1, 2, 3, 4)
+    yr = ref.conv4d(xr, ref.conv4d_weight_from_std(wr), b.double())
+    y = torch.empty((V, I, J, K, L, 16), dtype=F8, device=DEV)
+    C.conv16f8_fwd(x, wq, b, y, ks, 1, 0, 1.0 / wsc)
+    y_ref = torch.relu(yr).permute(0, 2, 3, 4, 5, 1)
+    assert rel_l2(y.float(), y_ref) < 0.04          # e4m3 output rounding (3 mantissa bits)
+    # planar fp32, group-plane mode with 2 groups at the (i, j) plane
+    wp = (torch.randn(2, 16, 16, ks, ks, device=DEV) * 0.05).to(torch.bfloat16).float()
+    wpq = (pack_w16_planes(wp).float() * wsc).to(F8)
+    wpr = (wp * wsc).to(F8).double() / wsc
+    x2 = (torch.rand(2, V, I, J, K, L, 16, device=DEV) * 2).to(F8)
+    z = torch.empty((16, V, I, J, K, L), dtype=torch.float32, device=DEV)
+    C.conv16f8_fwd(x2, wpq, None, z, ks, 4, 0, 1.0 / wsc)
+    xx = x2.double().permute(0, 1, 2, 3, 6, 4, 5).reshape(2, V * I * J, 16, K, L)
+    zr = sum(torch.nn.functional.conv2d(xx[g], wpr[g], padding=ks // 2) for g in range(2))
+    zr = zr.reshape(V, I, J, 16, K, L).permute(3, 0, 1, 2, 4, 5)
+    assert relerr(z, zr) < 1e-4
+
+
+def test_immatchnet_fp8_nc_path():
+    """corr_dtype='fp8' (fp8 correlation + fp8 NC) vs the bf16 path."""
+    from ncnet_amd.models import ImMatchNet
+    torch.manual_seed(0)
+    m = ImMatchNet(use_cuda=True, ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1],
+                   relocalization_k_size=2).to(DEV).eval()
+    for p in m.NeighConsensus.parameters():   # positive biases: a populated ReLU pattern
+        if p.dim() == 1:
+            p.data.uniform_(0.05, 0.2)
+    batch = {"source_image": torch.randn(1, 3, 256, 320, device=DEV),
+             "target_image": torch.randn(1, 3, 256, 320, device=DEV)}
+    with torch.inference_mode():
+        c16, _ = m(batch)
+        m.corr_dtype = "fp8"
+        c8, _ = m(batch)
+    assert c8.shape == c16.shape
+    assert rel_l2(c8, c16) < 0.15
+
+
+def test_nc_forward_deterministic_and_fully_written():
+    """Two NC forwards are bitwise equal (no atomics / races) and every output
+    voxel is written: the output buffers of the conv kernels are NaN-poisoned
+    before launch."""
+    from ncnet_amd.ops.neigh_consensus import neigh_consensus
+    from ncnet_amd.ops.packing import pack_w16
+    torch.manual_seed(13)
+    ws = [torch.randn(5, 16, 1, 5, 5, 5, device=DEV) * 0.05, torch.randn(5, 16, 16, 5, 5, 5, device=DEV) * 0.05,
+          torch.randn(5, 1, 16, 5, 5, 5, device=DEV) * 0.05]
+    bs = [torch.rand(16, device=DEV) * 0.1, torch.rand(16, device=DEV) * 0.1, torch.rand(1, device=DEV) * 0.1]
+    x = torch.rand(2, 1, 9, 11, 9, 11, device=DEV)
+    with torch.no_grad():
+        y1 = neigh_consensus(x, ws, bs, [16, 16, 1])
+        y2 = neigh_consensus(x, ws, bs, [16, 16, 1])
+    assert torch.equal(y1, y2)
+    assert torch.isfinite(y1).all()
+    C = _ext.ext()
+    xs = torch.rand(2, 9, 11, 30, 27, 16, device=DEV).to(torch.bfloat16)
+    w = pack_w16(torch.randn(16, 16, 5, 5, 5, 5, device=DEV) * 0.05)
+    y = torch.full_like(xs, float("nan"))
+    C.conv16_fwd(xs, w, torch.zeros(16, device=DEV), None, y, 5, 1, 0)
+    assert torch.isfinite(y.float()).all()
+    z = torch.full((5, 2, 9, 11, 30, 27), float("nan"), device=DEV)
+    C.conv16_fwd(xs, w, None, None, z, 5, 3, 1)
+    assert torch.isfinite(z).all()
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,pad,res,relu", [(64, 64, 3, 1, 1, False, True), (128, 256, 1, 1, 0, True, True),
+                                                            (256, 128, 3, 2, 1, False, True), (64, 256, 1, 2, 0, False, False),
+                                                            (128, 192, 3, 1, 1, True, False)])
+def test_conv2d_nhwc_kernel(cin, cout, k, stride, pad, res, relu):
+    """NHWC implicit-GEMM conv (+bias, +residual, ReLU) vs F.conv2d in fp64 on bf16 inputs."""
+    C = _ext.ext()
+    torch.manual_seed(17)
+    cl = torch.channels_last
+    x = torch.randn(2, cin, 19, 23, device=DEV).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(cout, cin, k, k, device=DEV) * 0.05).to(torch.bfloat16).contiguous(memory_format=cl)
+    b = torch.randn(cout, device=DEV)
+    yr = torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride, pad)
+    r = None
+    if res:
+        r = torch.randn(yr.shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=cl)
+        yr = yr + r.double()
+    if relu:
+        yr = torch.relu(yr)
+    y = torch.empty(yr.shape, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=cl)
+    C.conv2d_nhwc(x, w, b, r, y, stride, pad, 1 if relu else 0)
+    assert relerr(y, yr) < 1e-2

@@ -41,3 +41,11 @@ def test_plot_roundtrip(tmp_path):
     save_plot(str(tmp_path / "x.png"))
     plt.close("all")
     assert (tmp_path / "x.png").exists()
+
+
+def test_runtime_config_from_env():
+    from ncnet_amd.config import RuntimeConfig
+    c = RuntimeConfig.from_env({"NCNET_NC_ENC": "jc", "NCNET_WGRAD_VARIANT": "2", "NCNET_TRUNK_GRAPH": "0"})
+    assert c.nc_encoding == "jc" and c.wgrad_variant == 2 and not c.trunk_graph and c.trunk_plan
+    assert RuntimeConfig.from_env({"NCNET_NC_JC": "0"}).nc_encoding == "direct"
+    assert set(c.as_dict()) >= {"nc_encoding", "wgrad_variant", "conv16_variant"}
