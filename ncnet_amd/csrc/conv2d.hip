@@ -8,8 +8,9 @@
 // channels-last (NHWC) bf16, W is [Cout][KH][KW][Cin] (a channels-last conv
 // weight), bias fp32.  A k-step is one tap x 64 input channels, so the
 // im2col gather is one 128-B row load per pixel (zero outside the image) and
-// never materialised.  128 x BN output tile per 4-wave workgroup (BN = 128:
-// 2x2 waves of 64x64; BN = 64 for the 64-channel layers: 4x1 waves of 32x64),
+// never materialised.  BM x BN output tile per 4-wave workgroup (BN = 128:
+// 2x2 waves; BN = 64 for the 64-channel layers: 4x1 waves; BM = 64 for grids
+// that would not fill the chip),
 // v_mfma_f32_16x16x32_bf16, XOR-swizzled LDS rows, register double buffer,
 // XCD-aware tile order.  The epilogue fuses bias, the bottleneck residual and
 // ReLU, so a bottleneck is exactly four kernels and no elementwise passes
@@ -20,7 +21,7 @@
 namespace ncnet {
 
 namespace cv {
-constexpr int BM = 128, BK = 64;
+constexpr int BK = 64;
 __device__ __forceinline__ uint32_t toff(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ (row & 7)) << 4)); }
 }  // namespace cv
 
@@ -30,14 +31,17 @@ struct Conv2dArgs {
   int M, tiles_m, tiles_n, relu;
 };
 
-template <int BN>
+// BM x BN output tile: BM = 128, or 64 when the grid would not fill the chip
+// (layer3 at the training size: 157 x 2 tiles of 128 on 256 CUs).
+template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void conv2d_nhwc_kernel(Conv2dArgs p) {
   using namespace cv;
   constexpr int WN = BN == 128 ? 2 : 1;          // waves along N
   constexpr int WMW = 4 / WN;                    // waves along M
-  constexpr int TM = BM / WMW / 16;              // 16-row MFMA tiles per wave (4 or 2)
+  constexpr int TM = BM / WMW / 16;              // 16-row MFMA tiles per wave
   constexpr int TN = BN / WN / 16;               // 16-col MFMA tiles per wave (4)
-  constexpr int BCH = BN * 8 / 256;              // B chunks per thread (4 or 2)
+  constexpr int ACH = BM * 8 / 256;              // A chunks per thread
+  constexpr int BCH = BN * 8 / 256;              // B chunks per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* As = smem;
   char* Bs = smem + BM * 128;
@@ -49,11 +53,11 @@ __global__ __launch_bounds__(256, 2) void conv2d_nhwc_kernel(Conv2dArgs p) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int ch = threadIdx.x & 7;
 
-  // this thread's 4 A rows (pixels): image base offset and top-left input coordinate
-  int a_hi0[4], a_wi0[4];
-  size_t a_base[4];
+  // this thread's ACH A rows (pixels): image base offset and top-left input coordinate
+  int a_hi0[ACH], a_wi0[ACH];
+  size_t a_base[ACH];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
+  for (int m = 0; m < ACH; ++m) {
     const int row = (threadIdx.x >> 3) + 32 * m;
     const int pix = m0 + row;
     if (pix < p.M) {
@@ -71,12 +75,12 @@ __global__ __launch_bounds__(256, 2) void conv2d_nhwc_kernel(Conv2dArgs p) {
   const int cpt = p.Cin / BK;                    // k-steps per tap
   const int nk = p.KH * p.KW * cpt;
 
-  u32x4 ra[4], rb[BCH];
+  u32x4 ra[ACH], rb[BCH];
   auto load = [&](int ks) {
     const int tap = ks / cpt, c0 = (ks - tap * cpt) * BK;
     const int dh = tap / p.KW, dw = tap - dh * p.KW;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < ACH; ++m) {
       const int hi = a_hi0[m] + dh, wi = a_wi0[m] + dw;
       u32x4 v = {0u, 0u, 0u, 0u};
       if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.Wd)
@@ -92,7 +96,7 @@ __global__ __launch_bounds__(256, 2) void conv2d_nhwc_kernel(Conv2dArgs p) {
   };
   auto store = [&]() {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) *(u32x4*)(As + toff((threadIdx.x >> 3) + 32 * m, ch)) = ra[m];
+    for (int m = 0; m < ACH; ++m) *(u32x4*)(As + toff((threadIdx.x >> 3) + 32 * m, ch)) = ra[m];
 #pragma unroll
     for (int m = 0; m < BCH; ++m) *(u32x4*)(Bs + toff((threadIdx.x >> 3) + 32 * m, ch)) = rb[m];
   };
@@ -179,11 +183,15 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
   p.M = N * p.Ho * p.Wo;
   p.relu = relu;
   const int BN = (Cout % 128 == 0) ? 128 : 64;
-  p.tiles_m = cdiv(p.M, cv::BM);
   p.tiles_n = Cout / BN;
+  // 128-row tiles unless that leaves fewer than two workgroups per CU
+  const int BM = (cdiv(p.M, 128) * p.tiles_n < 512) ? 64 : 128;
+  p.tiles_m = cdiv(p.M, BM);
   dim3 grid((unsigned)(p.tiles_m * p.tiles_n)), block(256);
-  const size_t lds = (size_t)(cv::BM + BN) * 128;
-  if (BN == 128) hipLaunchKernelGGL((conv2d_nhwc_kernel<128>), grid, block, lds, stream, p);
-  else hipLaunchKernelGGL((conv2d_nhwc_kernel<64>), grid, block, lds, stream, p);
+  const size_t lds = (size_t)(BM + BN) * 128;
+#define LC2(BMV, BNV) hipLaunchKernelGGL((conv2d_nhwc_kernel<BMV, BNV>), grid, block, lds, stream, p)
+  if (BM == 128) { if (BN == 128) LC2(128, 128); else LC2(128, 64); }
+  else { if (BN == 128) LC2(64, 128); else LC2(64, 64); }
+#undef LC2
   return (int)hipGetLastError();
 }

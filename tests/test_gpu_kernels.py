@@ -431,15 +431,19 @@ def test_nc_forward_deterministic_and_fully_written():
     assert torch.isfinite(z).all()
 
 
-@pytest.mark.parametrize("cin,cout,k,stride,pad,res,relu", [(64, 64, 3, 1, 1, False, True), (128, 256, 1, 1, 0, True, True),
-                                                            (256, 128, 3, 2, 1, False, True), (64, 256, 1, 2, 0, False, False),
-                                                            (128, 192, 3, 1, 1, True, False)])
-def test_conv2d_nhwc_kernel(cin, cout, k, stride, pad, res, relu):
-    """NHWC implicit-GEMM conv (+bias, +residual, ReLU) vs F.conv2d in fp64 on bf16 inputs."""
+@pytest.mark.parametrize("cin,cout,k,stride,pad,res,relu,shape", [
+    (64, 64, 3, 1, 1, False, True, (2, 19, 23)), (128, 256, 1, 1, 0, True, True, (2, 19, 23)),
+    (256, 128, 3, 2, 1, False, True, (2, 19, 23)), (64, 256, 1, 2, 0, False, False, (2, 19, 23)),
+    (128, 192, 3, 1, 1, True, False, (2, 19, 23)),
+    # large enough for the 128-row tiles (>= 512 workgroups)
+    (64, 128, 3, 1, 1, True, True, (4, 129, 127)), (64, 64, 1, 1, 0, False, True, (4, 129, 127))])
+def test_conv2d_nhwc_kernel(cin, cout, k, stride, pad, res, relu, shape):
+    """NHWC implicit-GEMM conv (+bias, +residual, ReLU) vs F.conv2d in fp64 on bf16 inputs
+    (both the 64- and 128-row tile variants)."""
     C = _ext.ext()
     torch.manual_seed(17)
     cl = torch.channels_last
-    x = torch.randn(2, cin, 19, 23, device=DEV).to(torch.bfloat16).contiguous(memory_format=cl)
+    x = torch.randn(shape[0], cin, shape[1], shape[2], device=DEV).to(torch.bfloat16).contiguous(memory_format=cl)
     w = (torch.randn(cout, cin, k, k, device=DEV) * 0.05).to(torch.bfloat16).contiguous(memory_format=cl)
     b = torch.randn(cout, device=DEV)
     yr = torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride, pad)
