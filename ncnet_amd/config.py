@@ -15,7 +15,7 @@ import os
 class RuntimeConfig:
     nc_encoding: str = "ij"          # NCNET_NC_ENC: ij | ijfull | jc | direct
     wgrad_variant: int = 3           # NCNET_WGRAD_VARIANT
-    conv16_variant: int = 2          # NCNET_CONV16_VARIANT
+    conv16_variant: int = 3          # NCNET_CONV16_VARIANT
     trunk_plan: bool = True          # NCNET_TRUNK_PLAN
     trunk_graph: bool = True         # NCNET_TRUNK_GRAPH
     force_torch: bool = False        # NCNET_FORCE_TORCH
@@ -29,7 +29,7 @@ class RuntimeConfig:
             enc = "direct"
         return cls(nc_encoding=enc,
                    wgrad_variant=int(e.get("NCNET_WGRAD_VARIANT", "3")),
-                   conv16_variant=int(e.get("NCNET_CONV16_VARIANT", "2")),
+                   conv16_variant=int(e.get("NCNET_CONV16_VARIANT", "3")),
                    trunk_plan=e.get("NCNET_TRUNK_PLAN", "1") != "0",
                    trunk_graph=e.get("NCNET_TRUNK_GRAPH", "1") != "0",
                    force_torch=e.get("NCNET_FORCE_TORCH", "0") == "1",

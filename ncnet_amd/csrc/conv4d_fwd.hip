@@ -21,6 +21,7 @@
 #include "common.h"
 #include <hip/hip_fp8.h>
 #include <stdlib.h>
+#include <type_traits>
 
 namespace ncnet {
 
@@ -39,6 +40,7 @@ struct ConvGeom {
   float oscale;       // fp8 kernel: accumulator scale (1 / weight scale)
   int npg;            // > 0: "group planes" mode (v2 only): plane s is the (i, j)
   long long gstride;  //   plane of input group s at X + s * gstride, weights plane s
+  int njb;            // v3: output j-blocks of R planes per (v, i)
 };
 
 // Decode the workgroup's output tile.
@@ -356,6 +358,8 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
     // draining the in-flight plane DMA (plain s_barrier, LDS counter only)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (s + 1 < nplanes) issue_w(s + 1);
+    // per-tile branches kept: the branch-free body needs 129 VGPRs (> 128,
+    // one workgroup per CU instead of two: 6.4 -> 9.4 ms measured)
 #pragma unroll
     for (int tt = 0; tt < MAXT; ++tt) {
       if (wave + NW * tt < ntile) {
@@ -379,6 +383,176 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
       if (vi < nvox && kg < g.K && lg < g.L)
         store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4),
                      (size_t)g.V * g.I * g.J * g.K * g.L, g.nco);
+    }
+  }
+}
+
+// ===========================================================================
+// conv16v3_fwd: 16 -> 16 (full (di, dj) plane sum) with the X operand reused
+// from registers across output j-planes.
+//
+// conv16v2 reads one X fragment from LDS per MFMA (a ds_read_b128 = 4 LDS
+// cycles per 16-cycle MFMA per SIMD: the LDS array is as busy as the matrix
+// cores).  Here a workgroup owns R consecutive output planes (v, i, j0..j0+R-1)
+// of one (k, l) tile.  Input plane (i+di-P, j') feeds output planes
+// j = j' - dj + P for every dj, so each X fragment read from LDS is multiplied
+// by up to KS weight fragments (one per dj) into KS different accumulator
+// sets.  Per workgroup and di the R + KS - 1 input j-planes stream through two
+// LDS buffers (LDS-DMA, one plane ahead) and the KS dj-slices of the di
+// weights (KS x 13 KB for KS = 5) sit in LDS; LDS reads per MFMA drop from
+// 1.2 to ~0.56 and each staged plane is used R_eff ~ 2.8 times instead of once.
+//  * accumulators [R][MAXT] (100 VGPRs): the j' loop is unrolled at compile
+//    time (static_for) so every accumulator index is static;
+//  * weight slot dj of the next di is refilled as soon as its last consumer
+//    plane (R - 1 + dj) has passed a barrier -- no stall between di steps;
+//  * 8 waves x 5 voxel tiles, 1 workgroup per CU (128 KB LDS for KS = 5).
+// Plane geometry (RS = TL + 8, halo zero-fill, row DMA) as conv16v2.
+// ===========================================================================
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+template <int KS, int R, int EPI>
+__global__ __launch_bounds__(512, 1) void conv16v3_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
+                                                              const float* __restrict__ bias,
+                                                              const bf16* __restrict__ M, bf16* __restrict__ Y,
+                                                              ConvGeom g) {
+  constexpr int P = KS / 2;
+  constexpr int NT = KS * KS;
+  constexpr int NQ = (NT + 1) / 2;
+  constexpr int NW = 8;
+  constexpr int MAXT = 5;
+  constexpr int S = R + KS - 1;  // input j-planes per di
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int plane_bytes = g.PR * g.RS * 32;
+  char* wbuf = smem + 2 * plane_bytes;  // [KS dj][NQ][64 lanes] x 16 B
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int lt = bid % g.nlt; bid /= g.nlt;
+  const int kt = bid % g.nkt; bid /= g.nkt;
+  const int jb = bid % g.njb; bid /= g.njb;
+  const int ti = bid % g.I, tv = bid / g.I;
+  const int k0 = kt * g.TK, l0 = lt * g.TL, j0 = jb * R;
+  const int di_lo = max(0, P - ti), di_hi = min(KS, g.I + P - ti);
+  const int nvox = g.TK * g.TL;
+  const int ntile = (nvox + 15) >> 4;
+
+  for (int o = threadIdx.x * 16; o < 2 * plane_bytes; o += NW * 64 * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
+
+  uint32_t vbase[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    int vi = (wave + NW * tt) * 16 + (lane & 15);
+    if (vi >= nvox) vi = 0;
+    int kk = vi / g.TL, ll = vi - kk * g.TL;
+    vbase[tt] = (uint32_t)((kk * g.RS + ll) * 32 + ((lane >> 4) & 1) * 16);
+  }
+  uint32_t toff[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    int tap = 2 * q + (lane >> 5);
+    if (tap >= NT) tap = NT - 1;
+    int dk = tap / KS, dl = tap - dk * KS;
+    toff[q] = (uint32_t)((dk * g.RS + dl) * 32);
+  }
+  f32x4 acc[R][MAXT];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lstart = max(0, l0 - P), lend = min(g.L, l0 - P + g.RW);
+  const int nchunk = 2 * (lend - lstart);
+  const int col0 = lstart - (l0 - P);
+
+  auto issue_x = [&](int di, int jp, char* buf) {
+    const bf16* xp = X + plane_offset(g, tv, ti + di - P, jp, 16);
+    for (int r = wave; r < g.PR; r += NW) {
+      const int kg = k0 - P + r;
+      if (kg >= 0 && kg < g.K && lane < nchunk) {
+        const bf16* src = xp + ((size_t)kg * g.L + lstart) * 16 + lane * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(void, buf + (r * g.RS + col0) * 32), 16, 0, 0);
+      }
+    }
+  };
+  auto issue_w = [&](int di, int dj) {
+    const u32x4* wp = Wp + (size_t)(di * KS + dj) * (NQ * 64);
+    for (int q = wave; q < NQ; q += NW)
+      __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + (dj * NQ + q) * 1024),
+                                       16, 0, 0);
+  };
+
+  __syncthreads();  // zero-fill complete before any DMA lands
+  for (int dj = 0; dj < KS; ++dj) issue_w(di_lo, dj);
+  if (j0 - P >= 0 && j0 - P < g.J) issue_x(di_lo, j0 - P, smem);
+  int n = 0;  // linear plane counter: buffer parity
+  for (int di = di_lo; di < di_hi; ++di) {
+    static_for<0, S>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      __syncthreads();  // plane n (and weights issued earlier) landed; plane n-1 consumed
+      char* cur = smem + (n & 1) * plane_bytes;
+      {
+        const int ndi = (s + 1 == S) ? di + 1 : di;
+        const int njp = j0 - P + ((s + 1 == S) ? 0 : s + 1);
+        if (ndi < di_hi && njp >= 0 && njp < g.J) issue_x(ndi, njp, smem + ((n + 1) & 1) * plane_bytes);
+      }
+      // weight slot dj is last read by plane R - 1 + dj: refill it for di + 1
+      if constexpr (s >= R) {
+        if (di + 1 < di_hi) issue_w(di + 1, s - R);
+      }
+      if constexpr (s == 0) {
+        if (di > di_lo) issue_w(di, KS - 1);
+      }
+      const int jp = j0 - P + s;
+      if (jp >= 0 && jp < g.J) {
+        constexpr int dlo = (s - R + 1) > 0 ? (s - R + 1) : 0;
+        constexpr int dhi = s < KS - 1 ? s : KS - 1;  // inclusive
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          bf16x8 a[KS];
+          static_for<dlo, dhi + 1>([&](auto dc) {
+            constexpr int dj = decltype(dc)::value;
+            a[dj] = lds_read16(wbuf, ((dj * NQ + q) * 64 + lane) * 16);
+          });
+          // no per-tile validity branch: tiles past ntile read voxel 0 and are
+          // never stored (a divergent branch here splits the block and
+          // serialises every LDS read with its MFMAs)
+#pragma unroll
+          for (int tt = 0; tt < MAXT; ++tt) {
+            const bf16x8 xf = lds_read16(cur, vbase[tt] + toff[q]);
+            static_for<dlo, dhi + 1>([&](auto dc) {
+              constexpr int dj = decltype(dc)::value;
+              acc[s - dj][tt] = mfma16(a[dj], xf, acc[s - dj][tt]);
+            });
+          }
+        }
+      }
+      ++n;
+    });
+  }
+
+  const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = j0 + r;
+    if (j >= g.J) break;
+    const size_t vbase_out = plane_offset(g, tv, ti, j, 1);
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      int tile = wave + NW * tt;
+      if (tile < ntile) {
+        int vi = tile * 16 + (lane & 15);
+        int kk = vi / g.TL, ll = vi - kk * g.TL;
+        int kg = k0 + kk, lg = l0 + ll;
+        if (vi < nvox && kg < g.K && lg < g.L)
+          store16<EPI>(acc[r][tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco);
+      }
     }
   }
 }
@@ -418,6 +592,7 @@ __global__ __launch_bounds__(512, 2) void conv16f8_fwd_kernel(const uint8_t* __r
   const int nplanes = g.npg > 0 ? g.npg : (di_hi - di_lo) * ndj;
   const int nvox = g.TK * g.TL;
   const int ntile = (nvox + 15) >> 4;
+  const bool full_wave = __builtin_amdgcn_readfirstlane(wave + NW * (MAXT - 1) < ntile);
 
   for (int o = threadIdx.x * 16; o < 2 * plane_bytes; o += NW * 64 * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
 
@@ -476,16 +651,20 @@ __global__ __launch_bounds__(512, 2) void conv16f8_fwd_kernel(const uint8_t* __r
     for (int q = 0; q < NQ; ++q) wf[q] = *(const long*)(wbuf + (q * 64 + lane) * 8);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (s + 1 < nplanes) issue_w(s + 1);
+    auto tiles = [&](auto fullc) {   // branch-free body for full waves (see conv16v2)
+      constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-    for (int tt = 0; tt < MAXT; ++tt) {
-      if (wave + NW * tt < ntile) {
+      for (int tt = 0; tt < MAXT; ++tt) {
+        if (FULL || wave + NW * tt < ntile) {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const long xf = *(const long*)(cur + vbase[tt] + toff[q]);
-          acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(wf[q], xf, acc[tt], 0, 0, 0);
+          for (int q = 0; q < NQ; ++q) {
+            const long xf = *(const long*)(cur + vbase[tt] + toff[q]);
+            acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(wf[q], xf, acc[tt], 0, 0, 0);
+          }
         }
       }
-    }
+    };
+    if (full_wave) tiles(std::true_type{}); else tiles(std::false_type{});
   }
 
   const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);
@@ -810,6 +989,7 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.RW = g.RS;
   g.dj_center = 0;
   g.npg = 0; g.gstride = 0; g.nco = 16; g.oscale = 1.f;
+  g.njb = J;
   return g;
 }
 
@@ -826,12 +1006,10 @@ static void pick_tile(int K, int L, int& tk, int& tl) {
   while (tk * tl > 640) { if (tl > tk) --tl; else --tk; }
 }
 
+// read per launch (cheap) so tests can switch variants inside one process
 static int conv16_variant() {
-  static int v = [] {
-    const char* e = getenv("NCNET_CONV16_VARIANT");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
+  const char* e = getenv("NCNET_CONV16_VARIANT");
+  return e ? atoi(e) : 3;
 }
 
 // npg > 0: group-planes mode -- X holds npg input groups [npg][V,I,J,K,L,16]
@@ -847,12 +1025,27 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
   g.npg = npg;
   g.gstride = (long long)V * I * J * K * L * 16;
   g.nco = nco;
-  if (npg > 0 && !(conv16_variant() == 2 && g.RW <= 32)) return -3;   // v2 only
-  if (epi == EPI_F32X16 && !(conv16_variant() == 2 && g.RW <= 32)) return -3;
+  const int variant = conv16_variant();
+  const bool lds_dma = variant >= 2 && g.RW <= 32;
+  if ((npg > 0 || epi == EPI_F32X16) && !lds_dma) return -3;   // v2 only
   if (g.PR * g.RS * 2 > 8 * 256) return -1;
   int nq = (KS * KS + 1) / 2;
   const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
-  if (conv16_variant() == 2 && g.RW <= 32) {
+  if (lds_dma && variant == 3 && npg == 0 && !dj_center && (epi == EPI_BIAS_RELU || epi == EPI_MASK) &&
+      (KS == 5 || KS == 3)) {
+    // full (di, dj) sum: R = 5 output j-planes per workgroup, X reused across dj
+    constexpr int R = 5;
+    g.RS = tl + ((KS - 1 + 7) / 8) * 8;
+    g.njb = cdiv(J, R);
+    size_t lds3 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)KS * nq * 1024;
+    dim3 grid3((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block3(512);
+#define L16V3(KSV, EPIV) hipLaunchKernelGGL((conv16v3_fwd_kernel<KSV, R, EPIV>), grid3, block3, lds3, stream, x, w, bias, m, y, g)
+    if (KS == 5) { if (epi == EPI_BIAS_RELU) L16V3(5, EPI_BIAS_RELU); else L16V3(5, EPI_MASK); }
+    else { if (epi == EPI_BIAS_RELU) L16V3(3, EPI_BIAS_RELU); else L16V3(3, EPI_MASK); }
+#undef L16V3
+    return (int)hipGetLastError();
+  }
+  if (lds_dma) {
     // Row stride RS = TL + 8: a 16-voxel tile that wraps to the next row then
     // jumps 256 B (the full 64-bank period), so every ds_read_b128 lane group
     // stays conflict-free (a TL + KS - 1 stride cost ~1/3 extra LDS cycles).

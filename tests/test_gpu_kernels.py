@@ -35,10 +35,13 @@ def test_extension_loaded():
     import ncnet_amd._C as C  # noqa: F401
 
 
+@pytest.mark.parametrize("variant", ["3", "2"])
 @pytest.mark.parametrize("ks,shape", [(5, (2, 25, 25, 25, 25)), (3, (1, 7, 9, 11, 13)), (3, (1, 3, 2, 30, 27)),
-                                      (5, (1, 6, 5, 26, 29))])
-def test_conv16_fwd(ks, shape):
+                                      (5, (1, 6, 5, 26, 29)), (5, (1, 4, 12, 9, 7))])
+def test_conv16_fwd(ks, shape, variant, monkeypatch):
+    """conv16 forward (v3: X reused over 5 output j-planes; v2: one plane per workgroup)."""
     from ncnet_amd.ops.packing import pack_w16
+    monkeypatch.setenv("NCNET_CONV16_VARIANT", variant)
     torch.manual_seed(0)
     V, I, J, K, L = shape
     x = torch.rand(V, 16, I, J, K, L, device=DEV)
