@@ -47,6 +47,22 @@ __device__ __forceinline__ bf16x8 cat8(const bf16x4& lo, const bf16x4& hi) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// The same fragments as 32-bit lanes: register copies / concatenations of
+// bf16 vectors can be legalised element-wise (16-bit shifts + v_perm per
+// element); moving them as u32 vectors keeps them plain VGPR moves.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2 lds_read_tr16u(const char* lds_base, uint32_t byte_off) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds_base + byte_off));
+  return __builtin_bit_cast(u32x2, v);
+}
+__device__ __forceinline__ u32x4 cat4u(const u32x2& lo, const u32x2& hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3);
+}
+__device__ __forceinline__ f32x4 mfma16u(const u32x4& a, const u32x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                 0);
+}
+
 __device__ __forceinline__ bf16x8 lds_read16(const char* lds_base, uint32_t byte_off) {
   return *(const bf16x8*)(lds_base + byte_off);
 }

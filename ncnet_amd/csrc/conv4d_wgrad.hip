@@ -405,9 +405,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
     for (int d = 0; d < KS; ++d) acc[m][d] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < EXP; ++e) accx[e] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ones;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) ones[q] = f2bf(1.f);
+  const u32x4 ones = {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};   // bf16 1.0 x 8
 
   const int c_lo = grp * g.cpg, c_hi = min(g.ncols, c_lo + g.cpg);
   const int nch = (g.VT >> 6);            // chunks per half (VT multiple of 64)
@@ -505,28 +503,30 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
         gslot[d] = (uint32_t)((d >= di_lo && d <= di_hi) ? (base + ii - d + P) % NS : NS) * gbytes;
       // software pipeline: the next chunk's G fragments and the next tap's X
       // fragment are in flight while the current MFMAs run
-      bf16x8 bcur[KS], bnxt[KS];
+      // fragments held as u32 vectors (see cat4u in common.h)
+      // ping-pong by chunk parity (compile-time after unrolling: no copies)
+      u32x4 bfr[2][KS];
 #pragma unroll
       for (int d = 0; d < KS; ++d)
-        bcur[d] = cat8(lds_read_tr16(gbuf, gslot[d] + ga_base), lds_read_tr16(gbuf, gslot[d] + ga_base + 512));
+        bfr[0][d] = cat4u(lds_read_tr16u(gbuf, gslot[d] + ga_base), lds_read_tr16u(gbuf, gslot[d] + ga_base + 512));
 #pragma unroll
       for (int u = 0; u < MAXC; ++u) {
         if (u < nch) {
           const uint32_t pa0 = pav0[u], pa1 = pav1[u];
-          bf16x8 afr = cat8(lds_read_tr16(xc, pa0 + toff[0]), lds_read_tr16(xc, pa1 + toff[0]));
+          u32x4 afr = cat4u(lds_read_tr16u(xc, pa0 + toff[0]), lds_read_tr16u(xc, pa1 + toff[0]));
           if (u + 1 < nch) {
             const uint32_t gn = ga_base + (u + 1) * 1024;
 #pragma unroll
             for (int d = 0; d < KS; ++d)
-              bnxt[d] = cat8(lds_read_tr16(gbuf, gslot[d] + gn), lds_read_tr16(gbuf, gslot[d] + gn + 512));
+              bfr[(u + 1) & 1][d] = cat4u(lds_read_tr16u(gbuf, gslot[d] + gn), lds_read_tr16u(gbuf, gslot[d] + gn + 512));
           }
 #pragma unroll
           for (int m = 0; m < TPG; ++m) {
-            bf16x8 afn = afr;
+            u32x4 afn = afr;
             if (m + 1 < TPG || tg > 0)
-              afn = cat8(lds_read_tr16(xc, pa0 + toff[m + 1]), lds_read_tr16(xc, pa1 + toff[m + 1]));
+              afn = cat4u(lds_read_tr16u(xc, pa0 + toff[m + 1]), lds_read_tr16u(xc, pa1 + toff[m + 1]));
 #pragma unroll
-            for (int d = 0; d < KS; ++d) acc[m][d] = mfma16(afr, bcur[d], acc[m][d]);
+            for (int d = 0; d < KS; ++d) acc[m][d] = mfma16u(afr, bfr[u & 1][d], acc[m][d]);
             afr = afn;
           }
           if (tg > 0) {   // last tap (afr), this group's di range (B re-read from LDS)
@@ -536,16 +536,12 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
               const int d = xdi_lo + e;
               if (d < xdi_hi) {
                 const uint32_t gsx = (uint32_t)((d >= di_lo && d <= di_hi) ? (base + ii - d + P) % NS : NS) * gbytes;
-                bf16x8 bx = cat8(lds_read_tr16(gbuf, gsx + ga), lds_read_tr16(gbuf, gsx + ga + 512));
-                accx[e] = mfma16(afr, bx, accx[e]);
+                u32x4 bx = cat4u(lds_read_tr16u(gbuf, gsx + ga), lds_read_tr16u(gbuf, gsx + ga + 512));
+                accx[e] = mfma16u(afr, bx, accx[e]);
               }
             }
           }
-          if (center_blk && tg == 0) accb = mfma16(ones, bcur[P], accb);
-          if (u + 1 < nch) {
-#pragma unroll
-            for (int d = 0; d < KS; ++d) bcur[d] = bnxt[d];
-          }
+          if (center_blk && tg == 0) accb = mfma16u(ones, bfr[u & 1][P], accb);
         }
       }
     }
