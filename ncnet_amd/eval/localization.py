@@ -20,8 +20,8 @@ match -> pose -> localization-rate chain can run without MATLAB:
   ``evaluate_queries`` for the per-floor top-1 check (:20-67).
 * ``resize_longest``: longest side <= 1920 px (lib_matlab/at_imageresize_nc4d.m).
 
-Dense pose verification (synthetic view rendering + dense SIFT, M4-M6) needs
-the InLoc scan point clouds and VLFeat; it stays out of scope.
+Dense pose verification (synthetic view rendering + dense SIFT, M4-M6) is in
+``pose_verification.py``; match / curve plots (M7, M11) in ``utils/plot.py``.
 """
 from __future__ import annotations
 

@@ -61,10 +61,18 @@ def test_point_transfer_demo(workdir):
 
 
 def test_inloc_localize_synthetic(workdir):
+    """P3P LO-RANSAC on the shortlist's top-1 pano (whose matches support a
+    wrong pose in the synthetic scene) fails; dense pose verification
+    re-ranks the candidates and recovers every query."""
     import inloc_localize
-    est, rate = inloc_localize.main(["--synthetic", "2", "--out", os.path.join(workdir, "poses.npz")])
-    assert len(est) == 2 and rate[-1] == 1.0
+    args = ["--synthetic", "2", "--ransac_iters", "2000", "--out", os.path.join(workdir, "poses.npz")]
+    est, rate = inloc_localize.main(args)
+    assert len(est) == 2 and rate[-1] == 0.0
     assert os.path.exists(os.path.join(workdir, "poses.npz"))
+    est_pv, rate_pv = inloc_localize.main(args + ["--pv", "--plot", os.path.join(workdir, "curves.png")])
+    assert len(est_pv) == 2 and rate_pv[-1] == 1.0
+    assert os.path.exists(os.path.join(workdir, "curves.png"))
+    assert os.path.exists("error_NCNet_PV.txt")
 
 
 def test_reference_refposes_parse():
