@@ -9,7 +9,9 @@ sharded over ranks (torchrun) and existing outputs are skipped (resume).
 
 Extras: --synthetic_queries N builds a fake shortlist and random images in a
 temp dir (smoke / benchmark without the dataset); --ncons_* for
-checkpoint-less runs; --output_dir (default matches/).
+checkpoint-less runs; --output_dir (default matches/); --fp8 (e4m3
+correlation + NC on the fp8 MFMA); --volume_parallel (under torchrun, every
+pair's volume is sharded over all ranks instead of sharding the queries).
 """
 from __future__ import annotations
 
@@ -77,6 +79,11 @@ def main(argv=None):
     ap.add_argument("--synthetic_queries", type=int, default=0)
     ap.add_argument("--ncons_kernel_sizes", nargs="+", type=int, default=[3, 3])
     ap.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 1])
+    ap.add_argument("--fp8", action="store_true",
+                    help="OCP fp8 e4m3 correlation operands + fp8 NeighConsensus (MI355X fp8 MFMA)")
+    ap.add_argument("--volume_parallel", action="store_true",
+                    help="all ranks cooperate on every pair, sharding its 4D volume along the A rows "
+                         "(ncnet_amd/parallel/volume_parallel.py); default: queries sharded over ranks")
     args = ap.parse_args(argv)
     ctx = init_distributed()
 
@@ -86,10 +93,19 @@ def main(argv=None):
         args.inloc_shortlist, args.query_path, args.pano_path = make_synthetic_inloc(
             tmp, args.synthetic_queries, args.n_panos)
         args.n_queries = args.synthetic_queries
+    torch.manual_seed(1)   # checkpoint-less (synthetic) runs: the same random NC weights on every launch
     model = ImMatchNet(use_cuda=ctx.device.type == "cuda", checkpoint=args.checkpoint or None,
                        ncons_kernel_sizes=args.ncons_kernel_sizes, ncons_channels=args.ncons_channels,
-                       half_precision=True, relocalization_k_size=args.k_size).to(ctx.device)
+                       half_precision=True, relocalization_k_size=args.k_size,
+                       corr_dtype="fp8" if args.fp8 else "bf16").to(ctx.device)
     model.eval()
+    vp = None
+    if args.volume_parallel and ctx.world_size > 1:
+        from ncnet_amd.parallel.dist import broadcast_module
+        from ncnet_amd.parallel.volume_parallel import VolumeParallelMatcher
+        broadcast_module(model, ctx)
+        vp = VolumeParallelMatcher(model, ctx)
+    q_start, q_step = (0, 1) if vp is not None else (ctx.rank, ctx.world_size)
     folder = output_folder(args.inloc_shortlist, args.image_size, args.k_size, args.matching_both_directions,
                            args.flip_matching_direction, args.softmax, args.checkpoint)
     out_dir = os.path.join(args.output_dir, folder)
@@ -102,7 +118,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     npairs = 0
     with torch.inference_mode():
-        for q in range(ctx.rank, nq, ctx.world_size):
+        for q in range(q_start, nq, q_step):
             path = os.path.join(out_dir, f"{q + 1}.mat")
             if os.path.exists(path):
                 continue
@@ -112,14 +128,16 @@ def main(argv=None):
             for idx in range(min(args.n_panos, len(panos[q]))):
                 tgt = prepare_image(read_image(os.path.join(args.pano_path, panos[q][idx])), args.image_size,
                                     args.k_size, ctx.device)
-                out = model({"source_image": src, "target_image": tgt})
+                pair = {"source_image": src, "target_image": tgt}
+                out = vp.forward(pair) if vp is not None else model(pair)
                 corr4d, delta4d = out if args.k_size > 1 else (out, None)
                 m = pair_matches(corr4d, delta4d, args.k_size, args.softmax, args.matching_both_directions,
                                  args.flip_matching_direction).double().cpu().numpy()
                 n = min(len(m), N)
                 matches[0, idx, :n] = m[:n]
                 npairs += 1
-            save_query(path, matches, queries[q], pano_all)
+            if vp is None or ctx.is_main:
+                save_query(path, matches, queries[q], pano_all)
             if ctx.is_main:
                 print(f"query {q + 1}/{nq} ({npairs} pairs, {npairs / (time.perf_counter() - t0):.2f} pairs/s/rank)",
                       flush=True)

@@ -253,8 +253,7 @@ class ImMatchNet(nn.Module):
                 corr4d, delta = correlation_pool2(fa, fb, ha, wa, hb, wb)
             else:
                 corr4d = correlation(fa, fb).view(b, 1, ha, wa, hb, wb)
-                corr4d, *delta = maxpool4d(corr4d, k)
-                delta = tuple(delta)
+                corr4d, delta = maxpool4d(corr4d, k)
         else:
             corr4d = correlation(fa, fb).view(b, 1, ha, wa, hb, wb)
         corr4d = self.process_correlation(corr4d)

@@ -12,6 +12,11 @@ random-init weights); the images are resized exactly like eval_inloc
 Prints one JSON line with ms/pair and a per-stage breakdown (CUDA events).
 
     python scripts/bench_inloc.py --image-size 1600 --pairs 5 --warmup 2
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 scripts/bench_inloc.py --image-size 3200 --fp8 --volume-parallel
+
+--volume-parallel: every pair's volume is sharded along its A rows over all
+ranks (ncnet_amd/parallel/volume_parallel.py); the latency is the max over
+ranks and includes the final gather of the volume (no per-stage breakdown).
 """
 from __future__ import annotations
 
@@ -43,7 +48,10 @@ def main():
     ap.add_argument("--fp8", action="store_true", help="OCP fp8 correlation operands (MX-fp8 MFMA)")
     ap.add_argument("--impl", choices=["hip", "reference"], default="hip",
                     help="reference: the reference algorithm in plain PyTorch-ROCm (fp32 backbone, fp16 volume)")
+    ap.add_argument("--volume-parallel", action="store_true")
     a = ap.parse_args()
+    if a.volume_parallel:
+        return bench_volume_parallel(a)
     dev = torch.device("cuda")
     torch.manual_seed(0)
     model = ImMatchNet(use_cuda=True, ncons_kernel_sizes=a.ncons_kernel_sizes, ncons_channels=a.ncons_channels,
@@ -121,6 +129,59 @@ def main():
         "stages_ms": {k: round(v / a.pairs, 3) for k, v in stages.items()},
         "matches": nmatch, "matches_contract": n_matches(a.image_size, a.k, True),
     }))
+
+
+def bench_volume_parallel(a):
+    from ncnet_amd.parallel.dist import all_reduce_max_float, barrier, broadcast_module, destroy, init_distributed
+    from ncnet_amd.parallel.volume_parallel import VolumeParallelMatcher
+
+    ctx = init_distributed()
+    dev = ctx.device
+    torch.manual_seed(0)
+    model = ImMatchNet(use_cuda=dev.type == "cuda", ncons_kernel_sizes=a.ncons_kernel_sizes,
+                       ncons_channels=a.ncons_channels, half_precision=True, relocalization_k_size=a.k,
+                       corr_dtype="fp8" if a.fp8 else "bf16").to(dev).eval()
+    broadcast_module(model, ctx)
+    vp = VolumeParallelMatcher(model, ctx)
+    h, w = target_size(a.src_hw[0], a.src_hw[1], a.image_size, a.k)
+    g = torch.Generator(device=dev).manual_seed(0)
+    batch = {"source_image": torch.randn(1, 3, h, w, device=dev, generator=g),
+             "target_image": torch.randn(1, 3, h, w, device=dev, generator=g)}
+    nmatch = 0
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    def one():
+        nonlocal nmatch
+        with torch.inference_mode():
+            out = vp.forward(batch)
+            corr4d, delta = out if a.k > 1 else (out, None)
+            if not a.no_matches and ctx.is_main:
+                nmatch = int(pair_matches(corr4d, delta, a.k, True, True).shape[0])
+
+    for _ in range(a.warmup):
+        one()
+    sync()
+    barrier(ctx)
+    t0 = time.perf_counter()
+    for _ in range(a.pairs):
+        one()
+    sync()
+    barrier(ctx)
+    ms = all_reduce_max_float((time.perf_counter() - t0) * 1e3 / a.pairs, ctx)
+    if ctx.is_main:
+        fs = (h // 16 // a.k, w // 16 // a.k)
+        print(json.dumps({
+            "metric": "InLoc dense matching latency per pair (fwd, k=%d relocalization, volume parallel)" % a.k,
+            "value": round(ms, 3), "unit": "ms/pair", "higher_is_better": False, "pairs_per_s": round(1e3 / ms, 3),
+            "n_gpus": ctx.world_size, "pairs": a.pairs, "warmup": a.warmup, "impl": "hip",
+            "dtype": "fp8-corr/bf16" if a.fp8 else "bf16", "data": "synthetic (random 4:3 images, random-init weights)",
+            "config": {"image": [h, w], "volume": list(fs) * 2, "ncons": [a.ncons_kernel_sizes, a.ncons_channels],
+                       "k": a.k, "parallelism": f"vp{ctx.world_size}"},
+            "matches": nmatch}))
+    destroy(ctx)
 
 
 if __name__ == "__main__":

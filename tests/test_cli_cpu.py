@@ -84,3 +84,27 @@ def test_reference_refposes_parse():
     refs = inloc_localize.load_refposes(path)
     assert len(refs) == 198 + 131
     assert refs[0]["P"].shape == (3, 4) and refs[0]["floor"] == "DUC1"
+
+
+def test_inloc_export_volume_parallel_torchrun(workdir):
+    """eval_inloc.py --volume_parallel under torchrun (2 ranks, gloo): every
+    pair's volume sharded over both ranks; the exported matches equal the
+    single-process export."""
+    import subprocess
+    import sys
+
+    import eval_inloc
+    from scipy.io import loadmat
+    common = ["--synthetic_queries", "1", "--n_panos", "2", "--image_size", "256", "--k_size", "2"]
+    single = eval_inloc.main(common + ["--output_dir", "single"])
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29733", os.path.join(root, "eval_inloc.py")] + common + [
+           "--output_dir", "vp", "--volume_parallel"]
+    out = subprocess.run(cmd, cwd=str(workdir), env=env, capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    a = loadmat(os.path.join(single, "1.mat"))["matches"]
+    b = loadmat(os.path.join("vp", os.path.basename(single), "1.mat"))["matches"]
+    assert a.shape == b.shape
+    assert np.allclose(a, b, rtol=1e-5, atol=1e-7)

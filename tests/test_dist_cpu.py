@@ -91,3 +91,49 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 4
     assert rec["value"] > 0 and rec["steps"] == 1 and rec["warmup"] == 1
+
+
+def _vp_worker(rank, world, port, out_dir, k_size, ks):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.parallel.dist import broadcast_module, destroy, init_distributed
+    from ncnet_amd.parallel.volume_parallel import VolumeParallelMatcher
+    ctx = init_distributed(device="cpu")
+    torch.manual_seed(7)
+    m = ImMatchNet(ncons_kernel_sizes=ks, ncons_channels=[16] * (len(ks) - 1) + [1], use_cuda=False,
+                   relocalization_k_size=k_size).eval()
+    broadcast_module(m, ctx)
+    g = torch.Generator().manual_seed(3)
+    batch = {"source_image": torch.randn(1, 3, 256, 192, generator=g),
+             "target_image": torch.randn(1, 3, 192, 256, generator=g)}
+    out = VolumeParallelMatcher(m, ctx).forward(batch)
+    if rank == 0:
+        torch.save({"state": m.state_dict(), "out": out, "batch": batch}, os.path.join(out_dir, "vp.pt"))
+    destroy(ctx)
+
+
+@pytest.mark.parametrize("world,k_size,ks", [(2, 2, [3, 3]), (3, 1, [3, 3]), (2, 2, [5, 3])])
+def test_volume_parallel_matches_single_process(tmp_path, world, k_size, ks):
+    """A-row-sharded correlation / MutualMatching / NeighConsensus (one halo
+    exchange) / MutualMatching over gloo == the single-process model."""
+    port = _free_port()
+    mp.spawn(_vp_worker, args=(world, port, str(tmp_path), k_size, ks), nprocs=world, join=True)
+    res = torch.load(str(tmp_path / "vp.pt"), weights_only=True)
+    from ncnet_amd.models import ImMatchNet
+    m = ImMatchNet(ncons_kernel_sizes=ks, ncons_channels=[16] * (len(ks) - 1) + [1], use_cuda=False,
+                   relocalization_k_size=k_size).eval()
+    m.load_state_dict(res["state"])
+    with torch.inference_mode():
+        ref = m(res["batch"])
+    if k_size > 1:
+        corr, delta = res["out"]
+        rc, rd = ref
+        assert corr.shape == rc.shape
+        assert torch.allclose(corr, rc, rtol=1e-4, atol=1e-6)
+        for a, b in zip(delta, rd):
+            assert torch.equal(a.long(), b.long())
+    else:
+        assert res["out"].shape == ref.shape
+        assert torch.allclose(res["out"], ref, rtol=1e-4, atol=1e-6)
