@@ -54,6 +54,17 @@ USE_IJ = ENC in ("ij", "ijfull")
 
 def _out_ij_fwd(ks: int) -> bool:
     return ENC == "ijfull" or (ENC == "ij" and ks * ks <= 16)
+
+
+# The Cout=1 layer's data gradient on the ij encoding: the group-plane conv
+# reads ijpack(g, -1), which the weight gradient has already built, and
+# writes the 16-channel masked gradient directly (no planar fp32 partials), so
+# it replaces jpack + a KS-plane jc pass.  NCNET_NC_OUT_DGRAD=jc reverts.
+OUT_DGRAD = _os.environ.get("NCNET_NC_OUT_DGRAD", "ij")
+
+
+def _out_ij_dgrad(ks: int) -> bool:
+    return _out_ij_fwd(ks) or (USE_IJ and OUT_DGRAD == "ij")
 # wgrad16 kernel: 3 = sliding G-plane ring (default), 2 = 8-wave LDS-DMA per
 # (di, dj) plane, 1 = 4-wave register-staged
 WGRAD_VARIANT = int(_os.environ.get("NCNET_WGRAD_VARIANT", "3"))
@@ -256,15 +267,13 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
             dw = ij_out_grad(torch.stack([p[0][0] for p in parts]), cin)
             qc = (ks // 2) * ks + ks // 2            # combo (P, P): its channel of ijpack(g, -1) is g itself
             db = parts[qc // 16][1][qc % 16].reshape(1)
-            del gs
             if li > 0 or need_dx0:
                 gi_ = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
-                if _out_ij_fwd(ks):
-                    gs = torch.empty((G,) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
-                    C.ijpack(g, gs, ks, -1)
+                if _out_ij_dgrad(ks):                # reuses ijpack(g, -1) of the weight gradient
                     wd = pack_w16_planes(plane_dgrad_weights(ij_out_weights(w)))
                     C.conv16_fwd(gs, wd, None, mask_prev, gi_, ks, 2 if mask_prev is not None else 0, 0)
                 else:                                # j encoding: 1 pass over the KS dj = P planes
+                    del gs
                     gs = torch.empty(tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
                     C.jpack(g, gs, ks, -1)
                     wt = transpose_for_dgrad(jc_out_weights(w))
