@@ -17,6 +17,7 @@
 // (MIOpen: conv + separate bias pass + PyTorch ReLU / add passes).
 // Requires Cin % 64 == 0 and Cout % 64 == 0 (every ResNet conv but the stem).
 #include "common.h"
+#include <stdlib.h>
 
 namespace ncnet {
 
@@ -167,6 +168,175 @@ __global__ __launch_bounds__(256, 2) void conv2d_nhwc_kernel(Conv2dArgs p) {
   }
 }
 
+
+// ===========================================================================
+// conv2d_nhwc_v2: the same implicit GEMM fed by LDS-DMA through a 4-stage
+// ring (BK = 32 = one tap x 32 channels per stage), so global loads run three
+// k-steps ahead of the MFMAs with no staging VGPRs and no LDS store
+// instructions, and each k-step costs one barrier (v1: register double buffer,
+// a load -> store -> barrier -> compute -> barrier sequence per k-step that
+// leaves the matrix cores idle during the LDS stores).
+//  * every wave issues exactly APW + BPW DMA wave-instructions per stage
+//    (out-of-image im2col rows read a 16-byte zero block instead of being
+//    masked), so the wait for stage ks is a compile-time vmcnt;
+//  * 64-byte LDS rows, chunk c of row r at (c ^ swz(r)) with
+//    swz(r) = (r & 1) ^ ((r >> 1) & 2): conflict-free for the ds_read_b128
+//    lane groups of the 16x16x32 fragments (searched offline);
+//  * the DMA source is swizzled instead of the destination (a DMA
+//    instruction writes 1 KB contiguously).
+// ===========================================================================
+__device__ const uint4 g_zero16 = {0u, 0u, 0u, 0u};
+
+namespace cv2 {
+constexpr int BK = 32;
+__device__ __forceinline__ int swz(int r) { return (r & 1) ^ ((r >> 1) & 2); }
+__device__ __forceinline__ uint32_t roff(int row, int chunk) { return (uint32_t)(row * 64 + ((chunk ^ swz(row)) << 4)); }
+}  // namespace cv2
+
+template <int N>
+__device__ __forceinline__ void c2_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// NW waves (4: 2x2 / 4x1 of 64x64 / 32x64; 8: 4x2 of 64x64 for the 256x128
+// tile, 85 FLOP per L2 byte instead of 64), NSTG ring stages.
+template <int BM, int BN, int NW, int NSTG>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void conv2d_nhwc_v2_kernel(Conv2dArgs p) {
+  using namespace cv2;
+  constexpr int NS = NSTG;
+  constexpr int NT = NW * 64;
+  constexpr int WN = BN == 128 ? 2 : 1;
+  constexpr int WMW = NW / WN;
+  constexpr int TM = BM / WMW / 16;
+  constexpr int TN = BN / WN / 16;
+  constexpr int APW = BM / (16 * NW);            // A DMA instructions (16 rows each) per wave per stage
+  constexpr int BPW = BN / (16 * NW);
+  static_assert(APW >= 1 && BPW >= 1 && TM >= 1, "tile / wave mismatch");
+  constexpr int PER = APW + BPW;
+  constexpr int STAGE = (BM + BN) * 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = bid % p.tiles_n, tm = bid / p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int pos = lane & 3;
+
+  // this lane's A rows (one per DMA instruction): image base and top-left input coordinate
+  int a_hi0[APW], a_wi0[APW], a_chunk[APW];
+  size_t a_base[APW];
+#pragma unroll
+  for (int m = 0; m < APW; ++m) {
+    const int row = 16 * (wave * APW + m) + (lane >> 2);
+    const int pix = m0 + row;
+    a_chunk[m] = pos ^ swz(row);
+    if (pix < p.M) {
+      const int wo = pix % p.Wo, t = pix / p.Wo, ho = t % p.Ho, n = t / p.Ho;
+      a_hi0[m] = ho * p.stride - p.pad;
+      a_wi0[m] = wo * p.stride - p.pad;
+      a_base[m] = (size_t)n * p.H * p.Wd;
+    } else {
+      a_hi0[m] = -(1 << 28);
+      a_wi0[m] = 0;
+      a_base[m] = 0;
+    }
+  }
+  const bf16* b_ptr[BPW];
+#pragma unroll
+  for (int m = 0; m < BPW; ++m) {
+    const int row = 16 * (wave * BPW + m) + (lane >> 2);
+    b_ptr[m] = p.W + (size_t)(n0 + row) * (p.KH * p.KW * p.Cin) + (pos ^ swz(row)) * 8;
+  }
+  const int cpt = p.Cin / BK;
+  const int nk = p.KH * p.KW * cpt;
+  const bf16* zero = (const bf16*)&g_zero16;
+
+  auto issue = [&](int ks, int buf) {
+    const int tap = ks / cpt, c0 = (ks - tap * cpt) * BK;
+    const int dh = tap / p.KW, dw = tap - dh * p.KW;
+    char* sb = smem + buf * STAGE;
+#pragma unroll
+    for (int m = 0; m < APW; ++m) {
+      const int hi = a_hi0[m] + dh, wi = a_wi0[m] + dw;
+      const bool ok = hi >= 0 && hi < p.H && wi >= 0 && wi < p.Wd;
+      const bf16* src = ok ? p.X + (a_base[m] + (size_t)hi * p.Wd + wi) * p.Cin + c0 + a_chunk[m] * 8 : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(void, sb + (wave * APW + m) * 1024), 16, 0, 0);
+    }
+    const int kk = tap * p.Cin + c0;
+#pragma unroll
+    for (int m = 0; m < BPW; ++m)
+      __builtin_amdgcn_global_load_lds((const void*)(b_ptr[m] + kk),
+                                       LDS_PTR(void, sb + BM * 64 + (wave * BPW + m) * 1024), 16, 0, 0);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+  const int fr = lane & 15, fq = lane >> 4;
+  int buf = 0;
+  for (int ks = 0; ks < nk; ++ks) {
+    // stage ks landed once at most the stages issued after it remain in flight
+    const int after = min(NS - 2, nk - 1 - ks);
+    if (NS >= 4 && after >= 2) c2_wait_barrier<2 * PER>();
+    else if (after >= 1) c2_wait_barrier<PER>();
+    else c2_wait_barrier<0>();
+    if (ks + NS - 1 < nk) issue(ks + NS - 1, (buf + NS - 1) % NS);   // the buffer consumed at ks - 1
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * 64;
+    bf16x8 af[TM], bfv[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = lds_read16(As, roff(wm * TM * 16 + i * 16 + fr, fq));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfv[j] = lds_read16(Bs, roff(wn * TN * 16 + j * 16 + fr, fq));
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfv[j], acc[i][j]);
+    buf = (buf + 1 == NS) ? 0 : buf + 1;
+  }
+  __syncthreads();   // all fragment reads done before the epilogue reuses the LDS
+
+  bf16* Ts = (bf16*)smem;                         // BM * BN * 2 <= NS * STAGE bytes
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wn * TN * 16 + j * 16 + fr;
+    const float b = p.bias[n0 + col];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ts[(wm * TM * 16 + i * 16 + 4 * fq + r) * BN + col] = f2bf(acc[i][j][r] + b);
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+#pragma unroll
+  for (int c = threadIdx.x; c < BM * CPR; c += NT) {
+    const int row = c / CPR, cc = c - row * CPR;
+    const int pix = m0 + row;
+    if (pix < p.M) {
+      bf16x8 v = *(const bf16x8*)(Ts + row * BN + cc * 8);
+      const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
+      if (p.R) {
+        const bf16x8 rr = *(const bf16x8*)(p.R + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[e]));
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf(bf2f(v[e]), 0.f));
+      }
+      *(bf16x8*)(p.Y + o) = v;
+    }
+  }
+}
+
 }  // namespace ncnet
 
 using namespace ncnet;
@@ -174,7 +344,7 @@ using namespace ncnet;
 extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias, const void* R, void* Y, int N, int H,
                                  int Wd, int Cin, int Cout, int KH, int KW, int stride, int pad, int relu,
                                  hipStream_t stream) {
-  if (Cin % 64 || Cout % 64 || stride < 1) return -1;
+  if (Cin % 64 || Cout % 64 || stride < 1) return -1;   // (v2 needs Cin % 32; both kernels share the check)
   Conv2dArgs p;
   p.X = (const bf16*)X; p.W = (const bf16*)W; p.bias = bias; p.R = (const bf16*)R; p.Y = (bf16*)Y;
   p.N = N; p.H = H; p.Wd = Wd; p.Cin = Cin; p.Cout = Cout; p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad;
@@ -188,6 +358,31 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
   const int BM = (cdiv(p.M, 128) * p.tiles_n < 512) ? 64 : 128;
   p.tiles_m = cdiv(p.M, BM);
   dim3 grid((unsigned)(p.tiles_m * p.tiles_n)), block(256);
+  // Variant choice (measured per ResNet layer, scripts/conv_bench.py): the
+  // 256 x 128 DMA-ring tile wins wherever it still gives >= 1.5 workgroups
+  // per CU (3200-px InLoc layers 2-3: 3x3 convs 610-670 -> 760-790 TFLOP/s);
+  // smaller grids and the 64-channel layers stay on the v1 kernel.
+  // NCNET_CONV2D_VARIANT=1 / 2 forces v1 / the DMA ring (with 128-row tiles
+  // unless NCNET_CONV2D_BIG is set or the grid is large).
+  const char* ev = getenv("NCNET_CONV2D_VARIANT");
+  const int variant = ev ? atoi(ev) : 0;
+  const int t256 = cdiv(p.M, 256) * p.tiles_n;
+  const bool big = BN == 128 && (variant == 0 ? t256 >= 384 : (t256 >= 512 || (t256 >= 256 && getenv("NCNET_CONV2D_BIG"))));
+  if (big && variant != 1) {
+    p.tiles_m = cdiv(p.M, 256);
+    dim3 g2((unsigned)(p.tiles_m * p.tiles_n)), b2(512);
+    const size_t lds = (size_t)3 * (256 + BN) * 64;
+    hipLaunchKernelGGL((conv2d_nhwc_v2_kernel<256, 128, 8, 3>), g2, b2, lds, stream, p);
+    return (int)hipGetLastError();
+  }
+  if (variant == 2) {
+    const size_t lds = (size_t)4 * (BM + BN) * 64;
+#define LC3(BMV, BNV) hipLaunchKernelGGL((conv2d_nhwc_v2_kernel<BMV, BNV, 4, 4>), grid, block, lds, stream, p)
+    if (BM == 128) { if (BN == 128) LC3(128, 128); else LC3(128, 64); }
+    else { if (BN == 128) LC3(64, 128); else LC3(64, 64); }
+#undef LC3
+    return (int)hipGetLastError();
+  }
   const size_t lds = (size_t)(BM + BN) * 128;
 #define LC2(BMV, BNV) hipLaunchKernelGGL((conv2d_nhwc_kernel<BMV, BNV>), grid, block, lds, stream, p)
   if (BM == 128) { if (BN == 128) LC2(128, 128); else LC2(128, 64); }
