@@ -39,6 +39,13 @@ int ncnet_softmax_max_bwd(const float*, const float*, const int*, const float*, 
                           const float*, const float*, float*, int, int, int, hipStream_t);
 int ncnet_maxpool4d(const void*, int, float*, uint8_t*, int, int, int, int, int, int, hipStream_t);
 int ncnet_transpose(const void*, void*, int, int, int, int, hipStream_t);
+int ncnet_conv1to16_kl(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int,
+                       hipStream_t);
+int ncnet_conv16to1_kl(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, int, float,
+                       hipStream_t);
+void ncnet_kl_tiles(int, int, int, int, int, int*, int*);
+int ncnet_nc_fused_k3(const void*, const void*, const float*, const void*, const float*, float*, int, int, int, int,
+                      int, int, int, int, int, hipStream_t);
 }
 
 namespace {
@@ -449,6 +456,72 @@ void conv16f8_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int
      "conv16f8_fwd");
 }
 
+// kl kernels (conv4d_kl.hip): in-plane (dk, dl) shifts resolved in LDS.
+// conv1to16_kl: X bf16 [V,I,J,K,L] -> Y [V,I,J,K,L,16] bf16 (or fp8 e4m3, epi 1 only);
+// Wp bf16 [ceil(ks^4/32), 64, 8]; epi 1: bias[16] + ReLU, 2: ReLU mask M [V,I,J,K,L,16] bf16.
+void conv1to16_kl(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks,
+                  int64_t epi) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
+  TORCH_CHECK(ks == 3 || ks == 5, "conv1to16_kl: ks must be 3 or 5");
+  TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
+  auto ys = X.sizes().vec(); ys.push_back(16);
+  const bool f8 = Y.scalar_type() == at::kFloat8_e4m3fn;
+  check(Y, "Y", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
+  check_shape(Y, "Y", ys);
+  const int64_t nk = ks * ks * ks * ks;
+  check_shape(Wp, "Wp", {(nk + 31) / 32, 64, 8});
+  TORCH_CHECK(epi == 1 || epi == 2, "conv1to16_kl: epi must be 1 (bias+ReLU) or 2 (mask)");
+  TORCH_CHECK(!(f8 && epi == 2), "conv1to16_kl: fp8 output only with bias+ReLU");
+  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
+  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", ys); }
+  ok(ncnet_conv1to16_kl(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), X.size(0),
+                        X.size(1), X.size(2), X.size(3), X.size(4), ks, epi, f8 ? 1 : 0, cur_stream(X)),
+     "conv1to16_kl");
+}
+
+// conv16to1_kl: X [V,I,J,K,L,16] bf16 or fp8 -> Y fp32 [V,I,J,K,L] = act(oscale * conv + bias);
+// Wp [ks*ks + 1, ceil(ks*ks/16), 16, 16] in X's dtype (plane, combo tile, combo, channel; last plane zero).
+void conv16to1_kl(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t relu, double oscale) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  const bool f8 = X.scalar_type() == at::kFloat8_e4m3fn;
+  check(X, "X", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
+  check(Wp, "Wp", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
+  check(Y, "Y", at::kFloat);
+  TORCH_CHECK(ks == 3 || ks == 5, "conv16to1_kl: ks must be 3 or 5");
+  TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
+  check_shape(Y, "Y", {X.size(0), X.size(1), X.size(2), X.size(3), X.size(4)});
+  check_shape(Wp, "Wp", {ks * ks + 1, (ks * ks + 15) / 16, 16, 16});
+  if (bias.has_value() && bias->defined()) { check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
+  ok(ncnet_conv16to1_kl(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), (float*)Y.data_ptr(), X.size(0), X.size(1),
+                        X.size(2), X.size(3), X.size(4), ks, relu ? 1 : 0, f8 ? 1 : 0, (float)oscale, cur_stream(X)),
+     "conv16to1_kl");
+}
+
+// Fused NC (1 -> 16 -> 1, k = 3): X bf16 [V,I,J,K,L] -> Y fp32 [V,I,J,K,L];
+// W1p / W2p bf16 [5, 64, 8]; b1 [16], b2 [1] fp32; tile (TK, TL), R planes and IR rows per workgroup.
+void nc_fused_k3(Tensor X, Tensor W1p, Tensor b1, Tensor W2p, Tensor b2, Tensor Y, int64_t R, int64_t IR, int64_t TK,
+                 int64_t TL) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(W1p, "W1p", at::kBFloat16); check(W2p, "W2p", at::kBFloat16);
+  check(b1, "b1", at::kFloat); check(b2, "b2", at::kFloat); check(Y, "Y", at::kFloat);
+  TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
+  check_shape(Y, "Y", X.sizes().vec());
+  check_shape(W1p, "W1p", {5, 64, 8}); check_shape(W2p, "W2p", {5, 64, 8});
+  check_shape(b1, "b1", {16}); check_shape(b2, "b2", {1});
+  TORCH_CHECK(R >= 1 && IR >= 1 && TK >= 1 && TL >= 1, "nc_fused_k3: bad tiling");
+  ok(ncnet_nc_fused_k3(X.data_ptr(), W1p.data_ptr(), (const float*)b1.data_ptr(), W2p.data_ptr(),
+                       (const float*)b2.data_ptr(), (float*)Y.data_ptr(), X.size(0), X.size(1), X.size(2), X.size(3),
+                       X.size(4), (int)R, (int)IR, (int)TK, (int)TL, cur_stream(X)),
+     "nc_fused_k3");
+}
+
+std::vector<int64_t> kl_tiles(int64_t which, int64_t K, int64_t L, int64_t ks, int64_t f8) {
+  int tk = 0, tl = 0;
+  ncnet_kl_tiles((int)which, (int)K, (int)L, (int)ks, (int)f8, &tk, &tl);
+  return {tk, tl};
+}
+
 // NHWC implicit-GEMM conv with fused bias (+ residual) (+ ReLU).  X [N,Cin,H,W],
 // W [Cout,Cin,KH,KW], R / Y [N,Cout,Ho,Wo]: all bf16 channels-last; bias fp32 [Cout].
 void conv2d_nhwc(Tensor X, Tensor W, Tensor bias, c10::optional<Tensor> R, Tensor Y, int64_t stride, int64_t pad,
@@ -504,4 +577,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_max_bwd", &softmax_max_bwd);
   m.def("maxpool4d", &maxpool4d);
   m.def("transpose", &transpose);
+  m.def("conv1to16_kl", &conv1to16_kl);
+  m.def("conv16to1_kl", &conv16to1_kl);
+  m.def("kl_tiles", &kl_tiles);
+  m.def("nc_fused_k3", &nc_fused_k3);
 }

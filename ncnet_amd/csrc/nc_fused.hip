@@ -1,0 +1,268 @@
+// Fused NeighConsensus for the InLoc network (ncons_kernel_sizes 3,3 /
+// ncons_channels 16,1; reference eval_inloc.py:50-57 with lib/model.py:122-153):
+//
+//   h = relu(conv4d_3(x0; W1) + b1)        1 -> 16 channels
+//   y = relu(conv4d_3(h;  W2) + b2)        16 -> 1 channel
+//
+// in ONE kernel, per volume, with the 16-channel hidden activation never
+// leaving LDS.  The layer-by-layer path writes h (1.8-3.6 GB at 3200 px), the
+// ij-packed layer-1 input (1.8 GB) and 9 channel-planar fp32 partials of the
+// last layer (4 GB) to HBM and reads them back; here HBM sees x0 once and y
+// once.
+//
+// Work decomposition: a workgroup owns output rows [i0, i1), output planes
+// j0 .. j0+R-1 and a (k, l) tile TK x TL, and STREAMS the volume along i:
+//   for each hidden row ih (i0-1 .. i1), for each hidden plane j'' (j0-1 .. j0+R):
+//     A  S tile: the ij-packed layer-1 input of plane (ih, j'') over the
+//        (k, l) tile + 2-voxel halo -- channel c = (di1, dj1) holds
+//        x0(ih+di1-1, j''+dj1-1, k, l) -- gathered from global (L1/L2-hot)
+//        by a register prefetch issued one plane ahead, written as bf16x16.
+//     B  layer 1: h(ih, j'') over the tile + 1-voxel halo = a 16 -> 16 plane
+//        conv over the (dk, dl) taps of S (v_mfma_f32_16x16x32_bf16, A =
+//        weights of 2 taps x 16 combos, B = S at the tap shift), + b1, ReLU,
+//        zero outside the volume (layer 2's "same" padding), bf16 into LDS.
+//     C  layer 2: z_q(ih, j'') for the 9 plane combos q = (di2, dj2) over the
+//        tile (MFMA rows = combos, K = taps x 16 channels of h), accumulated
+//        into an LDS ring of 3 output rows x R planes at
+//        (ih - di2 + 1, j'' - dj2 + 1).
+//   output row ih-1 is complete after hidden row ih: + b2, ReLU, store fp32.
+// Every ring address (row slot, plane, voxel) is only ever touched by the
+// lane that owns that voxel of the tile (static voxel -> wave/lane map, and
+// distinct combos of one plane land on distinct ring addresses), so the ring
+// needs no atomics and no barriers; two barriers per hidden plane order the
+// S and h buffers.
+#include "common.h"
+#include <stdlib.h>
+
+namespace ncnet {
+
+struct NCFGeom {
+  int V, I, J, K, L;
+  int TK, TL, R, IR;        // tile, planes per workgroup, output rows per workgroup
+  int nkt, nlt, njb, nib;
+  int SRS, HRS;             // LDS row strides (voxels) of the S and h tiles
+};
+
+constexpr int NCF_NW = 8;          // waves per workgroup
+constexpr int NCF_MAXT1 = 4;       // layer-1 tiles per wave: (TK+2)(TL+2) <= 512 voxels
+constexpr int NCF_MAXT2 = 3;       // layer-2 tiles per wave: TK*TL <= 384 voxels
+
+__global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ W1p,
+                                                             const float* __restrict__ b1,
+                                                             const u32x4* __restrict__ W2p,
+                                                             const float* __restrict__ b2, float* __restrict__ Y,
+                                                             NCFGeom g) {
+  constexpr int NQ = 5;            // tap pairs of the 3x3 (dk, dl) taps
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int TK = g.TK, TL = g.TL;
+  const int SR = TK + 4, SW = TL + 4;        // S tile (layer-1 input): tile + 2 halo
+  const int HR = TK + 2, HW = TL + 2;        // h tile (layer-2 input): tile + 1 halo
+  char* S = smem;
+  char* H = S + SR * g.SRS * 32;
+  float* ring = (float*)(H + HR * g.HRS * 32);
+  u32x4* wl = (u32x4*)(ring + 3 * g.R * TK * TL);   // [2 layers][5 tap pairs][64 lanes] fragments
+  const int nvox = TK * TL;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int lt = bid % g.nlt; bid /= g.nlt;
+  const int kt = bid % g.nkt; bid /= g.nkt;
+  const int jb = bid % g.njb; bid /= g.njb;
+  const int ib = bid % g.nib;
+  const int v = bid / g.nib;
+  const int k0 = kt * TK, l0 = lt * TL, j0 = jb * g.R, i0 = ib * g.IR;
+  const int i1 = min(g.I, i0 + g.IR);
+  const int R = min(g.R, g.J - j0);
+  const size_t KL = (size_t)g.K * g.L;
+  const int KLi = g.K * g.L;
+  const uint16_t* xv = (const uint16_t*)(X + (size_t)v * g.I * g.J * KL);   // one volume < 2^31 elements
+
+  // ---- static maps --------------------------------------------------------
+  // the S voxel owned by this thread (phase A): (TK+4)(TL+4) <= 512
+  int s_lds, s_goff;
+  bool s_in;
+  {
+    const int e = threadIdx.x;
+    const int r = e / SW, c = e - r * SW;
+    const int kg = k0 - 2 + r, lg = l0 - 2 + c;
+    s_lds = (e < SR * SW) ? (r * g.SRS + c) * 32 : -1;
+    s_in = e < SR * SW && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
+    s_goff = s_in ? kg * g.L + lg : 0;
+  }
+  // layer-1 tiles: h ext voxels e = tile*16 + (lane & 15) over HR x HW
+  const int nt1 = (HR * HW + 15) >> 4;
+  uint32_t b1off[NCF_MAXT1], h_wr[NCF_MAXT1];
+  bool h_in[NCF_MAXT1], h_ok[NCF_MAXT1];
+#pragma unroll
+  for (int t = 0; t < NCF_MAXT1; ++t) {
+    int e = (wave + NCF_NW * t) * 16 + (lane & 15);
+    const bool ok = e < HR * HW;
+    if (!ok) e = 0;
+    const int r = e / HW, c = e - r * HW;
+    b1off[t] = (uint32_t)((r * g.SRS + c) * 32 + ((lane >> 4) & 1) * 16);
+    h_wr[t] = (uint32_t)((r * g.HRS + c) * 32 + 8 * (lane >> 4));
+    const int kg = k0 - 1 + r, lg = l0 - 1 + c;
+    h_ok[t] = ok;    // lanes past the h region of the last tile must not write (their e was clamped to 0)
+    h_in[t] = ok && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
+  }
+  // layer-2 tiles: output voxels vi = tile*16 + (lane & 15) over TK x TL
+  const int nt2 = (nvox + 15) >> 4;
+  uint32_t b2off[NCF_MAXT2];
+  int vo[NCF_MAXT2];
+#pragma unroll
+  for (int t = 0; t < NCF_MAXT2; ++t) {
+    int vi = (wave + NCF_NW * t) * 16 + (lane & 15);
+    vo[t] = vi < nvox ? vi : -1;
+    if (vi >= nvox) vi = 0;
+    const int kk = vi / TL, ll = vi - kk * TL;
+    b2off[t] = (uint32_t)((kk * g.HRS + ll) * 32 + ((lane >> 4) & 1) * 16);
+  }
+  // tap offsets of the pair q: tap 2q + (lane >> 5) (the 10th tap is padding with zero weights)
+  uint32_t toff1[NQ], toff2[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    int tap = 2 * q + (lane >> 5);
+    if (tap > 8) tap = 8;
+    const int dk = tap / 3, dl = tap - dk * 3;
+    toff1[q] = (uint32_t)((dk * g.SRS + dl) * 32);
+    toff2[q] = (uint32_t)((dk * g.HRS + dl) * 32);
+  }
+  for (int o = threadIdx.x; o < NQ * 64; o += 512) { wl[o] = W1p[o]; wl[NQ * 64 + o] = W2p[o]; }
+  const int co0 = 4 * (lane >> 4);
+  float bias1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bias1[r] = b1[co0 + r];
+  const float bias2 = b2[0];
+
+  // zero the output ring (3 row slots x R planes x TK*TL)
+  for (int o = threadIdx.x; o < 3 * g.R * nvox; o += 512) ring[o] = 0.f;
+
+  const int ih_lo = max(0, i0 - 1), ih_hi = min(g.I, i1 + 1);   // hidden rows [lo, hi)
+  const int jh_lo = max(0, j0 - 1), jh_hi = min(g.J, j0 + R + 1); // hidden planes [lo, hi)
+  const int nplane = jh_hi - jh_lo;
+  const int nsteps = (ih_hi - ih_lo) * nplane;
+
+  // ---- the S gather: 9 plane-shifted x0 values per S voxel ----------------
+  // Loads land in a register set that is only read (packed into the S tile)
+  // two planes later: the set of plane t+2 is issued right after plane t's
+  // set was written out, so no plane waits for its own gather.
+  auto gather = [&](int ih, int jh, uint32_t (&raw)[9]) {
+#pragma unroll
+    for (int c = 0; c < 9; ++c) {
+      const int ii = ih + c / 3 - 1, jj = jh + c % 3 - 1;
+      const bool pin = ii >= 0 && ii < g.I && jj >= 0 && jj < g.J;
+      raw[c] = (pin && s_in) ? (uint32_t)xv[(ii * g.J + jj) * KLi + s_goff] : 0u;
+    }
+  };
+  auto write_s = [&](const uint32_t (&raw)[9]) {
+    if (s_lds < 0) return;
+    *(u32x4*)(S + s_lds) = u32x4{raw[0] | (raw[1] << 16), raw[2] | (raw[3] << 16), raw[4] | (raw[5] << 16),
+                                 raw[6] | (raw[7] << 16)};
+    *(u32x4*)(S + s_lds + 16) = u32x4{raw[8], 0u, 0u, 0u};
+  };
+
+  auto flush = [&](int io) {   // output row io -> Y (this wave's voxels only)
+    const int slot = io % 3;
+#pragma unroll
+    for (int t = 0; t < NCF_MAXT2; ++t) {
+      if (vo[t] < 0 || (lane >> 4) != 0) continue;
+      const int kk = vo[t] / TL, ll = vo[t] - kk * TL;
+      const int kg = k0 + kk, lg = l0 + ll;
+      const bool ok = kg < g.K && lg < g.L;
+      for (int p = 0; p < R; ++p) {
+        float* rp = ring + (slot * g.R + p) * nvox + vo[t];
+        if (ok) Y[(((size_t)v * g.I + io) * g.J + j0 + p) * KL + (size_t)kg * g.L + lg] = fmaxf(*rp + bias2, 0.f);
+        *rp = 0.f;
+      }
+    }
+  };
+
+  // hidden plane (ih, jh = jh_lo + pj); its gather registers are refilled with
+  // the plane two steps ahead (gih, gpj), advanced incrementally (no divisions)
+  int ih = ih_lo, pj = 0, gih = ih_lo, gpj = 0;
+  auto advance = [&](int& a, int& b) {
+    if (++b == nplane) { b = 0; ++a; }
+  };
+  auto step = [&](uint32_t (&raw)[9]) {
+    const int jh = jh_lo + pj;
+    __syncthreads();                   // S and h of the previous plane fully consumed (and ring zeroed)
+    write_s(raw);
+    if (gih < ih_hi) gather(gih, jh_lo + gpj, raw);
+    advance(gih, gpj);
+    __syncthreads();                   // S complete
+    // ---- B: layer 1 -> h (bf16, zero outside the volume) ----
+#pragma unroll 2
+    for (int u = 0; u < NCF_MAXT1; ++u) {
+      if (wave + NCF_NW * u >= nt1) continue;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc = mfma16u(wl[q * 64 + lane], *(const u32x4*)(S + b1off[u] + toff1[q]), acc);
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = f2bf(h_in[u] ? fmaxf(acc[r] + bias1[r], 0.f) : 0.f);
+      if (h_ok[u]) *(bf16x4*)(H + h_wr[u]) = o;
+    }
+    __syncthreads();                   // h complete
+    // ---- C: layer 2 combos -> ring ----
+#pragma unroll 2
+    for (int u = 0; u < NCF_MAXT2; ++u) {
+      if (wave + NCF_NW * u >= nt2) continue;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        acc = mfma16u(wl[(NQ + q) * 64 + lane], *(const u32x4*)(H + b2off[u] + toff2[q]), acc);
+      if (vo[u] < 0) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = co0 + r;               // combo (di2, dj2)
+        if (c >= 9) continue;
+        const int io = ih - c / 3 + 1, p = jh - (c % 3) + 1 - j0;
+        if (io < i0 || io >= i1 || p < 0 || p >= R) continue;
+        ring[((io % 3) * g.R + p) * nvox + vo[u]] += acc[r];
+      }
+    }
+    // hidden row ih done: output row ih - 1 has all three contributions
+    if (pj + 1 == nplane && ih - 1 >= i0 && ih - 1 < i1) flush(ih - 1);
+    advance(ih, pj);
+  };
+
+  uint32_t rawA[9], rawB[9];
+  gather(gih, jh_lo + gpj, rawA);
+  advance(gih, gpj);
+  if (gih < ih_hi) gather(gih, jh_lo + gpj, rawB);
+  advance(gih, gpj);
+  for (int t = 0; t < nsteps; t += 2) {
+    step(rawA);
+    if (t + 1 < nsteps) step(rawB);
+  }
+  // rows whose last contributing hidden row is past the volume / the segment
+  for (int io = max(i0, ih_hi - 1); io < i1; ++io) flush(io);
+}
+
+}  // namespace ncnet
+
+using namespace ncnet;
+
+// x0 bf16 [V,I,J,K,L]; W1p / W2p bf16 [5][64][8] (pack_w16_planes of the ij layer weights);
+// b1 fp32 [16], b2 fp32 [1]; y fp32 [V,I,J,K,L].
+extern "C" int ncnet_nc_fused_k3(const void* X, const void* W1p, const float* b1, const void* W2p, const float* b2,
+                                 float* Y, int V, int I, int J, int K, int L, int R, int IR, int TK, int TL,
+                                 hipStream_t stream) {
+  NCFGeom g{};
+  g.V = V; g.I = I; g.J = J; g.K = K; g.L = L;
+  g.TK = TK; g.TL = TL; g.R = R; g.IR = IR;
+  if ((TK + 2) * (TL + 2) > NCF_NW * NCF_MAXT1 * 16 || TK * TL > NCF_NW * NCF_MAXT2 * 16 ||
+      (TK + 4) * (TL + 4) > 512 || R < 1 || IR < 1)
+    return -2;
+  g.nkt = cdiv(K, TK); g.nlt = cdiv(L, TL); g.njb = cdiv(J, R); g.nib = cdiv(I, IR);
+  g.SRS = TL + 10;   // S rows: a layer-1 tile wrapping from column TL+1 to 0 jumps 9 voxels (one 256-B bank period + 1)
+  g.HRS = TL + 8;    // h rows: a layer-2 tile wrapping from column TL-1 to 0 jumps 9 voxels
+  if ((long long)I * J * K * L >= (1ll << 31)) return -4;
+  size_t lds = (size_t)(TK + 4) * g.SRS * 32 + (size_t)(TK + 2) * g.HRS * 32 + (size_t)3 * R * TK * TL * 4 +
+               2 * 5 * 64 * 16;
+  if (lds > 160 * 1024) return -3;
+  dim3 grid((unsigned)((size_t)V * g.nib * g.njb * g.nkt * g.nlt)), block(512);
+  hipLaunchKernelGGL(nc_fused_k3_kernel, grid, block, lds, stream, (const bf16*)X, (const u32x4*)W1p, b1,
+                     (const u32x4*)W2p, b2, Y, g);
+  return (int)hipGetLastError();
+}

@@ -20,14 +20,16 @@ MI355X design:
 """
 from __future__ import annotations
 
+import functools
+
 import numpy as np
 import torch
 
 from . import _ext
 from . import reference as ref
 from .packing import (ij_groups, ij_in_grad, ij_in_weights, ij_out_grad, ij_out_weights, jc_in_grad, jc_in_weights,
-                      jc_out_grad, jc_out_weights, pack_w16, pack_w16_planes, pack_w1in, pack_w1out,
-                      plane_dgrad_weights, transpose_for_dgrad)
+                      jc_out_grad, jc_out_weights, kl_dgrad_in_weights, pack_kl_in, pack_kl_out, pack_w16,
+                      pack_w16_planes, pack_w1in, pack_w1out, plane_dgrad_weights, transpose_for_dgrad)
 
 HIP_KS = (3, 5)
 # 1-channel layers through the j-offset channel encoding (csrc/jshift.hip) on
@@ -36,13 +38,18 @@ HIP_KS = (3, 5)
 import os as _os
 
 # Encoding of the 1-channel layers: "ij" (default: both plane offsets in
-# channels, conv16 group-plane mode), "jc" (dj only), "direct" (conv1in /
-# conv1out / wgrad1 kernels).  NCNET_NC_JC=0 is the legacy spelling of "direct".
+# channels, conv16 group-plane mode), "kl" (forward and data-gradient convs on
+# the conv4d_kl.hip kernels, which resolve the in-plane (dk, dl) shifts in LDS
+# -- no shifted copies or channel-planar partials in HBM; the weight gradients
+# stay on the ij encoding; measured slower than ij at the 25^4 training shape:
+# 37.1 vs 31.3 ms/step), "jc" (dj only), "direct" (conv1in / conv1out / wgrad1
+# kernels).  NCNET_NC_JC=0 is the legacy spelling of "direct".
 ENC = _os.environ.get("NCNET_NC_ENC", "ij")
 if _os.environ.get("NCNET_NC_JC") == "0":
     ENC = "direct"
 USE_JC = ENC == "jc"
-USE_IJ = ENC in ("ij", "ijfull")
+USE_IJ = ENC in ("ij", "ijfull", "kl")
+USE_KL = ENC == "kl"
 # "ij" keeps the Cout=1 layer's forward and data gradient on the j encoding
 # (one conv pass with an 8-channel fp32 output beats two group-plane passes
 # with 16-channel planar outputs at 25^4: measured 1.97 vs 2.56 ms fwd) and
@@ -122,7 +129,11 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
         w = _std(w_ref)
         save.append(h)
         last = li == len(kinds) - 1
-        if kind == "1in" and USE_IJ:
+        if kind == "1in" and USE_KL:
+            # the backward ij-packs the saved 1-channel input for the weight gradient
+            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
+            C.conv1to16_kl(h, pack_kl_in(w), _pad_bias(b, 16), None, y, ks, 1)
+        elif kind == "1in" and USE_IJ:
             xs = torch.empty((ij_groups(ks), V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
             C.ijpack(h, xs, ks, 1)
             save[-1] = xs  # the backward needs the ij-packed input
@@ -140,6 +151,11 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
         elif kind == "16":
             y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
             C.conv16_fwd(h, pack_w16(w), _pad_bias(b, 16), None, y, ks, 1, 0)
+        elif USE_KL:   # "1out"
+            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
+            C.conv16to1_kl(h, pack_kl_out(w), _pad_bias(b, 1), y, ks, 1, 1.0)
+            if not last:
+                y = y.to(torch.bfloat16)
         elif USE_IJ and _out_ij_fwd(ks):   # "1out"
             G = ij_groups(ks)
             wz = pack_w16_planes(ij_out_weights(w))
@@ -269,7 +285,9 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
             db = parts[qc // 16][1][qc % 16].reshape(1)
             if li > 0 or need_dx0:
                 gi_ = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
-                if _out_ij_dgrad(ks):                # reuses ijpack(g, -1) of the weight gradient
+                if USE_KL and mask_prev is not None:  # 1 -> Cin conv with flipped taps, ReLU mask fused
+                    C.conv1to16_kl(g, pack_kl_in(kl_dgrad_in_weights(w)), None, mask_prev, gi_, ks, 2)
+                elif _out_ij_dgrad(ks):              # reuses ijpack(g, -1) of the weight gradient
                     wd = pack_w16_planes(plane_dgrad_weights(ij_out_weights(w)))
                     C.conv16_fwd(gs, wd, None, mask_prev, gi_, ks, 2 if mask_prev is not None else 0, 0)
                 else:                                # j encoding: 1 pass over the KS dj = P planes
@@ -280,7 +298,11 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
                     C.conv16_fwd(gs, pack_w16(wt), None, mask_prev, gi_, ks, 2 if mask_prev is not None else 0, 1)
                 g = gi_
                 del gs
-        elif kind == "1in" and USE_IJ:               # h is ijpack(X0) [G, ...]
+        elif kind == "1in" and USE_IJ:               # h is ijpack(X0) [G, ...] (kl: X0 itself)
+            if h.dim() == 5:
+                xs = torch.empty((ij_groups(ks),) + tuple(h.shape) + (16,), dtype=torch.bfloat16, device=h.device)
+                C.ijpack(h, xs, ks, 1)
+                h = xs
             G = h.shape[0]
             parts = [wgrad16_partials(C, h[gi], g, ks, ng, 2) for gi in range(G)]
             dw = ij_in_grad(torch.stack([p[0][0] for p in parts]), cout)
@@ -472,7 +494,10 @@ def _stack_fwd_fp8(x0: torch.Tensor, ws, bs, kinds) -> torch.Tensor:
     for li, (w_ref, b, kind) in enumerate(zip(ws, bs, kinds)):
         ks = w_ref.shape[0]
         w = _std(w_ref)
-        if kind == "1in":
+        if kind == "1in" and USE_KL:
+            y = torch.empty((V, I, J, K, L, 16), dtype=FP8, device=x0.device)
+            C.conv1to16_kl(h, pack_kl_in(w), _pad_bias(b, 16), None, y, ks, 1)
+        elif kind == "1in":
             G = ij_groups(ks)
             xs = torch.empty((G, V, I, J, K, L, 16), dtype=FP8, device=x0.device)
             C.ijpack(h, xs, ks, 1)
@@ -483,6 +508,12 @@ def _stack_fwd_fp8(x0: torch.Tensor, ws, bs, kinds) -> torch.Tensor:
             wq, osc = _fp8_weights(pack_w16(w))
             y = torch.empty((V, I, J, K, L, 16), dtype=FP8, device=x0.device)
             C.conv16f8_fwd(h, wq, _pad_bias(b, 16), y, ks, 1, 0, osc)
+        elif USE_KL:  # "1out"
+            wq, osc = _fp8_weights(pack_kl_out(w))
+            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
+            C.conv16to1_kl(h, wq, _pad_bias(b, 1), y, ks, 1, osc)
+            if li != len(kinds) - 1:
+                raise RuntimeError("fp8 NC path: the 1-channel output layer must be last")
         else:  # "1out"
             G, nq = ij_groups(ks), ks * ks
             wq, osc = _fp8_weights(pack_w16_planes(ij_out_weights(w)))
@@ -517,14 +548,104 @@ def neigh_consensus_fp8(x: torch.Tensor, weights, biases, kinds, symmetric: bool
     return y.reshape(V, 1, I, J, K, L)
 
 
+# ---------------------------------------------------------------------------
+# Fused InLoc NC (csrc/nc_fused.hip): kernel sizes (3, 3), channels (<=16, 1),
+# inference.  The hidden activation stays in LDS; HBM sees the input and the
+# output volume once.  NCNET_NC_FUSED=0 falls back to the layer-by-layer path.
+FUSED = _os.environ.get("NCNET_NC_FUSED", "1") != "0"
+_FUSED_LDS = 78 * 1024          # two workgroups per CU (160 KB LDS)
+
+
+def _cdiv(a: int, b: int) -> int:
+    return -(-a // b)
+
+
+@functools.lru_cache(maxsize=64)
+def fused_tiles(V: int, I: int, J: int, K: int, L: int):
+    """(TK, TL, R, IR) of nc_fused_k3: a (k, l) tile within the kernel's limits
+    ((TK+2)(TL+2) <= 512, TK*TL <= 384, (TK+4)(TL+4) <= 512) minimising the
+    padded layer-1 + layer-2 work, then R output planes per workgroup (as many
+    as the LDS ring allows) and row segments of IR rows until the grid has
+    ~2 workgroups per CU."""
+    best = None
+    for tk in range(1, min(K, 28) + 1):
+        for tl in range(1, min(L, 28) + 1):
+            if (tk + 2) * (tl + 2) > 512 or tk * tl > 384 or (tk + 4) * (tl + 4) > 512:
+                continue
+            n = _cdiv(K, tk) * _cdiv(L, tl)
+            cost = n * (_cdiv((tk + 2) * (tl + 2), 16) + _cdiv(tk * tl, 16))
+            if best is None or cost < best[0]:
+                best = (cost, tk, tl)
+    _, tk, tl = best
+    fixed = (tk + 4) * (tl + 10) * 32 + (tk + 2) * (tl + 8) * 32 + 2 * 5 * 64 * 16
+    r_max = max(1, (_FUSED_LDS - fixed) // (12 * tk * tl))
+    base = V * _cdiv(K, tk) * _cdiv(L, tl)
+
+    def nwg(r, ir):
+        return base * _cdiv(J, r) * _cdiv(I, ir)
+
+    # the kernel is latency-bound (two barriers per hidden plane): prefer >= ~500
+    # workgroups (two per CU), first by splitting rows (halo (IR+2)/IR), then
+    # planes ((R+2)/R).  Measured at 3200 px: 500 workgroups (R=10, IR=75)
+    # 4.3 ms vs 6.4 ms for 1000 (IR=37); at 1600 px R=4, IR=5 0.55 ms.
+    R, IR = min(J, r_max), I
+    while nwg(R, IR) < 500 and IR > 5:
+        IR = max(5, IR // 2)
+    while nwg(R, IR) < 500 and R > 4:
+        R -= 1
+    return tk, tl, R, IR
+
+
+def _fused_weights(weights, biases):
+    w1, w2 = _std(weights[0]), _std(weights[1])
+    W1p = pack_w16_planes(ij_in_weights(w1))[0].contiguous()
+    W2p = pack_w16_planes(ij_out_weights(w2))[0].contiguous()
+    return W1p, _pad_bias(biases[0], 16), W2p, _pad_bias(biases[1], 1)
+
+
+def _run_fused(xb: torch.Tensor, wts) -> torch.Tensor:
+    V, I, J, K, L = xb.shape
+    y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=xb.device)
+    tk, tl, R, IR = fused_tiles(V, I, J, K, L)
+    _ext.ext().nc_fused_k3(xb, *wts, y, R, IR, tk, tl)
+    return y
+
+
+def neigh_consensus_fused(x: torch.Tensor, weights, biases, symmetric: bool = True) -> torch.Tensor:
+    """Inference NeighConsensus of a (3, 3) / (<=16, 1) stack on the fused kernel."""
+    V, _, I, J, K, L = x.shape
+    R, Cc = I * J, K * L
+    wts = _fused_weights(weights, biases)
+    xb = x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous()
+    if not symmetric:
+        return _run_fused(xb, wts).reshape(V, 1, I, J, K, L)
+    xt = _swap_flat(xb.reshape(V, R, Cc), (I, J, K, L)).reshape(V, K, L, I, J)
+    if (I, J) == (K, L):
+        z = _run_fused(torch.cat((xb, xt), 0), wts)
+    else:
+        z = torch.cat((_run_fused(xb, wts).reshape(-1), _run_fused(xt, wts).reshape(-1)))
+    y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x.device)
+    _ext.ext().combine_fwd(z, y, R, Cc)
+    return y.reshape(V, 1, I, J, K, L)
+
+
+def _fused_ok(kinds, kernel_sizes, x) -> bool:
+    return (FUSED and not torch.is_grad_enabled() and list(kinds) == ["1in", "1out"]
+            and list(kernel_sizes) == [3, 3] and x.shape[2] * x.shape[3] * x.shape[4] * x.shape[5] < 2 ** 31)
+
+
 def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool = True, fp8: bool = False) -> torch.Tensor:
     """x: [V,1,I,J,K,L] fp32; weights in checkpoint layout [k, out, in, k, k, k].
 
-    ``fp8``: inference through the fp8 MFMA kernels (ignored when gradients
-    are required or the stack shape has no fp8 kernels)."""
+    Inference of the InLoc (3,3)/(16,1) stack runs on the fused kernel (bf16
+    operands, hidden layer kept on chip) whatever ``fp8`` says.  ``fp8``:
+    inference of other 1-in/1-out stacks through the fp8 MFMA kernels (ignored
+    when gradients are required or the stack shape has no fp8 kernels)."""
     kernel_sizes = [w.shape[0] for w in weights]
     kinds = layer_kinds(channels, kernel_sizes)
     if _ext.use_hip(x) and kinds is not None:
+        if _fused_ok(kinds, kernel_sizes, x):
+            return neigh_consensus_fused(x.float().contiguous(), weights, biases, symmetric)
         if fp8 and not torch.is_grad_enabled() and kinds[0] == "1in" and kinds[-1] == "1out":
             return neigh_consensus_fp8(x.float().contiguous(), weights, biases, kinds, symmetric)
         params = []

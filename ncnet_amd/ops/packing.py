@@ -204,3 +204,38 @@ def ij_out_grad(s: torch.Tensor, cin: int) -> torch.Tensor:
     ks = int(round(nt ** 0.5))
     d = s.permute(2, 0, 3, 1).reshape(16, G * 16, nt)[:cin, :nt]      # [ci, q, tap]
     return d.reshape(1, cin, ks, ks, ks, ks).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# kl kernels (csrc/conv4d_kl.hip): in-plane (dk, dl) shifts resolved in LDS.
+
+def pack_kl_in(w_std: torch.Tensor) -> torch.Tensor:
+    """Cin=1 -> Cout<=16 weights [co, 1, k, k, k, k] -> [ceil(k^4/32), 64, 8] bf16.
+
+    Lane l of K step s holds W[co=l&15, tap=32s+8(l>>4)+j] with the taps in
+    (di, dj, dk, dl) row-major order (zero past k^4 and for co >= Cout)."""
+    cout, ks = w_std.shape[0], w_std.shape[2]
+    nk = ks ** 4
+    ns = (nk + 31) // 32
+    wf = w_std.new_zeros((16, ns * 32), dtype=torch.float32)
+    wf[:cout, :nk] = w_std.reshape(cout, nk).float()
+    return wf.reshape(16, ns, 4, 8).permute(1, 2, 0, 3).reshape(ns, 64, 8).to(torch.bfloat16).contiguous()
+
+
+def kl_dgrad_in_weights(w_std: torch.Tensor) -> torch.Tensor:
+    """Data gradient of a Cout=1 layer as a 1 -> Cin conv: [1, ci, k^4] -> [ci, 1, k^4 flipped]."""
+    return transpose_for_dgrad(w_std)
+
+
+def pack_kl_out(w_std: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    """Cin<=16 -> Cout=1 weights [1, ci, k, k, k, k] -> [k*k + 1, ceil(k*k/16), 16, 16].
+
+    Entry [p=(di,dj), ct, r, c] = W[0, c, di, dj, dk, dl] for the in-plane combo
+    16*ct + r = dk*k + dl (zero past k*k, for c >= Cin and on the extra
+    all-zero plane k*k used to pad odd plane counts)."""
+    cin, ks = w_std.shape[1], w_std.shape[2]
+    nt = ks * ks
+    nct = (nt + 15) // 16
+    out = w_std.new_zeros((nt + 1, nct * 16, 16), dtype=torch.float32)
+    out[:nt, :nt, :cin] = w_std[0].float().permute(1, 2, 3, 4, 0).reshape(nt, nt, cin)
+    return out.reshape(nt + 1, nct, 16, 16).to(dtype).contiguous()
