@@ -18,7 +18,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from ncnet_amd.ops import _ext  # noqa: E402
 from ncnet_amd.ops.neigh_consensus import wgrad_groups  # noqa: E402
-from ncnet_amd.ops.packing import pack_w16, pack_w1in, pack_w1out  # noqa: E402
+from ncnet_amd.ops.packing import (ij_groups, ij_in_weights, pack_w16, pack_w16_planes, pack_w1in,  # noqa: E402
+                                   pack_w1out)
 
 
 def timeit(fn, reps):
@@ -72,6 +73,14 @@ def main():
     p3c = torch.empty((2 * n3c, ks, ks ** 2, 16, 16), device=dev)
     p3cb = torch.empty((2 * n3c, 16), device=dev)
     g16b = torch.empty_like(g16)
+    # ij encoding of the 1-channel layers (the training path): ijpack + group-plane conv + plane-only wgrad
+    G = ij_groups(ks)
+    xs = torch.empty((G,) + shp + (16,), device=dev, dtype=torch.bfloat16)
+    wij = pack_w16_planes(ij_in_weights(torch.randn(16, 1, ks, ks, ks, ks, device=dev) * 0.05))
+    from ncnet_amd.ops.neigh_consensus import wgrad_plane_groups
+    npg = wgrad_plane_groups(V * S * S * ((S + 24) // 25) ** 2)
+    pp = torch.empty((2 * npg, 1, ks * ks, 16, 16), device=dev)
+    ppb = torch.empty((2 * npg, 16), device=dev)
     taps = ks ** 4
     fl16 = 2.0 * nvox * taps * 256
     fl1 = 2.0 * nvox * taps * 16
@@ -90,6 +99,9 @@ def main():
         "wgrad16v2_center": (lambda: C.wgrad16(x16, g16, part16c, partb, ks, 1, 2), fl16 / ks),
         "wgrad16v3": (lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3), fl16),
         "wgrad16v3_center": (lambda: C.wgrad16(x16, g16, p3c, p3cb, ks, 1, 3), fl16 / ks),
+        "ijpack": (lambda: C.ijpack(x1, xs, ks, 1), None),
+        "ij_1in_conv": (lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1, 0), fl1),
+        "wgrad16v2_plane": (lambda: C.wgrad16(xs[0], g16, pp, ppb, ks, 2, 2), fl1 / G),
         "wgrad1_mode0": (lambda: C.wgrad1(g16, x1, part1, ks, 0, ng), fl1),
         "wgrad1_mode1": (lambda: C.wgrad1(x16, g1, part1, ks, 1, ng), fl1),
     }
