@@ -20,6 +20,7 @@
 //     Layer Cin=1: S = G (tile), P = X plane.  Layer Cout=1: S = X plane,
 //     P = G (tile), taps come out flipped (undone on the host).
 #include "common.h"
+#include <stdlib.h>
 
 namespace ncnet {
 
@@ -344,6 +345,7 @@ struct W3Geom {
   int PR, RS, RW;      // staged X rows, row stride, row width (voxels)
   int ncols, cpg;      // X-plane columns (v, jj, tile); columns per group
   int dj_center;
+  int flags;           // bit 0: s_setprio 1 for waves 4-7 (NCNET_WGRAD_FLAGS, tuning)
 };
 
 struct Col { int v, jj, a, nv, kf; };
@@ -467,22 +469,37 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
   int col = c_lo;
   while (col < c_hi && !col_ok(col)) col = next_col(col);
   // loaders: X (one plane per step), G (sequence over valid columns x gi)
+  // the loaders keep their column decoded (three runtime divisions, all on the
+  // scalar unit) and re-decode only when they move to the next column, not per step
   int xl_col = col, xl_ii = 0, xl_step = 0;
-  int gl_col = col, gl_gi = 0, gl_seq = 0;
+  int gl_col = col, gl_gi = 0, gl_seq = 0, gl_slot = 0;
+  Col xl_r = decode_col(g, col), gl_r = xl_r;
   auto load_x_next = [&]() {
     if (xl_col >= c_hi) return;
-    stage_x(decode_col(g, xl_col), xl_ii, xbuf + (xl_step & 1) * xbytes);
+    stage_x(xl_r, xl_ii, xbuf + (xl_step & 1) * xbytes);
     ++xl_step;
-    if (++xl_ii == g.I) { xl_ii = 0; xl_col = next_col(xl_col); }
+    if (++xl_ii == g.I) {
+      xl_ii = 0;
+      xl_col = next_col(xl_col);
+      if (xl_col < c_hi) xl_r = decode_col(g, xl_col);
+    }
   };
   auto load_g_upto = [&](int seq_max) {
     while (gl_col < c_hi && gl_seq <= seq_max) {
-      stage_g(decode_col(g, gl_col), gl_gi, gbuf + (gl_seq % NS) * gbytes);
+      stage_g(gl_r, gl_gi, gbuf + gl_slot * gbytes);
       ++gl_seq;
-      if (++gl_gi == g.I) { gl_gi = 0; gl_col = next_col(gl_col); }
+      if (++gl_slot == NS) gl_slot = 0;
+      if (++gl_gi == g.I) {
+        gl_gi = 0;
+        gl_col = next_col(gl_col);
+        if (gl_col < c_hi) gl_r = decode_col(g, gl_col);
+      }
     }
   };
 
+  // static priority for the second-dispatched half (waves 4-7 lose VALU
+  // arbitration to the older half on every step otherwise); wave-uniform guard
+  if ((g.flags & 1) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   __syncthreads();   // zero fill before any DMA lands
   load_x_next();
   load_g_upto(NS - 2);
@@ -497,10 +514,21 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
       // valid di: gi = ii - di + P in [0, I); invalid ones read the zero slot,
       // so every MFMA is issued unconditionally (<5% zero work at the I edges)
       const int di_lo = max(0, ii + P - g.I + 1), di_hi = min(KS - 1, ii + P);
+      const int s0 = (base + ii + P) % NS;   // ring slot of G plane gi = ii + P (di = 0)
       uint32_t gslot[KS];
 #pragma unroll
-      for (int d = 0; d < KS; ++d)
-        gslot[d] = (uint32_t)((d >= di_lo && d <= di_hi) ? (base + ii - d + P) % NS : NS) * gbytes;
+      for (int d = 0; d < KS; ++d) {
+        const int sd = s0 - d < 0 ? s0 - d + NS : s0 - d;
+        gslot[d] = (uint32_t)((d >= di_lo && d <= di_hi) ? sd : NS) * gbytes;
+      }
+      // the last tap's extra di values of this tap group (groups 1..3), hoisted out of the chunk loop
+      uint32_t gsxv[EXP];
+#pragma unroll
+      for (int e = 0; e < EXP; ++e) {
+        const int d = xdi_lo + e;
+        const int sd = s0 - d < 0 ? s0 - d + NS : s0 - d;
+        gsxv[e] = (uint32_t)((d >= di_lo && d <= di_hi) ? sd : NS) * gbytes;
+      }
       // software pipeline: the next chunk's G fragments and the next tap's X
       // fragment are in flight while the current MFMAs run
       // fragments held as u32 vectors (see cat4u in common.h)
@@ -535,8 +563,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
             for (int e = 0; e < EXP; ++e) {
               const int d = xdi_lo + e;
               if (d < xdi_hi) {
-                const uint32_t gsx = (uint32_t)((d >= di_lo && d <= di_hi) ? (base + ii - d + P) % NS : NS) * gbytes;
-                u32x4 bx = cat4u(lds_read_tr16u(gbuf, gsx + ga), lds_read_tr16u(gbuf, gsx + ga + 512));
+                u32x4 bx = cat4u(lds_read_tr16u(gbuf, gsxv[e] + ga), lds_read_tr16u(gbuf, gsxv[e] + ga + 512));
                 accx[e] = mfma16u(afr, bx, accx[e]);
               }
             }
@@ -816,6 +843,10 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
   g.ncols = V * J * g.ntl;
   g.cpg = cdiv(g.ncols, ngroups);
   g.dj_center = dj_center;
+  {
+    const char* e = getenv("NCNET_WGRAD_FLAGS");   // read per launch: tests / kbench switch it in-process
+    g.flags = e ? atoi(e) : 0;
+  }
   if (g.RW > 32) return -1;                 // one wave-instruction per staged row
   if (g.VT > 384) return -1;                // <= 6 chunks per half
   size_t lds = 2 * (size_t)g.PR * g.RS * 32 + (size_t)(KS + 2) * g.VT * 32;

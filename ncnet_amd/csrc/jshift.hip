@@ -21,6 +21,7 @@
 // taps only: 2.5x (KS=5) / 3x (KS=3) fewer MFMAs than the j encoding.
 #include "common.h"
 #include <hip/hip_fp8.h>
+#include <stdlib.h>
 
 namespace ncnet {
 
@@ -116,6 +117,39 @@ __global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, vo
   }
 }
 
+// ijpack v2 (bf16 output, opt-in NCNET_IJPACK_V=2): one thread per 16-byte
+// output chunk (8 channels of one voxel), grid (plane, group), so every
+// wave-store is 1 KB of contiguous bytes.  Measured SLOWER than v1 at the
+// training shape (64 x 25^4, KS=5: 0.736 vs 0.571 ms, profiles/r1s3_kbench.json):
+// each lane then issues 8 scalar 2-byte gathers per 16 bytes written instead of
+// 16 per 32, and the lane pairs of one voxel read different planes.
+template <typename T, int KS>
+__global__ __launch_bounds__(256) void ijpack2_kernel(const T* __restrict__ X, bf16* __restrict__ S, long long nvox,
+                                                      int I, int J, int KL, int sgn) {
+  constexpr int P = KS / 2, NQ = KS * KS;
+  const long long plane = blockIdx.x;       // (v*I + i)*J + j, block-uniform
+  const int grp = blockIdx.y;
+  const int j = (int)(blockIdx.x % J);
+  const int i = (int)((blockIdx.x / J) % I);
+  const T* xp = X + plane * KL;
+  bf16* sp = S + ((long long)grp * nvox + plane * KL) * 16;
+  for (int ch = threadIdx.x; ch < 2 * KL; ch += 256) {
+    const int kl = ch >> 1, h = ch & 1;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int q = 16 * grp + 8 * h + e;
+      float v = 0.f;
+      if (q < NQ) {
+        const int ii = i + sgn * (q / KS - P), jj = j + sgn * (q % KS - P);
+        if (ii >= 0 && ii < I && jj >= 0 && jj < J) v = (float)xp[((ii - i) * J + (jj - j)) * KL + kl];
+      }
+      o[e] = f2bf(v);
+    }
+    *(bf16x8*)(sp + ch * 8) = o;
+  }
+}
+
 // Z is channel-planar by combo: Z[q][voxel] (conv16 planar fp32 epilogue).
 template <int KS>
 __global__ __launch_bounds__(256) void ijsum_kernel(const float* __restrict__ Z, const float* __restrict__ bias,
@@ -165,6 +199,16 @@ extern "C" int ncnet_jsum(const float* Z8, const float* bias, float* y, int V, i
 extern "C" int ncnet_ijpack(const void* X, int x_is_bf16, void* S, int V, int I, int J, int K, int L, int KS, int sgn,
                             int s_fp8, hipStream_t stream) {
   long long nvox = (long long)V * I * J * K * L;
+  const char* ev = getenv("NCNET_IJPACK_V");
+  if (!s_fp8 && ev && atoi(ev) == 2) {
+    dim3 grid2((unsigned)(V * I * J), (unsigned)((KS * KS + 15) / 16));
+#define IJP2(T, KSV) hipLaunchKernelGGL((ijpack2_kernel<T, KSV>), grid2, dim3(256), 0, stream, (const T*)X, (bf16*)S, nvox, I, J, K * L, sgn)
+    if (KS == 5) { if (x_is_bf16) IJP2(bf16, 5); else IJP2(float, 5); }
+    else if (KS == 3) { if (x_is_bf16) IJP2(bf16, 3); else IJP2(float, 3); }
+    else return -1;
+#undef IJP2
+    return (int)hipGetLastError();
+  }
   dim3 grid((unsigned)(V * I * J), (unsigned)((K * L + 255) / 256));
 #define IJP(T, KSV) do { if (s_fp8) hipLaunchKernelGGL((ijpack_kernel<T, KSV, true>), grid, dim3(256), 0, stream, (const T*)X, S, nvox, I, J, K * L, sgn); \
                          else hipLaunchKernelGGL((ijpack_kernel<T, KSV, false>), grid, dim3(256), 0, stream, (const T*)X, S, nvox, I, J, K * L, sgn); } while (0)

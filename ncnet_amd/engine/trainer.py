@@ -7,7 +7,9 @@ Differences from the reference, all semantics-preserving:
 * evaluation (``mode='test'``) runs under ``torch.inference_mode`` (the
   reference builds graphs it never uses, train.py:170-174);
 * gradients are averaged over ranks with one bucketed RCCL all-reduce;
-* optional NaN/Inf guard skips a step whose loss is not finite.
+* optional NaN/Inf guard skips a step whose loss is not finite;
+* with a ``utils.timing.SegmentTimer`` installed (train.py --segment_timing)
+  every logged record carries mean per-segment GPU milliseconds.
 """
 from __future__ import annotations
 
@@ -21,6 +23,7 @@ import torch
 
 from ..ops.loss import weak_loss_from_corr
 from ..parallel.dist import DistContext, GradBucket, all_reduce_mean
+from ..utils.timing import active as active_timer, segment
 
 
 def weak_loss(model, batch, normalization: str | None = "softmax", alpha: float = 30) -> torch.Tensor:
@@ -52,16 +55,20 @@ class Trainer:
         if self.fault_step >= 0 and self.global_step == self.fault_step:
             raise RuntimeError(f"injected fault at step {self.global_step} (NCNET_FAULT_STEP)")
         self.opt.zero_grad(set_to_none=True)
-        loss = weak_loss(self.model, batch, self.normalization)
-        loss.backward()
-        self.bucket.allreduce()
-        if self.nan_guard:
-            finite = torch.isfinite(loss)
-            # stay asynchronous: zero the grads of a non-finite step instead of branching on the host
-            for p in self.bucket.params:
-                if p.grad is not None:
-                    p.grad.mul_(finite.to(p.grad.dtype))
-        self.opt.step()
+        with segment("forward"):
+            loss = weak_loss(self.model, batch, self.normalization)
+        with segment("backward"):
+            loss.backward()
+        with segment("allreduce"):
+            self.bucket.allreduce()
+        with segment("optimizer"):
+            if self.nan_guard:
+                finite = torch.isfinite(loss)
+                # stay asynchronous: zero the grads of a non-finite step instead of branching on the host
+                for p in self.bucket.params:
+                    if p.grad is not None:
+                        p.grad.mul_(finite.to(p.grad.dtype))
+            self.opt.step()
         self.global_step += 1
         return loss.detach()
 
@@ -98,6 +105,9 @@ class Trainer:
                        "pairs": pairs, "pairs_per_s": pairs / max(dt, 1e-9)}
                 if self.ctx.device.type == "cuda":
                     rec["hbm_peak_gb"] = torch.cuda.max_memory_allocated(self.ctx.device) / 2 ** 30
+                timer = active_timer()
+                if timer is not None and timer.enabled:
+                    rec["segments_ms"] = timer.collect()
                 self._log(rec)
         mean = float(all_reduce_mean(total / max(n, 1), self.ctx))
         if self.ctx.is_main:

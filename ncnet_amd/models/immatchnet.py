@@ -26,6 +26,7 @@ from ..ops.conv4d import Conv4d
 from ..ops.correlation import correlation, correlation_pool2, l2norm_pack, l2norm_pack_fp8, maxpool4d as _maxpool4d
 from ..ops.mutual import mutual_matching
 from ..ops.neigh_consensus import neigh_consensus
+from ..utils.timing import segment
 from .backbones import FrozenResNetPlan, build_trunk, fold_frozen_bn
 
 # Frozen bf16 trunk: pre-cast execution plan (default) or autocast (NCNET_TRUNK_PLAN=0).
@@ -163,6 +164,21 @@ def _load_reference_checkpoint(path: str):
     return ck
 
 
+_MAPS: dict = {}
+
+
+def _pair_maps(b: int, device):
+    """Batch index maps of the positive pairs (a_i, b_i) followed by the rolled
+    negatives (a_{i+1}, b_i) (train.py:137), cached per (b, device)."""
+    key = (b, str(device))
+    m = _MAPS.get(key)
+    if m is None:
+        ar = torch.arange(b, device=device, dtype=torch.int32)
+        m = (torch.cat((ar, torch.roll(ar, -1))), torch.cat((ar, ar)))
+        _MAPS[key] = m
+    return m
+
+
 class ImMatchNet(nn.Module):
     def __init__(self, feature_extraction_cnn: str = "resnet101", feature_extraction_last_layer: str = "",
                  feature_extraction_model_file: str | None = None, return_correlation: bool = False,
@@ -232,10 +248,13 @@ class ImMatchNet(nn.Module):
 
     def process_correlation(self, corr4d: torch.Tensor) -> torch.Tensor:
         """MutualMatching -> NeighConsensus -> MutualMatching (lib/model.py:274-276)."""
-        corr4d = MutualMatching(corr4d)
+        with segment("mutual_matching"):
+            corr4d = MutualMatching(corr4d)
         self.NeighConsensus.fp8 = self.corr_dtype == "fp8"
-        corr4d = self.NeighConsensus(corr4d)
-        return MutualMatching(corr4d)
+        with segment("neigh_consensus"):
+            corr4d = self.NeighConsensus(corr4d)
+        with segment("mutual_matching"):
+            return MutualMatching(corr4d)
 
     def forward(self, tnf_batch):
         src, tgt = tnf_batch["source_image"], tnf_batch["target_image"]
@@ -269,11 +288,10 @@ class ImMatchNet(nn.Module):
         the source *features* -- the backbone runs once on 2B images instead
         of 4B."""
         b = src.shape[0]
-        f, (h, w) = self.extract(torch.cat((src, tgt), 0))
+        with segment("backbone"):
+            f, (h, w) = self.extract(torch.cat((src, tgt), 0))
         fa, fb = f[:b], f[b:]
-        dev = f.device
-        ar = torch.arange(b, device=dev, dtype=torch.int32)
-        amap = torch.cat((ar, torch.roll(ar, -1)))
-        bmap = torch.cat((ar, ar))
-        corr = correlation(fa, fb, amap, bmap).view(2 * b, 1, h, w, h, w)
+        amap, bmap = _pair_maps(b, f.device)
+        with segment("correlation"):
+            corr = correlation(fa, fb, amap, bmap).view(2 * b, 1, h, w, h, w)
         return self.process_correlation(corr)

@@ -48,6 +48,24 @@ class SoftmaxMaxScoreFn(torch.autograd.Function):
         return gx * g, None, None
 
 
+_WEIGHTS: dict = {}
+
+
+def _loss_weights(b: int, R: int, Cc: int, device):
+    """Per-volume weights of score_neg - score_pos: -1/(2bR), -1/(2bCc) for the
+    b positive volumes, + for the b negatives.  Built on the device by fill
+    kernels (no pageable host->device copy per step) and cached per shape."""
+    key = (b, R, Cc, str(device))
+    w = _WEIGHTS.get(key)
+    if w is None:
+        sign = torch.ones(2 * b, dtype=torch.float32, device=device)
+        sign[:b] = -1.0
+        w = (sign / (2.0 * b * R), sign / (2.0 * b * Cc))
+        if not (sign.is_cuda and torch.cuda.is_current_stream_capturing()):
+            _WEIGHTS[key] = w
+    return w
+
+
 def weak_loss_from_corr(corr4d: torch.Tensor, n_pos: int, normalization: str | None = "softmax") -> torch.Tensor:
     """loss = score_neg - score_pos for a [2B,1,I,J,K,L] volume whose first B
     entries are the positive pairs and last B the negatives."""
@@ -58,9 +76,7 @@ def weak_loss_from_corr(corr4d: torch.Tensor, n_pos: int, normalization: str | N
     R, Cc = i * j, k * l
     if _ext.use_hip(corr4d) and normalization == "softmax":
         x3 = corr4d.reshape(V, R, Cc)
-        sign = torch.cat((-torch.ones(b), torch.ones(b))).to(corr4d.device)
-        wr = (sign / (2.0 * b * R)).float()
-        wc = (sign / (2.0 * b * Cc)).float()
+        wr, wc = _loss_weights(b, R, Cc, corr4d.device)
         return SoftmaxMaxScoreFn.apply(x3, wr, wc)
     pos = ref.match_score(corr4d[:b], normalization)
     neg = ref.match_score(corr4d[b:], normalization)

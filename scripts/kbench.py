@@ -22,6 +22,21 @@ from ncnet_amd.ops.packing import (ij_groups, ij_in_weights, pack_w16, pack_w16_
                                    pack_w1out)
 
 
+def with_env(key, val, fn):
+    """Run fn with os.environ[key] = val (the launchers read their tuning switches per call)."""
+    def run():
+        old = os.environ.get(key)
+        os.environ[key] = val
+        try:
+            fn()
+        finally:
+            if old is None:
+                os.environ.pop(key, None)
+            else:
+                os.environ[key] = old
+    return run
+
+
 def timeit(fn, reps):
     fn()
     torch.cuda.synchronize()
@@ -100,6 +115,8 @@ def main():
         "wgrad16v3": (lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3), fl16),
         "wgrad16v3_center": (lambda: C.wgrad16(x16, g16, p3c, p3cb, ks, 1, 3), fl16 / ks),
         "ijpack": (lambda: C.ijpack(x1, xs, ks, 1), None),
+        "ijpack_v2": (with_env("NCNET_IJPACK_V", "2", lambda: C.ijpack(x1, xs, ks, 1)), None),
+        "wgrad16v3_prio": (with_env("NCNET_WGRAD_FLAGS", "1", lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3)), fl16),
         "ij_1in_conv": (lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1, 0), fl1),
         "wgrad16v2_plane": (lambda: C.wgrad16(xs[0], g16, pp, ppb, ks, 2, 2), fl1 / G),
         "wgrad1_mode0": (lambda: C.wgrad1(g16, x1, part1, ks, 0, ng), fl1),

@@ -276,6 +276,43 @@ def test_wgrad16_kernel(variant, ks, shape, monkeypatch):
     assert relerr(sbc, sb) < 1e-5
 
 
+@pytest.mark.parametrize("flags", ["0", "1"])
+def test_wgrad16v3_priority_flag(flags, monkeypatch):
+    """wgrad16v3 with the waves-4..7 s_setprio tuning bit: same sums as the oracle."""
+    import importlib
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    monkeypatch.setattr(nc, "WGRAD_VARIANT", 3)
+    monkeypatch.setenv("NCNET_WGRAD_FLAGS", flags)
+    torch.manual_seed(12)
+    V, I, J, K, L, ks = 2, 6, 5, 25, 25, 5
+    x = torch.rand(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
+    g = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
+    wr = torch.zeros(ks, 16, 16, ks, ks, ks, device=DEV, dtype=torch.float64, requires_grad=True)
+    (ref.conv4d(x.double().permute(0, 5, 1, 2, 3, 4), wr, None) * g.double().permute(0, 5, 1, 2, 3, 4)).sum().backward()
+    s, sb = nc.wgrad16_partials(_ext.ext(), x, g, ks, 1, False)
+    assert relerr(nc._reduce_wgrad16(s, ks, 16, 16), ref.conv4d_weight_to_std(wr.grad)) < 1e-3
+    assert relerr(sb, g.double().sum(dim=(0, 1, 2, 3, 4))) < 1e-3
+
+
+@pytest.mark.parametrize("version", ["1", "2"])
+@pytest.mark.parametrize("ks,sgn,shape,dtype", [(5, 1, (2, 6, 7, 25, 25), torch.bfloat16),
+                                                (5, -1, (1, 5, 4, 9, 11), torch.float32),
+                                                (3, 1, (1, 4, 5, 30, 26), torch.bfloat16),
+                                                (3, -1, (2, 3, 3, 7, 5), torch.bfloat16)])
+def test_ijpack_kernel(version, ks, sgn, shape, dtype, monkeypatch):
+    """ijpack (both kernel versions) vs the torch emulation of the ij encoding:
+    S[g][v,i,j,k,l,c] = X[v, i+sgn*(di-P), j+sgn*(dj-P), k, l], q = 16g + c."""
+    from tests.test_kernel_emulation import _ijpack
+    monkeypatch.setenv("NCNET_IJPACK_V", version)
+    torch.manual_seed(13)
+    x = torch.randn(shape, device=DEV).to(dtype)
+    G = (ks * ks + 15) // 16
+    s = torch.full((G,) + shape + (16,), float("nan"), device=DEV, dtype=torch.bfloat16)
+    _ext.ext().ijpack(x, s, ks, sgn)
+    want = _ijpack(x.float().cpu(), ks, sgn).permute(0, 1, 3, 4, 5, 6, 2).to(torch.bfloat16)
+    assert torch.equal(s.cpu(), want)
+
+
 def test_bias_act_kernel():
     C = _ext.ext()
     torch.manual_seed(5)

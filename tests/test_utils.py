@@ -49,3 +49,54 @@ def test_runtime_config_from_env():
     assert c.nc_encoding == "jc" and c.wgrad_variant == 2 and not c.trunk_graph and c.trunk_plan
     assert RuntimeConfig.from_env({"NCNET_NC_JC": "0"}).nc_encoding == "direct"
     assert set(c.as_dict()) >= {"nc_encoding", "wgrad_variant", "conv16_variant"}
+
+
+def test_segment_timer_cpu():
+    from ncnet_amd.utils.timing import SegmentTimer, segment, set_active
+    t = SegmentTimer(device="cpu")
+    set_active(t)
+    try:
+        for _ in range(3):
+            with segment("a"):
+                torch.ones(10).sum()
+        with segment("b"):
+            pass
+    finally:
+        set_active(None)
+    ms = t.collect()
+    assert set(ms) == {"a", "b"} and all(v >= 0 for v in ms.values())
+    assert t.collect() == {}
+    with segment("ignored"):   # no active timer: null context
+        pass
+
+
+def test_affine_tnf_identity_and_resize():
+    from ncnet_amd.data.transforms import AffineTnf, gpu_normalize_resize, resize_bilinear
+    img = torch.rand(2, 3, 12, 16)
+    out = AffineTnf(12, 16)(img)
+    assert torch.allclose(out, img, atol=1e-5)            # identity theta, align_corners=True
+    r = resize_bilinear(img, 6, 8)
+    assert torch.allclose(AffineTnf(6, 8)(img), r, atol=1e-5)
+    u8 = (torch.rand(1, 3, 12, 16) * 255).to(torch.uint8)
+    n = gpu_normalize_resize(u8, 12, 16)
+    assert torch.allclose(normalize_image(u8.float() / 255.0), n, atol=1e-5)
+
+
+def test_train_segment_timing_and_profile(tmp_path):
+    import json
+    import train
+    old = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        train.main(["--synthetic", "4", "--batch_size", "2", "--image_size", "64", "--ncons_kernel_sizes", "3", "3",
+                    "--ncons_channels", "16", "1", "--max_steps", "2", "--segment_timing", "--profile", "prof",
+                    "--metrics", "m.jsonl"])
+        assert os.path.exists("prof/train_profile.txt") and os.path.exists("prof/train_trace.json")
+        train.main(["--synthetic", "4", "--batch_size", "2", "--image_size", "64", "--ncons_kernel_sizes", "3", "3",
+                    "--ncons_channels", "16", "1", "--num_epochs", "1", "--segment_timing", "--metrics", "m.jsonl",
+                    "--result-model-dir", "models"])
+        recs = [json.loads(x) for x in open("m.jsonl")]
+        seg = [r["segments_ms"] for r in recs if r["mode"] == "train" and "segments_ms" in r]
+        assert seg and {"backbone", "correlation", "neigh_consensus", "backward", "optimizer"} <= set(seg[0])
+    finally:
+        os.chdir(old)

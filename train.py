@@ -9,6 +9,11 @@ Same flags and defaults as the reference, plus:
   --max_steps S        stop after S training steps (smoke / profiling)
   --metrics PATH       JSONL metrics (rank 0)
   --dtype bf16|fp32    backbone compute dtype (NC path is always bf16 MFMA on GPU)
+  --segment_timing     HIP-event timers per step segment (backbone, correlation,
+                       mutual_matching, neigh_consensus, forward, backward,
+                       allreduce, optimizer), written to the --metrics records
+  --profile DIR        torch.profiler (ROCm activity) over the --max_steps loop,
+                       kernel table + chrome trace under DIR (rank 0)
 
 Multi-GPU: launch with torchrun (one process per GPU); gradients are averaged
 with one bucketed RCCL all-reduce, every rank trains on its own shard.
@@ -32,6 +37,7 @@ from ncnet_amd.engine.checkpoint import capture_rng, load_checkpoint, restore_rn
 from ncnet_amd.engine.trainer import Trainer  # noqa: E402
 from ncnet_amd.models import ImMatchNet  # noqa: E402
 from ncnet_amd.parallel.dist import barrier, broadcast_module, destroy, init_distributed, shard_indices  # noqa: E402
+from ncnet_amd.utils.timing import SegmentTimer, set_active  # noqa: E402
 
 
 def build_parser():
@@ -58,6 +64,8 @@ def build_parser():
     p.add_argument("--metrics", type=str, default="")
     p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--segment_timing", action="store_true")
+    p.add_argument("--profile", type=str, default="")
     return p
 
 
@@ -147,10 +155,19 @@ def main(argv=None):
     if ctx.is_main:
         print("Checkpoint name: " + checkpoint_name)
 
+    timer = SegmentTimer(device=ctx.device) if args.segment_timing else None
+    set_active(timer)
     trainer = Trainer(model, optimizer, ctx, metrics_path=args.metrics or None)
     if args.max_steps:
         # bounded run (smoke / profiling)
         model.train()
+        prof = None
+        if args.profile and ctx.is_main:
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if ctx.device.type == "cuda":
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            prof = torch.profiler.profile(activities=acts)
+            prof.__enter__()
         t0 = time.perf_counter()
         steps = 0
         while steps < args.max_steps:
@@ -158,14 +175,25 @@ def main(argv=None):
                 loss = trainer.train_step(trainer.to_device(batch))
                 steps += 1
                 if ctx.is_main and (steps % max(1, args.log_interval) == 0):
-                    print(f"step {steps} loss {float(loss):.6f}", flush=True)
+                    msg = f"step {steps} loss {float(loss):.6f}"
+                    if timer is not None:
+                        msg += " " + " ".join(f"{k}={v:.2f}ms" for k, v in timer.collect().items())
+                    print(msg, flush=True)
                 if steps >= args.max_steps:
                     break
         if ctx.device.type == "cuda":
             torch.cuda.synchronize()
+        if prof is not None:
+            prof.__exit__(None, None, None)
+            os.makedirs(args.profile, exist_ok=True)
+            sort = "cuda_time_total" if ctx.device.type == "cuda" else "cpu_time_total"
+            with open(os.path.join(args.profile, "train_profile.txt"), "w") as f:
+                f.write(prof.key_averages().table(sort_by=sort, row_limit=60))
+            prof.export_chrome_trace(os.path.join(args.profile, "train_trace.json"))
         if ctx.is_main:
             dt = time.perf_counter() - t0
             print(f"{steps} steps in {dt:.2f}s ({steps * args.batch_size * ctx.world_size / dt:.1f} pairs/s)")
+        set_active(None)
         destroy(ctx)
         return
 
@@ -185,6 +213,7 @@ def main(argv=None):
         barrier(ctx)
     if ctx.is_main:
         print("Done!")
+    set_active(None)
     destroy(ctx)
 
 
