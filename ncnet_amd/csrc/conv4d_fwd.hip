@@ -327,9 +327,13 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
   const int col0 = lstart - (t.l0 - P);
 
   auto issue_x = [&](int s, char* buf) {
-    const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-    const bf16* xp = g.npg > 0 ? X + s * g.gstride + plane_offset(g, t.v, t.i, t.j, 16)
-                               : X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
+    const bf16* xp;
+    if (g.npg > 0) {
+      xp = X + s * g.gstride + plane_offset(g, t.v, t.i, t.j, 16);
+    } else {
+      const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
+      xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
+    }
     for (int r = wave; r < g.PR; r += NW) {
       const int kg = t.k0 - P + r;
       if (kg >= 0 && kg < g.K && lane < nchunk) {
@@ -339,8 +343,8 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
     }
   };
   auto issue_w = [&](int s) {
-    const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-    const u32x4* wp = Wp + (size_t)(g.npg > 0 ? s : di * KS + dj) * (NQ * 64);
+    const int wplane = g.npg > 0 ? s : (di_lo + s / ndj) * KS + dj_lo + s % ndj;
+    const u32x4* wp = Wp + (size_t)wplane * (NQ * 64);
     for (int q = wave; q < NQ; q += NW)
       __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + q * 1024), 16, 0, 0);
   };

@@ -45,6 +45,21 @@ __device__ __forceinline__ Item decode_item(const WGeom& g, int it) {
   return r;
 }
 
+// Advance a decoded item to item + 1 (same order as decode_item).
+__device__ __forceinline__ void next_item(const WGeom& g, Item& r) {
+  r.l0 += g.TL;
+  if (r.l0 < g.nlt * g.TL) return;
+  r.l0 = 0;
+  r.k0 += g.TK;
+  if (r.k0 < g.nkt * g.TK) return;
+  r.k0 = 0;
+  if (++r.j < g.J) return;
+  r.j = 0;
+  if (++r.i < g.I) return;
+  r.i = 0;
+  ++r.v;
+}
+
 __device__ __forceinline__ size_t plane_off(const WGeom& g, int v, int i, int j, int C) {
   return ((((size_t)v * g.I + i) * g.J + j) * (size_t)g.K * g.L) * C;
 }
@@ -257,8 +272,10 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
   const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
 
   __syncthreads();  // zero fill done before any DMA lands
-  for (int it = it_lo; it < it_hi; ++it) {
-    const Item r = decode_item(g, it);
+  // items are consecutive: decode the first one, then step the (l, k, j, i, v)
+  // tile counters instead of four runtime divisions (scalar unit) per item
+  Item r = decode_item(g, it_lo);
+  for (int it = it_lo; it < it_hi; ++it, next_item(g, r)) {
     const int ii = r.i + di - P, jj = r.j + dj - P;
     if (ii < 0 || ii >= g.I || jj < 0 || jj >= g.J) continue;   // uniform over the block
     // Stage X plane rows (corner (k0-P, l0-P)) and G tile rows (corner (k0, l0)):
