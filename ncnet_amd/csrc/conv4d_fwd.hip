@@ -40,7 +40,8 @@ struct ConvGeom {
   float oscale;       // fp8 kernel: accumulator scale (1 / weight scale)
   int npg;            // > 0: "group planes" mode (v2 only): plane s is the (i, j)
   long long gstride;  //   plane of input group s at X + s * gstride, weights plane s
-  int njb;            // v3: output j-blocks of R planes per (v, i)
+  int njb;            // output j-blocks per (v, i): J, or cdiv(J, R) (v3) / cdiv(J, tpw) (v2 group planes)
+  int tpw;            // v2 group-plane mode: consecutive output j-tiles per workgroup (1 otherwise)
 };
 
 // Decode the workgroup's output tile.
@@ -50,7 +51,7 @@ __device__ __forceinline__ TileId decode_tile(const ConvGeom& g) {
   TileId t;
   int lt = bid % g.nlt; bid /= g.nlt;
   int kt = bid % g.nkt; bid /= g.nkt;
-  t.j = bid % g.J; bid /= g.J;
+  t.j = (bid % g.njb) * g.tpw; bid /= g.njb;
   t.i = bid % g.I; t.v = bid / g.I;
   t.k0 = kt * g.TK; t.l0 = lt * g.TL;
   return t;
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(256, 2) void conv16_fwd_kernel(const bf16* __restri
 //  * halo/out-of-volume voxels are zeroed once (fixed positions for the tile).
 // Requires RW = TL + KS - 1 <= 32.
 // ===========================================================================
-template <int KS, int EPI>
+template <int KS, int EPI, bool MT>
 __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
                                                               const float* __restrict__ bias,
                                                               const bf16* __restrict__ M, bf16* __restrict__ Y,
@@ -326,10 +327,11 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
   const int nchunk = 2 * (lend - lstart);
   const int col0 = lstart - (t.l0 - P);
 
-  auto issue_x = [&](int s, char* buf) {
+  // plane s of output j-tile t.j + jt (jt > 0 only in multi-tile group-plane mode)
+  auto issue_x = [&](int jt, int s, char* buf) {
     const bf16* xp;
     if (g.npg > 0) {
-      xp = X + s * g.gstride + plane_offset(g, t.v, t.i, t.j, 16);
+      xp = X + s * g.gstride + plane_offset(g, t.v, t.i, t.j + jt, 16);
     } else {
       const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
       xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
@@ -349,19 +351,45 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
       __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + q * 1024), 16, 0, 0);
   };
 
+  const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
+  auto store_tile = [&](int jt) {
+    const size_t vbase_out = plane_offset(g, t.v, t.i, t.j + jt, 1);
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      int tile = wave + NW * tt;
+      if (tile < ntile) {
+        int vi = tile * 16 + (lane & 15);
+        int kk = vi / g.TL, ll = vi - kk * g.TL;
+        int kg = t.k0 + kk, lg = t.l0 + ll;
+        if (vi < nvox && kg < g.K && lg < g.L)
+          store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco);
+      }
+    }
+  };
+  // MT (group-plane mode, tpw > 1): the workgroup computes ntl consecutive
+  // output j-tiles with the same (k0, l0) -- so the zeroed halo is shared -- as
+  // ONE plane stream: the DMA of the next tile's first plane is in flight while
+  // the current tile finishes and stores, instead of every workgroup paying its
+  // first plane's latency with nothing to overlap it.
+  const int ntl = MT ? min(g.tpw, g.J - t.j) : 1;
+  const int ntot = nplanes * ntl;
+
   __syncthreads();  // zero-fill complete before any DMA lands
-  if (nplanes > 0) { issue_x(0, smem); issue_w(0); }
-  for (int s = 0; s < nplanes; ++s) {
+  if (ntot > 0) { issue_x(0, 0, smem); issue_w(0); }
+  int jt = 0, sp = 0;      // tile / plane of step s
+  int njt = 0, nsp = 1;    // tile / plane of step s + 1
+  if (nsp == nplanes) { nsp = 0; njt = 1; }
+  for (int s = 0; s < ntot; ++s) {
     __syncthreads();  // drains this wave's DMA (vmcnt 0) and orders every wave's plane s + weights s
     char* cur = smem + (s & 1) * plane_bytes;
-    if (s + 1 < nplanes) issue_x(s + 1, smem + ((s + 1) & 1) * plane_bytes);
+    if (s + 1 < ntot) issue_x(njt, nsp, smem + ((s + 1) & 1) * plane_bytes);
     bf16x8 wf[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) wf[q] = lds_read16(wbuf, (q * 64 + lane) * 16);
     // weights in registers in every wave -> release the weight buffer without
     // draining the in-flight plane DMA (plain s_barrier, LDS counter only)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (s + 1 < nplanes) issue_w(s + 1);
+    if (s + 1 < ntot) issue_w(nsp);
     // per-tile branches kept: the branch-free body needs 129 VGPRs (> 128,
     // one workgroup per CU instead of two: 6.4 -> 9.4 ms measured)
 #pragma unroll
@@ -374,21 +402,15 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
         }
       }
     }
-  }
-
-  const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);
+    if (MT && sp == nplanes - 1) {
+      store_tile(jt);
 #pragma unroll
-  for (int tt = 0; tt < MAXT; ++tt) {
-    int tile = wave + NW * tt;
-    if (tile < ntile) {
-      int vi = tile * 16 + (lane & 15);
-      int kk = vi / g.TL, ll = vi - kk * g.TL;
-      int kg = t.k0 + kk, lg = t.l0 + ll;
-      if (vi < nvox && kg < g.K && lg < g.L)
-        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4),
-                     (size_t)g.V * g.I * g.J * g.K * g.L, g.nco);
+      for (int tt = 0; tt < MAXT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    jt = njt; sp = nsp;
+    if (++nsp == nplanes) { nsp = 0; ++njt; }
   }
+  if (!MT || ntot == 0) store_tile(0);
 }
 
 // ===========================================================================
@@ -993,7 +1015,7 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.RW = g.RS;
   g.dj_center = 0;
   g.npg = 0; g.gstride = 0; g.nco = 16; g.oscale = 1.f;
-  g.njb = J;
+  g.njb = J; g.tpw = 1;
   return g;
 }
 
@@ -1008,6 +1030,12 @@ static void pick_tile(int K, int L, int& tk, int& tl) {
   tl = L <= 25 ? L : 25;
   // keep TK*TL <= 640 (MAXT * 4 waves * 16 voxels)
   while (tk * tl > 640) { if (tl > tk) --tl; else --tk; }
+}
+
+// output j-tiles per workgroup of the group-plane conv (read per launch: tests / kbench switch it)
+static int gp_tpw() {
+  const char* e = getenv("NCNET_GP_TPW");
+  return e ? atoi(e) : 5;
 }
 
 // read per launch (cheap) so tests can switch variants inside one process
@@ -1055,8 +1083,12 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
     // stays conflict-free (a TL + KS - 1 stride cost ~1/3 extra LDS cycles).
     g.RS = tl + ((KS - 1 + 7) / 8) * 8;
     size_t lds2 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
-    dim3 grid2((unsigned)(V * I * J * g.nkt * g.nlt)), block2(512);
-#define L16V2(KSV, EPIV) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV>), grid2, block2, lds2, stream, x, w, bias, m, y, g)
+    // group planes: tpw consecutive output j-tiles per workgroup (NCNET_GP_TPW, default 5)
+    const bool mt = npg > 0 && gp_tpw() > 1;
+    if (mt) { g.tpw = gp_tpw(); g.njb = cdiv(J, g.tpw); }
+    dim3 grid2((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block2(512);
+#define L16V2(KSV, EPIV) do { if (mt) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, true>), grid2, block2, lds2, stream, x, w, bias, m, y, g); \
+                              else hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, false>), grid2, block2, lds2, stream, x, w, bias, m, y, g); } while (0)
     if (KS == 5) {
       if (epi == EPI_BIAS_RELU) L16V2(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2(5, EPI_MASK);
       else if (epi == EPI_F32) L16V2(5, EPI_F32); else if (epi == EPI_F32X16) L16V2(5, EPI_F32X16);

@@ -118,6 +118,9 @@ def main():
         "ijpack_v2": (with_env("NCNET_IJPACK_V", "2", lambda: C.ijpack(x1, xs, ks, 1)), None),
         "wgrad16v3_prio": (with_env("NCNET_WGRAD_FLAGS", "1", lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3)), fl16),
         "ij_1in_conv": (lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1, 0), fl1),
+        "ij_1in_conv_tpw1": (with_env("NCNET_GP_TPW", "1", lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1, 0)), fl1),
+        "ij_out_dgrad": (lambda: C.conv16_fwd(xs, wij, None, x16, y16, ks, 2, 0), fl1),
+        "ij_out_dgrad_tpw1": (with_env("NCNET_GP_TPW", "1", lambda: C.conv16_fwd(xs, wij, None, x16, y16, ks, 2, 0)), fl1),
         "wgrad16v2_plane": (lambda: C.wgrad16(xs[0], g16, pp, ppb, ks, 2, 2), fl1 / G),
         "wgrad1_mode0": (lambda: C.wgrad1(g16, x1, part1, ks, 0, ng), fl1),
         "wgrad1_mode1": (lambda: C.wgrad1(x16, g1, part1, ks, 1, ng), fl1),

@@ -498,3 +498,39 @@ def test_conv2d_nhwc_kernel(cin, cout, k, stride, pad, res, relu, shape):
     y = torch.empty(yr.shape, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=cl)
     C.conv2d_nhwc(x, w, b, r, y, stride, pad, 1 if relu else 0)
     assert relerr(y, yr) < 1e-2
+
+
+@pytest.mark.parametrize("ks,shape", [(5, (2, 6, 7, 25, 25)), (3, (1, 4, 9, 30, 27)), (5, (1, 3, 12, 9, 7))])
+def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch):
+    """The multi-tile group-plane conv16v2 (NCNET_GP_TPW consecutive j-tiles per
+    workgroup, one plane stream) does the same MFMAs in the same order as one
+    tile per workgroup: outputs are bitwise equal for the bias+ReLU, ReLU-mask
+    and planar-fp32 epilogues, including a ragged last j-block; and the bias+ReLU
+    output matches the fp64 oracle of the 1 -> 16 layer."""
+    from ncnet_amd.ops.packing import ij_groups, ij_in_weights, pack_w16_planes
+    torch.manual_seed(14)
+    C = _ext.ext()
+    V, I, J, K, L = shape
+    G = ij_groups(ks)
+    x0 = torch.rand(shape, device=DEV).to(torch.bfloat16)
+    xs = torch.empty((G,) + shape + (16,), device=DEV, dtype=torch.bfloat16)
+    C.ijpack(x0, xs, ks, 1)
+    w = torch.randn(16, 1, ks, ks, ks, ks, device=DEV) * 0.1
+    b = torch.randn(16, device=DEV) * 0.1
+    wp = pack_w16_planes(ij_in_weights(w))
+    m = (torch.rand(shape + (16,), device=DEV) > 0.5).to(torch.bfloat16)
+    outs = {}
+    for tpw in ("1", "5", "3"):
+        monkeypatch.setenv("NCNET_GP_TPW", tpw)
+        y1 = torch.full(shape + (16,), float("nan"), device=DEV, dtype=torch.bfloat16)
+        C.conv16_fwd(xs, wp, b, None, y1, ks, 1, 0)
+        y2 = torch.full(shape + (16,), float("nan"), device=DEV, dtype=torch.bfloat16)
+        C.conv16_fwd(xs, wp, None, m, y2, ks, 2, 0)
+        z = torch.full((16,) + shape, float("nan"), device=DEV)
+        C.conv16_fwd(xs, wp, None, None, z, ks, 4, 0)
+        outs[tpw] = (y1, y2, z)
+    for tpw in ("5", "3"):
+        for a, r in zip(outs[tpw], outs["1"]):
+            assert not torch.isnan(a).any() and torch.equal(a, r)
+    yr = torch.relu(ref.conv4d(bf(x0.float()).unsqueeze(1), ref.conv4d_weight_from_std(bf(w)), b.double()))
+    assert relerr(outs["5"][0].permute(0, 5, 1, 2, 3, 4), yr) < 1e-2
