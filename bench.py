@@ -57,7 +57,7 @@ def main(argv=None):
     args = ap.parse_args(argv)
 
     from ncnet_amd.config import RuntimeConfig
-    from ncnet_amd.engine.trainer import weak_loss
+    from ncnet_amd.engine.trainer import make_adam, weak_loss
     from ncnet_amd.models import ImMatchNet
     from ncnet_amd.parallel.dist import GradBucket, all_reduce_max_float, barrier, broadcast_module, init_distributed
 
@@ -71,7 +71,7 @@ def main(argv=None):
     model.train()
     params = [p for p in model.parameters() if p.requires_grad]
     broadcast_module(model, ctx)
-    opt = torch.optim.Adam(params, lr=5e-4)
+    opt = make_adam(params, 5e-4)
     bucket = GradBucket(params, ctx)
 
     # a small pool of synthetic batches (random normalised images), generated on device

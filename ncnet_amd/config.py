@@ -20,6 +20,8 @@ class RuntimeConfig:
     trunk_graph: bool = True         # NCNET_TRUNK_GRAPH
     force_torch: bool = False        # NCNET_FORCE_TORCH
     allow_torch_fallback: bool = False  # NCNET_ALLOW_TORCH_FALLBACK
+    fused_adam: bool = False         # NCNET_FUSED_ADAM
+    gp_tpw: int = 5                  # NCNET_GP_TPW: output j-tiles per workgroup of the group-plane conv
 
     @classmethod
     def from_env(cls, env=None) -> "RuntimeConfig":
@@ -33,7 +35,9 @@ class RuntimeConfig:
                    trunk_plan=e.get("NCNET_TRUNK_PLAN", "1") != "0",
                    trunk_graph=e.get("NCNET_TRUNK_GRAPH", "1") != "0",
                    force_torch=e.get("NCNET_FORCE_TORCH", "0") == "1",
-                   allow_torch_fallback=e.get("NCNET_ALLOW_TORCH_FALLBACK", "0") == "1")
+                   allow_torch_fallback=e.get("NCNET_ALLOW_TORCH_FALLBACK", "0") == "1",
+                   fused_adam=e.get("NCNET_FUSED_ADAM", "0") == "1",
+                   gp_tpw=int(e.get("NCNET_GP_TPW", "5")))
 
     def as_dict(self) -> dict:
         return dataclasses.asdict(self)

@@ -334,7 +334,7 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
       xp = X + s * g.gstride + plane_offset(g, t.v, t.i, t.j + jt, 16);
     } else {
       const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-      xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
+      xp = X + plane_offset(g, t.v, t.i + di - P, t.j + jt + dj - P, 16);
     }
     for (int r = wave; r < g.PR; r += NW) {
       const int kg = t.k0 - P + r;
@@ -1083,7 +1083,11 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
     // stays conflict-free (a TL + KS - 1 stride cost ~1/3 extra LDS cycles).
     g.RS = tl + ((KS - 1 + 7) / 8) * 8;
     size_t lds2 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
-    // group planes: tpw consecutive output j-tiles per workgroup (NCNET_GP_TPW, default 5)
+    // group planes: tpw consecutive output j-tiles per workgroup (NCNET_GP_TPW,
+    // default 5).  Not for the dj-centre planes: there one tile per workgroup
+    // keeps the 5 i-neighbour planes shared through L2 by concurrently running
+    // workgroups, and the multi-tile stream measured slower (1.73 vs 1.58 ms at
+    // 64 x 25^4, profiles/r1s3_kbench_djc.json)
     const bool mt = npg > 0 && gp_tpw() > 1;
     if (mt) { g.tpw = gp_tpw(); g.njb = cdiv(J, g.tpw); }
     dim3 grid2((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block2(512);

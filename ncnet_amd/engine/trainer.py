@@ -26,6 +26,17 @@ from ..parallel.dist import DistContext, GradBucket, all_reduce_mean
 from ..utils.timing import active as active_timer, segment
 
 
+def make_adam(params, lr: float) -> torch.optim.Optimizer:
+    """Adam as in train.py:71.  NCNET_FUSED_ADAM=1 selects
+    torch's fused multi-tensor kernel; the default stays foreach because the
+    fused step measured slower end to end on MI355X (536-537 vs 540-541
+    pairs/s, two interleaved runs each, profiles/r1s3_adam_ab.txt).  Same
+    state_dict layout either way, so checkpoints interchange."""
+    params = list(params)
+    fused = os.environ.get("NCNET_FUSED_ADAM", "0") == "1" and bool(params) and params[0].is_cuda
+    return torch.optim.Adam(params, lr=lr, fused=True) if fused else torch.optim.Adam(params, lr=lr)
+
+
 def weak_loss(model, batch, normalization: str | None = "softmax", alpha: float = 30) -> torch.Tensor:
     """score_neg - score_pos (train.py:110-156). ``alpha`` is unused, as in the reference."""
     src, tgt = batch["source_image"], batch["target_image"]

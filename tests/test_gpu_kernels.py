@@ -534,3 +534,4 @@ def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch):
             assert not torch.isnan(a).any() and torch.equal(a, r)
     yr = torch.relu(ref.conv4d(bf(x0.float()).unsqueeze(1), ref.conv4d_weight_from_std(bf(w)), b.double()))
     assert relerr(outs["5"][0].permute(0, 5, 1, 2, 3, 4), yr) < 1e-2
+

@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from ncnet_amd.data import ImagePairDataset, NormalizeImageDict, SyntheticPairDataset  # noqa: E402
 from ncnet_amd.engine.checkpoint import capture_rng, load_checkpoint, restore_rng, save_checkpoint  # noqa: E402
-from ncnet_amd.engine.trainer import Trainer  # noqa: E402
+from ncnet_amd.engine.trainer import Trainer, make_adam  # noqa: E402
 from ncnet_amd.models import ImMatchNet  # noqa: E402
 from ncnet_amd.parallel.dist import barrier, broadcast_module, destroy, init_distributed, shard_indices  # noqa: E402
 from ncnet_amd.utils.timing import SegmentTimer, set_active  # noqa: E402
@@ -113,7 +113,7 @@ def main(argv=None):
         print("Trainable parameters:")
         for i, p in enumerate(params):
             print(f"{i + 1}: {tuple(p.shape)}")
-    optimizer = torch.optim.Adam(params, lr=args.lr)
+    optimizer = make_adam(params, args.lr)
 
     size = (args.image_size, args.image_size)
     if args.synthetic:
