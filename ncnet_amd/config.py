@@ -22,6 +22,8 @@ class RuntimeConfig:
     allow_torch_fallback: bool = False  # NCNET_ALLOW_TORCH_FALLBACK
     fused_adam: bool = False         # NCNET_FUSED_ADAM
     gp_tpw: int = 5                  # NCNET_GP_TPW: output j-tiles per workgroup of the group-plane conv
+    nt_store: bool = True            # NCNET_NT_STORE: non-temporal Conv4d epilogue stores
+    ijpack_version: int = 0          # NCNET_IJPACK_V: 0 = v1 + non-temporal stores (default), 1-3 variants
 
     @classmethod
     def from_env(cls, env=None) -> "RuntimeConfig":
@@ -37,7 +39,9 @@ class RuntimeConfig:
                    force_torch=e.get("NCNET_FORCE_TORCH", "0") == "1",
                    allow_torch_fallback=e.get("NCNET_ALLOW_TORCH_FALLBACK", "0") == "1",
                    fused_adam=e.get("NCNET_FUSED_ADAM", "0") == "1",
-                   gp_tpw=int(e.get("NCNET_GP_TPW", "5")))
+                   gp_tpw=int(e.get("NCNET_GP_TPW", "5")),
+                   nt_store=e.get("NCNET_NT_STORE", "1") != "0",
+                   ijpack_version=int(e.get("NCNET_IJPACK_V", "0")))
 
     def as_dict(self) -> dict:
         return dataclasses.asdict(self)

@@ -42,6 +42,7 @@ struct ConvGeom {
   long long gstride;  //   plane of input group s at X + s * gstride, weights plane s
   int njb;            // output j-blocks per (v, i): J, or cdiv(J, R) (v3) / cdiv(J, tpw) (v2 group planes)
   int tpw;            // v2 group-plane mode: consecutive output j-tiles per workgroup (1 otherwise)
+  int nt;             // v2 / v3 epilogues: non-temporal output stores (NCNET_NT_STORE)
 };
 
 // Decode the workgroup's output tile.
@@ -113,16 +114,23 @@ __device__ __forceinline__ size_t plane_offset(const ConvGeom& g, int v, int i, 
 
 // Epilogue for a [16 co x 16 voxel] accumulator tile: lane holds co = 4(l>>4)+r
 // of voxel (l & 15).
+// nt: streaming (non-temporal) stores -- the volumes written here (0.1-1.6 GB)
+// never stay in the 4 MB L2s, so a write-allocating store only evicts the
+// operands the running kernel is still reading.
 template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
                                         const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0,
-                                        int nco = 16) {
+                                        int nco = 16, bool nt = false) {
   if (EPI == EPI_F32 || EPI == EPI_F32X16) {
     // channel-planar fp32 [nco][nvox_all] (only the channels a consumer reads):
     // 16 lanes write 16 consecutive voxels of one channel
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (co0 + r < nco) ((float*)Y)[(size_t)(co0 + r) * nvox_all + vox_index] = acc[r];
+      if (co0 + r < nco) {
+        float* dst = (float*)Y + (size_t)(co0 + r) * nvox_all + vox_index;
+        if (nt) __builtin_nontemporal_store(acc[r], dst);
+        else *dst = acc[r];
+      }
     return;
   }
   float o[4];
@@ -140,7 +148,8 @@ __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, 
   bf16x4 out;
 #pragma unroll
   for (int r = 0; r < 4; ++r) out[r] = f2bf(o[r]);
-  *(bf16x4*)(Y + vox_index * 16 + co0) = out;
+  if (nt) __builtin_nontemporal_store(__builtin_bit_cast(u32x2, out), (u32x2*)(Y + vox_index * 16 + co0));
+  else *(bf16x4*)(Y + vox_index * 16 + co0) = out;
 }
 
 // ===========================================================================
@@ -362,7 +371,7 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
         int kk = vi / g.TL, ll = vi - kk * g.TL;
         int kg = t.k0 + kk, lg = t.l0 + ll;
         if (vi < nvox && kg < g.K && lg < g.L)
-          store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco);
+          store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco, g.nt);
       }
     }
   };
@@ -577,7 +586,8 @@ __global__ __launch_bounds__(512, 1) void conv16v3_fwd_kernel(const bf16* __rest
         int kk = vi / g.TL, ll = vi - kk * g.TL;
         int kg = k0 + kk, lg = l0 + ll;
         if (vi < nvox && kg < g.K && lg < g.L)
-          store16<EPI>(acc[r][tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco);
+          store16<EPI>(acc[r][tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco,
+                       g.nt);
       }
     }
   }
@@ -1016,6 +1026,11 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.dj_center = 0;
   g.npg = 0; g.gstride = 0; g.nco = 16; g.oscale = 1.f;
   g.njb = J; g.tpw = 1;
+  {
+    // default on: conv16v3 5.51 -> 5.31 ms at 64 x 25^4 (profiles/r1s3_kbench_nt.json)
+    const char* e = getenv("NCNET_NT_STORE");   // read per launch: tests / kbench switch it in-process
+    g.nt = e ? atoi(e) : 1;
+  }
   return g;
 }
 

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void jsum_kernel(const float* __restrict__ Z8,
 
 // ---------------------------------------------------------------------------
 // F8OUT: S is OCP fp8 e4m3 [G][..][16] (inference path), else bf16.
-template <typename T, int KS, bool F8OUT>
+template <typename T, int KS, bool F8OUT, bool NT = false>
 __global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, void* __restrict__ S, long long nvox,
                                                      int I, int J, int KL, int sgn) {
   constexpr int P = KS / 2, NQ = KS * KS, G = (NQ + 15) / 16;
@@ -111,8 +111,13 @@ __global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, vo
 #pragma unroll
       for (int c = 0; c < 16; ++c) h[c >> 3][c & 7] = f2bf(vals[c]);
       bf16x8* o = (bf16x8*)((bf16*)S + ((long long)g * nvox + e) * 16);
-      o[0] = h[0];
-      o[1] = h[1];
+      if (NT) {   // streaming (non-temporal) stores: the 1.6 GB output never fits L2
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, h[0]), (u32x4*)o);
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, h[1]), (u32x4*)o + 1);
+      } else {
+        o[0] = h[0];
+        o[1] = h[1];
+      }
     }
   }
 }
@@ -147,6 +152,44 @@ __global__ __launch_bounds__(256) void ijpack2_kernel(const T* __restrict__ X, b
       o[e] = f2bf(v);
     }
     *(bf16x8*)(sp + ch * 8) = o;
+  }
+}
+
+// ijpack v3 (bf16 output, NCNET_IJPACK_V=3): a workgroup owns a range of KLT
+// voxels of one output plane (v, i, j).  The KS*KS shifted source planes of
+// that range are first staged in LDS with coalesced loads (one 1-channel row
+// per combo), then every thread writes whole 16-byte chunks (8 channels of a
+// voxel) read back from LDS: each wave-store is 1 KB of contiguous bytes.
+template <typename T, int KS>
+__global__ __launch_bounds__(256) void ijpack3_kernel(const T* __restrict__ X, bf16* __restrict__ S, long long nvox,
+                                                      int I, int J, int KL, int KLT, int sgn) {
+  constexpr int P = KS / 2, NQ = KS * KS, G = (NQ + 15) / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* src = (bf16*)smem;                   // [NQ][KLT]
+  const long long plane = blockIdx.x;        // (v*I + i)*J + j, block-uniform
+  const int j = (int)(blockIdx.x % J);
+  const int i = (int)((blockIdx.x / J) % I);
+  const int kl0 = blockIdx.y * KLT, n = min(KLT, KL - kl0);
+  for (int q = 0; q < NQ; ++q) {
+    const int ii = i + sgn * (q / KS - P), jj = j + sgn * (q % KS - P);
+    const bool ok = ii >= 0 && ii < I && jj >= 0 && jj < J;   // uniform over the block
+    const T* xp = X + (plane + (long long)(ii - i) * J + (jj - j)) * KL + kl0;
+    for (int e = threadIdx.x; e < n; e += 256) src[q * KLT + e] = ok ? f2bf((float)xp[e]) : f2bf(0.f);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    bf16* sp = S + ((long long)g * nvox + plane * KL + kl0) * 16;
+    for (int ch = threadIdx.x; ch < 2 * n; ch += 256) {
+      const int vox = ch >> 1, h = ch & 1;
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int q = 16 * g + 8 * h + e;
+        o[e] = q < NQ ? src[q * KLT + vox] : f2bf(0.f);
+      }
+      *(bf16x8*)(sp + ch * 8) = o;
+    }
   }
 }
 
@@ -200,6 +243,26 @@ extern "C" int ncnet_ijpack(const void* X, int x_is_bf16, void* S, int V, int I,
                             int s_fp8, hipStream_t stream) {
   long long nvox = (long long)V * I * J * K * L;
   const char* ev = getenv("NCNET_IJPACK_V");
+  if (!s_fp8 && !(ev && atoi(ev) >= 1 && atoi(ev) <= 3)) {   // default: v1 with non-temporal stores
+    dim3 grid4((unsigned)(V * I * J), (unsigned)((K * L + 255) / 256));
+#define IJP4(T, KSV) hipLaunchKernelGGL((ijpack_kernel<T, KSV, false, true>), grid4, dim3(256), 0, stream, (const T*)X, S, nvox, I, J, K * L, sgn)
+    if (KS == 5) { if (x_is_bf16) IJP4(bf16, 5); else IJP4(float, 5); }
+    else if (KS == 3) { if (x_is_bf16) IJP4(bf16, 3); else IJP4(float, 3); }
+    else return -1;
+#undef IJP4
+    return (int)hipGetLastError();
+  }
+  if (!s_fp8 && ev && atoi(ev) == 3) {
+    const int KLT = min(K * L, 1024);
+    dim3 grid3((unsigned)(V * I * J), (unsigned)((K * L + KLT - 1) / KLT));
+    const size_t lds = (size_t)KS * KS * KLT * 2;
+#define IJP3(T, KSV) hipLaunchKernelGGL((ijpack3_kernel<T, KSV>), grid3, dim3(256), lds, stream, (const T*)X, (bf16*)S, nvox, I, J, K * L, KLT, sgn)
+    if (KS == 5) { if (x_is_bf16) IJP3(bf16, 5); else IJP3(float, 5); }
+    else if (KS == 3) { if (x_is_bf16) IJP3(bf16, 3); else IJP3(float, 3); }
+    else return -1;
+#undef IJP3
+    return (int)hipGetLastError();
+  }
   if (!s_fp8 && ev && atoi(ev) == 2) {
     dim3 grid2((unsigned)(V * I * J), (unsigned)((KS * KS + 15) / 16));
 #define IJP2(T, KSV) hipLaunchKernelGGL((ijpack2_kernel<T, KSV>), grid2, dim3(256), 0, stream, (const T*)X, (bf16*)S, nvox, I, J, K * L, sgn)

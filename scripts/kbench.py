@@ -101,8 +101,10 @@ def main():
     fl1 = 2.0 * nvox * taps * 16
     cases = {
         "conv16_fwd": (lambda: C.conv16_fwd(x16, w16, b16, None, y16, ks, 1, 0), fl16),
+        "conv16_fwd_nt": (with_env("NCNET_NT_STORE", "1", lambda: C.conv16_fwd(x16, w16, b16, None, y16, ks, 1, 0)), fl16),
         "conv16_dgrad_mask": (lambda: C.conv16_fwd(g16, w16, None, x16, y16, ks, 2, 0), fl16),
         "conv16_center_f32": (lambda: C.conv16_fwd(x16, w16, None, None, z8, ks, 3, 1), fl16 / ks),
+        "conv16_center_f32_nt": (with_env("NCNET_NT_STORE", "1", lambda: C.conv16_fwd(x16, w16, None, None, z8, ks, 3, 1)), fl16 / ks),
         "jpack": (lambda: C.jpack(x1, g16b, ks, 1), None),
         "jsum": (lambda: C.jsum(z8, b1, y1, ks, 1, 1), None),
         "conv1in_fwd": (lambda: C.conv1in_fwd(x1, w1i, b16, None, y16, ks, 1), fl1),
@@ -116,10 +118,14 @@ def main():
         "wgrad16v3_center": (lambda: C.wgrad16(x16, g16, p3c, p3cb, ks, 1, 3), fl16 / ks),
         "ijpack": (lambda: C.ijpack(x1, xs, ks, 1), None),
         "ijpack_v2": (with_env("NCNET_IJPACK_V", "2", lambda: C.ijpack(x1, xs, ks, 1)), None),
+        "ijpack_v3": (with_env("NCNET_IJPACK_V", "3", lambda: C.ijpack(x1, xs, ks, 1)), None),
+        "ijpack_v1": (with_env("NCNET_IJPACK_V", "1", lambda: C.ijpack(x1, xs, ks, 1)), None),
         "wgrad16v3_prio": (with_env("NCNET_WGRAD_FLAGS", "1", lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3)), fl16),
         "ij_1in_conv": (lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1, 0), fl1),
+        "ij_1in_conv_nt": (with_env("NCNET_NT_STORE", "1", lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1, 0)), fl1),
         "ij_1in_conv_tpw1": (with_env("NCNET_GP_TPW", "1", lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1, 0)), fl1),
         "ij_out_dgrad": (lambda: C.conv16_fwd(xs, wij, None, x16, y16, ks, 2, 0), fl1),
+        "ij_out_dgrad_nt": (with_env("NCNET_NT_STORE", "1", lambda: C.conv16_fwd(xs, wij, None, x16, y16, ks, 2, 0)), fl1),
         "ij_out_dgrad_tpw1": (with_env("NCNET_GP_TPW", "1", lambda: C.conv16_fwd(xs, wij, None, x16, y16, ks, 2, 0)), fl1),
         "wgrad16v2_plane": (lambda: C.wgrad16(xs[0], g16, pp, ppb, ks, 2, 2), fl1 / G),
         "wgrad1_mode0": (lambda: C.wgrad1(g16, x1, part1, ks, 0, ng), fl1),

@@ -294,11 +294,12 @@ def test_wgrad16v3_priority_flag(flags, monkeypatch):
     assert relerr(sb, g.double().sum(dim=(0, 1, 2, 3, 4))) < 1e-3
 
 
-@pytest.mark.parametrize("version", ["1", "2"])
+@pytest.mark.parametrize("version", ["1", "2", "3", "4"])
 @pytest.mark.parametrize("ks,sgn,shape,dtype", [(5, 1, (2, 6, 7, 25, 25), torch.bfloat16),
                                                 (5, -1, (1, 5, 4, 9, 11), torch.float32),
                                                 (3, 1, (1, 4, 5, 30, 26), torch.bfloat16),
-                                                (3, -1, (2, 3, 3, 7, 5), torch.bfloat16)])
+                                                (3, -1, (2, 3, 3, 7, 5), torch.bfloat16),
+                                                (5, 1, (1, 3, 4, 40, 30), torch.bfloat16)])
 def test_ijpack_kernel(version, ks, sgn, shape, dtype, monkeypatch):
     """ijpack (both kernel versions) vs the torch emulation of the ij encoding:
     S[g][v,i,j,k,l,c] = X[v, i+sgn*(di-P), j+sgn*(dj-P), k, l], q = 16g + c."""
@@ -535,3 +536,29 @@ def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch):
     yr = torch.relu(ref.conv4d(bf(x0.float()).unsqueeze(1), ref.conv4d_weight_from_std(bf(w)), b.double()))
     assert relerr(outs["5"][0].permute(0, 5, 1, 2, 3, 4), yr) < 1e-2
 
+
+
+def test_nontemporal_epilogue_stores_bitwise(monkeypatch):
+    """NCNET_NT_STORE=1 (streaming epilogue stores) writes the same bytes as the
+    default stores for the v3 16->16 conv, the ReLU-mask data gradient and the
+    planar fp32 dj-centre epilogue."""
+    from ncnet_amd.ops.packing import jc_out_weights, pack_w16
+    torch.manual_seed(16)
+    C = _ext.ext()
+    shape = (2, 6, 7, 25, 25)
+    x = torch.rand(shape + (16,), device=DEV).to(torch.bfloat16)
+    w = pack_w16(torch.randn(16, 16, 5, 5, 5, 5, device=DEV) * 0.05)
+    wz = pack_w16(jc_out_weights(torch.randn(1, 16, 5, 5, 5, 5, device=DEV) * 0.05))
+    b = torch.randn(16, device=DEV) * 0.1
+    outs = {}
+    for nt in ("0", "1"):
+        monkeypatch.setenv("NCNET_NT_STORE", nt)
+        y = torch.full_like(x, float("nan"))
+        C.conv16_fwd(x, w, b, None, y, 5, 1, 0)
+        yd = torch.full_like(x, float("nan"))
+        C.conv16_fwd(x, w, None, x, yd, 5, 2, 0)
+        z = torch.full((5,) + shape, float("nan"), device=DEV)
+        C.conv16_fwd(x, wz, None, None, z, 5, 3, 1)
+        outs[nt] = (y, yd, z)
+    for a, r in zip(outs["1"], outs["0"]):
+        assert not torch.isnan(a).any() and torch.equal(a, r)
