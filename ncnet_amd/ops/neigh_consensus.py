@@ -257,6 +257,46 @@ def _reduce_wgrad1(part: torch.Tensor, ks: int, mode: int, c16: int) -> torch.Te
     return s.permute(4, 0, 1, 2, 3).reshape(1, 16, ks, ks, ks, ks)[:, :c16]
 
 
+# Weight gradients of the 16->16 and Cout=1 layers on a second HIP stream
+# (NCNET_BWD_OVERLAP=0 disables): they depend only on the layer input and the
+# incoming gradient, so wgrad(l) runs while the data-gradient chain continues
+# on the main stream (dgrad(l) -> dgrad(l-1) -> ...).  The first layer's
+# weight gradient stays on the main stream, which is idle by then.
+BWD_OVERLAP = _os.environ.get("NCNET_BWD_OVERLAP", "1") == "1"
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(dev: torch.device):
+    st = _SIDE_STREAMS.get(dev.index)
+    if st is None:
+        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return st
+
+
+class _OnSide:
+    """Run a block on the side stream after everything queued on ``main``;
+    inputs are marked in use by the side stream, outputs by ``main``."""
+
+    def __init__(self, main, side, inputs):
+        self.main, self.side, self.inputs = main, side, inputs
+        self.ctx = None
+
+    def __enter__(self):
+        if self.side is None:
+            return self
+        self.side.wait_stream(self.main)
+        for t in self.inputs:
+            t.record_stream(self.side)
+        self.ctx = torch.cuda.stream(self.side)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
 def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool):
     """g_last: grad w.r.t. the last conv's PRE-activation (bf16, 1ch).
     Returns (dW list in checkpoint layout, db list, g_x0 fp32 or None)."""
@@ -265,6 +305,10 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
     dws, dbs = [None] * nl, [None] * nl
     g = g_last
     gx0 = None
+    main = side = None
+    if BWD_OVERLAP and g_last.is_cuda:
+        main = torch.cuda.current_stream(g_last.device)
+        side = _side_stream(g_last.device)
     for li in range(nl - 1, -1, -1):
         kind, w_ref, h = kinds[li], ws[li], saved[li]
         ks = w_ref.shape[0]
@@ -279,10 +323,12 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
             G = ij_groups(ks)
             gs = torch.empty((G,) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
             C.ijpack(g, gs, ks, -1)                  # adjoint of ijsum
-            parts = [wgrad16_partials(C, h, gs[gi], ks, ng, 2) for gi in range(G)]
-            dw = ij_out_grad(torch.stack([p[0][0] for p in parts]), cin)
-            qc = (ks // 2) * ks + ks // 2            # combo (P, P): its channel of ijpack(g, -1) is g itself
-            db = parts[qc // 16][1][qc % 16].reshape(1)
+            with _OnSide(main, side, (h, gs)):
+                parts = [wgrad16_partials(C, h, gs[gi], ks, ng, 2) for gi in range(G)]
+                dw = ij_out_grad(torch.stack([p[0][0] for p in parts]), cin)
+                qc = (ks // 2) * ks + ks // 2        # combo (P, P): its channel of ijpack(g, -1) is g itself
+                db = parts[qc // 16][1][qc % 16].reshape(1)
+                del parts
             if li > 0 or need_dx0:
                 gi_ = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
                 if USE_KL and mask_prev is not None:  # 1 -> Cin conv with flipped taps, ReLU mask fused
@@ -355,9 +401,11 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
                 C.conv1in_fwd(g, pack_w1in(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0)
                 g = gi
         elif kind == "16":
-            sw, sb = wgrad16_partials(C, h, g, ks, ng, False)
-            dw = _reduce_wgrad16(sw, ks, cout, cin)
-            db = sb[:cout]
+            with _OnSide(main, side, (h, g)):
+                sw, sb = wgrad16_partials(C, h, g, ks, ng, False)
+                dw = _reduce_wgrad16(sw, ks, cout, cin)
+                db = sb[:cout]
+                del sw, sb
             if li > 0 or need_dx0:
                 gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
                 wt = transpose_for_dgrad(w)
@@ -375,9 +423,13 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
                 wt = transpose_for_dgrad(w)  # [1, 16, k^4]
                 C.conv1out_fwd(g, pack_w1out(wt), None, gi, ks, 0)
                 gx0 = gi
-        dws[li] = ref.conv4d_weight_from_std(dw)
+        dws[li] = dw
         dbs[li] = db
-    return dws, dbs, gx0
+    if side is not None:
+        main.wait_stream(side)
+        for t in dws + dbs:          # produced on the side stream, consumed (and freed) on main
+            t.record_stream(main)
+    return [ref.conv4d_weight_from_std(d) for d in dws], dbs, gx0
 
 
 def _swap_flat(x: torch.Tensor, shape_ab):
