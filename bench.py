@@ -7,7 +7,8 @@ NC-Net (5,5,5 / 16,16,1) at 400x400, bf16, synthetic pairs, random init
 
 One process per GPU (torchrun env for N > 1; RCCL all-reduce of gradients).
 A step is exactly what train.py does per batch: zero_grad, backbone on the
-pair images, correlation of positive and rolled-negative pairs, MutualMatching,
+pair images (queued one step ahead on a side stream while the frozen trunk
+allows it: engine/trainer.py TrunkPrefetcher), correlation of positive and rolled-negative pairs, MutualMatching,
 symmetric NeighConsensus, MutualMatching, weak loss, backward, gradient
 all-reduce, Adam step.  K steps are timed between barrier+synchronize fences
 and the max over ranks is reported.  ``value`` is whole-job pairs/s.
@@ -57,7 +58,7 @@ def main(argv=None):
     args = ap.parse_args(argv)
 
     from ncnet_amd.config import RuntimeConfig
-    from ncnet_amd.engine.trainer import make_adam, weak_loss
+    from ncnet_amd.engine.trainer import TrunkPrefetcher, make_adam, weak_loss_from_features
     from ncnet_amd.models import ImMatchNet
     from ncnet_amd.parallel.dist import GradBucket, all_reduce_max_float, barrier, broadcast_module, init_distributed
 
@@ -81,9 +82,15 @@ def main(argv=None):
              "target_image": torch.randn(args.batch, 3, s, s, device=dev, generator=gen)} for _ in range(2)]
 
     if args.impl == "hip":
-        def step(batch):
+        pre = TrunkPrefetcher(model)
+
+        def step(batch, nxt):
+            # as Trainer.train_step: the backbone of the next batch is queued on
+            # a side stream behind this step (one backbone pass per step)
             opt.zero_grad(set_to_none=True)
-            loss = weak_loss(model, batch)
+            feats = pre.take(batch)
+            pre.submit(nxt)
+            loss = weak_loss_from_features(model, feats)
             loss.backward()
             bucket.allreduce()
             opt.step()
@@ -92,7 +99,7 @@ def main(argv=None):
         from ncnet_amd.engine.reference_impl import ReferenceAlgorithm, reference_weak_loss
         alg = ReferenceAlgorithm(model, torch.float32 if args.ref_dtype == "fp32" else torch.bfloat16)
 
-        def step(batch):
+        def step(batch, nxt):
             opt.zero_grad(set_to_none=True)
             loss = reference_weak_loss(alg, batch)
             loss.backward()
@@ -104,8 +111,9 @@ def main(argv=None):
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    npool = len(pool)
     for w in range(args.warmup):
-        loss = step(pool[w % len(pool)])
+        loss = step(pool[w % npool], pool[(w + 1) % npool])
     sync()
     barrier(ctx)
     sync()
@@ -116,8 +124,11 @@ def main(argv=None):
                                                   torch.profiler.ProfilerActivity.CUDA])
         prof.__enter__()
     t0 = time.perf_counter()
+    # (the pool alternates, so timed step 0 takes the batch the last warmup
+    # step prefetched; the window holds exactly K backbone passes)
     for it in range(args.steps):
-        loss = step(pool[it % len(pool)])
+        j = args.warmup + it
+        loss = step(pool[j % npool], pool[(j + 1) % npool])
     sync()
     barrier(ctx)
     sync()

@@ -24,6 +24,8 @@ class RuntimeConfig:
     gp_tpw: int = 5                  # NCNET_GP_TPW: output j-tiles per workgroup of the group-plane conv
     nt_store: bool = True            # NCNET_NT_STORE: non-temporal Conv4d epilogue stores
     ijpack_version: int = 0          # NCNET_IJPACK_V: 0 = v1 + non-temporal stores (default), 1-3 variants
+    bwd_overlap: bool = True         # NCNET_BWD_OVERLAP: NC weight gradients on a side stream
+    trunk_prefetch: bool = True      # NCNET_TRUNK_PREFETCH: next batch's frozen backbone on a side stream
 
     @classmethod
     def from_env(cls, env=None) -> "RuntimeConfig":
@@ -41,7 +43,9 @@ class RuntimeConfig:
                    fused_adam=e.get("NCNET_FUSED_ADAM", "0") == "1",
                    gp_tpw=int(e.get("NCNET_GP_TPW", "5")),
                    nt_store=e.get("NCNET_NT_STORE", "1") != "0",
-                   ijpack_version=int(e.get("NCNET_IJPACK_V", "0")))
+                   ijpack_version=int(e.get("NCNET_IJPACK_V", "0")),
+                   bwd_overlap=e.get("NCNET_BWD_OVERLAP", "1") == "1",
+                   trunk_prefetch=e.get("NCNET_TRUNK_PREFETCH", "1") == "1")
 
     def as_dict(self) -> dict:
         return dataclasses.asdict(self)

@@ -44,6 +44,71 @@ def weak_loss(model, batch, normalization: str | None = "softmax", alpha: float 
     return weak_loss_from_corr(vols, src.shape[0], normalization)
 
 
+def weak_loss_from_features(model, feats, normalization: str | None = "softmax") -> torch.Tensor:
+    """weak_loss on backbone features ``(f, (h, w), b)`` from TrunkPrefetcher.take."""
+    f, hw, b = feats
+    return weak_loss_from_corr(model.weak_loss_volumes_from_features(f, hw, b), b, normalization)
+
+
+class TrunkPrefetcher:
+    """Software pipeline over training steps: the frozen backbone (+ L2-norm
+    packing) of batch t+1 runs on a side HIP stream while step t's
+    correlation / NeighConsensus forward+backward and optimizer step run on
+    the main stream.  The trunk's implicit-GEMM convs leave most of the chip
+    idle at 25x25 (layer3), so they fill in behind the NC kernels.
+
+    Every step still runs exactly one backbone pass (for the batch after it),
+    so a timed window of K steps contains K backbone passes.  Only valid when
+    no backbone parameter is trainable (the reference default,
+    ``--fe_finetune_params 0``): the features of batch t+1 must not depend on
+    step t's update.  Disabled otherwise, on CPU, and with
+    NCNET_TRUNK_PREFETCH=0; then ``take`` just runs the backbone in place.
+    """
+
+    def __init__(self, model):
+        self.model = model
+        dev = next(model.parameters()).device
+        fe_trainable = any(p.requires_grad for p in model.FeatureExtraction.parameters())
+        self.enabled = (dev.type == "cuda" and not fe_trainable
+                        and os.environ.get("NCNET_TRUNK_PREFETCH", "1") == "1")
+        self.stream = torch.cuda.Stream(device=dev) if self.enabled else None
+        self._pending = None
+
+    def _extract(self, batch):
+        src, tgt = batch["source_image"], batch["target_image"]
+        with torch.no_grad():
+            f, hw = self.model.extract(torch.cat((src, tgt), 0))
+        return f, hw, src.shape[0]
+
+    def submit(self, batch) -> None:
+        """Queue the backbone of ``batch`` (the NEXT step's) on the side stream."""
+        self._pending = None
+        if not self.enabled or batch is None:
+            return
+        main = torch.cuda.current_stream(self.stream.device)
+        self.stream.wait_stream(main)           # inputs ready; earlier work only
+        with torch.cuda.stream(self.stream):
+            f, hw, b = self._extract(batch)
+            done = torch.cuda.Event()
+            done.record(self.stream)
+        for t in (batch["source_image"], batch["target_image"]):
+            t.record_stream(self.stream)
+        self._pending = (batch, f, hw, b, done)
+
+    def take(self, batch):
+        """Backbone features of ``batch``: the prefetched ones if ``batch`` is
+        the one last submitted, else computed now on the current stream."""
+        pend, self._pending = self._pending, None
+        if pend is not None and pend[0] is batch:
+            _, f, hw, b, done = pend
+            main = torch.cuda.current_stream(self.stream.device)
+            main.wait_event(done)
+            f.record_stream(main)
+            return f, hw, b
+        with segment("backbone"):
+            return self._extract(batch)
+
+
 class Trainer:
     def __init__(self, model, optimizer, ctx: DistContext, normalization="softmax", nan_guard=True,
                  metrics_path: str | None = None, fault_step: int | None = None):
@@ -57,17 +122,22 @@ class Trainer:
         self.metrics_path = metrics_path if ctx.is_main else None
         self.global_step = 0
         self.fault_step = fault_step if fault_step is not None else int(os.environ.get("NCNET_FAULT_STEP", "-1"))
+        self.prefetch = TrunkPrefetcher(model)
 
     def to_device(self, batch):
         dev = self.ctx.device
         return {k: (v.to(dev, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()}
 
-    def train_step(self, batch) -> torch.Tensor:
+    def train_step(self, batch, next_batch=None) -> torch.Tensor:
+        """One step on ``batch``; ``next_batch`` (already on the device) gets
+        its backbone pass queued behind this step (TrunkPrefetcher)."""
         if self.fault_step >= 0 and self.global_step == self.fault_step:
             raise RuntimeError(f"injected fault at step {self.global_step} (NCNET_FAULT_STEP)")
         self.opt.zero_grad(set_to_none=True)
         with segment("forward"):
-            loss = weak_loss(self.model, batch, self.normalization)
+            feats = self.prefetch.take(batch)
+            self.prefetch.submit(next_batch)
+            loss = weak_loss_from_features(self.model, feats, self.normalization)
         with segment("backward"):
             loss.backward()
         with segment("allreduce"):
@@ -100,9 +170,16 @@ class Trainer:
         n = 0
         t0 = time.perf_counter()
         nb = len(loader)
-        for batch_idx, batch in enumerate(loader):
-            batch = self.to_device(batch)
-            loss = self.train_step(batch) if is_train else self.eval_step(batch)
+        it = iter(loader)
+        nxt = next(it, None)
+        nxt = self.to_device(nxt) if nxt is not None else None
+        batch_idx = -1
+        while nxt is not None:
+            batch_idx += 1
+            batch = nxt
+            nxt = next(it, None)          # one batch of lookahead: its backbone overlaps this step
+            nxt = self.to_device(nxt) if nxt is not None else None
+            loss = self.train_step(batch, nxt) if is_train else self.eval_step(batch)
             total += loss.float()
             n += 1
             if log_interval and batch_idx % log_interval == 0:

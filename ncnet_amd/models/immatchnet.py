@@ -289,7 +289,14 @@ class ImMatchNet(nn.Module):
         of 4B."""
         b = src.shape[0]
         with segment("backbone"):
-            f, (h, w) = self.extract(torch.cat((src, tgt), 0))
+            f, hw = self.extract(torch.cat((src, tgt), 0))
+        return self.weak_loss_volumes_from_features(f, hw, b)
+
+    def weak_loss_volumes_from_features(self, f: torch.Tensor, hw, b: int) -> torch.Tensor:
+        """``weak_loss_volumes`` after the backbone: ``f`` = extract() of the
+        2B images [source; target] (engine/trainer.py TrunkPrefetcher runs it
+        one step ahead on a side stream when the trunk is frozen)."""
+        h, w = hw
         fa, fb = f[:b], f[b:]
         amap, bmap = _pair_maps(b, f.device)
         with segment("correlation"):

@@ -269,7 +269,9 @@ _SIDE_STREAMS: dict = {}
 def _side_stream(dev: torch.device):
     st = _SIDE_STREAMS.get(dev.index)
     if st is None:
-        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+        # NCNET_BWD_SIDE_PRIO=-1: high-priority side stream (tuning knob)
+        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(
+            device=dev, priority=int(_os.environ.get("NCNET_BWD_SIDE_PRIO", "0")))
     return st
 
 

@@ -229,3 +229,22 @@ def test_extension_imports_when_built():
     if not os.path.exists(so):
         pytest.skip("extension not built")
     assert _ext.load() is not None
+
+
+def test_trunk_prefetcher_cpu_fallback():
+    """On CPU (and whenever the backbone is trainable) the prefetcher is off:
+    take() runs the backbone in place and the loss equals weak_loss."""
+    from ncnet_amd.engine.trainer import TrunkPrefetcher, weak_loss, weak_loss_from_features
+    from ncnet_amd.models import ImMatchNet
+
+    torch.manual_seed(0)
+    model = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], use_cuda=False)
+    model.eval()
+    batch = {"source_image": torch.randn(2, 3, 64, 64), "target_image": torch.randn(2, 3, 64, 64)}
+    pre = TrunkPrefetcher(model)
+    assert not pre.enabled
+    pre.submit(batch)
+    with torch.no_grad():
+        l1 = weak_loss_from_features(model, pre.take(batch))
+        l2 = weak_loss(model, batch)
+    assert torch.allclose(l1, l2, rtol=1e-6, atol=1e-9)

@@ -562,3 +562,45 @@ def test_nontemporal_epilogue_stores_bitwise(monkeypatch):
         outs[nt] = (y, yd, z)
     for a, r in zip(outs["1"], outs["0"]):
         assert not torch.isnan(a).any() and torch.equal(a, r)
+
+
+def _pipeline_run(monkeypatch, prefetch: bool, overlap: bool, steps: int = 3):
+    """Three Adam steps of the 5,5,5/16,16,1 model on alternating batches."""
+    from ncnet_amd.engine.trainer import TrunkPrefetcher, make_adam, weak_loss_from_features
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.ops import neigh_consensus as nc
+
+    monkeypatch.setenv("NCNET_TRUNK_PREFETCH", "1" if prefetch else "0")
+    monkeypatch.setattr(nc, "BWD_OVERLAP", overlap)
+    torch.manual_seed(0)
+    model = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1], dtype="bf16").to(DEV)
+    model.train()
+    params = [p for p in model.parameters() if p.requires_grad]
+    opt = make_adam(params, 5e-4)
+    g = torch.Generator(device=DEV).manual_seed(7)
+    pool = [{"source_image": torch.randn(4, 3, 200, 200, device=DEV, generator=g),
+             "target_image": torch.randn(4, 3, 200, 200, device=DEV, generator=g)} for _ in range(2)]
+    pre = TrunkPrefetcher(model)
+    assert pre.enabled == prefetch
+    losses = []
+    for it in range(steps):
+        opt.zero_grad(set_to_none=True)
+        feats = pre.take(pool[it % 2])
+        pre.submit(pool[(it + 1) % 2])
+        loss = weak_loss_from_features(model, feats)
+        loss.backward()
+        opt.step()
+        losses.append(loss.detach().clone())
+    torch.cuda.synchronize()
+    return torch.stack(losses).cpu(), [p.detach().clone().cpu() for p in params]
+
+
+def test_pipelined_step_equals_serial(monkeypatch):
+    """Trunk prefetch on a side stream + NC weight gradients on a side stream
+    must be bit-identical to the serial schedule (same kernels, same order of
+    accumulation; only the stream placement differs)."""
+    l_ser, p_ser = _pipeline_run(monkeypatch, prefetch=False, overlap=False)
+    l_pip, p_pip = _pipeline_run(monkeypatch, prefetch=True, overlap=True)
+    assert torch.equal(l_ser, l_pip), (l_ser, l_pip)
+    for a, b in zip(p_ser, p_pip):
+        assert torch.equal(a, b)
