@@ -568,7 +568,9 @@ def _pipeline_run(monkeypatch, prefetch: bool, overlap: bool, steps: int = 3):
     """Three Adam steps of the 5,5,5/16,16,1 model on alternating batches."""
     from ncnet_amd.engine.trainer import TrunkPrefetcher, make_adam, weak_loss_from_features
     from ncnet_amd.models import ImMatchNet
-    from ncnet_amd.ops import neigh_consensus as nc
+    import importlib
+
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")   # the module, not the re-exported function
 
     monkeypatch.setenv("NCNET_TRUNK_PREFETCH", "1" if prefetch else "0")
     monkeypatch.setattr(nc, "BWD_OVERLAP", overlap)
