@@ -93,6 +93,25 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     assert rec["value"] > 0 and rec["steps"] == 1 and rec["warmup"] == 1
 
 
+def test_train_torchrun_two_ranks_cpu(tmp_path):
+    """train.py under torchrun with two gloo ranks: the Trainer's one-batch
+    lookahead loop (TrunkPrefetcher hand-off), sharded sampler, gradient
+    bucket and rank-0 checkpointing run end to end."""
+    import glob
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2", NCNET_FORCE_TORCH="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29733", os.path.join(root, "train.py"), "--synthetic", "8",
+           "--batch_size", "2", "--image_size", "64", "--ncons_kernel_sizes", "3", "3", "--ncons_channels", "16", "1",
+           "--num_epochs", "1", "--result-model-dir", "models"]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "Train Epoch: 1" in out.stdout and "Test set: Average loss" in out.stdout
+    assert glob.glob(str(tmp_path / "models" / "*_checkpoint_adam.pth.tar"))
+
+
 def _vp_worker(rank, world, port, out_dir, k_size, ks):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
