@@ -58,9 +58,10 @@ def main(argv=None):
     args = ap.parse_args(argv)
 
     from ncnet_amd.config import RuntimeConfig
-    from ncnet_amd.engine.trainer import TrunkPrefetcher, make_adam, weak_loss_from_features
+    from ncnet_amd.engine.trainer import Trainer, make_adam
     from ncnet_amd.models import ImMatchNet
-    from ncnet_amd.parallel.dist import GradBucket, all_reduce_max_float, barrier, broadcast_module, init_distributed
+    from ncnet_amd.parallel.dist import (GradBucket, all_reduce_max_float, barrier, broadcast_module, comm_info,
+                                         init_distributed)
 
     ctx = init_distributed()
     if ctx.world_size != args.gpus and ctx.is_main:
@@ -73,7 +74,6 @@ def main(argv=None):
     params = [p for p in model.parameters() if p.requires_grad]
     broadcast_module(model, ctx)
     opt = make_adam(params, 5e-4)
-    bucket = GradBucket(params, ctx)
 
     # a small pool of synthetic batches (random normalised images), generated on device
     gen = torch.Generator(device=dev).manual_seed(1234 + ctx.rank)   # (CPU: gloo smoke runs only)
@@ -82,20 +82,15 @@ def main(argv=None):
              "target_image": torch.randn(args.batch, 3, s, s, device=dev, generator=gen)} for _ in range(2)]
 
     if args.impl == "hip":
-        pre = TrunkPrefetcher(model)
+        trainer = Trainer(model, opt, ctx)
 
         def step(batch, nxt):
-            # as Trainer.train_step: the backbone of the next batch is queued on
-            # a side stream behind this step (one backbone pass per step)
-            opt.zero_grad(set_to_none=True)
-            feats = pre.take(batch)
-            pre.submit(nxt)
-            loss = weak_loss_from_features(model, feats)
-            loss.backward()
-            bucket.allreduce()
-            opt.step()
-            return loss
+            # exactly train.py's step (Trainer.train_step): the backbone of the
+            # next batch is queued on a side stream behind this step (one
+            # backbone pass per step), gradient all-reduce, guarded Adam
+            return trainer.train_step(batch, nxt)
     else:
+        bucket = GradBucket(params, ctx, opt)
         from ncnet_amd.engine.reference_impl import ReferenceAlgorithm, reference_weak_loss
         alg = ReferenceAlgorithm(model, torch.float32 if args.ref_dtype == "fp32" else torch.bfloat16)
 
@@ -103,6 +98,8 @@ def main(argv=None):
             opt.zero_grad(set_to_none=True)
             loss = reference_weak_loss(alg, batch)
             loss.backward()
+            if hasattr(opt, "mark_loss"):
+                opt.mark_loss(loss)
             bucket.allreduce()
             opt.step()
             return loss
@@ -166,6 +163,9 @@ def main(argv=None):
                        "per_gpu_batch": args.batch, "seq_len": None, "image_size": s,
                        "parallelism": f"dp{ctx.world_size}", "impl": args.impl,
                        "baseline_pairs_per_s_1gpu": base, "final_loss": float(loss.detach()),
+                       "comm": comm_info(ctx), "optimizer": type(opt).__name__,
+                       "hbm_peak_gb": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
+                                       if dev.type == "cuda" else None),
                        "runtime": RuntimeConfig.from_env().as_dict()},
         }
         print(json.dumps(rec), flush=True)

@@ -44,6 +44,10 @@ int ncnet_conv1to16_kl(const void*, const void*, const float*, const void*, void
 int ncnet_conv16to1_kl(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, int, float,
                        hipStream_t);
 void ncnet_kl_tiles(int, int, int, int, int, int*, int*);
+int ncnet_nonfinite_count(const float*, long long, int*, hipStream_t);
+int ncnet_adam_masked(float*, float*, float*, float*, long long, const int*, const float*, float, float, float, float,
+                      float, float, hipStream_t);
+int ncnet_adam_finalize(float*, int*, int*, hipStream_t);
 int ncnet_nc_fused_k3(const void*, const void*, const float*, const void*, const float*, float*, int, int, int, int,
                       int, int, int, int, int, hipStream_t);
 }
@@ -550,6 +554,36 @@ void conv2d_nhwc(Tensor X, Tensor W, Tensor bias, c10::optional<Tensor> R, Tenso
      "conv2d_nhwc");
 }
 
+// Guarded flat Adam (csrc/optim.hip).  g may be longer than p (trailing
+// loss-indicator slot); count / skipped int32 [1], step fp32 [1].
+void nonfinite_count(Tensor g, Tensor count) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  check(g, "g", at::kFloat); check(count, "count", at::kInt); check_shape(count, "count", {1});
+  ok(ncnet_nonfinite_count((const float*)g.data_ptr(), g.numel(), (int*)count.data_ptr(), cur_stream(g)), "nonfinite_count");
+}
+
+void adam_masked(Tensor p, Tensor g, Tensor m, Tensor v, Tensor count, Tensor step, double lr, double b1, double b2,
+                 double eps, double wd, double gscale) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  for (auto* t : {&p, &g, &m, &v, &step}) check(*t, "adam buffer", at::kFloat);
+  check(count, "count", at::kInt);
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() >= n && m.numel() == n && v.numel() == n, "adam_masked: buffer sizes differ");
+  TORCH_CHECK(step.numel() == 1 && count.numel() == 1, "adam_masked: step/count must have one element");
+  ok(ncnet_adam_masked((float*)p.data_ptr(), (float*)g.data_ptr(), (float*)m.data_ptr(), (float*)v.data_ptr(), n,
+                       (const int*)count.data_ptr(), (const float*)step.data_ptr(), (float)lr, (float)b1, (float)b2,
+                       (float)eps, (float)wd, (float)gscale, cur_stream(p)),
+     "adam_masked");
+}
+
+void adam_finalize(Tensor step, Tensor count, Tensor skipped) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(step.device());
+  check(step, "step", at::kFloat); check(count, "count", at::kInt); check(skipped, "skipped", at::kInt);
+  TORCH_CHECK(step.numel() == 1 && count.numel() == 1 && skipped.numel() == 1, "adam_finalize: scalars expected");
+  ok(ncnet_adam_finalize((float*)step.data_ptr(), (int*)count.data_ptr(), (int*)skipped.data_ptr(), cur_stream(step)),
+     "adam_finalize");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for ncnet_amd";
   m.def("conv16_fwd", &conv16_fwd);
@@ -581,4 +615,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv16to1_kl", &conv16to1_kl);
   m.def("kl_tiles", &kl_tiles);
   m.def("nc_fused_k3", &nc_fused_k3);
+  m.def("nonfinite_count", &nonfinite_count);
+  m.def("adam_masked", &adam_masked);
+  m.def("adam_finalize", &adam_finalize);
 }

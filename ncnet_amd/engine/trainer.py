@@ -7,7 +7,9 @@ Differences from the reference, all semantics-preserving:
 * evaluation (``mode='test'``) runs under ``torch.inference_mode`` (the
   reference builds graphs it never uses, train.py:170-174);
 * gradients are averaged over ranks with one bucketed RCCL all-reduce;
-* optional NaN/Inf guard skips a step whose loss is not finite;
+* NaN/Inf guard: a step whose loss or gradients are non-finite on any rank
+  is skipped exactly (parameters, Adam moments and step untouched), on the
+  device for FlatAdam (engine/optim.py);
 * with a ``utils.timing.SegmentTimer`` installed (train.py --segment_timing)
   every logged record carries mean per-segment GPU milliseconds.
 """
@@ -27,13 +29,24 @@ from ..utils.timing import active as active_timer, segment
 
 
 def make_adam(params, lr: float) -> torch.optim.Optimizer:
-    """Adam as in train.py:71.  NCNET_FUSED_ADAM=1 selects
-    torch's fused multi-tensor kernel; the default stays foreach because the
-    fused step measured slower end to end on MI355X (536-537 vs 540-541
-    pairs/s, two interleaved runs each, profiles/r1s3_adam_ab.txt).  Same
-    state_dict layout either way, so checkpoints interchange."""
+    """Adam as in train.py:71.
+
+    Default: ``FlatAdam`` (engine/optim.py) -- flat parameter/gradient
+    buffers, the gradient buffer doubles as the RCCL bucket, three HIP
+    launches per step and an exact asynchronous NaN/Inf step skip.
+    NCNET_ADAM=torch selects torch.optim.Adam (foreach), NCNET_ADAM=fused its
+    fused kernel.  The state_dict layout is torch.optim.Adam's in every case,
+    so checkpoints interchange."""
+    from .optim import FlatAdam
+
     params = list(params)
-    fused = os.environ.get("NCNET_FUSED_ADAM", "0") == "1" and bool(params) and params[0].is_cuda
+    kind = os.environ.get("NCNET_ADAM", "flat")
+    if os.environ.get("NCNET_FUSED_ADAM", "0") == "1":
+        kind = "fused"
+    if kind == "flat" and params and all(p.dtype == torch.float32 for p in params) \
+            and len({p.device for p in params}) == 1:
+        return FlatAdam(params, lr=lr)
+    fused = kind == "fused" and bool(params) and params[0].is_cuda
     return torch.optim.Adam(params, lr=lr, fused=True) if fused else torch.optim.Adam(params, lr=lr)
 
 
@@ -118,7 +131,8 @@ class Trainer:
         self.normalization = normalization
         self.nan_guard = nan_guard
         params = [p for p in model.parameters() if p.requires_grad]
-        self.bucket = GradBucket(params, ctx)
+        self.bucket = GradBucket(params, ctx, optimizer)
+        self.flat = getattr(optimizer, "flat_grad", None) is not None
         self.metrics_path = metrics_path if ctx.is_main else None
         self.global_step = 0
         self.fault_step = fault_step if fault_step is not None else int(os.environ.get("NCNET_FAULT_STEP", "-1"))
@@ -140,18 +154,31 @@ class Trainer:
             loss = weak_loss_from_features(self.model, feats, self.normalization)
         with segment("backward"):
             loss.backward()
+        if self.flat:
+            # loss-finite indicator rides in the gradient bucket: every rank's
+            # FlatAdam then skips the same (globally non-finite) step, with no host sync
+            self.opt.mark_loss(loss)
         with segment("allreduce"):
             self.bucket.allreduce()
         with segment("optimizer"):
-            if self.nan_guard:
-                finite = torch.isfinite(loss)
-                # stay asynchronous: zero the grads of a non-finite step instead of branching on the host
-                for p in self.bucket.params:
-                    if p.grad is not None:
-                        p.grad.mul_(finite.to(p.grad.dtype))
-            self.opt.step()
+            if self.nan_guard and not self.flat and not self._all_finite(loss):
+                self.opt.zero_grad(set_to_none=True)      # skip: params and optimizer state untouched
+            else:
+                self.opt.step()
         self.global_step += 1
         return loss.detach()
+
+    def _all_finite(self, loss) -> bool:
+        """Global finite check for optimizers without the flat guard (host sync)."""
+        ok = torch.isfinite(loss.detach()).all()
+        for p in self.bucket.params:
+            if p.grad is not None:
+                ok = ok & torch.isfinite(p.grad).all()
+        flag = ok.float().reshape(1)
+        if self.ctx.enabled:
+            import torch.distributed as dist
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item() > 0)
 
     @torch.inference_mode()
     def eval_step(self, batch) -> torch.Tensor:

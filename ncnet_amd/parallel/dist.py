@@ -39,12 +39,33 @@ class DistContext:
 
     @property
     def enabled(self) -> bool:
-        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+        """True whenever a process group exists -- including world size 1
+        under torchrun, so the RCCL collectives really execute there too."""
+        return dist.is_available() and dist.is_initialized()
 
 
-def init_distributed(device: str | None = None, timeout_s: int = 600) -> DistContext:
-    """Initialise from the environment; a no-op single-process context when
-    WORLD_SIZE is unset or 1."""
+def wants_process_group(world: int) -> bool:
+    """A process group is created for WORLD_SIZE > 1, for any torchrun launch
+    (TORCHELASTIC_RUN_ID is set by torch.distributed.run, also at
+    --nproc-per-node 1) and when NCNET_FORCE_PG=1.  A plain ``python bench.py``
+    stays collective-free."""
+    if world > 1:
+        return True
+    if os.environ.get("NCNET_FORCE_PG", "0") == "1":
+        return True
+    return bool(os.environ.get("TORCHELASTIC_RUN_ID"))
+
+
+def init_distributed(device: str | None = None, timeout_s: int | None = None) -> DistContext:
+    """Initialise from the environment (RANK / WORLD_SIZE / LOCAL_RANK /
+    MASTER_*).  Without a launcher (``wants_process_group`` False) this is a
+    single-process context with no process group.
+
+    ``timeout_s`` (default NCNET_PG_TIMEOUT_S or 600) is the rank-failure
+    detector: a collective that a dead or hung rank never joins raises on the
+    surviving ranks after that many seconds instead of hanging forever."""
+    if timeout_s is None:
+        timeout_s = int(os.environ.get("NCNET_PG_TIMEOUT_S", "600"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -55,7 +76,8 @@ def init_distributed(device: str | None = None, timeout_s: int = 600) -> DistCon
     else:
         dev = torch.device("cpu")
     backend = "none"
-    if world > 1:
+    if wants_process_group(world):
+        os.environ.setdefault("MASTER_PORT", "29500")
         backend = "nccl" if use_gpu else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
@@ -63,7 +85,21 @@ def init_distributed(device: str | None = None, timeout_s: int = 600) -> DistCon
             if use_gpu:
                 kw["device_id"] = dev
             dist.init_process_group(**kw)
+        backend = dist.get_backend()
     return DistContext(rank, world, local, dev, backend)
+
+
+def comm_info(ctx: DistContext) -> dict:
+    """What actually carried the collectives (recorded in bench/metrics JSON)."""
+    info = {"backend": dist.get_backend() if ctx.enabled else "none", "world_size": ctx.world_size,
+            "process_group": bool(ctx.enabled)}
+    if ctx.enabled and info["backend"] == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            info["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+        except Exception:  # pragma: no cover
+            info["rccl_version"] = None
+    return info
 
 
 def broadcast_parameters(params, ctx: DistContext, src: int = 0):
@@ -83,37 +119,53 @@ def broadcast_module(module: torch.nn.Module, ctx: DistContext, src: int = 0):
 
 
 class GradBucket:
-    """One flat fp32 gradient bucket for a fixed list of parameters."""
+    """One flat fp32 gradient bucket for a fixed list of parameters.
 
-    def __init__(self, params, ctx: DistContext):
+    With a ``FlatAdam`` optimizer (engine/optim.py) the bucket IS the
+    optimizer's flat gradient buffer (the ``.grad`` tensors are views into
+    it): the all-reduce runs in place, with no pack/unpack copies, and the
+    1/world average is folded into the Adam kernel (``grad_scale``).  The
+    buffer's trailing slot carries the loss-finite indicator, so the NaN guard
+    sees every rank's loss.  Other optimizers get a private bucket with
+    pack -> all-reduce -> average -> unpack.
+    """
+
+    def __init__(self, params, ctx: DistContext, optimizer=None):
         self.params = [p for p in params if p.requires_grad]
         self.ctx = ctx
+        self.inplace = getattr(optimizer, "flat_grad", None) is not None
+        self._work = None
+        if self.inplace:
+            self.flat = optimizer.flat_grad
+            optimizer.grad_scale = 1.0 / ctx.world_size if ctx.enabled else 1.0
+            return
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-        self._work = None
 
     def start(self):
-        """Pack grads and launch the (async) all-reduce."""
+        """Launch the (async) all-reduce (packing the grads first unless in place)."""
         if not self.ctx.enabled:
             return
-        off = 0
-        for p in self.params:
-            n = p.numel()
-            if p.grad is None:
-                self.flat[off:off + n].zero_()
-            else:
-                self.flat[off:off + n].copy_(p.grad.reshape(-1))
-            off += n
-        op = dist.ReduceOp.SUM
-        self._work = dist.all_reduce(self.flat, op=op, async_op=True)
+        if not self.inplace:
+            off = 0
+            for p in self.params:
+                n = p.numel()
+                if p.grad is None:
+                    self.flat[off:off + n].zero_()
+                else:
+                    self.flat[off:off + n].copy_(p.grad.reshape(-1))
+                off += n
+        self._work = dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, async_op=True)
 
     def finish(self):
-        """Wait and scatter the averaged gradients back."""
+        """Wait (and, for a private bucket, scatter the averaged gradients back)."""
         if not self.ctx.enabled or self._work is None:
             return
         self._work.wait()
         self._work = None
+        if self.inplace:
+            return
         self.flat.div_(self.ctx.world_size)
         off = 0
         for p in self.params:

@@ -1,0 +1,125 @@
+#!/usr/bin/env python
+"""Exercise every collective the framework issues, over the real backend.
+
+Launch under torchrun (any --nproc-per-node; on the one-GPU box: 1):
+
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port 29533 scripts/rccl_check.py [--out FILE]
+
+With GPUs the process group is "nccl" (= RCCL on ROCm); torchrun makes
+init_distributed create it even at world size 1 (parallel/dist.py
+wants_process_group).  Checks, each against a value computed locally:
+broadcast_module, GradBucket all-reduce (in-place FlatAdam bucket and the
+private pack/unpack bucket, averaging), all_reduce_max_float, all_reduce MAX /
+all_gather on tensors (volume parallelism), batch_isend_irecv with the ring
+neighbours (self at world 1), barrier(device_ids), and a VolumeParallelMatcher
+forward equal to the single-device model.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="")
+    args = ap.parse_args(argv)
+    from ncnet_amd.engine.optim import FlatAdam
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.parallel.dist import (GradBucket, all_reduce_max_float, barrier, broadcast_module, comm_info,
+                                         destroy, init_distributed)
+    from ncnet_amd.parallel.volume_parallel import VolumeParallelMatcher
+
+    ctx = init_distributed()
+    assert ctx.enabled, "no process group: launch under torchrun"
+    dev, r, w = ctx.device, ctx.rank, ctx.world_size
+    res = {"comm": comm_info(ctx)}
+
+    # broadcast_module: every rank ends with rank 0's weights
+    torch.manual_seed(10 + r)
+    m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], feature_extraction_cnn="resnet101").to(dev)
+    broadcast_module(m, ctx)
+    torch.manual_seed(10)
+    m0 = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1]).to(dev)
+    res["broadcast_module"] = all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), m0.state_dict().values()))
+
+    # in-place FlatAdam bucket: flat_grad holds the SUM; FlatAdam applies 1/world
+    ps = [torch.nn.Parameter(torch.zeros(1000, device=dev)), torch.nn.Parameter(torch.zeros(17, device=dev))]
+    opt = FlatAdam(ps, lr=1e-3)
+    bucket = GradBucket(ps, ctx, opt)
+    opt.zero_grad()
+    for i, p in enumerate(ps):
+        p.grad.fill_(float(r + 1 + i))
+    opt.mark_loss(torch.tensor(1.0, device=dev))
+    bucket.allreduce()
+    tot = sum(range(1, w + 1))
+    res["bucket_inplace_sum"] = bool(torch.allclose(ps[0].grad, torch.full_like(ps[0].grad, float(tot))) and
+                                     torch.allclose(ps[1].grad, torch.full_like(ps[1].grad, float(tot + w))))
+    res["bucket_inplace_scale"] = opt.grad_scale == 1.0 / w
+    opt.step()
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    res["flat_adam_step"] = opt.steps_taken == 1 and opt.skipped_steps == 0
+
+    # private bucket (torch Adam): pack -> all-reduce -> average -> unpack
+    qs = [torch.nn.Parameter(torch.zeros(33, device=dev))]
+    qs[0].grad = torch.full((33,), float(r + 1), device=dev)
+    GradBucket(qs, ctx).allreduce()
+    res["bucket_private_mean"] = bool(torch.allclose(qs[0].grad, torch.full_like(qs[0].grad, tot / w)))
+
+    res["all_reduce_max_float"] = all_reduce_max_float(float(r) + 0.5, ctx) == (w - 1) + 0.5
+
+    t = torch.full((4,), float(r), device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    res["all_reduce_max_tensor"] = bool((t == w - 1).all())
+    outs = [torch.empty(3, device=dev) for _ in range(w)]
+    dist.all_gather(outs, torch.full((3,), float(r), device=dev))
+    res["all_gather"] = all(bool((o == i).all()) for i, o in enumerate(outs))
+
+    # p2p with the ring neighbours (self-exchange at world 1), as exchange_halo issues it
+    send = torch.arange(8, device=dev, dtype=torch.float32) + 100 * r
+    recv = torch.empty(8, device=dev)
+    ops = [dist.P2POp(dist.isend, send, (r + 1) % w), dist.P2POp(dist.irecv, recv, (r - 1) % w)]
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    res["batch_isend_irecv"] = bool(torch.equal(recv, torch.arange(8, device=dev, dtype=torch.float32) +
+                                                100 * ((r - 1) % w)))
+
+    barrier(ctx)
+    res["barrier"] = True
+
+    # volume-parallel matcher == single-device forward (InLoc-style, k = 2)
+    m.relocalization_k_size = 2
+    m.eval()
+    g = torch.Generator(device=dev).manual_seed(5)
+    src = torch.randn(1, 3, 128, 160, device=dev, generator=g)
+    tgt = torch.randn(1, 3, 128, 160, device=dev, generator=g)
+    with torch.inference_mode():
+        full, delta = VolumeParallelMatcher(m, ctx).forward({"source_image": src, "target_image": tgt})
+        ref, rdelta = m({"source_image": src, "target_image": tgt})
+    res["volume_parallel_max_abs_err"] = float((full - ref.float()).abs().max())
+    res["volume_parallel"] = res["volume_parallel_max_abs_err"] < 1e-4 and all(
+        torch.equal(a.to(torch.uint8), b.to(torch.uint8)) for a, b in zip(delta, rdelta))
+
+    checks = [k for k, v in res.items() if isinstance(v, bool)]
+    res["all_ok"] = all(res[k] for k in checks)
+    if ctx.is_main:
+        line = json.dumps(res)
+        print(line, flush=True)
+        if args.out:
+            os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    destroy(ctx)
+    return 0 if res["all_ok"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
