@@ -100,3 +100,36 @@ def test_train_segment_timing_and_profile(tmp_path):
         assert seg and {"backbone", "correlation", "neigh_consensus", "backward", "optimizer"} <= set(seg[0])
     finally:
         os.chdir(old)
+
+
+def test_reference_pair_lists_ship():
+    """The reference's pair CSVs (datasets/*/image_pairs) are in the
+    tree at train.py's default --dataset_csv_path, with the reference counts."""
+    import os
+
+    from ncnet_amd.data.datasets import ImagePairDataset, PFPascalDataset
+
+    root = os.path.join(os.path.dirname(__file__), "..", "datasets")
+    pf = os.path.join(root, "pf-pascal", "image_pairs")
+    assert len(ImagePairDataset(pf, "train_pairs.csv", "unused")) == 2940
+    assert len(ImagePairDataset(pf, "val_pairs.csv", "unused")) == 308
+    ivd = os.path.join(root, "ivd", "image_pairs")
+    tr = ImagePairDataset(ivd, "train_pairs.csv", "unused")
+    assert len(tr) == 6932 and int(tr.flip.sum()) == 3466
+    assert len(ImagePairDataset(ivd, "val_pairs.csv", "unused")) == 758
+    test = PFPascalDataset(os.path.join(pf, "test_pairs.csv"), "unused", output_size=(400, 400))
+    assert len(test) == 299
+
+
+def test_fetch_assets_dry_run(capsys):
+    import importlib.util
+    import os
+
+    p = os.path.join(os.path.dirname(__file__), "..", "scripts", "fetch_assets.py")
+    spec = importlib.util.spec_from_file_location("fetch_assets", p)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    assert m.main(["pf-pascal", "models", "--dry-run"]) == 0
+    out = capsys.readouterr().out
+    assert "PF-dataset-PASCAL.zip" in out and "ncnet_ivd.pth.tar" in out
+    assert len(m.read_pairs_file(m.DATASETS / "ivd" / "urls.txt")) == 3708
