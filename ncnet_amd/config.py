@@ -13,9 +13,7 @@ import os
 
 @dataclasses.dataclass(frozen=True)
 class RuntimeConfig:
-    nc_encoding: str = "ij"          # NCNET_NC_ENC: ij | ijfull | jc | direct
-    wgrad_variant: int = 3           # NCNET_WGRAD_VARIANT
-    conv16_variant: int = 3          # NCNET_CONV16_VARIANT
+    nc_encoding: str = "ij"          # 1-channel NC layers: ij encoding (csrc/jshift.hip), the only one
     trunk_plan: bool = True          # NCNET_TRUNK_PLAN
     trunk_graph: bool = True         # NCNET_TRUNK_GRAPH
     force_torch: bool = False        # NCNET_FORCE_TORCH
@@ -23,27 +21,19 @@ class RuntimeConfig:
     fused_adam: bool = False         # NCNET_FUSED_ADAM
     gp_tpw: int = 5                  # NCNET_GP_TPW: output j-tiles per workgroup of the group-plane conv
     nt_store: bool = True            # NCNET_NT_STORE: non-temporal Conv4d epilogue stores
-    ijpack_version: int = 0          # NCNET_IJPACK_V: 0 = v1 + non-temporal stores (default), 1-3 variants
     bwd_overlap: bool = True         # NCNET_BWD_OVERLAP: NC weight gradients on a side stream
     trunk_prefetch: bool = True      # NCNET_TRUNK_PREFETCH: next batch's frozen backbone on a side stream
 
     @classmethod
     def from_env(cls, env=None) -> "RuntimeConfig":
         e = os.environ if env is None else env
-        enc = e.get("NCNET_NC_ENC", "ij")
-        if e.get("NCNET_NC_JC") == "0":
-            enc = "direct"
-        return cls(nc_encoding=enc,
-                   wgrad_variant=int(e.get("NCNET_WGRAD_VARIANT", "3")),
-                   conv16_variant=int(e.get("NCNET_CONV16_VARIANT", "3")),
-                   trunk_plan=e.get("NCNET_TRUNK_PLAN", "1") != "0",
+        return cls(trunk_plan=e.get("NCNET_TRUNK_PLAN", "1") != "0",
                    trunk_graph=e.get("NCNET_TRUNK_GRAPH", "1") != "0",
                    force_torch=e.get("NCNET_FORCE_TORCH", "0") == "1",
                    allow_torch_fallback=e.get("NCNET_ALLOW_TORCH_FALLBACK", "0") == "1",
                    fused_adam=e.get("NCNET_FUSED_ADAM", "0") == "1",
                    gp_tpw=int(e.get("NCNET_GP_TPW", "5")),
                    nt_store=e.get("NCNET_NT_STORE", "1") != "0",
-                   ijpack_version=int(e.get("NCNET_IJPACK_V", "0")),
                    bwd_overlap=e.get("NCNET_BWD_OVERLAP", "1") == "1",
                    trunk_prefetch=e.get("NCNET_TRUNK_PREFETCH", "1") == "1")
 

@@ -9,19 +9,14 @@
 #include <hip/hip_runtime.h>
 
 extern "C" {
-int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_conv1in_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_conv1out_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_wgrad16v3(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_jpack(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_jsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_wgrad16v3(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_ijpack(const void*, int, void*, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_conv16f8_fwd(const void*, const void*, const float*, void*, int, int, int, int, int, int, int, int, int, int, float, hipStream_t);
+int ncnet_conv16f8_fwd(const void*, const void*, const float*, void*, int, int, int, int, int, int, int, int, int, float, hipStream_t);
 int ncnet_ijsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_bias_act(void*, const float*, long long, int, int, hipStream_t);
 int ncnet_conv2d_nhwc(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_wgrad1(const void*, const void*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
 int ncnet_corr_gemm(const void*, const void*, void*, const int*, const int*, int, int, int, int, long long, long long,
@@ -39,11 +34,6 @@ int ncnet_softmax_max_bwd(const float*, const float*, const int*, const float*, 
                           const float*, const float*, float*, int, int, int, hipStream_t);
 int ncnet_maxpool4d(const void*, int, float*, uint8_t*, int, int, int, int, int, int, hipStream_t);
 int ncnet_transpose(const void*, void*, int, int, int, int, hipStream_t);
-int ncnet_conv1to16_kl(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int,
-                       hipStream_t);
-int ncnet_conv16to1_kl(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, int, float,
-                       hipStream_t);
-void ncnet_kl_tiles(int, int, int, int, int, int*, int*);
 int ncnet_nonfinite_count(const float*, long long, int*, hipStream_t);
 int ncnet_adam_masked(float*, float*, float*, float*, long long, const int*, const float*, float, float, float, float,
                       float, float, hipStream_t);
@@ -74,28 +64,27 @@ template <typename T>
 const T* opt_ptr(const c10::optional<Tensor>& t) { return t.has_value() && t->defined() ? (const T*)t->data_ptr() : nullptr; }
 
 int conv_pairs16(int ks) { return (ks * ks + 1) / 2; }
-int conv_m1(int ks) { return (ks + 3) / 4; }
-int conv_pairs1o(int ks) { return ((ks + 3) * (ks + 3) + 1) / 2; }
+// Conv4d kernel sizes with HIP kernels: 5 and 3 (NC-Net's), 1 and 7.
+void check_ks(int64_t ks) { TORCH_CHECK(ks == 1 || ks == 3 || ks == 5 || ks == 7, "Conv4d kernel size must be 1, 3, 5 or 7 (got ", ks, ")"); }
 
-// X [V,I,J,K,L,16] bf16 -> Y [V,I,J,K,L,16] bf16, or (epi 3) fp32 [V,I,J,K,L,8] raw channels 0..7.
-// dj_center: only the dj = P input planes (j-offset encoded in channels).
-// X [V,I,J,K,L,16] (planes (i+di-P, j+dj-P), dj_center: dj = P only) or
-// X [G,V,I,J,K,L,16] (group planes: G input groups at the (i, j) plane, Wp [G, ...]).
-// epi: 0 none, 1 bias+ReLU, 2 ReLU-mask M, 3/4 fp32 channel-planar [nco,V,I,J,K,L] (nco <= 8 / 16)
-void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi,
-                int64_t dj_center) {
+// X [V,I,J,K,L,16] (all KS*KS planes (i+di-P, j+dj-P)) or X [G,V,I,J,K,L,16]
+// (group planes: G input groups at the (i, j) plane, Wp [G, ...], in-plane taps only).
+// epi: 0 none -> bf16, 1 bias+ReLU -> bf16, 2 ReLU-mask M -> bf16,
+//      4 fp32 channel-planar [nco,V,I,J,K,L] (first nco <= 16 output channels).
+void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
+  check_ks(ks);
   const bool grp = X.dim() == 7;
   TORCH_CHECK((X.dim() == 6 || grp) && X.size(-1) == 16, "X must be [V,I,J,K,L,16] or [G,V,I,J,K,L,16]");
   const int64_t npg = grp ? X.size(0) : 0;
   std::vector<int64_t> vs(X.sizes().begin() + (grp ? 1 : 0), X.sizes().end());   // [V,I,J,K,L,16]
-  TORCH_CHECK(epi >= 0 && epi <= 4);
+  TORCH_CHECK(epi == 0 || epi == 1 || epi == 2 || epi == 4, "conv16_fwd: epi must be 0, 1, 2 or 4");
   int64_t nco = 16;
-  if (epi == 3 || epi == 4) {   // channel-planar fp32 [nco, V,I,J,K,L]: the first nco output channels
+  if (epi == 4) {
     check(Y, "Y", at::kFloat);
     nco = Y.size(0);
-    TORCH_CHECK(nco >= 1 && nco <= (epi == 3 ? 8 : 16), "planar output channels out of range");
+    TORCH_CHECK(nco >= 1 && nco <= 16, "planar output channels out of range");
     check_shape(Y, "Y", {nco, vs[0], vs[1], vs[2], vs[3], vs[4]});
   } else {
     check(Y, "Y", at::kBFloat16);
@@ -105,82 +94,34 @@ void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<T
   if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
   if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", vs); }
   ok(ncnet_conv16_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), vs[0],
-                      vs[1], vs[2], vs[3], vs[4], ks, epi, dj_center ? 1 : 0, (int)npg, (int)nco, cur_stream(X)),
+                      vs[1], vs[2], vs[3], vs[4], ks, epi, (int)npg, (int)nco, cur_stream(X)),
      "conv16_fwd");
 }
 
-// X [V,I,J,K,L] bf16 -> Y [V,I,J,K,L,16] bf16
-void conv1in_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi) {
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
-  check(X, "X", at::kBFloat16); check(Y, "Y", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
-  TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
-  auto ys = X.sizes().vec(); ys.push_back(16);
-  check_shape(Y, "Y", ys);
-  check_shape(Wp, "Wp", {ks * ks, conv_m1(ks), 64, 8});
-  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
-  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", ys); }
-  ok(ncnet_conv1in_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), X.size(0),
-                       X.size(1), X.size(2), X.size(3), X.size(4), ks, epi, cur_stream(X)), "conv1in_fwd");
-}
-
-// X [V,I,J,K,L,16] bf16 -> Y [V,I,J,K,L] fp32
-void conv1out_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t epi) {
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
-  check(X, "X", at::kBFloat16); check(Y, "Y", at::kFloat); check(Wp, "Wp", at::kBFloat16);
-  TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
-  check_shape(Y, "Y", {X.size(0), X.size(1), X.size(2), X.size(3), X.size(4)});
-  check_shape(Wp, "Wp", {ks * ks, conv_pairs1o(ks), 64, 8});
-  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
-  TORCH_CHECK(epi == 0 || epi == 1, "conv1out supports epi none / bias_relu");
-  ok(ncnet_conv1out_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), (float*)Y.data_ptr(), X.size(0), X.size(1),
-                        X.size(2), X.size(3), X.size(4), ks, epi, cur_stream(X)), "conv1out_fwd");
-}
-
-// part rows R: ngroups (variant 1) or 2 * ngroups (variants 2/3, one row per voxel-chunk half)
-void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t dj_center, int64_t variant) {
+// Weight gradient partials.  mode 0: all KS*KS plane offsets (di, dj); mode 2:
+// plane-only (ij-encoded 1-channel layers).  variant 3 (sliding G ring, mode 0,
+// KS 3/5) or 2.  part [rows = 2 * ngroups, mode ? 1 : ks*ks, ks*ks, 16, 16], partb [rows, 16].
+void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t mode, int64_t variant) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(G, "G", at::kBFloat16); check(part, "part", at::kFloat); check(partb, "partb", at::kFloat);
+  check_ks(ks);
   TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
-  TORCH_CHECK(variant >= 1 && variant <= 3, "wgrad16 variant must be 1, 2 or 3");
+  TORCH_CHECK(variant == 2 || variant == 3, "wgrad16 variant must be 2 or 3");
+  TORCH_CHECK(mode == 0 || mode == 2, "wgrad16 mode must be 0 (full) or 2 (plane-only)");
+  TORCH_CHECK(variant == 2 || (mode == 0 && (ks == 3 || ks == 5)), "wgrad16v3: full mode, ks 3 or 5");
   check_shape(G, "G", X.sizes().vec());
   const int64_t rows = part.size(0);
-  TORCH_CHECK(rows > 0 && (variant == 1 || rows % 2 == 0), "wgrad16 v2/v3 need an even number of partial rows");
-  TORCH_CHECK(dj_center >= 0 && dj_center <= 2 && (dj_center < 2 || variant == 2), "plane-only wgrad needs variant 2");
-  check_shape(part, "part", {rows, dj_center == 2 ? 1 : (dj_center ? ks : ks * ks), ks * ks, 16, 16});
+  TORCH_CHECK(rows > 0 && rows % 2 == 0, "wgrad16 needs an even number of partial rows");
+  check_shape(part, "part", {rows, mode == 2 ? 1 : ks * ks, ks * ks, 16, 16});
   check_shape(partb, "partb", {rows, 16});
   if (variant == 3) {
     ok(ncnet_wgrad16v3(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(0),
-                       X.size(1), X.size(2), X.size(3), X.size(4), ks, rows / 2, dj_center ? 1 : 0, cur_stream(X)),
+                       X.size(1), X.size(2), X.size(3), X.size(4), ks, rows / 2, cur_stream(X)),
        "wgrad16v3");
     return;
   }
   ok(ncnet_wgrad16(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(0), X.size(1),
-                   X.size(2), X.size(3), X.size(4), ks, variant == 2 ? rows / 2 : rows, (int)dj_center, variant,
-                   cur_stream(X)), "wgrad16");
-}
-
-// X [V,I,J,K,L] (bf16/fp32) -> S [V,I,J,K,L,16] bf16, S[..,c] = X[v,i,j+sgn*(c-P),k,l] (c < ks)
-void jpack(Tensor X, Tensor S, int64_t ks, int64_t sgn) {
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
-  TORCH_CHECK(X.is_cuda() && X.is_contiguous() && (X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kFloat));
-  TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
-  check(S, "S", at::kBFloat16);
-  check_shape(S, "S", {X.size(0), X.size(1), X.size(2), X.size(3), X.size(4), 16});
-  TORCH_CHECK(ks >= 1 && ks <= 8 && (sgn == 1 || sgn == -1));
-  ok(ncnet_jpack(X.data_ptr(), X.scalar_type() == at::kBFloat16, S.data_ptr(), X.size(0), X.size(1), X.size(2),
-                 X.size(3), X.size(4), ks, sgn, cur_stream(X)), "jpack");
-}
-
-// Z8 [>=ks,V,I,J,K,L] fp32 (channel-planar) -> y [V,I,J,K,L] fp32, y = act(b + sum_{c<ks} Z8[c][v,i,j+sgn*(c-P),k,l])
-void jsum(Tensor Z8, c10::optional<Tensor> bias, Tensor y, int64_t ks, int64_t relu, int64_t sgn) {
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(Z8.device());
-  check(Z8, "Z8", at::kFloat); check(y, "y", at::kFloat);
-  TORCH_CHECK(Z8.dim() == 6 && Z8.size(0) >= ks, "Z8 must be [>=ks,V,I,J,K,L]");
-  check_shape(y, "y", {Z8.size(1), Z8.size(2), Z8.size(3), Z8.size(4), Z8.size(5)});
-  if (bias.has_value()) { check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
-  TORCH_CHECK(ks >= 1 && ks <= 8 && (sgn == 1 || sgn == -1));
-  ok(ncnet_jsum((float*)Z8.data_ptr(), opt_ptr<float>(bias), (float*)y.data_ptr(), Z8.size(1), Z8.size(2), Z8.size(3),
-                Z8.size(4), Z8.size(5), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z8)), "jsum");
+                   X.size(2), X.size(3), X.size(4), ks, rows / 2, (int)mode, cur_stream(X)), "wgrad16");
 }
 
 // X [V,I,J,K,L] (bf16/fp32) -> S [G,V,I,J,K,L,16] bf16 (ij encoding, G = ceil(ks*ks/16))
@@ -188,7 +129,8 @@ void ijpack(Tensor X, Tensor S, int64_t ks, int64_t sgn) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   TORCH_CHECK(X.is_cuda() && X.is_contiguous() && (X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kFloat));
   TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
-  TORCH_CHECK(ks >= 1 && ks <= 5 && (sgn == 1 || sgn == -1));
+  check_ks(ks);
+  TORCH_CHECK(sgn == 1 || sgn == -1);
   const bool f8 = S.scalar_type() == at::kFloat8_e4m3fn;   // fp8 inference path
   check(S, "S", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
   check_shape(S, "S", {(ks * ks + 15) / 16, X.size(0), X.size(1), X.size(2), X.size(3), X.size(4), 16});
@@ -200,23 +142,13 @@ void ijpack(Tensor X, Tensor S, int64_t ks, int64_t sgn) {
 void ijsum(Tensor Z, c10::optional<Tensor> bias, Tensor y, int64_t ks, int64_t relu, int64_t sgn) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(Z.device());
   check(Z, "Z", at::kFloat); check(y, "y", at::kFloat);
-  TORCH_CHECK(ks >= 1 && ks <= 5 && (sgn == 1 || sgn == -1));
+  check_ks(ks);
+  TORCH_CHECK(sgn == 1 || sgn == -1);
   TORCH_CHECK(Z.dim() == 6 && Z.size(0) == ks * ks, "Z must be [ks*ks,V,I,J,K,L]");
   check_shape(y, "y", {Z.size(1), Z.size(2), Z.size(3), Z.size(4), Z.size(5)});
   if (bias.has_value()) { check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
   ok(ncnet_ijsum((float*)Z.data_ptr(), opt_ptr<float>(bias), (float*)y.data_ptr(), Z.size(1), Z.size(2), Z.size(3),
                  Z.size(4), Z.size(5), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z)), "ijsum");
-}
-
-void wgrad1(Tensor S16, Tensor P1, Tensor part, int64_t ks, int64_t mode, int64_t ngroups) {
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S16.device());
-  check(S16, "S16", at::kBFloat16); check(P1, "P1", at::kBFloat16); check(part, "part", at::kFloat);
-  TORCH_CHECK(S16.dim() == 6 && S16.size(5) == 16, "S16 must be [V,I,J,K,L,16]");
-  check_shape(P1, "P1", {S16.size(0), S16.size(1), S16.size(2), S16.size(3), S16.size(4)});
-  check_shape(part, "part", {ngroups, ks * ks, ks * ks, 16});
-  TORCH_CHECK(mode == 0 || mode == 1);
-  ok(ncnet_wgrad1(S16.data_ptr(), P1.data_ptr(), (float*)part.data_ptr(), S16.size(0), S16.size(1), S16.size(2),
-                  S16.size(3), S16.size(4), ks, mode, ngroups, cur_stream(S16)), "wgrad1");
 }
 
 // y: bf16, or OCP fp8 e4m3 holding fp8_scale * x / ||x|| (fp8_scale > 0)
@@ -434,10 +366,10 @@ void bias_act_(Tensor Y, Tensor b, int64_t relu) {
 // fp8 inference Conv4d 16->16: X fp8 [V,I,J,K,L,16] or [G,V,I,J,K,L,16] (group planes),
 // Wp fp8 [planes, ceil(ks*ks/2), 64, 8] (weights * wscale), oscale = 1 / wscale.
 // epi 1: Y fp8 [V,I,J,K,L,16] = relu(oscale * acc + bias); epi 4: Y fp32 planar [nco, V,I,J,K,L].
-void conv16f8_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t epi, int64_t dj_center,
-                  double oscale) {
+void conv16f8_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t epi, double oscale) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kFloat8_e4m3fn); check(Wp, "Wp", at::kFloat8_e4m3fn);
+  check_ks(ks);
   const bool grp = X.dim() == 7;
   TORCH_CHECK((X.dim() == 6 || grp) && X.size(-1) == 16, "X must be [V,I,J,K,L,16] or [G,V,I,J,K,L,16]");
   const int64_t npg = grp ? X.size(0) : 0;
@@ -456,50 +388,8 @@ void conv16f8_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int
   }
   check_shape(Wp, "Wp", {grp ? npg : ks * ks, conv_pairs16(ks), 64, 8});
   ok(ncnet_conv16f8_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), Y.data_ptr(), vs[0], vs[1], vs[2], vs[3],
-                        vs[4], ks, epi, dj_center ? 1 : 0, (int)npg, (int)nco, (float)oscale, cur_stream(X)),
+                        vs[4], ks, epi, (int)npg, (int)nco, (float)oscale, cur_stream(X)),
      "conv16f8_fwd");
-}
-
-// kl kernels (conv4d_kl.hip): in-plane (dk, dl) shifts resolved in LDS.
-// conv1to16_kl: X bf16 [V,I,J,K,L] -> Y [V,I,J,K,L,16] bf16 (or fp8 e4m3, epi 1 only);
-// Wp bf16 [ceil(ks^4/32), 64, 8]; epi 1: bias[16] + ReLU, 2: ReLU mask M [V,I,J,K,L,16] bf16.
-void conv1to16_kl(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks,
-                  int64_t epi) {
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
-  check(X, "X", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
-  TORCH_CHECK(ks == 3 || ks == 5, "conv1to16_kl: ks must be 3 or 5");
-  TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
-  auto ys = X.sizes().vec(); ys.push_back(16);
-  const bool f8 = Y.scalar_type() == at::kFloat8_e4m3fn;
-  check(Y, "Y", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
-  check_shape(Y, "Y", ys);
-  const int64_t nk = ks * ks * ks * ks;
-  check_shape(Wp, "Wp", {(nk + 31) / 32, 64, 8});
-  TORCH_CHECK(epi == 1 || epi == 2, "conv1to16_kl: epi must be 1 (bias+ReLU) or 2 (mask)");
-  TORCH_CHECK(!(f8 && epi == 2), "conv1to16_kl: fp8 output only with bias+ReLU");
-  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
-  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", ys); }
-  ok(ncnet_conv1to16_kl(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), X.size(0),
-                        X.size(1), X.size(2), X.size(3), X.size(4), ks, epi, f8 ? 1 : 0, cur_stream(X)),
-     "conv1to16_kl");
-}
-
-// conv16to1_kl: X [V,I,J,K,L,16] bf16 or fp8 -> Y fp32 [V,I,J,K,L] = act(oscale * conv + bias);
-// Wp [ks*ks + 1, ceil(ks*ks/16), 16, 16] in X's dtype (plane, combo tile, combo, channel; last plane zero).
-void conv16to1_kl(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t relu, double oscale) {
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
-  const bool f8 = X.scalar_type() == at::kFloat8_e4m3fn;
-  check(X, "X", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
-  check(Wp, "Wp", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
-  check(Y, "Y", at::kFloat);
-  TORCH_CHECK(ks == 3 || ks == 5, "conv16to1_kl: ks must be 3 or 5");
-  TORCH_CHECK(X.dim() == 6 && X.size(5) == 16, "X must be [V,I,J,K,L,16]");
-  check_shape(Y, "Y", {X.size(0), X.size(1), X.size(2), X.size(3), X.size(4)});
-  check_shape(Wp, "Wp", {ks * ks + 1, (ks * ks + 15) / 16, 16, 16});
-  if (bias.has_value() && bias->defined()) { check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {1}); }
-  ok(ncnet_conv16to1_kl(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), (float*)Y.data_ptr(), X.size(0), X.size(1),
-                        X.size(2), X.size(3), X.size(4), ks, relu ? 1 : 0, f8 ? 1 : 0, (float)oscale, cur_stream(X)),
-     "conv16to1_kl");
 }
 
 // Fused NC (1 -> 16 -> 1, k = 3): X bf16 [V,I,J,K,L] -> Y fp32 [V,I,J,K,L];
@@ -518,12 +408,6 @@ void nc_fused_k3(Tensor X, Tensor W1p, Tensor b1, Tensor W2p, Tensor b2, Tensor 
                        (const float*)b2.data_ptr(), (float*)Y.data_ptr(), X.size(0), X.size(1), X.size(2), X.size(3),
                        X.size(4), (int)R, (int)IR, (int)TK, (int)TL, cur_stream(X)),
      "nc_fused_k3");
-}
-
-std::vector<int64_t> kl_tiles(int64_t which, int64_t K, int64_t L, int64_t ks, int64_t f8) {
-  int tk = 0, tl = 0;
-  ncnet_kl_tiles((int)which, (int)K, (int)L, (int)ks, (int)f8, &tk, &tl);
-  return {tk, tl};
 }
 
 // NHWC implicit-GEMM conv with fused bias (+ residual) (+ ReLU).  X [N,Cin,H,W],
@@ -587,12 +471,7 @@ void adam_finalize(Tensor step, Tensor count, Tensor skipped) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for ncnet_amd";
   m.def("conv16_fwd", &conv16_fwd);
-  m.def("conv1in_fwd", &conv1in_fwd);
-  m.def("conv1out_fwd", &conv1out_fwd);
   m.def("wgrad16", &wgrad16);
-  m.def("wgrad1", &wgrad1);
-  m.def("jpack", &jpack);
-  m.def("jsum", &jsum);
   m.def("ijpack", &ijpack);
   m.def("conv16f8_fwd", &conv16f8_fwd);
   m.def("ijsum", &ijsum);
@@ -611,9 +490,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_max_bwd", &softmax_max_bwd);
   m.def("maxpool4d", &maxpool4d);
   m.def("transpose", &transpose);
-  m.def("conv1to16_kl", &conv1to16_kl);
-  m.def("conv16to1_kl", &conv16to1_kl);
-  m.def("kl_tiles", &kl_tiles);
   m.def("nc_fused_k3", &nc_fused_k3);
   m.def("nonfinite_count", &nonfinite_count);
   m.def("adam_masked", &adam_masked);

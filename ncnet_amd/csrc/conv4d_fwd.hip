@@ -12,12 +12,10 @@
 // that fall outside the volume are skipped.  Bias + ReLU (forward) or the
 // ReLU-mask of the previous layer (data-gradient) are fused in the epilogue.
 //
-//   conv16_fwd   Cin=16 -> Cout=16 : MFMA D[co][voxel], K = 2 taps x 16 ci.
-//   conv1in_fwd  Cin=1  -> Cout=16 : K = 4 kernel rows x 8-wide l-windows built
-//                                    in LDS (16-byte aligned operand reads).
-//   conv1out_fwd Cin=16 -> Cout=1  : the 16 MFMA columns are 4x4 (k,l) output
-//                                    shifts of an anchor grid (weights shifted
-//                                    on the host), so N=1 still uses the MFMA.
+//   Cin=16 -> Cout=16 : MFMA D[co][voxel], K = 2 taps x 16 ci (conv16v2 / v3).
+//   The 1-channel layers run on the same kernels through the ij encoding
+//   (csrc/jshift.hip): group-plane mode, in-plane (dk, dl) taps only.
+//   Wider layers are channel blocks of 16 (ops/neigh_consensus.py).
 #include "common.h"
 #include <hip/hip_fp8.h>
 #include <stdlib.h>
@@ -25,9 +23,10 @@
 
 namespace ncnet {
 
-// EPI_F32: raw fp32 accumulators of channels 0..7 into Y as float[..., 8]
-// (the j-shift-encoded 16 -> 1 layers, summed afterwards by jsum).
-enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32 = 3, EPI_F32X16 = 4 };  // F32*: channel-planar fp32
+// EPI_F32X16: raw fp32 accumulators of the first nco channels, channel-planar
+// [nco][V,I,J,K,L] (ij-encoded Cout=1 partials summed by ijsum, or the per
+// input-block partials of a layer wider than 16 channels).
+enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32X16 = 4 };
 
 struct ConvGeom {
   int V, I, J, K, L;  // volume dims
@@ -35,8 +34,7 @@ struct ConvGeom {
   int nkt, nlt;       // tiles along k, l
   int PR, RS;         // staged plane rows / row stride (voxels)
   int RW;             // staged row width (voxels, <= RS)
-  int dj_center;      // 1: only the dj = P planes (j-offset encoded in channels)
-  int nco;            // planar fp32 epilogues: output channels written (<= 8 / 16)
+    int nco;            // planar fp32 epilogue: output channels written (<= 16)
   float oscale;       // fp8 kernel: accumulator scale (1 / weight scale)
   int npg;            // > 0: "group planes" mode (v2 only): plane s is the (i, j)
   long long gstride;  //   plane of input group s at X + s * gstride, weights plane s
@@ -58,56 +56,6 @@ __device__ __forceinline__ TileId decode_tile(const ConvGeom& g) {
   return t;
 }
 
-// ---------------------------------------------------------------------------
-// Plane staging for 16-channel volumes: a (PR x RS) window of voxels whose
-// (0,0) corner sits at volume (kb, lb); out-of-volume voxels are zero.
-// Each 16-byte chunk is half a voxel (8 channels).
-template <int MAXCH>
-struct Stage16 {
-  u32x4 r[MAXCH];
-  __device__ __forceinline__ void load(const bf16* __restrict__ plane_ptr, const ConvGeom& g, int kb, int lb, int nchunk) {
-#pragma unroll
-    for (int m = 0; m < MAXCH; ++m) {
-      int c = threadIdx.x + m * 256;
-      u32x4 val = {0u, 0u, 0u, 0u};
-      if (c < nchunk) {
-        int pos = c >> 1, h = c & 1;
-        int row = pos / g.RS, col = pos - row * g.RS;
-        int kg = kb + row, lg = lb + col;
-        if (kg >= 0 && kg < g.K && lg >= 0 && lg < g.L)
-          val = *(const u32x4*)(plane_ptr + ((size_t)(kg * g.L + lg) * 16 + h * 8));
-      }
-      r[m] = val;
-    }
-  }
-  __device__ __forceinline__ void store(char* lds, int nchunk) {
-#pragma unroll
-    for (int m = 0; m < MAXCH; ++m) {
-      int c = threadIdx.x + m * 256;
-      if (c < nchunk) *(u32x4*)(lds + c * 16) = r[m];
-    }
-  }
-};
-
-template <int MAXW>
-struct StageW {
-  u32x4 r[MAXW];
-  __device__ __forceinline__ void load(const u32x4* __restrict__ src, int n) {
-#pragma unroll
-    for (int m = 0; m < MAXW; ++m) {
-      int c = threadIdx.x + m * 256;
-      r[m] = (c < n) ? src[c] : u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  __device__ __forceinline__ void store(char* lds, int n) {
-#pragma unroll
-    for (int m = 0; m < MAXW; ++m) {
-      int c = threadIdx.x + m * 256;
-      if (c < n) *(u32x4*)(lds + c * 16) = r[m];
-    }
-  }
-};
-
 __device__ __forceinline__ size_t plane_offset(const ConvGeom& g, int v, int i, int j, int C) {
   return ((((size_t)v * g.I + i) * g.J + j) * (size_t)g.K * g.L) * C;
 }
@@ -121,7 +69,7 @@ template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
                                         const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0,
                                         int nco = 16, bool nt = false) {
-  if (EPI == EPI_F32 || EPI == EPI_F32X16) {
+  if (EPI == EPI_F32X16) {
     // channel-planar fp32 [nco][nvox_all] (only the channels a consumer reads):
     // 16 lanes write 16 consecutive voxels of one channel
 #pragma unroll
@@ -153,122 +101,6 @@ __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, 
 }
 
 // ===========================================================================
-// conv16_fwd: Cin = 16, Cout = 16.
-// Wp: [KS*KS planes][NQ pairs][64 lanes] x 16 B fragments where lane l of pair
-// q holds W[co=l&15][ci=8((l>>4)&1)+0..7] of tap 2q+(l>>5) (zero past KS*KS).
-// ===========================================================================
-template <int KS, int EPI>
-__global__ __launch_bounds__(256, 2) void conv16_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
-                                                            const float* __restrict__ bias,
-                                                            const bf16* __restrict__ M, bf16* __restrict__ Y,
-                                                            ConvGeom g) {
-  constexpr int P = KS / 2;
-  constexpr int NT = KS * KS;
-  constexpr int NQ = (NT + 1) / 2;
-  constexpr int MAXT = 10;       // 16-voxel tiles per wave (TK*TL <= 640)
-  constexpr int MAXCH = 8;       // PR*RS*2 <= 2048 chunks
-  constexpr int WCH = NQ * 64;
-  constexpr int MAXW = (WCH + 255) / 256;
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* plane = smem;
-  char* wlds = smem + g.PR * g.RS * 32;
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const TileId t = decode_tile(g);
-  const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
-  const int dj_lo = g.dj_center ? P : max(0, P - t.j), dj_hi = g.dj_center ? P + 1 : min(KS, g.J + P - t.j);
-  const int ndj = dj_hi - dj_lo;
-  const int nplanes = (di_hi - di_lo) * ndj;
-  const int nchunk = g.PR * g.RS * 2;
-  const int nvox = g.TK * g.TL;
-  const int ntile = (nvox + 15) >> 4;
-
-  // Per-lane operand addresses.
-  uint32_t vbase[MAXT];
-#pragma unroll
-  for (int tt = 0; tt < MAXT; ++tt) {
-    int vi = (wave + 4 * tt) * 16 + (lane & 15);
-    if (vi >= nvox) vi = 0;
-    int kk = vi / g.TL, ll = vi - kk * g.TL;
-    vbase[tt] = (uint32_t)((kk * g.RS + ll) * 32 + ((lane >> 4) & 1) * 16);
-  }
-  uint32_t toff[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    int tap = 2 * q + (lane >> 5);
-    if (tap >= NT) tap = NT - 1;
-    int dk = tap / KS, dl = tap - dk * KS;
-    toff[q] = (uint32_t)((dk * g.RS + dl) * 32);
-  }
-
-  f32x4 acc[MAXT];
-#pragma unroll
-  for (int tt = 0; tt < MAXT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  Stage16<MAXCH> sx;
-  StageW<MAXW> sw;
-  auto plane_src = [&](int s, const bf16*& xp, const u32x4*& wp) {
-    int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-    xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
-    wp = Wp + (size_t)(di * KS + dj) * WCH;
-  };
-  if (nplanes > 0) {
-    const bf16* xp; const u32x4* wp;
-    plane_src(0, xp, wp);
-    sx.load(xp, g, t.k0 - P, t.l0 - P, nchunk);
-    sw.load(wp, WCH);
-    sx.store(plane, nchunk);
-    sw.store(wlds, WCH);
-  }
-  __syncthreads();
-
-  for (int s = 0; s < nplanes; ++s) {
-    bf16x8 wf[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) wf[q] = lds_read16(wlds, (q * 64 + lane) * 16);
-    const bool more = (s + 1) < nplanes;
-    if (more) {
-      const bf16* xp; const u32x4* wp;
-      plane_src(s + 1, xp, wp);
-      sx.load(xp, g, t.k0 - P, t.l0 - P, nchunk);
-      sw.load(wp, WCH);
-    }
-#pragma unroll
-    for (int tt = 0; tt < MAXT; ++tt) {
-      if (wave + 4 * tt < ntile) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          bf16x8 xf = lds_read16(plane, vbase[tt] + toff[q]);
-          acc[tt] = mfma16(wf[q], xf, acc[tt]);
-        }
-      }
-    }
-    __syncthreads();
-    if (more) {
-      sx.store(plane, nchunk);
-      sw.store(wlds, WCH);
-    }
-    __syncthreads();
-  }
-
-  // Epilogue.
-  const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);  // voxel index of (k=0,l=0)
-#pragma unroll
-  for (int tt = 0; tt < MAXT; ++tt) {
-    int tile = wave + 4 * tt;
-    if (tile < ntile) {
-      int vi = tile * 16 + (lane & 15);
-      int kk = vi / g.TL, ll = vi - kk * g.TL;
-      int kg = t.k0 + kk, lg = t.l0 + ll;
-      if (vi < nvox && kg < g.K && lg < g.L)
-        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4),
-                     (size_t)g.V * g.I * g.J * g.K * g.L, g.nco);
-    }
-  }
-}
-
-// ===========================================================================
 // conv16v2_fwd: same math as conv16_fwd, restructured for occupancy and
 // copy/compute overlap:
 //  * 8 waves per workgroup, 5 voxel tiles per wave (20 accumulator VGPRs);
@@ -283,10 +115,11 @@ __global__ __launch_bounds__(256, 2) void conv16_fwd_kernel(const bf16* __restri
 //    flying) releases the buffer and plane s+1's weights stream in behind the
 //    remaining tiles.  2 x 30.6 KB + 13 KB keeps two workgroups per CU.
 //  * halo/out-of-volume voxels are zeroed once (fixed positions for the tile).
-// Requires RW = TL + KS - 1 <= 32.
+// Requires RW = TL + KS - 1 <= 32.  KS = 7 keeps its 25 weight fragments in
+// registers at one workgroup per CU (256 VGPRs) instead of two.
 // ===========================================================================
 template <int KS, int EPI, bool MT>
-__global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
+__global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
                                                               const float* __restrict__ bias,
                                                               const bf16* __restrict__ M, bf16* __restrict__ Y,
                                                               ConvGeom g) {
@@ -303,7 +136,7 @@ __global__ __launch_bounds__(512, 2) void conv16v2_fwd_kernel(const bf16* __rest
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const TileId t = decode_tile(g);
   const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
-  const int dj_lo = g.dj_center ? P : max(0, P - t.j), dj_hi = g.dj_center ? P + 1 : min(KS, g.J + P - t.j);
+  const int dj_lo = max(0, P - t.j), dj_hi = min(KS, g.J + P - t.j);
   const int ndj = dj_hi - dj_lo;
   const int nplanes = g.npg > 0 ? g.npg : (di_hi - di_lo) * ndj;
   const int nvox = g.TK * g.TL;
@@ -606,7 +439,7 @@ __global__ __launch_bounds__(512, 1) void conv16v3_fwd_kernel(const bf16* __rest
 //            EPI_F32X16   -> channel-planar fp32 partials (ijsum input).
 // ===========================================================================
 template <int KS, int EPI>
-__global__ __launch_bounds__(512, 2) void conv16f8_fwd_kernel(const uint8_t* __restrict__ X,
+__global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16f8_fwd_kernel(const uint8_t* __restrict__ X,
                                                               const uint8_t* __restrict__ Wp,
                                                               const float* __restrict__ bias, void* __restrict__ Y,
                                                               ConvGeom g) {
@@ -623,7 +456,7 @@ __global__ __launch_bounds__(512, 2) void conv16f8_fwd_kernel(const uint8_t* __r
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const TileId t = decode_tile(g);
   const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
-  const int dj_lo = g.dj_center ? P : max(0, P - t.j), dj_hi = g.dj_center ? P + 1 : min(KS, g.J + P - t.j);
+  const int dj_lo = max(0, P - t.j), dj_hi = min(KS, g.J + P - t.j);
   const int ndj = dj_hi - dj_lo;
   const int nplanes = g.npg > 0 ? g.npg : (di_hi - di_lo) * ndj;
   const int nvox = g.TK * g.TL;
@@ -733,297 +566,17 @@ __global__ __launch_bounds__(512, 2) void conv16f8_fwd_kernel(const uint8_t* __r
   }
 }
 
-// ===========================================================================
-// conv1in_fwd: Cin = 1, Cout = 16.
-// The staged plane is expanded in LDS into 8-wide l-windows
-// win[r][c] = plane[r][c .. c+7] so every MFMA operand read is one aligned
-// 16-byte ds_read.  K per MFMA = 4 kernel rows (dk) x 8 window taps (dl).
-// Wp: [KS*KS planes][NM][64 lanes] x 16 B, lane l of MFMA m holds
-// W[co=l&15][di][dj][dk=4m+(l>>4)][dl=0..7] (zero for dk,dl >= KS).
-// ===========================================================================
-template <int KS, int EPI>
-__global__ __launch_bounds__(256, 2) void conv1in_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
-                                                             const float* __restrict__ bias,
-                                                             const bf16* __restrict__ M, bf16* __restrict__ Y,
-                                                             ConvGeom g) {
-  constexpr int P = KS / 2;
-  constexpr int NM = (KS + 3) / 4;
-  constexpr int MAXT = 10;
-  constexpr int WCH = NM * 64;
-  constexpr int MAXE = 8;  // raw plane elements per thread (PR*RW <= 2048)
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int RW = g.TL + KS - 1 + 8;              // raw row width (elements), room for windows
-  char* win = smem;                              // PR * TL windows x 16 B
-  char* raw = smem + g.PR * g.TL * 16;           // PR * RW bf16
-  char* wlds = raw + ((g.PR * RW * 2 + 15) & ~15);
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const TileId t = decode_tile(g);
-  const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
-  const int dj_lo = max(0, P - t.j), dj_hi = min(KS, g.J + P - t.j);
-  const int ndj = dj_hi - dj_lo;
-  const int nplanes = (di_hi - di_lo) * ndj;
-  const int nraw = g.PR * RW;
-  const int nwin = g.PR * g.TL;
-  const int nvox = g.TK * g.TL;
-  const int ntile = (nvox + 15) >> 4;
-
-  uint32_t vbase[MAXT];
-#pragma unroll
-  for (int tt = 0; tt < MAXT; ++tt) {
-    int vi = (wave + 4 * tt) * 16 + (lane & 15);
-    if (vi >= nvox) vi = 0;
-    int kk = vi / g.TL, ll = vi - kk * g.TL;
-    vbase[tt] = (uint32_t)((kk * g.TL + ll) * 16);
-  }
-  uint32_t roff[NM];
-#pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    int dk = 4 * m + (lane >> 4);
-    if (dk >= KS) dk = KS - 1;
-    roff[m] = (uint32_t)(dk * g.TL * 16);
-  }
-
-  f32x4 acc[MAXT];
-#pragma unroll
-  for (int tt = 0; tt < MAXT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16 rr[MAXE];
-  u32x4 wr = {0u, 0u, 0u, 0u};
-  auto load_plane = [&](int s) {
-    int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-    const bf16* xp = X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 1);
-    const int kb = t.k0 - P, lb = t.l0 - P;
-#pragma unroll
-    for (int m = 0; m < MAXE; ++m) {
-      int e = threadIdx.x + m * 256;
-      bf16 val = f2bf(0.f);
-      if (e < nraw) {
-        int row = e / RW, col = e - row * RW;
-        int kg = kb + row, lg = lb + col;
-        if (col < g.TL + KS - 1 && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L) val = xp[(size_t)kg * g.L + lg];
-      }
-      rr[m] = val;
-    }
-    const u32x4* wp = Wp + (size_t)(di * KS + dj) * WCH;
-    if (threadIdx.x < WCH) wr = wp[threadIdx.x];
-  };
-  auto store_raw = [&]() {
-#pragma unroll
-    for (int m = 0; m < MAXE; ++m) {
-      int e = threadIdx.x + m * 256;
-      if (e < nraw) ((bf16*)raw)[e] = rr[m];
-    }
-    if (threadIdx.x < WCH) *(u32x4*)(wlds + threadIdx.x * 16) = wr;
-  };
-  auto build_windows = [&]() {
-    for (int w = threadIdx.x; w < nwin; w += 256) {
-      int row = w / g.TL, c = w - row * g.TL;
-      const bf16* src = (const bf16*)raw + row * RW + c;
-      bf16x8 o;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] = src[q];
-      *(bf16x8*)(win + w * 16) = o;
-    }
-  };
-
-  if (nplanes > 0) {
-    load_plane(0);
-    store_raw();
-  }
-  __syncthreads();
-  if (nplanes > 0) build_windows();
-  __syncthreads();
-
-  for (int s = 0; s < nplanes; ++s) {
-    bf16x8 wf[NM];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) wf[m] = lds_read16(wlds, (m * 64 + lane) * 16);
-    const bool more = (s + 1) < nplanes;
-    if (more) load_plane(s + 1);
-#pragma unroll
-    for (int tt = 0; tt < MAXT; ++tt) {
-      if (wave + 4 * tt < ntile) {
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-          bf16x8 xf = lds_read16(win, vbase[tt] + roff[m]);
-          acc[tt] = mfma16(wf[m], xf, acc[tt]);
-        }
-      }
-    }
-    __syncthreads();
-    if (more) store_raw();
-    __syncthreads();
-    if (more) build_windows();
-    __syncthreads();
-  }
-
-  const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);
-#pragma unroll
-  for (int tt = 0; tt < MAXT; ++tt) {
-    int tile = wave + 4 * tt;
-    if (tile < ntile) {
-      int vi = tile * 16 + (lane & 15);
-      int kk = vi / g.TL, ll = vi - kk * g.TL;
-      int kg = t.k0 + kk, lg = t.l0 + ll;
-      if (vi < nvox && kg < g.K && lg < g.L)
-        store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4));
-    }
-  }
-}
-
-// ===========================================================================
-// conv1out_fwd: Cin = 16, Cout = 1 (fp32 output).
-// Anchors a = (4ak, 4al) cover the tile; MFMA column s = (sk, sl) in 4x4 is the
-// output voxel a + s.  With tau = s + d in [0, KS+3)^2:
-//   Y[a + s] = sum_tau Xpad[a + tau] . W'[tau][s],  W'[tau][s] = W[tau - s]
-// A operand = W' (rows s, K = 2 taus x 16 ci), B operand = X at the anchors.
-// The waves split the tau pairs (K-split) and reduce through LDS at the end.
-// Wp: [KS*KS planes][NPAIR][64 lanes] x 16 B.
-// ===========================================================================
-template <int KS, int EPI>
-__global__ __launch_bounds__(256, 2) void conv1out_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
-                                                              const float* __restrict__ bias,
-                                                              float* __restrict__ Y, ConvGeom g) {
-  constexpr int P = KS / 2;
-  constexpr int TS = KS + 3;                 // tau extent per dim
-  constexpr int NPAIR = (TS * TS + 1) / 2;
-  constexpr int PPW = (NPAIR + 3) / 4;       // pairs per wave
-  constexpr int MAXA = 4;                    // anchor tiles (na*nb <= 64)
-  constexpr int MAXCH = 8;                   // PR*RS*2 <= 2048 (PR, RS <= 32)
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* plane = smem;  // PR x RS x 32 B, reused for the cross-wave reduction
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const TileId t = decode_tile(g);
-  const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
-  const int dj_lo = max(0, P - t.j), dj_hi = min(KS, g.J + P - t.j);
-  const int ndj = dj_hi - dj_lo;
-  const int nplanes = (di_hi - di_lo) * ndj;
-  const int nchunk = g.PR * g.RS * 2;
-  const int na = (g.TK + 3) >> 2, nb = (g.TL + 3) >> 2;
-  const int nanch = na * nb;
-  const int natile = (nanch + 15) >> 4;
-
-  uint32_t abase[MAXA];
-#pragma unroll
-  for (int at = 0; at < MAXA; ++at) {
-    int ai = at * 16 + (lane & 15);
-    if (ai >= nanch) ai = 0;
-    int ak = ai / nb, al = ai - ak * nb;
-    abase[at] = (uint32_t)(((4 * ak) * g.RS + 4 * al) * 32 + ((lane >> 4) & 1) * 16);
-  }
-  uint32_t toff[PPW];
-#pragma unroll
-  for (int q = 0; q < PPW; ++q) {
-    int pr = wave * PPW + q;
-    int tau = 2 * pr + (lane >> 5);
-    if (tau >= TS * TS) tau = TS * TS - 1;
-    int tk = tau / TS, tl = tau - tk * TS;
-    toff[q] = (uint32_t)((tk * g.RS + tl) * 32);
-  }
-
-  f32x4 acc[MAXA];
-#pragma unroll
-  for (int at = 0; at < MAXA; ++at) acc[at] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  Stage16<MAXCH> sx;
-  auto plane_ptr = [&](int s) {
-    int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-    return X + plane_offset(g, t.v, t.i + di - P, t.j + dj - P, 16);
-  };
-  auto wptr = [&](int s) {
-    int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-    return Wp + (size_t)(di * KS + dj) * NPAIR * 64;
-  };
-  bf16x8 wcur[PPW], wnext[PPW];
-  if (nplanes > 0) {
-    sx.load(plane_ptr(0), g, t.k0 - P, t.l0 - P, nchunk);
-    const u32x4* wp = wptr(0);
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-      int pr = min(wave * PPW + q, NPAIR - 1);
-      wcur[q] = __builtin_bit_cast(bf16x8, wp[pr * 64 + lane]);
-    }
-    sx.store(plane, nchunk);
-  }
-  __syncthreads();
-
-  for (int s = 0; s < nplanes; ++s) {
-    const bool more = (s + 1) < nplanes;
-    if (more) {
-      sx.load(plane_ptr(s + 1), g, t.k0 - P, t.l0 - P, nchunk);
-      const u32x4* wp = wptr(s + 1);
-#pragma unroll
-      for (int q = 0; q < PPW; ++q) {
-        int pr = min(wave * PPW + q, NPAIR - 1);
-        wnext[q] = __builtin_bit_cast(bf16x8, wp[pr * 64 + lane]);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-      if (wave * PPW + q < NPAIR) {
-#pragma unroll
-        for (int at = 0; at < MAXA; ++at) {
-          if (at < natile) {
-            bf16x8 xf = lds_read16(plane, abase[at] + toff[q]);
-            acc[at] = mfma16(wcur[q], xf, acc[at]);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (more) {
-      sx.store(plane, nchunk);
-#pragma unroll
-      for (int q = 0; q < PPW; ++q) wcur[q] = wnext[q];
-    }
-    __syncthreads();
-  }
-
-  // Cross-wave K reduction: red[wave][at][r][lane].
-  float* red = (float*)smem;
-#pragma unroll
-  for (int at = 0; at < MAXA; ++at)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[((wave * MAXA + at) * 4 + r) * 64 + lane] = acc[at][r];
-  __syncthreads();
-  const size_t vbase_out = plane_offset(g, t.v, t.i, t.j, 1);
-  const float b0 = (EPI == EPI_BIAS_RELU) ? bias[0] : 0.f;
-  for (int e = threadIdx.x; e < MAXA * 4 * 64; e += 256) {
-    int at = e / 256, r = (e >> 6) & 3, ln = e & 63;
-    if (at >= natile) continue;
-    float sum = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) sum += red[((w * MAXA + at) * 4 + r) * 64 + ln];
-    int sidx = 4 * (ln >> 4) + r;
-    int ai = at * 16 + (ln & 15);
-    if (ai >= nanch) continue;
-    int ak = ai / nb, al = ai - ak * nb;
-    int kk = 4 * ak + (sidx >> 2), ll = 4 * al + (sidx & 3);
-    int kg = t.k0 + kk, lg = t.l0 + ll;
-    if (kk < g.TK && ll < g.TL && kg < g.K && lg < g.L) {
-      float x = sum;
-      if (EPI == EPI_BIAS_RELU) x = fmaxf(x + b0, 0.f);
-      Y[vbase_out + (size_t)kg * g.L + lg] = x;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Host launchers.
 // ---------------------------------------------------------------------------
-static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int tl, int extra_rows, int extra_cols) {
+static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int tl) {
   ConvGeom g;
   g.V = V; g.I = I; g.J = J; g.K = K; g.L = L;
   g.TK = tk; g.TL = tl;
   g.nkt = cdiv(K, tk); g.nlt = cdiv(L, tl);
-  g.PR = tk + KS - 1 + extra_rows;
-  g.RS = tl + KS - 1 + extra_cols;
-  g.RW = g.RS;
-  g.dj_center = 0;
+  g.PR = tk + KS - 1;
+  g.RW = tl + KS - 1;
+  g.RS = g.RW;
   g.npg = 0; g.gstride = 0; g.nco = 16; g.oscale = 1.f;
   g.njb = J; g.tpw = 1;
   {
@@ -1043,7 +596,7 @@ using namespace ncnet;
 static void pick_tile(int K, int L, int& tk, int& tl) {
   tk = K <= 25 ? K : 25;
   tl = L <= 25 ? L : 25;
-  // keep TK*TL <= 640 (MAXT * 4 waves * 16 voxels)
+  // keep TK*TL <= 640 (MAXT * 8 waves * 16 voxels)
   while (tk * tl > 640) { if (tl > tk) --tl; else --tk; }
 }
 
@@ -1053,36 +606,36 @@ static int gp_tpw() {
   return e ? atoi(e) : 5;
 }
 
-// read per launch (cheap) so tests can switch variants inside one process
-static int conv16_variant() {
-  const char* e = getenv("NCNET_CONV16_VARIANT");
-  return e ? atoi(e) : 3;
-}
+// KS = 5 and 3 are NC-Net's kernel sizes (lib/model.py:125-139 defaults, the
+// InLoc and PF-Pascal checkpoints); 1 and 7 complete the general Conv4d.
+#define KS_DISPATCH(M, ...) \
+  do { if (KS == 5) M(5, __VA_ARGS__); else if (KS == 3) M(3, __VA_ARGS__); \
+       else if (KS == 7) M(7, __VA_ARGS__); else if (KS == 1) M(1, __VA_ARGS__); else return -2; } while (0)
 
-// npg > 0: group-planes mode -- X holds npg input groups [npg][V,I,J,K,L,16]
-// and Y = sum_s conv_(dk,dl)(X[s] plane (i,j), Wp plane s): the (di, dj)
-// offsets live in the channels (ij encoding, csrc/jshift.hip).
+// X [V,I,J,K,L,16] (all KS*KS planes (i+di-P, j+dj-P)), or npg > 0: group-planes
+// mode -- X holds npg input groups [npg][V,I,J,K,L,16] and
+// Y = sum_s conv_(dk,dl)(X[s] plane (i,j), Wp plane s): the (di, dj) offsets
+// live in the channels (ij encoding, csrc/jshift.hip) or s indexes 16-channel
+// input blocks of a wider layer.
 extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias, const void* M, void* Y,
-                                int V, int I, int J, int K, int L, int KS, int epi, int dj_center, int npg,
-                                int nco, hipStream_t stream) {
+                                int V, int I, int J, int K, int L, int KS, int epi, int npg, int nco,
+                                hipStream_t stream) {
   int tk, tl;
   pick_tile(K, L, tk, tl);
-  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, 0, 0);
-  g.dj_center = dj_center;
+  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl);
   g.npg = npg;
   g.gstride = (long long)V * I * J * K * L * 16;
   g.nco = nco;
-  const int variant = conv16_variant();
-  const bool lds_dma = variant >= 2 && g.RW <= 32;
-  if ((npg > 0 || epi == EPI_F32X16) && !lds_dma) return -3;   // v2 only
-  if (g.PR * g.RS * 2 > 8 * 256) return -1;
-  int nq = (KS * KS + 1) / 2;
+  if (g.RW > 32) return -1;   // one LDS-DMA wave-instruction per staged row
+  // Row stride RS = TL + 8: a 16-voxel tile that wraps to the next row then
+  // jumps 256 B (the full 64-bank period), so every ds_read_b128 lane group
+  // stays conflict-free (a TL + KS - 1 stride cost ~1/3 extra LDS cycles).
+  g.RS = tl + ((KS - 1 + 7) / 8) * 8;
+  const int nq = (KS * KS + 1) / 2;
   const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
-  if (lds_dma && variant == 3 && npg == 0 && !dj_center && (epi == EPI_BIAS_RELU || epi == EPI_MASK) &&
-      (KS == 5 || KS == 3)) {
+  if (npg == 0 && (epi == EPI_BIAS_RELU || epi == EPI_MASK) && (KS == 5 || KS == 3)) {
     // full (di, dj) sum: R = 5 output j-planes per workgroup, X reused across dj
     constexpr int R = 5;
-    g.RS = tl + ((KS - 1 + 7) / 8) * 8;
     g.njb = cdiv(J, R);
     size_t lds3 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)KS * nq * 1024;
     dim3 grid3((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block3(512);
@@ -1092,56 +645,28 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
 #undef L16V3
     return (int)hipGetLastError();
   }
-  if (lds_dma) {
-    // Row stride RS = TL + 8: a 16-voxel tile that wraps to the next row then
-    // jumps 256 B (the full 64-bank period), so every ds_read_b128 lane group
-    // stays conflict-free (a TL + KS - 1 stride cost ~1/3 extra LDS cycles).
-    g.RS = tl + ((KS - 1 + 7) / 8) * 8;
-    size_t lds2 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
-    // group planes: tpw consecutive output j-tiles per workgroup (NCNET_GP_TPW,
-    // default 5).  Not for the dj-centre planes: there one tile per workgroup
-    // keeps the 5 i-neighbour planes shared through L2 by concurrently running
-    // workgroups, and the multi-tile stream measured slower (1.73 vs 1.58 ms at
-    // 64 x 25^4, profiles/r1s3_kbench_djc.json)
-    const bool mt = npg > 0 && gp_tpw() > 1;
-    if (mt) { g.tpw = gp_tpw(); g.njb = cdiv(J, g.tpw); }
-    dim3 grid2((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block2(512);
-#define L16V2(KSV, EPIV) do { if (mt) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, true>), grid2, block2, lds2, stream, x, w, bias, m, y, g); \
-                              else hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, false>), grid2, block2, lds2, stream, x, w, bias, m, y, g); } while (0)
-    if (KS == 5) {
-      if (epi == EPI_BIAS_RELU) L16V2(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2(5, EPI_MASK);
-      else if (epi == EPI_F32) L16V2(5, EPI_F32); else if (epi == EPI_F32X16) L16V2(5, EPI_F32X16);
-      else L16V2(5, EPI_NONE);
-    } else if (KS == 3) {
-      if (epi == EPI_BIAS_RELU) L16V2(3, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2(3, EPI_MASK);
-      else if (epi == EPI_F32) L16V2(3, EPI_F32); else if (epi == EPI_F32X16) L16V2(3, EPI_F32X16);
-      else L16V2(3, EPI_NONE);
-    } else return -2;
+  size_t lds2 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
+  // group planes: tpw consecutive output j-tiles per workgroup (NCNET_GP_TPW,
+  // default 5): the next tile's first plane DMA overlaps the current epilogue
+  const bool mt = npg > 0 && gp_tpw() > 1;
+  if (mt) { g.tpw = gp_tpw(); g.njb = cdiv(J, g.tpw); }
+  dim3 grid2((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block2(512);
+#define L16V2E(KSV, EPIV) do { if (mt) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, true>), grid2, block2, lds2, stream, x, w, bias, m, y, g); \
+                               else hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, false>), grid2, block2, lds2, stream, x, w, bias, m, y, g); } while (0)
+#define L16V2(KSV, _) do { if (epi == EPI_BIAS_RELU) L16V2E(KSV, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2E(KSV, EPI_MASK); \
+                           else if (epi == EPI_F32X16) L16V2E(KSV, EPI_F32X16); else L16V2E(KSV, EPI_NONE); } while (0)
+  KS_DISPATCH(L16V2, 0);
 #undef L16V2
-    return (int)hipGetLastError();
-  }
-  size_t lds = (size_t)g.PR * g.RS * 32 + (size_t)nq * 64 * 16;
-  dim3 grid((unsigned)(V * I * J * g.nkt * g.nlt)), block(256);
-#define L16(KSV, EPIV) hipLaunchKernelGGL((conv16_fwd_kernel<KSV, EPIV>), grid, block, lds, stream, x, w, bias, m, y, g)
-  if (KS == 5) {
-    if (epi == EPI_BIAS_RELU) L16(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16(5, EPI_MASK);
-    else if (epi == EPI_F32) L16(5, EPI_F32); else L16(5, EPI_NONE);
-  } else if (KS == 3) {
-    if (epi == EPI_BIAS_RELU) L16(3, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16(3, EPI_MASK);
-    else if (epi == EPI_F32) L16(3, EPI_F32); else L16(3, EPI_NONE);
-  } else return -2;
-#undef L16
+#undef L16V2E
   return (int)hipGetLastError();
 }
 
 // fp8 (OCP e4m3) inference Conv4d 16 -> 16; epi 1 (fp8 out) or 4 (planar fp32), oscale = 1 / weight scale.
 extern "C" int ncnet_conv16f8_fwd(const void* X, const void* Wp, const float* bias, void* Y, int V, int I, int J, int K,
-                                  int L, int KS, int epi, int dj_center, int npg, int nco, float oscale,
-                                  hipStream_t stream) {
+                                  int L, int KS, int epi, int npg, int nco, float oscale, hipStream_t stream) {
   int tk, tl;
   pick_tile(K, L, tk, tl);
-  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, 0, 0);
-  g.dj_center = dj_center;
+  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl);
   g.npg = npg;
   g.gstride = (long long)V * I * J * K * L * 16;
   g.nco = nco;
@@ -1152,55 +677,10 @@ extern "C" int ncnet_conv16f8_fwd(const void* X, const void* Wp, const float* bi
   size_t lds = 2 * (size_t)g.PR * g.RS * 16 + (size_t)nq * 512;
   dim3 grid((unsigned)(V * I * J * g.nkt * g.nlt)), block(512);
   const uint8_t* x = (const uint8_t*)X; const uint8_t* w = (const uint8_t*)Wp;
-#define LF8(KSV, EPIV) hipLaunchKernelGGL((conv16f8_fwd_kernel<KSV, EPIV>), grid, block, lds, stream, x, w, bias, Y, g)
-  if (KS == 5) { if (epi == EPI_BIAS_RELU) LF8(5, EPI_BIAS_RELU); else if (epi == EPI_F32X16) LF8(5, EPI_F32X16); else return -2; }
-  else if (KS == 3) { if (epi == EPI_BIAS_RELU) LF8(3, EPI_BIAS_RELU); else if (epi == EPI_F32X16) LF8(3, EPI_F32X16); else return -2; }
-  else return -2;
+#define LF8(KSV, _) do { if (epi == EPI_BIAS_RELU) hipLaunchKernelGGL((conv16f8_fwd_kernel<KSV, EPI_BIAS_RELU>), grid, block, lds, stream, x, w, bias, Y, g); \
+                         else if (epi == EPI_F32X16) hipLaunchKernelGGL((conv16f8_fwd_kernel<KSV, EPI_F32X16>), grid, block, lds, stream, x, w, bias, Y, g); \
+                         else return -2; } while (0)
+  KS_DISPATCH(LF8, 0);
 #undef LF8
-  return (int)hipGetLastError();
-}
-
-extern "C" int ncnet_conv1in_fwd(const void* X, const void* Wp, const float* bias, const void* M, void* Y,
-                                 int V, int I, int J, int K, int L, int KS, int epi, hipStream_t stream) {
-  int tk, tl;
-  pick_tile(K, L, tk, tl);
-  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, 0, 0);
-  int RW = tl + KS - 1 + 8;
-  if (g.PR * RW > 8 * 256) return -1;
-  int nm = (KS + 3) / 4;
-  size_t lds = (size_t)g.PR * tl * 16 + (((size_t)g.PR * RW * 2 + 15) & ~(size_t)15) + (size_t)nm * 64 * 16;
-  dim3 grid((unsigned)(V * I * J * g.nkt * g.nlt)), block(256);
-  const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
-#define L1(KSV, EPIV) hipLaunchKernelGGL((conv1in_fwd_kernel<KSV, EPIV>), grid, block, lds, stream, x, w, bias, m, y, g)
-  if (KS == 5) {
-    if (epi == EPI_BIAS_RELU) L1(5, EPI_BIAS_RELU); else if (epi == EPI_MASK) L1(5, EPI_MASK); else L1(5, EPI_NONE);
-  } else if (KS == 3) {
-    if (epi == EPI_BIAS_RELU) L1(3, EPI_BIAS_RELU); else if (epi == EPI_MASK) L1(3, EPI_MASK); else L1(3, EPI_NONE);
-  } else return -2;
-#undef L1
-  return (int)hipGetLastError();
-}
-
-extern "C" int ncnet_conv1out_fwd(const void* X, const void* Wp, const float* bias, float* Y,
-                                  int V, int I, int J, int K, int L, int KS, int epi, hipStream_t stream) {
-  int tk, tl;
-  pick_tile(K, L, tk, tl);
-  // anchors on a 4-grid: stage 4*ceil(T/4) + KS - 1 rows/cols
-  int pr = 4 * cdiv(tk, 4) + KS - 1, rs = 4 * cdiv(tl, 4) + KS - 1;
-  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl, pr - (tk + KS - 1), rs - (tl + KS - 1));
-  if (g.PR * g.RS * 2 > 8 * 256) return -1;
-  if (cdiv(tk, 4) * cdiv(tl, 4) > 64) return -1;
-  size_t lds = (size_t)g.PR * g.RS * 32;
-  size_t red = (size_t)4 * 4 * 4 * 64 * 4;
-  if (lds < red) lds = red;
-  dim3 grid((unsigned)(V * I * J * g.nkt * g.nlt)), block(256);
-  const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp;
-#define LO(KSV, EPIV) hipLaunchKernelGGL((conv1out_fwd_kernel<KSV, EPIV>), grid, block, lds, stream, x, w, bias, Y, g)
-  if (KS == 5) {
-    if (epi == EPI_BIAS_RELU) LO(5, EPI_BIAS_RELU); else LO(5, EPI_NONE);
-  } else if (KS == 3) {
-    if (epi == EPI_BIAS_RELU) LO(3, EPI_BIAS_RELU); else LO(3, EPI_NONE);
-  } else return -2;
-#undef LO
   return (int)hipGetLastError();
 }

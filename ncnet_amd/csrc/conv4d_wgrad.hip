@@ -8,17 +8,14 @@
 // (di,dj) slice of dW in accumulators while it walks its group's output tiles
 // and writes one fp32 partial per group (summed by a tiny reduction).
 //
-//   wgrad16 (Cin=16, Cout=16): per 32-voxel K chunk, the G^T operand is read
-//     once (ds_read_b64_tr_b16) and reused by every tap; the X^T operand is the
+//   wgrad16v2 (per (di,dj) plane offset, or plane-only for the ij-encoded
+//     1-channel layers): per 32-voxel K chunk, the G^T operand is read once
+//     (ds_read_b64_tr_b16) and reused by every tap; the X^T operand is the
 //     staged plane read at the tap's shift, also through the transposing read
 //     (each lane of the 16-lane group addresses its own voxel row, so arbitrary
 //     shifts cost nothing).  Bias gradient is one extra MFMA with A = ones in
 //     the (P,P) workgroups, which see every output tile exactly once.
-//   wgrad1 (one 1-channel operand): D[c16][tap] = sum_u S[u][c16] * P[u + tap]
-//     with S the 16-channel operand (tr-read, shared by all taps) and P the
-//     1-channel operand expanded into 8-wide l-windows; 16 taps per MFMA.
-//     Layer Cin=1: S = G (tile), P = X plane.  Layer Cout=1: S = X plane,
-//     P = G (tile), taps come out flipped (undone on the host).
+//   wgrad16v3 (the 16 -> 16 training layers): sliding G-plane ring, below.
 #include "common.h"
 #include <stdlib.h>
 
@@ -30,8 +27,8 @@ struct WGeom {
   int PR, RS;          // staged X plane rows / row stride (wgrad16)
   int RW;              // staged row width (voxels, <= RS)
   int nitems, ipg;     // output tiles, tiles per group
-  int dj_center;       // 1: only the (di, dj = P) offsets (j-offset encoded in channels);
-                       // 2: only (P, P) (v2: ij encoding, both offsets in channels)
+  int dj_center;       // 0: all KS*KS (di, dj) offsets; 2: only (P, P) (plane-only:
+                       // ij encoding or 16-channel input blocks, offsets in channels)
 };
 
 struct Item { int v, i, j, k0, l0; };
@@ -65,152 +62,6 @@ __device__ __forceinline__ size_t plane_off(const WGeom& g, int v, int i, int j,
 }
 
 // ===========================================================================
-template <int KS>
-__global__ __launch_bounds__(256, 2) void wgrad16_kernel(const bf16* __restrict__ X, const bf16* __restrict__ G,
-                                                         float* __restrict__ part, float* __restrict__ partb,
-                                                         WGeom g) {
-  constexpr int P = KS / 2;
-  constexpr int NT = KS * KS;
-  constexpr int TPW = (NT + 3) / 4;   // taps per wave
-  constexpr int MAXX = 8;             // X plane chunks per thread (<= 2048)
-  constexpr int MAXG = 5;             // G tile chunks per thread (<= 1280)
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nvox = g.TK * g.TL;
-  const int nv32 = (nvox + 31) & ~31;
-  char* plane = smem;
-  char* gt = smem + g.PR * g.RS * 32;
-  int* voff = (int*)(gt + nv32 * 32);
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int NDD = g.dj_center ? KS : NT;   // plane offsets handled by the grid
-  const int dd = lb % NDD, grp = lb / NDD;
-  const int di = g.dj_center ? dd : dd / KS, dj = g.dj_center ? P : dd % KS;
-  const bool center = (di == P && dj == P);
-
-  for (int e = threadIdx.x; e < nv32; e += 256) {
-    int kk = e / g.TL, ll = e - kk * g.TL;
-    voff[e] = (e < nvox) ? (kk * g.RS + ll) * 32 : 0;
-  }
-
-  uint32_t toffw[TPW];
-#pragma unroll
-  for (int tt = 0; tt < TPW; ++tt) {
-    int tap = min(wave + 4 * tt, NT - 1);
-    int dk = tap / KS, dl = tap - dk * KS;
-    toffw[tt] = (uint32_t)((dk * g.RS + dl) * 32);
-  }
-  f32x4 acc[TPW];
-#pragma unroll
-  for (int tt = 0; tt < TPW; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
-  bf16x8 ones;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) ones[q] = f2bf(1.f);
-
-  const int it_lo = grp * g.ipg, it_hi = min(g.nitems, it_lo + g.ipg);
-  const int nchx = g.PR * g.RS * 2, nchg = nv32 * 2;
-
-  // Tile list: items whose input plane is inside the volume.
-  auto valid_item = [&](int it, Item& r) {
-    r = decode_item(g, it);
-    int ii = r.i + di - P, jj = r.j + dj - P;
-    return ii >= 0 && ii < g.I && jj >= 0 && jj < g.J;
-  };
-  u32x4 rx[MAXX], rg[MAXG];
-  auto load = [&](const Item& r) {
-    const bf16* xp = X + plane_off(g, r.v, r.i + di - P, r.j + dj - P, 16);
-    const bf16* gp = G + plane_off(g, r.v, r.i, r.j, 16);
-    const int kb = r.k0 - P, lb0 = r.l0 - P;
-#pragma unroll
-    for (int m = 0; m < MAXX; ++m) {
-      int c = threadIdx.x + m * 256;
-      u32x4 val = {0u, 0u, 0u, 0u};
-      if (c < nchx) {
-        int pos = c >> 1, h = c & 1;
-        int row = pos / g.RS, col = pos - row * g.RS;
-        int kg = kb + row, lg = lb0 + col;
-        if (kg >= 0 && kg < g.K && lg >= 0 && lg < g.L) val = *(const u32x4*)(xp + ((size_t)(kg * g.L + lg) * 16 + h * 8));
-      }
-      rx[m] = val;
-    }
-#pragma unroll
-    for (int m = 0; m < MAXG; ++m) {
-      int c = threadIdx.x + m * 256;
-      u32x4 val = {0u, 0u, 0u, 0u};
-      if (c < nchg) {
-        int vi = c >> 1, h = c & 1;
-        int kk = vi / g.TL, ll = vi - kk * g.TL;
-        int kg = r.k0 + kk, lg = r.l0 + ll;
-        if (vi < nvox && kg < g.K && lg < g.L) val = *(const u32x4*)(gp + ((size_t)(kg * g.L + lg) * 16 + h * 8));
-      }
-      rg[m] = val;
-    }
-  };
-  auto store = [&]() {
-#pragma unroll
-    for (int m = 0; m < MAXX; ++m) {
-      int c = threadIdx.x + m * 256;
-      if (c < nchx) *(u32x4*)(plane + c * 16) = rx[m];
-    }
-#pragma unroll
-    for (int m = 0; m < MAXG; ++m) {
-      int c = threadIdx.x + m * 256;
-      if (c < nchg) *(u32x4*)(gt + c * 16) = rg[m];
-    }
-  };
-
-  // find first valid item
-  int cur = it_lo;
-  Item rcur;
-  while (cur < it_hi && !valid_item(cur, rcur)) ++cur;
-  if (cur < it_hi) { load(rcur); store(); }
-  __syncthreads();
-
-  const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-  const int nchunk = nv32 >> 5;
-  while (cur < it_hi) {
-    int nxt = cur + 1;
-    Item rn;
-    while (nxt < it_hi && !valid_item(nxt, rn)) ++nxt;
-    const bool more = nxt < it_hi;
-    if (more) load(rn);
-
-    for (int c = 0; c < nchunk; ++c) {
-      const int vb0 = c * 32 + gq * 8 + qq, vb1 = vb0 + 4;
-      bf16x8 bfr = cat8(lds_read_tr16(gt, vb0 * 32 + pp * 8), lds_read_tr16(gt, vb1 * 32 + pp * 8));
-      const uint32_t pa0 = voff[vb0] + pp * 8, pa1 = voff[vb1] + pp * 8;
-#pragma unroll
-      for (int tt = 0; tt < TPW; ++tt) {
-        if (wave + 4 * tt < NT) {
-          bf16x8 afr = cat8(lds_read_tr16(plane, pa0 + toffw[tt]), lds_read_tr16(plane, pa1 + toffw[tt]));
-          acc[tt] = mfma16(afr, bfr, acc[tt]);
-        }
-      }
-      if (center && wave == 0) accb = mfma16(ones, bfr, accb);
-    }
-    __syncthreads();
-    if (more) store();
-    __syncthreads();
-    cur = nxt;
-    rcur = rn;
-  }
-
-  // D[row = ci = 4(l>>4)+r][col = co = l&15]
-  float* pout = part + ((size_t)grp * NDD + dd) * NT * 256;
-#pragma unroll
-  for (int tt = 0; tt < TPW; ++tt) {
-    int tap = wave + 4 * tt;
-    if (tap < NT) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pout[tap * 256 + (4 * (lane >> 4) + r) * 16 + (lane & 15)] = acc[tt][r];
-    }
-  }
-  if (center && wave == 0 && lane < 16) partb[grp * 16 + lane] = accb[0];
-}
-
-// ===========================================================================
 // wgrad16v2: same math as wgrad16, restructured like conv16v2:
 //  * 8 waves = 4 tap groups x 2 halves of the voxel K-chunks; each half writes
 //    its own partial row (part is [2*ngroups, ...]), so no in-kernel reduction;
@@ -239,9 +90,9 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tg = wave & 3, half = wave >> 2;
   const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int NDD = g.dj_center == 2 ? 1 : (g.dj_center ? KS : NT);
+  const int NDD = g.dj_center == 2 ? 1 : NT;
   const int dd = lb % NDD, grp = lb / NDD;
-  const int di = g.dj_center == 2 ? P : (g.dj_center ? dd : dd / KS), dj = g.dj_center ? P : dd % KS;
+  const int di = g.dj_center == 2 ? P : dd / KS, dj = g.dj_center == 2 ? P : dd % KS;
   const bool center = (di == P && dj == P);
 
   for (int o = threadIdx.x * 16; o < plane_bytes + nv32 * 32; o += NW * 64 * 16)
@@ -361,7 +212,6 @@ struct W3Geom {
   int VT, ntl;         // voxels per tile (multiple of 64), tiles per plane
   int PR, RS, RW;      // staged X rows, row stride, row width (voxels)
   int ncols, cpg;      // X-plane columns (v, jj, tile); columns per group
-  int dj_center;
   int flags;           // bit 0: s_setprio 1 for waves 4-7 (NCNET_WGRAD_FLAGS, tuning)
 };
 
@@ -398,11 +248,11 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> scalar branches
   const int tg = wave & 3, half = wave >> 2;
   const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int NDJ = g.dj_center ? 1 : KS;
+  const int NDJ = KS;
   const int djx = lb % NDJ, grp = lb / NDJ;
-  const int dj = g.dj_center ? P : djx;
+  const int dj = djx;
   const bool center_blk = (dj == P);
-  const int NDD = g.dj_center ? KS : NT;
+  const int NDD = NT;
 
   for (int o = threadIdx.x * 16; o < 2 * xbytes + (NS + 1) * gbytes; o += NW * 64 * 16)
     *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
@@ -598,7 +448,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
     const int tap = tg + 4 * m;
 #pragma unroll
     for (int d = 0; d < KS; ++d) {
-      const int ddi = g.dj_center ? d : d * KS + dj;
+      const int ddi = d * KS + dj;
       float* pout = part + (((size_t)row * NDD + ddi) * NT + tap) * 256;
 #pragma unroll
       for (int r = 0; r < 4; ++r) pout[(4 * (lane >> 4) + r) * 16 + (lane & 15)] = acc[m][d][r];
@@ -608,185 +458,13 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
   for (int e = 0; e < EXP; ++e) {
     const int d = xdi_lo + e;
     if (d < xdi_hi) {
-      const int ddi = g.dj_center ? d : d * KS + dj;
+      const int ddi = d * KS + dj;
       float* pout = part + (((size_t)row * NDD + ddi) * NT + (NT - 1)) * 256;
 #pragma unroll
       for (int r = 0; r < 4; ++r) pout[(4 * (lane >> 4) + r) * 16 + (lane & 15)] = accx[e][r];
     }
   }
   if (center_blk && tg == 0 && lane < 16) partb[row * 16 + lane] = accb[0];
-}
-
-// ===========================================================================
-struct W1Geom {
-  WGeom w;
-  int mode;                 // 0: S = G (16ch tile), P = X (1ch plane); 1: S = X (16ch plane), P = G (1ch tile)
-  int SR, SC, SCV;          // S rows, cols (multiple of 8), valid cols
-  int PRR, PWC, RW;         // P rows, window starts per row, raw row width
-  int s_ok, s_ol, p_ok, p_ol;  // origins relative to the tile corner (k0, l0)
-};
-
-template <int KS>
-__global__ __launch_bounds__(256, 2) void wgrad1_kernel(const bf16* __restrict__ S16, const bf16* __restrict__ P1,
-                                                        float* __restrict__ part, W1Geom q) {
-  constexpr int P = KS / 2;
-  constexpr int NT = KS * KS;
-  constexpr int NTM = (NT + 15) / 16;
-  constexpr int MAXS = 8;   // S chunks per thread (<= 2048)
-  constexpr int MAXE = 8;   // P raw elements per thread (<= 2048)
-  const WGeom& g = q.w;
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sreg = smem;                                   // (SR+1) x SC x 32 B
-  char* win = sreg + (q.SR + 1) * q.SC * 32;           // (PRR+1) x PWC x 16 B
-  char* raw = win + (q.PRR + 1) * q.PWC * 16;          // (PRR+1) x RW x 2 B
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int dd = lb % NT, grp = lb / NT;
-  const int di = dd / KS, dj = dd % KS;
-
-  f32x4 acc[NTM];
-#pragma unroll
-  for (int m = 0; m < NTM; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int it_lo = grp * g.ipg, it_hi = min(g.nitems, it_lo + g.ipg);
-  const int nchs = (q.SR + 1) * q.SC * 2;
-  const int nraw = (q.PRR + 1) * q.RW;
-  const int nwin = (q.PRR + 1) * q.PWC;
-  const int segs = q.SC >> 3;
-  const int nrun = q.SR * segs;
-  const int nchk = (nrun + 3) >> 2;
-
-  auto valid_item = [&](int it, Item& r) {
-    r = decode_item(g, it);
-    int ii = r.i + di - P, jj = r.j + dj - P;
-    return ii >= 0 && ii < g.I && jj >= 0 && jj < g.J;
-  };
-  u32x4 rs[MAXS];
-  bf16 rp[MAXE];
-  auto load = [&](const Item& r) {
-    // plane of the "shifted" operand is (i+di-P, j+dj-P); of the tile operand (i, j)
-    const int si = q.mode == 0 ? r.i : r.i + di - P, sj = q.mode == 0 ? r.j : r.j + dj - P;
-    const int pi = q.mode == 0 ? r.i + di - P : r.i, pj = q.mode == 0 ? r.j + dj - P : r.j;
-    const bf16* sp = S16 + plane_off(g, r.v, si, sj, 16);
-    const bf16* ppt = P1 + plane_off(g, r.v, pi, pj, 1);
-    // valid boxes: the tile operand is restricted to the output tile
-    const int tk_hi = min(g.K, r.k0 + g.TK), tl_hi = min(g.L, r.l0 + g.TL);
-    const int s_klo = q.mode == 0 ? r.k0 : 0, s_khi = q.mode == 0 ? tk_hi : g.K;
-    const int s_llo = q.mode == 0 ? r.l0 : 0, s_lhi = q.mode == 0 ? tl_hi : g.L;
-    const int p_klo = q.mode == 1 ? r.k0 : 0, p_khi = q.mode == 1 ? tk_hi : g.K;
-    const int p_llo = q.mode == 1 ? r.l0 : 0, p_lhi = q.mode == 1 ? tl_hi : g.L;
-#pragma unroll
-    for (int m = 0; m < MAXS; ++m) {
-      int c = threadIdx.x + m * 256;
-      u32x4 val = {0u, 0u, 0u, 0u};
-      if (c < nchs) {
-        int pos = c >> 1, h = c & 1;
-        int row = pos / q.SC, col = pos - row * q.SC;
-        int kg = r.k0 + q.s_ok + row, lg = r.l0 + q.s_ol + col;
-        if (row < q.SR && col < q.SCV && kg >= s_klo && kg < s_khi && lg >= s_llo && lg < s_lhi)
-          val = *(const u32x4*)(sp + ((size_t)(kg * g.L + lg) * 16 + h * 8));
-      }
-      rs[m] = val;
-    }
-#pragma unroll
-    for (int m = 0; m < MAXE; ++m) {
-      int e = threadIdx.x + m * 256;
-      bf16 val = f2bf(0.f);
-      if (e < nraw) {
-        int row = e / q.RW, col = e - row * q.RW;
-        int kg = r.k0 + q.p_ok + row, lg = r.l0 + q.p_ol + col;
-        if (row < q.PRR && kg >= p_klo && kg < p_khi && lg >= p_llo && lg < p_lhi) val = ppt[(size_t)kg * g.L + lg];
-      }
-      rp[m] = val;
-    }
-  };
-  auto store = [&]() {
-#pragma unroll
-    for (int m = 0; m < MAXS; ++m) {
-      int c = threadIdx.x + m * 256;
-      if (c < nchs) *(u32x4*)(sreg + c * 16) = rs[m];
-    }
-#pragma unroll
-    for (int m = 0; m < MAXE; ++m) {
-      int e = threadIdx.x + m * 256;
-      if (e < nraw) ((bf16*)raw)[e] = rp[m];
-    }
-  };
-  auto build = [&]() {
-    for (int w = threadIdx.x; w < nwin; w += 256) {
-      int row = w / q.PWC, c = w - row * q.PWC;
-      const bf16* src = (const bf16*)raw + row * q.RW + c;
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = src[e];
-      *(bf16x8*)(win + w * 16) = o;
-    }
-  };
-
-  // per-lane tap offsets (column = tap)
-  int tdk[NTM], tdl[NTM];
-#pragma unroll
-  for (int m = 0; m < NTM; ++m) {
-    int tap = min(16 * m + (lane & 15), NT - 1);
-    tdk[m] = tap / KS; tdl[m] = tap - tdk[m] * KS;
-  }
-
-  int cur = it_lo;
-  Item rcur;
-  while (cur < it_hi && !valid_item(cur, rcur)) ++cur;
-  if (cur < it_hi) { load(rcur); store(); }
-  __syncthreads();
-  if (cur < it_hi) build();
-  __syncthreads();
-
-  const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-  while (cur < it_hi) {
-    int nxt = cur + 1;
-    Item rn;
-    while (nxt < it_hi && !valid_item(nxt, rn)) ++nxt;
-    const bool more = nxt < it_hi;
-    if (more) load(rn);
-
-    for (int ch = wave; ch < nchk; ch += 4) {
-      int run = ch * 4 + gq;
-      int row = q.SR, seg = 0;       // padding runs read the zero row
-      if (run < nrun) { row = run / segs; seg = run - row * segs; }
-      const uint32_t sbase = (uint32_t)((row * q.SC + seg * 8 + qq) * 32 + pp * 8);
-      bf16x8 afr = cat8(lds_read_tr16(sreg, sbase), lds_read_tr16(sreg, sbase + 4 * 32));
-#pragma unroll
-      for (int m = 0; m < NTM; ++m) {
-        bf16x8 bfr = lds_read16(win, ((row + tdk[m]) * q.PWC + seg * 8 + tdl[m]) * 16);
-        acc[m] = mfma16(afr, bfr, acc[m]);
-      }
-    }
-    __syncthreads();
-    if (more) store();
-    __syncthreads();
-    if (more) build();
-    __syncthreads();
-    cur = nxt;
-    rcur = rn;
-  }
-
-  // cross-wave reduction (reuse sreg): red[wave][m][r][lane]
-  float* red = (float*)smem;
-#pragma unroll
-  for (int m = 0; m < NTM; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[((wave * NTM + m) * 4 + r) * 64 + lane] = acc[m][r];
-  __syncthreads();
-  float* pout = part + ((size_t)grp * NT + dd) * NT * 16;
-  for (int e = threadIdx.x; e < NTM * 4 * 64; e += 256) {
-    int m = e / 256, r = (e >> 6) & 3, ln = e & 63;
-    float sum = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) sum += red[((w * NTM + m) * 4 + r) * 64 + ln];
-    int tap = 16 * m + (ln & 15);
-    int c16 = 4 * (ln >> 4) + r;
-    if (tap < NT) pout[tap * 16 + c16] = sum;
-  }
 }
 
 }  // namespace ncnet
@@ -811,44 +489,38 @@ static WGeom make_wgeom(int V, int I, int J, int K, int L, int KS, int ngroups) 
   return g;
 }
 
-// part: [R][KS*KS (or KS when dj_center)][KS*KS][16 ci][16 co] fp32; partb: [R][16]
-// R = ngroups (variant 1) or 2 * ngroups (variant 2: one row per voxel-chunk half).
+#define KS_DISPATCH(M, ...) \
+  do { if (KS == 5) M(5, __VA_ARGS__); else if (KS == 3) M(3, __VA_ARGS__); \
+       else if (KS == 7) M(7, __VA_ARGS__); else if (KS == 1) M(1, __VA_ARGS__); else return -2; } while (0)
+
+// wgrad16v2.  part: [2 * ngroups][KS*KS (mode 0) or 1 (mode 2)][KS*KS][16 ci][16 co]
+// fp32 (one row per voxel-chunk half); partb: [2 * ngroups][16].
 extern "C" int ncnet_wgrad16(const void* X, const void* G, float* part, float* partb, int V, int I, int J, int K,
-                             int L, int KS, int ngroups, int dj_center, int variant, hipStream_t stream) {
+                             int L, int KS, int ngroups, int dj_center, hipStream_t stream) {
   WGeom g = make_wgeom(V, I, J, K, L, KS, ngroups);
+  if (dj_center != 0 && dj_center != 2) return -3;
   g.dj_center = dj_center;
   int nv32 = (g.TK * g.TL + 31) & ~31;
-  size_t lds = (size_t)g.PR * g.RS * 32 + (size_t)nv32 * 32 + (size_t)nv32 * 4;
-  dim3 grid((unsigned)((dj_center == 2 ? 1 : (dj_center ? KS : KS * KS)) * ngroups));
+  dim3 grid((unsigned)((dj_center == 2 ? 1 : KS * KS) * ngroups));
   const bf16* x = (const bf16*)X; const bf16* gg = (const bf16*)G;
-  if (dj_center == 2 && variant != 2) return -3;   // plane-only mode: v2 kernel
-  if (variant == 2) {
-    if (g.RW > 32 || g.TL > 32) return -1;   // one wave-instruction per staged row
-    // row stride TL + 8: a row wrap inside an 8-voxel read group jumps 256 B
-    // (bank period), keeping the transposed reads conflict-free
-    g.RS = g.TL + ((KS - 1 + 7) / 8) * 8;
-    if (g.PR * g.RS * 32 > 65535) return -1;  // 16-bit voxel offset table
-    lds = (size_t)g.PR * g.RS * 32 + (size_t)nv32 * 32 + (size_t)nv32 * 2;
-    dim3 block(512);
-    if (KS == 5) hipLaunchKernelGGL((wgrad16v2_kernel<5>), grid, block, lds, stream, x, gg, part, partb, g);
-    else if (KS == 3) hipLaunchKernelGGL((wgrad16v2_kernel<3>), grid, block, lds, stream, x, gg, part, partb, g);
-    else return -2;
-    return (int)hipGetLastError();
-  }
-  if (g.PR * g.RS * 2 > 8 * 256) return -1;
-  if (nv32 * 2 > 5 * 256) return -1;
-  dim3 block(256);
-  if (KS == 5) hipLaunchKernelGGL((wgrad16_kernel<5>), grid, block, lds, stream, x, gg, part, partb, g);
-  else if (KS == 3) hipLaunchKernelGGL((wgrad16_kernel<3>), grid, block, lds, stream, x, gg, part, partb, g);
-  else return -2;
+  if (g.RW > 32 || g.TL > 32) return -1;   // one wave-instruction per staged row
+  // row stride TL + 8: a row wrap inside an 8-voxel read group jumps 256 B
+  // (bank period), keeping the transposed reads conflict-free
+  g.RS = g.TL + ((KS - 1 + 7) / 8) * 8;
+  if (g.PR * g.RS * 32 > 65535) return -1;  // 16-bit voxel offset table
+  size_t lds = (size_t)g.PR * g.RS * 32 + (size_t)nv32 * 32 + (size_t)nv32 * 2;
+  dim3 block(512);
+#define WG2(KSV, _) hipLaunchKernelGGL((wgrad16v2_kernel<KSV>), grid, block, lds, stream, x, gg, part, partb, g)
+  KS_DISPATCH(WG2, 0);
+#undef WG2
   return (int)hipGetLastError();
 }
 
-// v3: ngroups column groups per dj (grid = ngroups * (dj_center ? 1 : KS)).
+// v3: ngroups column groups per dj (grid = ngroups * KS).
 // Tile rule (mirrored in ops/neigh_consensus.py wgrad_v3_groups):
 // ntl = ceil(K*L / 320), VT = roundup(ceil(K*L / ntl), 64).
 extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float* partb, int V, int I, int J, int K,
-                               int L, int KS, int ngroups, int dj_center, hipStream_t stream) {
+                               int L, int KS, int ngroups, hipStream_t stream) {
   W3Geom g;
   g.V = V; g.I = I; g.J = J; g.K = K; g.L = L;
   const int KL = K * L;
@@ -859,7 +531,6 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
   g.PR = (g.VT - 1) / L + 2 + KS - 1;
   g.ncols = V * J * g.ntl;
   g.cpg = cdiv(g.ncols, ngroups);
-  g.dj_center = dj_center;
   {
     const char* e = getenv("NCNET_WGRAD_FLAGS");   // read per launch: tests / kbench switch it in-process
     g.flags = e ? atoi(e) : 0;
@@ -868,42 +539,10 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
   if (g.VT > 384) return -1;                // <= 6 chunks per half
   size_t lds = 2 * (size_t)g.PR * g.RS * 32 + (size_t)(KS + 2) * g.VT * 32;
   if (lds > 160 * 1024) return -1;
-  dim3 grid((unsigned)((dj_center ? 1 : KS) * ngroups)), block(512);
+  dim3 grid((unsigned)(KS * ngroups)), block(512);
   const bf16* x = (const bf16*)X; const bf16* gg = (const bf16*)G;
   if (KS == 5) hipLaunchKernelGGL((wgrad16v3_kernel<5>), grid, block, lds, stream, x, gg, part, partb, g);
   else if (KS == 3) hipLaunchKernelGGL((wgrad16v3_kernel<3>), grid, block, lds, stream, x, gg, part, partb, g);
-  else return -2;
-  return (int)hipGetLastError();
-}
-
-// mode 0: S16 = G (grad of a Cin=1 -> 16 conv, 16ch), P1 = X (1ch input)   -> part[grp][dd][tap][co]
-// mode 1: S16 = X (16ch input of a 16 -> 1 conv),   P1 = G (1ch grad)      -> part[grp][dd][flipped tap][ci]
-extern "C" int ncnet_wgrad1(const void* S16, const void* P1, float* part, int V, int I, int J, int K, int L, int KS,
-                            int mode, int ngroups, hipStream_t stream) {
-  W1Geom q;
-  q.w = make_wgeom(V, I, J, K, L, KS, ngroups);
-  const int TK = q.w.TK, TL = q.w.TL, P = KS / 2;
-  q.mode = mode;
-  if (mode == 0) {
-    q.SR = TK; q.SCV = TL; q.s_ok = 0; q.s_ol = 0;
-    q.p_ok = -P; q.p_ol = -P;
-  } else {
-    q.SR = TK + KS - 1; q.SCV = TL + KS - 1; q.s_ok = -P; q.s_ol = -P;
-    q.p_ok = -(KS - 1); q.p_ol = -(KS - 1);
-  }
-  q.SC = (q.SCV + 7) & ~7;
-  q.PRR = q.SR + KS - 1;
-  q.PWC = q.SC + KS - 1;
-  q.RW = q.PWC + 8;
-  if ((q.SR + 1) * q.SC * 2 > 8 * 256) return -1;
-  if ((q.PRR + 1) * q.RW > 8 * 256) return -1;
-  size_t lds = (size_t)(q.SR + 1) * q.SC * 32 + (size_t)(q.PRR + 1) * q.PWC * 16 + (size_t)(q.PRR + 1) * q.RW * 2;
-  const int NTM = (KS * KS + 15) / 16;
-  size_t red = (size_t)4 * NTM * 4 * 64 * 4;
-  if (lds < red) lds = red;
-  dim3 grid((unsigned)(KS * KS * ngroups)), block(256);
-  if (KS == 5) hipLaunchKernelGGL((wgrad1_kernel<5>), grid, block, lds, stream, (const bf16*)S16, (const bf16*)P1, part, q);
-  else if (KS == 3) hipLaunchKernelGGL((wgrad1_kernel<3>), grid, block, lds, stream, (const bf16*)S16, (const bf16*)P1, part, q);
   else return -2;
   return (int)hipGetLastError();
 }

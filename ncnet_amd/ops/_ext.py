@@ -10,6 +10,7 @@ Dispatch policy (used by every op in ``ncnet_amd.ops``):
 """
 from __future__ import annotations
 
+import collections
 import os
 
 import torch
@@ -59,3 +60,22 @@ def ext():
     if m is None:
         raise RuntimeError(f"ncnet_amd HIP extension unavailable: {_ERR!r}")
     return m
+
+
+# Which implementation each NC-Net op dispatched to, per process (tests and
+# bench.py read it: a GPU run must show HIP paths, never "torch_fallback").
+DISPATCH: collections.Counter = collections.Counter()
+
+
+def count(path: str) -> None:
+    DISPATCH[path] += 1
+
+
+def torch_fallback(what: str) -> None:
+    """Called before a GPU op would run a PyTorch oracle instead of a HIP
+    kernel: raises unless NCNET_ALLOW_TORCH_FALLBACK=1 (no silent fallbacks)."""
+    if not fallback_allowed():
+        raise NotImplementedError(
+            f"{what}: no HIP kernel for this configuration on the GPU; set NCNET_ALLOW_TORCH_FALLBACK=1 "
+            "to run the PyTorch reference path instead")
+    count("torch_fallback")

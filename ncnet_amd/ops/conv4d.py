@@ -9,8 +9,10 @@ on ``nn.Module`` directly -- the reference's ``_ConvNd`` subclass no longer
 constructs on modern torch.
 
 On GPU the op runs the HIP implicit-GEMM kernels (forward, data gradient,
-weight gradient); in the NC-Net model the fused stack in
-``neigh_consensus.py`` is used instead of per-layer calls.
+weight gradient) through ``neigh_consensus.conv_layer`` -- the same
+channel-blocked / ij-encoded layer path as the NC stack, so any channel
+counts work; in the NC-Net model the fused stack in ``neigh_consensus.py``
+is used instead of per-layer calls.
 """
 from __future__ import annotations
 
@@ -21,89 +23,64 @@ import torch.nn as nn
 
 from . import _ext
 from . import reference as ref
-from .neigh_consensus import _reduce_wgrad1, _reduce_wgrad16, wgrad16_partials, wgrad_groups
-from .packing import pack_w16, pack_w1in, pack_w1out, transpose_for_dgrad
+from .neigh_consensus import HIP_KS, _layer_wgrad, blocks_to_ncl, conv_layer, planar_to_blocks
+from .packing import ij_groups, transpose_for_dgrad
 
 
-def _to_cl(x: torch.Tensor, c16: bool) -> torch.Tensor:
-    """[N, C, I, J, K, L] -> channels-last bf16 ([N,I,J,K,L] if 1ch else padded to 16)."""
-    n, c = x.shape[:2]
-    if not c16:
+def _kind(cin: int, cout: int) -> str:
+    return "11" if cin == 1 and cout == 1 else "1in" if cin == 1 else "1out" if cout == 1 else "16"
+
+
+def _to_repr(x: torch.Tensor, c: int) -> torch.Tensor:
+    """[N, C, I, J, K, L] -> the HIP layer representation: bf16 [N,I,J,K,L] (C = 1)
+    or bf16 channels-last blocks [NB, N, I, J, K, L, 16]."""
+    if c == 1:
         return x[:, 0].to(torch.bfloat16).contiguous()
-    y = x.permute(0, 2, 3, 4, 5, 1)
-    if c < 16:
-        y = torch.nn.functional.pad(y, (0, 16 - c))
-    return y.to(torch.bfloat16).contiguous()
+    return planar_to_blocks(x.float().transpose(0, 1))
 
 
-def _from_cl(y: torch.Tensor, c: int) -> torch.Tensor:
-    if y.dim() == 5:
-        return y.unsqueeze(1)
-    return y[..., :c].permute(0, 5, 1, 2, 3, 4)
-
-
-def _conv_cl(xcl: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, mask=None) -> torch.Tensor:
-    """Channels-last conv without bias; returns fp32/bf16 channels-last."""
-    C = _ext.ext()
-    ks = w_std.shape[-1]
-    shp = xcl.shape[:5]
-    if cin == 1:
-        y = torch.empty(tuple(shp) + (16,), dtype=torch.bfloat16, device=xcl.device)
-        C.conv1in_fwd(xcl, pack_w1in(w_std), None, mask, y, ks, 2 if mask is not None else 0)
-    elif cout == 1:
-        y = torch.empty(tuple(shp), dtype=torch.float32, device=xcl.device)
-        C.conv1out_fwd(xcl, pack_w1out(w_std), None, y, ks, 0)
-    else:
-        y = torch.empty(tuple(shp) + (16,), dtype=torch.bfloat16, device=xcl.device)
-        C.conv16_fwd(xcl, pack_w16(w_std), None, mask, y, ks, 2 if mask is not None else 0, 0)
-    return y
+def _from_out(y: torch.Tensor, c: int) -> torch.Tensor:
+    """conv_layer f32 output -> [N, C, I, J, K, L]."""
+    return y.unsqueeze(1) if c == 1 else y.transpose(0, 1)
 
 
 def hip_supported(cin: int, cout: int, ks: int) -> bool:
-    return ks in (3, 5) and cin <= 16 and cout <= 16 and not (cin == 1 and cout == 1)
+    return ks in HIP_KS and cin >= 1 and cout >= 1
 
 
 class Conv4dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_ref, bias):
-        n, cin = x.shape[:2]
-        cout = w_ref.shape[1]
+        cin, cout = x.shape[1], w_ref.shape[1]
         w_std = ref.conv4d_weight_to_std(w_ref).float()
-        xcl = _to_cl(x, cin > 1)
-        y = _conv_cl(xcl, w_std, cin, cout)
-        out = _from_cl(y, cout).float()
-        if bias is not None:
-            out = out + bias.float().view(1, -1, 1, 1, 1, 1)
-        ctx.save_for_backward(xcl, w_ref)
+        h = _to_repr(x, cin)
+        y = _from_out(conv_layer(h, w_std, cin, cout, bias=bias, relu=False, f32=True), cout)
+        ctx.save_for_backward(h, w_ref)
         ctx.meta = (cin, cout, bias is not None, x.dtype)
-        return out.contiguous().to(x.dtype)
+        return y.contiguous().to(x.dtype)
 
     @staticmethod
     def backward(ctx, g):
-        xcl, w_ref = ctx.saved_tensors
+        h, w_ref = ctx.saved_tensors
         cin, cout, has_bias, dt = ctx.meta
         C = _ext.ext()
         ks = w_ref.shape[0]
         w_std = ref.conv4d_weight_to_std(w_ref).float()
-        gcl = _to_cl(g.float(), cout > 1)
-        V, I, J, K, L = xcl.shape[:5]
-        ng = wgrad_groups(ks, V * I * J * ((K + 24) // 25) * ((L + 24) // 25))
+        gr = _to_repr(g, cout)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            wt = transpose_for_dgrad(w_std)
-            gx = _from_cl(_conv_cl(gcl, wt, cout, cin), cin).float().to(dt)
+            gx = _from_out(conv_layer(gr, transpose_for_dgrad(w_std), cout, cin, relu=False, f32=True), cin).to(dt)
         if ctx.needs_input_grad[1]:
+            kind = _kind(cin, cout)
+            xin = h
             if cin == 1:
-                part = torch.empty((ng, ks * ks, ks * ks, 16), dtype=torch.float32, device=g.device)
-                C.wgrad1(gcl, xcl, part, ks, 0, ng)
-                dw = _reduce_wgrad1(part, ks, 0, cout)
-            elif cout == 1:
-                part = torch.empty((ng, ks * ks, ks * ks, 16), dtype=torch.float32, device=g.device)
-                C.wgrad1(xcl, gcl, part, ks, 1, ng)
-                dw = _reduce_wgrad1(part, ks, 1, cin)
-            else:
-                sw, _ = wgrad16_partials(C, xcl, gcl, ks, ng, False)
-                dw = _reduce_wgrad16(sw, ks, cout, cin)
+                xin = torch.empty((ij_groups(ks),) + tuple(h.shape) + (16,), dtype=torch.bfloat16, device=h.device)
+                C.ijpack(h, xin, ks, 1)
+            gs = None
+            if kind == "1out":
+                gs = torch.empty((ij_groups(ks),) + tuple(gr.shape) + (16,), dtype=torch.bfloat16, device=h.device)
+                C.ijpack(gr, gs, ks, -1)
+            dw, _ = _layer_wgrad(C, kind, xin, gr, gs, ks, cin, cout)
             gw = ref.conv4d_weight_from_std(dw).to(w_ref.dtype)
         if has_bias and ctx.needs_input_grad[2]:
             gb = g.float().sum(dim=(0, 2, 3, 4, 5))
@@ -115,11 +92,16 @@ def conv4d(data: torch.Tensor, filters: torch.Tensor, bias=None, permute_filters
     """"Same"-padded 4D conv.  ``filters`` is ``[out, in, k, k, k, k]`` when
     ``permute_filters`` (as in lib/conv4d.py:16-17), else pre-permuted
     ``[k, out, in, k, k, k]``.  ``use_half`` is accepted for API parity; the
-    GPU path always computes in bf16 with fp32 accumulation."""
+    GPU path always computes in bf16 with fp32 accumulation (any channel
+    counts, kernel sizes 1/3/5/7; others raise unless
+    NCNET_ALLOW_TORCH_FALLBACK=1)."""
     w_ref = ref.conv4d_weight_from_std(filters) if permute_filters else filters
     cin, cout, ks = w_ref.shape[2], w_ref.shape[1], w_ref.shape[0]
-    if _ext.use_hip(data) and hip_supported(cin, cout, ks):
-        return Conv4dFn.apply(data, w_ref, bias)
+    if _ext.use_hip(data):
+        if hip_supported(cin, cout, ks):
+            _ext.count("conv4d_hip")
+            return Conv4dFn.apply(data, w_ref, bias)
+        _ext.torch_fallback(f"Conv4d kernel size {ks}")
     return ref.conv4d(data, w_ref.to(data.dtype), None if bias is None else bias.to(data.dtype))
 
 

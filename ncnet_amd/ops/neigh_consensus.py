@@ -10,100 +10,118 @@ MI355X design:
   batch of volumes for every Conv4d launch: the swapped branch is built once
   as a bf16 transposed copy of the 1-channel input (0.8 MB per volume) instead
   of permuting the 16-channel activations;
-* hidden activations are channels-last bf16 ``[V, I, J, K, L, 16]``; channel
-  counts below 16 are zero-padded (zero weights and bias keep them at 0);
+* hidden activations are channels-last bf16 blocks of 16 channels
+  ``[NB, V, I, J, K, L, 16]``; channel counts that are not a multiple of 16
+  are zero-padded (zero weights and bias keep them at 0);
+* every layer runs on the conv16 MFMA kernels (csrc/conv4d_fwd.hip): 16-channel
+  blocks directly (one call per output block; input blocks beyond the first
+  are summed as fp32 partials), 1-channel operands through the ij encoding
+  (csrc/jshift.hip: the (di, dj) plane offsets move into the channel axis);
+  kernel sizes 1, 3, 5, 7 (reference: any size, lib/conv4d.py:58-82);
 * bias + ReLU are fused into each conv's epilogue; the backward runs the
   data-gradient convs with the previous layer's ReLU mask fused into their
-  epilogue, and the weight gradients with the MFMA wgrad kernels;
+  epilogue, and the weight gradients with the MFMA wgrad kernels (16 -> 16
+  layers and Cout=1 layers on a side HIP stream, overlapped with the
+  data-gradient chain);
 * ``y = z1 + z2^T`` (the branch un-swap) and, in backward, its transpose plus
   the last layer's ReLU mask are single tiled kernels.
+There is no silent PyTorch fallback on the GPU: a configuration without HIP
+kernels (even kernel sizes) raises unless NCNET_ALLOW_TORCH_FALLBACK=1.
 """
 from __future__ import annotations
 
 import functools
+import os as _os
 
 import numpy as np
 import torch
 
 from . import _ext
 from . import reference as ref
-from .packing import (ij_groups, ij_in_grad, ij_in_weights, ij_out_grad, ij_out_weights, jc_in_grad, jc_in_weights,
-                      jc_out_grad, jc_out_weights, kl_dgrad_in_weights, pack_kl_in, pack_kl_out, pack_w16,
-                      pack_w16_planes, pack_w1in, pack_w1out, plane_dgrad_weights, transpose_for_dgrad)
+from .packing import (ij_groups, ij_in_grad, ij_in_weights, ij_out_grad, ij_out_weights, pack_w16, pack_w16_planes,
+                      plane_dgrad_weights, transpose_for_dgrad)
 
-HIP_KS = (3, 5)
-# 1-channel layers through the j-offset channel encoding (csrc/jshift.hip) on
-# the conv16 / wgrad16 kernels; NCNET_NC_JC=0 selects the dedicated
-# 1-channel kernels (conv1in / conv1out / wgrad1) instead.
-import os as _os
-
-# Encoding of the 1-channel layers: "ij" (default: both plane offsets in
-# channels, conv16 group-plane mode), "kl" (forward and data-gradient convs on
-# the conv4d_kl.hip kernels, which resolve the in-plane (dk, dl) shifts in LDS
-# -- no shifted copies or channel-planar partials in HBM; the weight gradients
-# stay on the ij encoding; measured slower than ij at the 25^4 training shape:
-# 37.1 vs 31.3 ms/step), "jc" (dj only), "direct" (conv1in / conv1out / wgrad1
-# kernels).  NCNET_NC_JC=0 is the legacy spelling of "direct".
-ENC = _os.environ.get("NCNET_NC_ENC", "ij")
-if _os.environ.get("NCNET_NC_JC") == "0":
-    ENC = "direct"
-USE_JC = ENC == "jc"
-USE_IJ = ENC in ("ij", "ijfull", "kl")
-USE_KL = ENC == "kl"
-# "ij" keeps the Cout=1 layer's forward and data gradient on the j encoding
-# (one conv pass with an 8-channel fp32 output beats two group-plane passes
-# with 16-channel planar outputs at 25^4: measured 1.97 vs 2.56 ms fwd) and
-# uses the ij encoding for its weight gradient (plane-only wgrad, 1.5 vs
-# 1.8 ms); "ijfull" runs that layer entirely on the ij encoding.  At KS = 3
-# the ij encoding has a single group (one pass over one plane instead of 3
-# planes), so it is used there in all modes.
+HIP_KS = (1, 3, 5, 7)
 
 
-def _out_ij_fwd(ks: int) -> bool:
-    return ENC == "ijfull" or (ENC == "ij" and ks * ks <= 16)
-
-
-# The Cout=1 layer's data gradient on the ij encoding: the group-plane conv
-# reads ijpack(g, -1), which the weight gradient has already built, and
-# writes the 16-channel masked gradient directly (no planar fp32 partials), so
-# it replaces jpack + a KS-plane jc pass.  NCNET_NC_OUT_DGRAD=jc reverts.
-OUT_DGRAD = _os.environ.get("NCNET_NC_OUT_DGRAD", "ij")
-
-
-def _out_ij_dgrad(ks: int) -> bool:
-    return _out_ij_fwd(ks) or (USE_IJ and OUT_DGRAD == "ij")
-# wgrad16 kernel: 3 = sliding G-plane ring (default), 2 = 8-wave LDS-DMA per
-# (di, dj) plane, 1 = 4-wave register-staged
-WGRAD_VARIANT = int(_os.environ.get("NCNET_WGRAD_VARIANT", "3"))
+def nblocks(c: int) -> int:
+    return (c + 15) // 16
 
 
 def layer_kinds(channels, kernel_sizes):
-    """Kernel family per layer or None if the stack needs the torch path."""
-    kinds = []
-    cin = 1
-    for idx, (c, k) in enumerate(zip(channels, kernel_sizes)):
-        if k not in HIP_KS or c > 16 or cin > 16:
+    """Per layer ``"1in"`` (Cin=1 -> Cout>1), ``"16"`` (Cin>1 -> Cout>1),
+    ``"1out"`` (Cin>1 -> Cout=1) or ``"11"`` (1 -> 1); None if some kernel
+    size has no HIP kernel (only odd sizes 1..7 do)."""
+    kinds, cin = [], 1
+    for c, k in zip(channels, kernel_sizes):
+        if k not in HIP_KS or c < 1:
             return None
-        if cin == 1 and (c == 1 or idx > 0):
-            return None
-        if cin == 1:
-            kinds.append("1in")
-        elif c == 1:
-            kinds.append("1out")
-        else:
-            kinds.append("16")
+        kinds.append("11" if cin == 1 and c == 1 else "1in" if cin == 1 else "1out" if c == 1 else "16")
         cin = c
-    if not kinds or kinds[-1] != "1out":
-        return None
     return kinds
 
 
-def wgrad_groups(ks: int, nitems: int) -> int:
-    """Number of K-split groups of the wgrad kernels (~3000 workgroups for the
-    KS*KS plane offsets; measured on MI355X: 120 groups at KS=5 beat 20 by 1.4x)."""
+def wgrad_v3_ok(shape, ks: int) -> bool:
+    """wgrad16v3 (sliding G ring): KS 3/5, full-width X rows L + ks - 1 <= 32."""
+    return ks in (3, 5) and shape[4] + ks - 1 <= 32
+
+
+def wgrad_v3_groups(shape, ks: int) -> int:
+    """Column groups per dj for wgrad16v3: ~2 workgroups per CU, never more
+    than the columns (v, j, tile).  Tile rule mirrors ncnet_wgrad16v3."""
+    V, I, J, K, L = shape[:5]
+    ntl = -(-(K * L) // 320)
+    ncols = V * J * ntl
+    target = max(1, 512 // ks)
     env = _os.environ.get("NCNET_WGRAD_GROUPS")
-    target = int(env) if env else 3072 // (ks * ks)
+    if env:
+        target = int(env)
+    return max(1, min(target, ncols))
+
+
+def wgrad_groups(ks: int, nitems: int) -> int:
+    """K-split groups of wgrad16v2 in full mode (~3000 workgroups over the
+    KS*KS plane offsets; 120 groups at KS=5 beat 20 by 1.4x on MI355X)."""
+    env = _os.environ.get("NCNET_WGRAD_GROUPS")
+    target = int(env) if env else max(1, 3072 // (ks * ks))
     return max(1, min(target, nitems))
+
+
+def wgrad_plane_groups(nitems: int) -> int:
+    """Groups of the plane-only wgrad (grid = groups): ~3 workgroups per CU."""
+    env = _os.environ.get("NCNET_WGRAD_PLANE_GROUPS")
+    return max(1, min(int(env) if env else 768, nitems))
+
+
+def _nitems(shape) -> int:
+    V, I, J, K, L = shape[:5]
+    return V * I * J * ((K + 24) // 25) * ((L + 24) // 25)
+
+
+def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, plane_only: bool):
+    """Weight-gradient partials of a 16 -> 16 block and their reduction.
+
+    ``plane_only`` False: all (di, dj) plane offsets (wgrad16v3 when it fits,
+    else wgrad16v2); True: the (P, P) plane only (ij-encoded 1-channel layers,
+    wgrad16v2).  Returns (s, sb): s [dd, tap, ci, co], sb [16] = sum of g16
+    over all voxels (bias gradient, the kernels' ones-MFMA)."""
+    shape = x16.shape[:5]
+    if plane_only:
+        variant, ng = 2, wgrad_plane_groups(_nitems(shape))
+    elif wgrad_v3_ok(shape, ks):
+        variant, ng = 3, wgrad_v3_groups(shape, ks)
+    else:
+        variant, ng = 2, wgrad_groups(ks, _nitems(shape))
+    ndd = 1 if plane_only else ks * ks
+    part = torch.empty((2 * ng, ndd, ks * ks, 16, 16), dtype=torch.float32, device=x16.device)
+    partb = torch.empty((2 * ng, 16), dtype=torch.float32, device=x16.device)
+    C.wgrad16(x16, g16, part, partb, ks, 2 if plane_only else 0, variant)
+    return part.sum(0), partb.sum(0)
+
+
+def _reduce_wgrad16(s: torch.Tensor, ks: int, cout: int, cin: int) -> torch.Tensor:
+    # s [dd, tap, ci, co] -> std [co, ci, di, dj, dk, dl]
+    return s.permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks, ks)[:cout, :cin]
 
 
 def _std(w_ref: torch.Tensor) -> torch.Tensor:
@@ -119,145 +137,159 @@ def _pad_bias(b: torch.Tensor, n: int) -> torch.Tensor:
     return out
 
 
+def _blk(t: torch.Tensor, a: int, n: int) -> slice:
+    return slice(16 * a, min(n, 16 * a + 16))
+
+
+def planar_to_blocks(z: torch.Tensor) -> torch.Tensor:
+    """fp32 planar [C, V, I, J, K, L] -> bf16 channels-last blocks [NB, V, I, J, K, L, 16]."""
+    c = z.shape[0]
+    nb = nblocks(c)
+    if c < 16 * nb:
+        z = torch.cat((z, z.new_zeros((16 * nb - c,) + tuple(z.shape[1:]))))
+    return z.view((nb, 16) + tuple(z.shape[1:])).permute(0, 2, 3, 4, 5, 6, 1).to(torch.bfloat16).contiguous()
+
+
+def blocks_to_ncl(h: torch.Tensor, c: int) -> torch.Tensor:
+    """bf16 blocks [NB, V, I, J, K, L, 16] -> [V, C, I, J, K, L] (a view-based permute)."""
+    nb = h.shape[0]
+    x = h.permute(1, 0, 6, 2, 3, 4, 5).reshape((h.shape[1], nb * 16) + tuple(h.shape[2:6]))
+    return x[:, :c]
+
+
+def _ij_in_planes(w_std: torch.Tensor) -> torch.Tensor:
+    """[co<=16, 1, k^4] -> group-plane weights [G, nq, 64, 8]."""
+    return pack_w16_planes(ij_in_weights(w_std))
+
+
+def _ij_out_planes(w_std: torch.Tensor, nbi: int) -> torch.Tensor:
+    """[1, ci, k^4] -> [G, nbi, nq, 64, 8]: combo group g, input block a."""
+    per = [pack_w16_planes(ij_out_weights(w_std[:, 16 * a:16 * a + 16])) for a in range(nbi)]
+    return torch.stack(per, 1).contiguous()
+
+
+def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=None, relu: bool = True,
+               mask=None, f32: bool = False, xs=None) -> torch.Tensor:
+    """One "same" Conv4d on the HIP kernels, any channel counts.
+
+    h: the 1-channel input [V,I,J,K,L] (bf16/fp32) when cin == 1, else bf16
+    blocks [NBi, V,I,J,K,L,16]; ``xs``: ijpack(h, +1) if already built.
+    Output (pre-activation + bias, then ReLU if ``relu``; or * (mask > 0)):
+      f32=False: bf16 blocks [NBo, ...,16] (cout > 1) / fp32 [V,I,J,K,L] (cout == 1)
+      f32=True : fp32 planar [cout, V,I,J,K,L] (cout > 1) / fp32 [V,I,J,K,L].
+    ``mask`` (bf16 blocks like the output, cout > 1, f32=False only) replaces
+    bias/ReLU by the data-gradient epilogue y = acc * (mask > 0)."""
+    C = _ext.ext()
+    ks = w_std.shape[-1]
+    shp = tuple(h.shape[:5]) if cin == 1 else tuple(h.shape[1:6])
+    dev = h.device
+    nbo, nbi = nblocks(cout), nblocks(cin)
+    if cin == 1:
+        if xs is None:
+            xs = torch.empty((ij_groups(ks),) + shp + (16,), dtype=torch.bfloat16, device=dev)
+            C.ijpack(h.contiguous(), xs, ks, 1)
+        if cout == 1:                      # 1 -> 1: one output channel of the group-plane conv
+            z = torch.empty((1,) + shp, dtype=torch.float32, device=dev)
+            C.conv16_fwd(xs, _ij_in_planes(w_std), None, None, z, ks, 4)
+            y = z[0]
+            if bias is not None:
+                y = y + bias.float().view(1)
+            return torch.relu(y) if relu else y
+        outs = []
+        for b in range(nbo):
+            wb = _ij_in_planes(w_std[_blk(w_std, b, cout)])
+            outs.append(_epilogue_call(C, xs, wb, bias, b, cout, relu, mask, f32, shp, ks))
+        return _gather(outs, f32, cout)
+    if cout == 1:                          # ij encoding: combo-planar partials, shift-summed by ijsum
+        G, nq = ij_groups(ks), ks * ks
+        wz = _ij_out_planes(w_std, nbi)
+        z = torch.empty((nq,) + shp, dtype=torch.float32, device=dev)
+        for gi in range(G):
+            C.conv16_fwd(h, wz[gi], None, None, z[16 * gi:min(nq, 16 * gi + 16)], ks, 4)
+        y = torch.empty(shp, dtype=torch.float32, device=dev)
+        C.ijsum(z, None if bias is None else _pad_bias(bias, 1), y, ks, 1 if relu else 0, 1)
+        return y
+    if nbi == 1:
+        outs = [_epilogue_call(C, h[0], pack_w16(w_std[_blk(w_std, b, cout), :16]), bias, b, cout, relu, mask, f32,
+                               shp, ks) for b in range(nbo)]
+        return _gather(outs, f32, cout)
+    # several input blocks: fp32 partials per (out, in) block pair, summed before the activation
+    outs = []
+    for b in range(nbo):
+        sl = _blk(w_std, b, cout)
+        nco = sl.stop - sl.start
+        acc = None
+        for a in range(nbi):
+            z = torch.empty((nco,) + shp, dtype=torch.float32, device=dev)
+            C.conv16_fwd(h[a], pack_w16(w_std[sl, 16 * a:16 * a + 16]), None, None, z, ks, 4)
+            acc = z if acc is None else acc.add_(z)
+        if bias is not None and mask is None:
+            acc += bias[sl].float().view(-1, 1, 1, 1, 1, 1)
+        if mask is not None:
+            acc = acc * (blocks_to_ncl(mask[b:b + 1], nco).transpose(0, 1) > 0)
+        elif relu:
+            acc = torch.relu_(acc)
+        outs.append(acc)
+    z = torch.cat(outs) if len(outs) > 1 else outs[0]
+    return z if f32 else planar_to_blocks(z)
+
+
+def _epilogue_call(C, x, wp, bias, b, cout, relu, mask, f32, shp, ks):
+    sl = slice(16 * b, min(cout, 16 * b + 16))
+    nco = sl.stop - sl.start
+    if f32:
+        z = torch.empty((nco,) + shp, dtype=torch.float32, device=x.device)
+        C.conv16_fwd(x, wp, None, None, z, ks, 4)
+        if bias is not None:
+            z += bias[sl].float().view(-1, 1, 1, 1, 1, 1)
+        return torch.relu_(z) if relu else z
+    y = torch.empty(shp + (16,), dtype=torch.bfloat16, device=x.device)
+    if mask is not None:
+        C.conv16_fwd(x, wp, None, mask[b], y, ks, 2)
+    elif relu:
+        bb = torch.zeros(16, device=x.device) if bias is None else _pad_bias(bias[sl], 16)
+        C.conv16_fwd(x, wp, bb, None, y, ks, 1)
+    else:
+        if bias is not None:
+            raise RuntimeError("internal: bf16 output without ReLU takes no bias")
+        C.conv16_fwd(x, wp, None, None, y, ks, 0)
+    return y
+
+
+def _gather(outs, f32: bool, cout: int):
+    if f32:
+        return torch.cat(outs) if len(outs) > 1 else outs[0]
+    return torch.stack(outs) if len(outs) > 1 else outs[0].unsqueeze(0)
+
+
 def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
-    """x0: [V,I,J,K,L] bf16 -> z fp32 [V,I,J,K,L]; appends layer inputs to save."""
+    """x0: [V,I,J,K,L] bf16 -> last layer's ReLU output, fp32: [V,I,J,K,L] if it
+    has one channel, else planar [C, V,I,J,K,L].  Appends, per layer, what its
+    backward reads: the ij-packed input (1-channel inputs) or the bf16 input blocks."""
     C = _ext.ext()
     h = x0
-    V, I, J, K, L = x0.shape
-    for li, (w_ref, b, kind) in enumerate(zip(ws, bs, kinds)):
-        ks = w_ref.shape[0]
+    nl = len(kinds)
+    cin = 1
+    for li, (w_ref, b) in enumerate(zip(ws, bs)):
         w = _std(w_ref)
-        save.append(h)
-        last = li == len(kinds) - 1
-        if kind == "1in" and USE_KL:
-            # the backward ij-packs the saved 1-channel input for the weight gradient
-            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
-            C.conv1to16_kl(h, pack_kl_in(w), _pad_bias(b, 16), None, y, ks, 1)
-        elif kind == "1in" and USE_IJ:
-            xs = torch.empty((ij_groups(ks), V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
-            C.ijpack(h, xs, ks, 1)
-            save[-1] = xs  # the backward needs the ij-packed input
-            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
-            C.conv16_fwd(xs, pack_w16_planes(ij_in_weights(w)), _pad_bias(b, 16), None, y, ks, 1, 0)
-        elif kind == "1in" and USE_JC:
-            xs = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
-            C.jpack(h, xs, ks, 1)
-            save[-1] = xs  # the backward needs the j-packed input
-            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
-            C.conv16_fwd(xs, pack_w16(jc_in_weights(w)), _pad_bias(b, 16), None, y, ks, 1, 1)
-        elif kind == "1in":
-            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
-            C.conv1in_fwd(h, pack_w1in(w), _pad_bias(b, 16), None, y, ks, 1)
-        elif kind == "16":
-            y = torch.empty((V, I, J, K, L, 16), dtype=torch.bfloat16, device=x0.device)
-            C.conv16_fwd(h, pack_w16(w), _pad_bias(b, 16), None, y, ks, 1, 0)
-        elif USE_KL:   # "1out"
-            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
-            C.conv16to1_kl(h, pack_kl_out(w), _pad_bias(b, 1), y, ks, 1, 1.0)
-            if not last:
-                y = y.to(torch.bfloat16)
-        elif USE_IJ and _out_ij_fwd(ks):   # "1out"
-            G = ij_groups(ks)
-            wz = pack_w16_planes(ij_out_weights(w))
-            nq = ks * ks
-            z = torch.empty((nq, V, I, J, K, L), dtype=torch.float32, device=x0.device)   # planar by combo
-            hx = h.unsqueeze(0)
-            for gi in range(G):
-                C.conv16_fwd(hx, wz[gi:gi + 1], None, None, z[16 * gi:min(nq, 16 * gi + 16)], ks, 4, 0)
-            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
-            C.ijsum(z, _pad_bias(b, 1), y, ks, 1, 1)
-            del z
-            if not last:
-                y = y.to(torch.bfloat16)
-        elif USE_JC or USE_IJ:
-            z8 = torch.empty((ks, V, I, J, K, L), dtype=torch.float32, device=x0.device)   # planar, dj = 0..ks-1
-            C.conv16_fwd(h, pack_w16(jc_out_weights(w)), None, None, z8, ks, 3, 1)
-            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
-            C.jsum(z8, _pad_bias(b, 1), y, ks, 1, 1)
-            del z8
-            if not last:
-                y = y.to(torch.bfloat16)
+        ks, cout = w.shape[-1], w.shape[0]
+        last = li == nl - 1
+        xs = None
+        if cin == 1:
+            xs = torch.empty((ij_groups(ks),) + tuple(h.shape) + (16,), dtype=torch.bfloat16, device=h.device)
+            C.ijpack(h.contiguous(), xs, ks, 1)
+            save.append((xs, h) if li > 0 else xs)   # mid-stack 1-channel inputs also serve as ReLU masks
         else:
-            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
-            C.conv1out_fwd(h, pack_w1out(w), _pad_bias(b, 1), y, ks, 1)
-            if not last:
-                y = y.to(torch.bfloat16)
+            save.append(h)
+        y = conv_layer(h, w, cin, cout, bias=b, relu=True, f32=last and cout > 1, xs=xs)
+        if cout == 1 and not last:
+            y = y.to(torch.bfloat16)
         h = y
+        cin = cout
     return h
 
 
-def wgrad_v3_ok(shape, ks: int) -> bool:
-    """wgrad16v3 stages full-width X rows: L + ks - 1 <= 32."""
-    return shape[4] + ks - 1 <= 32
-
-
-def wgrad_v3_groups(shape, ks: int, dj_center: bool) -> int:
-    """Column groups per dj for wgrad16v3: ~2 workgroups per CU in full mode
-    (KS dj values), ~1 per CU in dj-centre mode, never more than the columns
-    (v, j, tile).  Tile rule mirrors ncnet_wgrad16v3."""
-    V, I, J, K, L = shape[:5]
-    ntl = -(-(K * L) // 320)
-    ncols = V * J * ntl
-    target = 256 if dj_center else max(1, 512 // ks)
-    env = _os.environ.get("NCNET_WGRAD_GROUPS")
-    if env:
-        target = int(env)
-    return max(1, min(target, ncols))
-
-
-def wgrad_plane_groups(nitems: int) -> int:
-    """Groups of the plane-only wgrad (grid = groups): ~3 workgroups per CU."""
-    env = _os.environ.get("NCNET_WGRAD_PLANE_GROUPS")
-    return max(1, min(int(env) if env else 768, nitems))
-
-
-def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, ng: int, dj_center):
-    """Run the wgrad16 kernel and reduce its per-group partials.
-
-    ``dj_center``: False/0 all (di, dj) plane offsets, True/1 dj = P only (j
-    encoding), 2 only (P, P) (ij encoding, plane-only).  Returns (s, sb): s
-    [dd, tap, ci, co], sb [16] = sum of g16 over all voxels (bias gradient,
-    from the kernel's ones-MFMA in the centre block).  Variant 3 (sliding G
-    ring) serves modes 0/1, variant 2 (8-wave LDS-DMA) mode 2 and volumes too
-    wide for v3.
-    """
-    mode = int(dj_center)
-    variant = WGRAD_VARIANT
-    if mode == 2 or (variant == 3 and not wgrad_v3_ok(x16.shape, ks)):
-        variant = 2
-    if mode == 2:
-        V, I, J, K, L = x16.shape[:5]
-        ng = wgrad_plane_groups(V * I * J * ((K + 24) // 25) * ((L + 24) // 25))
-    elif variant == 3:
-        ng = wgrad_v3_groups(x16.shape, ks, bool(mode))
-    rows = ng * (2 if variant >= 2 else 1)
-    ndd = 1 if mode == 2 else (ks if mode else ks * ks)
-    part = torch.empty((rows, ndd, ks * ks, 16, 16), dtype=torch.float32, device=x16.device)
-    partb = torch.empty((rows, 16), dtype=torch.float32, device=x16.device)
-    C.wgrad16(x16, g16, part, partb, ks, mode, variant)
-    return part.sum(0), partb.sum(0)
-
-
-def _reduce_wgrad16(s: torch.Tensor, ks: int, cout: int, cin: int) -> torch.Tensor:
-    # s [dd, tap, ci, co] -> std [co, ci, di, dj, dk, dl]
-    return s.permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks, ks)[:cout, :cin]
-
-
-def _reduce_wgrad16_center(s: torch.Tensor, ks: int) -> torch.Tensor:
-    # s [di, tap, ci, co] (dj = P only) -> [co, ci, di, dk, dl]
-    return s.permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks)
-
-
-def _reduce_wgrad1(part: torch.Tensor, ks: int, mode: int, c16: int) -> torch.Tensor:
-    s = part.sum(0)  # [dd, tap, c16]
-    if mode == 0:    # -> [co, 1, di, dj, dk, dl]
-        return s.permute(2, 0, 1).reshape(16, 1, ks, ks, ks, ks)[:c16]
-    # mode 1: tap index is flipped per (dk, dl): -> [1, ci, di, dj, dk, dl]
-    s = s.reshape(ks, ks, ks, ks, 16).flip(2, 3)
-    return s.permute(4, 0, 1, 2, 3).reshape(1, 16, ks, ks, ks, ks)[:, :c16]
-
-
-# Weight gradients of the 16->16 and Cout=1 layers on a second HIP stream
+# Weight gradients of the layers after the first on a second HIP stream
 # (NCNET_BWD_OVERLAP=0 disables): they depend only on the layer input and the
 # incoming gradient, so wgrad(l) runs while the data-gradient chain continues
 # on the main stream (dgrad(l) -> dgrad(l-1) -> ...).  The first layer's
@@ -299,9 +331,55 @@ class _OnSide:
         return False
 
 
+def _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout):
+    """dW [cout, cin, k^4] (std) and db [cout] of one layer.  xin: ij-packed
+    input (cin == 1) or input blocks; g: gradient w.r.t. the pre-activation
+    (blocks, or 1-channel); gs = ijpack(g, -1) for 1-channel outputs."""
+    G = ij_groups(ks)
+    dev = g.device
+    if kind == "1in":
+        dw = torch.empty((cout, 1) + (ks,) * 4, device=dev)
+        db = torch.empty(cout, device=dev)
+        for b in range(nblocks(cout)):
+            sl = slice(16 * b, min(cout, 16 * b + 16))
+            parts = [wgrad16_partials(C, xin[gi], g[b], ks, True) for gi in range(G)]
+            dw[sl] = ij_in_grad(torch.stack([p[0][0] for p in parts]), sl.stop - sl.start)
+            db[sl] = parts[0][1][:sl.stop - sl.start]
+        return dw, db
+    if kind == "16":
+        dw = torch.empty((cout, cin) + (ks,) * 4, device=dev)
+        db = torch.empty(cout, device=dev)
+        for b in range(nblocks(cout)):
+            so = slice(16 * b, min(cout, 16 * b + 16))
+            for a in range(nblocks(cin)):
+                si = slice(16 * a, min(cin, 16 * a + 16))
+                sw, sb = wgrad16_partials(C, xin[a], g[b], ks, False)
+                dw[so, si] = _reduce_wgrad16(sw, ks, so.stop - so.start, si.stop - si.start)
+                if a == 0:
+                    db[so] = sb[:so.stop - so.start]
+        return dw, db
+    qc = (ks // 2) * ks + ks // 2        # combo (P, P): its channel of ijpack(g, -1) is g itself
+    if kind == "1out":
+        dw = torch.empty((1, cin) + (ks,) * 4, device=dev)
+        db = None
+        for a in range(nblocks(cin)):
+            si = slice(16 * a, min(cin, 16 * a + 16))
+            parts = [wgrad16_partials(C, xin[a], gs[gi], ks, True) for gi in range(G)]
+            dw[:, si] = ij_out_grad(torch.stack([p[0][0] for p in parts]), si.stop - si.start)
+            if a == 0:
+                db = parts[qc // 16][1][qc % 16].reshape(1)
+        return dw, db
+    # "11": the 1-channel gradient as channel 0 of a 16-channel operand
+    g16 = torch.zeros(tuple(g.shape) + (16,), dtype=torch.bfloat16, device=dev)
+    g16[..., 0] = g
+    parts = [wgrad16_partials(C, xin[gi], g16, ks, True) for gi in range(G)]
+    return ij_in_grad(torch.stack([p[0][0] for p in parts]), 1), parts[0][1][:1].clone()
+
+
 def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool):
-    """g_last: grad w.r.t. the last conv's PRE-activation (bf16, 1ch).
-    Returns (dW list in checkpoint layout, db list, g_x0 fp32 or None)."""
+    """g_last: grad w.r.t. the last conv's PRE-activation, bf16: [V,I,J,K,L] for
+    a 1-channel output, else blocks [NB, V,I,J,K,L,16].
+    Returns (dW list in checkpoint layout, db list, grad of x0 fp32 or None)."""
     C = _ext.ext()
     nl = len(kinds)
     dws, dbs = [None] * nl, [None] * nl
@@ -312,119 +390,41 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
         main = torch.cuda.current_stream(g_last.device)
         side = _side_stream(g_last.device)
     for li in range(nl - 1, -1, -1):
-        kind, w_ref, h = kinds[li], ws[li], saved[li]
-        ks = w_ref.shape[0]
+        kind = kinds[li]
+        w = _std(ws[li])
+        ks = w.shape[-1]
         cout = channels[li]
         cin = 1 if li == 0 else channels[li - 1]
-        w = _std(w_ref)
-        V, I, J, K, L = h.shape[1:6] if h.dim() == 7 else h.shape[:5]
-        nitems = V * I * J * ((K + 24) // 25) * ((L + 24) // 25)
-        ng = wgrad_groups(ks, nitems)
-        mask_prev = h if li > 0 else None   # ReLU output of the previous layer
-        if kind == "1out" and USE_IJ:
-            G = ij_groups(ks)
-            gs = torch.empty((G,) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
-            C.ijpack(g, gs, ks, -1)                  # adjoint of ijsum
-            with _OnSide(main, side, (h, gs)):
-                parts = [wgrad16_partials(C, h, gs[gi], ks, ng, 2) for gi in range(G)]
-                dw = ij_out_grad(torch.stack([p[0][0] for p in parts]), cin)
-                qc = (ks // 2) * ks + ks // 2        # combo (P, P): its channel of ijpack(g, -1) is g itself
-                db = parts[qc // 16][1][qc % 16].reshape(1)
-                del parts
-            if li > 0 or need_dx0:
-                gi_ = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
-                if USE_KL and mask_prev is not None:  # 1 -> Cin conv with flipped taps, ReLU mask fused
-                    C.conv1to16_kl(g, pack_kl_in(kl_dgrad_in_weights(w)), None, mask_prev, gi_, ks, 2)
-                elif _out_ij_dgrad(ks):              # reuses ijpack(g, -1) of the weight gradient
-                    wd = pack_w16_planes(plane_dgrad_weights(ij_out_weights(w)))
-                    C.conv16_fwd(gs, wd, None, mask_prev, gi_, ks, 2 if mask_prev is not None else 0, 0)
-                else:                                # j encoding: 1 pass over the KS dj = P planes
-                    del gs
-                    gs = torch.empty(tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
-                    C.jpack(g, gs, ks, -1)
-                    wt = transpose_for_dgrad(jc_out_weights(w))
-                    C.conv16_fwd(gs, pack_w16(wt), None, mask_prev, gi_, ks, 2 if mask_prev is not None else 0, 1)
-                g = gi_
-                del gs
-        elif kind == "1in" and USE_IJ:               # h is ijpack(X0) [G, ...] (kl: X0 itself)
-            if h.dim() == 5:
-                xs = torch.empty((ij_groups(ks),) + tuple(h.shape) + (16,), dtype=torch.bfloat16, device=h.device)
-                C.ijpack(h, xs, ks, 1)
-                h = xs
-            G = h.shape[0]
-            parts = [wgrad16_partials(C, h[gi], g, ks, ng, 2) for gi in range(G)]
-            dw = ij_in_grad(torch.stack([p[0][0] for p in parts]), cout)
-            db = parts[0][1][:cout]
-            if li > 0:
-                raise RuntimeError("internal: 1in layer must be first")
-            if need_dx0:
-                wd = pack_w16_planes(plane_dgrad_weights(ij_in_weights(w)))
-                nq = ks * ks
-                z = torch.empty((nq, V, I, J, K, L), dtype=torch.float32, device=h.device)
-                gx = g.unsqueeze(0)
-                for gi in range(G):
-                    C.conv16_fwd(gx, wd[gi:gi + 1], None, None, z[16 * gi:min(nq, 16 * gi + 16)], ks, 4, 0)
-                gx0 = torch.empty((V, I, J, K, L), dtype=torch.float32, device=h.device)
-                C.ijsum(z, None, gx0, ks, 0, -1)      # adjoint of ijpack(+1)
-        elif kind == "1out" and USE_JC:
-            gs = torch.empty(tuple(g.shape) + (16,), dtype=torch.bfloat16, device=h.device)
-            C.jpack(g, gs, ks, -1)                   # adjoint of jsum
-            sw, sb = wgrad16_partials(C, h, gs, ks, ng, True)
-            dw = jc_out_grad(_reduce_wgrad16_center(sw, ks), cin)
-            db = sb[ks // 2].reshape(1)              # channel P of jpack(g, -1) is g itself
-            if li > 0 or need_dx0:
-                gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
-                wt = transpose_for_dgrad(jc_out_weights(w))
-                C.conv16_fwd(gs, pack_w16(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0, 1)
-                g = gi
-            del gs
-        elif kind == "1in" and USE_JC:               # h is jpack(X0) (16ch)
-            sw, sb = wgrad16_partials(C, h, g, ks, ng, True)
-            dw = jc_in_grad(_reduce_wgrad16_center(sw, ks), cout)
-            db = sb[:cout]
-            if li > 0:
-                raise RuntimeError("internal: 1in layer must be first")
-            if need_dx0:
-                z8 = torch.empty((ks,) + tuple(h.shape[:5]), dtype=torch.float32, device=h.device)
-                wt = transpose_for_dgrad(jc_in_weights(w))
-                C.conv16_fwd(g, pack_w16(wt), None, None, z8, ks, 3, 1)
-                gx0 = torch.empty(tuple(h.shape[:5]), dtype=torch.float32, device=h.device)
-                C.jsum(z8, None, gx0, ks, 0, -1)      # adjoint of jpack(+1)
-        elif kind == "1out":
-            if g.dim() == 6:
-                raise RuntimeError("internal: 1out layer expects a 1-channel gradient")
-            part = torch.empty((ng, ks * ks, ks * ks, 16), dtype=torch.float32, device=h.device)
-            C.wgrad1(h, g, part, ks, 1, ng)
-            dw = _reduce_wgrad1(part, ks, 1, cin)
-            db = g.float().sum().reshape(1)
-            if li > 0 or need_dx0:
-                gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
-                wt = transpose_for_dgrad(w)  # [16(ci as out), 1, k^4]
-                C.conv1in_fwd(g, pack_w1in(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0)
-                g = gi
-        elif kind == "16":
-            with _OnSide(main, side, (h, g)):
-                sw, sb = wgrad16_partials(C, h, g, ks, ng, False)
-                dw = _reduce_wgrad16(sw, ks, cout, cin)
-                db = sb[:cout]
-                del sw, sb
-            if li > 0 or need_dx0:
-                gi = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
-                wt = transpose_for_dgrad(w)
-                C.conv16_fwd(g, pack_w16(wt), None, mask_prev, gi, ks, 2 if mask_prev is not None else 0, 0)
-                g = gi
-        else:  # "1in": h is the 1-channel input
-            part = torch.empty((ng, ks * ks, ks * ks, 16), dtype=torch.float32, device=h.device)
-            C.wgrad1(g, h, part, ks, 0, ng)
-            dw = _reduce_wgrad1(part, ks, 0, cout)
-            db = g.float().sum(dim=(0, 1, 2, 3, 4))[:cout]
-            if li > 0:
-                raise RuntimeError("internal: 1in layer must be first")
-            if need_dx0:
-                gi = torch.empty(h.shape, dtype=torch.float32, device=h.device)
-                wt = transpose_for_dgrad(w)  # [1, 16, k^4]
-                C.conv1out_fwd(g, pack_w1out(wt), None, gi, ks, 0)
-                gx0 = gi
+        sv = saved[li]
+        if cin == 1:
+            xin, hin = (sv if li > 0 else (sv, None))
+        else:
+            xin = hin = sv
+        gs = None
+        if cout == 1 and kind == "1out":
+            gs = torch.empty((ij_groups(ks),) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=g.device)
+            C.ijpack(g, gs, ks, -1)                  # adjoint of ijsum: shared by wgrad and dgrad
+        on_side = li > 0
+        with _OnSide(main if on_side else None, side if on_side else None,
+                     tuple(t for t in (xin, g, gs) if t is not None)):
+            dw, db = _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout)
+        if li > 0 or need_dx0:
+            if kind == "1out":                       # reuses ijpack(g, -1) of the weight gradient
+                gi_ = []
+                for a in range(nblocks(cin)):
+                    wp = pack_w16_planes(plane_dgrad_weights(ij_out_weights(w[:, 16 * a:16 * a + 16])))
+                    y = torch.empty(tuple(hin.shape[1:]), dtype=torch.bfloat16, device=g.device)
+                    C.conv16_fwd(gs, wp, None, hin[a], y, ks, 2)
+                    gi_.append(y)
+                g = torch.stack(gi_)
+            elif cin == 1:                           # gradient w.r.t. a 1-channel input (fp32)
+                gx = conv_layer(g, transpose_for_dgrad(w), cout, 1, relu=False)
+                if li == 0:
+                    gx0 = gx
+                else:                                # mid-stack: the previous layer's ReLU mask
+                    g = (gx * (hin > 0)).to(torch.bfloat16)
+            else:                                    # "16": masked by the previous layer's ReLU output
+                g = conv_layer(g, transpose_for_dgrad(w), cout, cin, relu=False, mask=hin)
         dws[li] = dw
         dbs[li] = db
     if side is not None:
@@ -444,81 +444,128 @@ def _swap_flat(x: torch.Tensor, shape_ab):
     return out
 
 
+def _combine_multi(z1: torch.Tensor, z2: torch.Tensor, dims) -> torch.Tensor:
+    """Symmetric combine of multi-channel outputs: z1 planar [C, V, I, J, K, L],
+    z2 planar [C, V, K, L, I, J] -> y [V, C, I, J, K, L] fp32."""
+    return (z1 + z2.permute(0, 1, 4, 5, 2, 3)).transpose(0, 1).contiguous()
+
+
 class NeighConsensusFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, symmetric, kinds, channels, *params):
         ws, bs = params[0::2], params[1::2]
         V, _, I, J, K, L = x.shape
         R, Cc = I * J, K * L
+        cl = channels[-1]
         xb = x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous()
         saved_layers = []
+        square = (I, J) == (K, L)
         if symmetric:
             xt = _swap_flat(xb.reshape(V, R, Cc), (I, J, K, L)).reshape(V, K, L, I, J)
-            if (I, J) == (K, L):
-                x0 = torch.cat((xb, xt), 0)
-                z = _stack_fwd(x0, ws, bs, kinds, saved_layers)
+            if square:
+                z = _stack_fwd(torch.cat((xb, xt), 0), ws, bs, kinds, saved_layers)
                 branches = [saved_layers]
+                z1, z2 = (z[:V], z[V:]) if cl == 1 else (z[:, :V], z[:, V:])
             else:
                 s1, s2 = [], []
                 z1 = _stack_fwd(xb, ws, bs, kinds, s1)
                 z2 = _stack_fwd(xt, ws, bs, kinds, s2)
-                z = torch.cat((z1.reshape(-1), z2.reshape(-1)))
                 branches = [s1, s2]
-            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x.device)
-            _ext.ext().combine_fwd(z, y, R, Cc)
+            if cl == 1:
+                if not square:
+                    z = torch.cat((z1.reshape(-1), z2.reshape(-1)))
+                y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x.device)
+                _ext.ext().combine_fwd(z.reshape(-1), y, R, Cc)
+                y = y.reshape(V, 1, I, J, K, L)
+            else:
+                if not square:
+                    z = torch.cat((z1.reshape(cl, -1), z2.reshape(cl, -1)), 1)
+                y = _combine_multi(z1, z2, (V, I, J, K, L))
         else:
             z = _stack_fwd(xb, ws, bs, kinds, saved_layers)
             branches = [saved_layers]
-            y = z
+            y = z.reshape(V, 1, I, J, K, L) if cl == 1 else z.transpose(0, 1).contiguous()
         ctx.symmetric = symmetric
         ctx.kinds = kinds
         ctx.channels = channels
         ctx.dims = (V, I, J, K, L)
         ctx.nbranch = len(branches)
-        flat = [t for br in branches for t in br]
-        ctx.nper = len(branches[0])
+        flat = []
+        ctx.layout = []
+        for br in branches:
+            lay = []
+            for t in br:
+                if isinstance(t, tuple):
+                    flat.extend(t)
+                    lay.append(2)
+                else:
+                    flat.append(t)
+                    lay.append(1)
+            ctx.layout.append(lay)
         ctx.save_for_backward(z, *params, *flat)
-        return y.reshape(V, 1, I, J, K, L)
+        return y
 
     @staticmethod
     def backward(ctx, gy):
         z, *rest = ctx.saved_tensors
         nparam = 2 * len(ctx.kinds)
-        params, flat = rest[:nparam], rest[nparam:]
+        params, flat = rest[:nparam], list(rest[nparam:])
         ws = params[0::2]
         V, I, J, K, L = ctx.dims
         R, Cc = I * J, K * L
+        cl = ctx.channels[-1]
         need_dx0 = ctx.needs_input_grad[0]
-        gy = gy.reshape(V, R, Cc).float().contiguous()
-        if ctx.symmetric:
-            gz = torch.empty(z.numel(), dtype=torch.bfloat16, device=gy.device)
-            _ext.ext().combine_bwd(gy, z, gz, R, Cc)
-        else:
-            gz = (gy.reshape(-1) * (z.reshape(-1) > 0)).to(torch.bfloat16)
-        branches = [list(flat[b * ctx.nper:(b + 1) * ctx.nper]) for b in range(ctx.nbranch)]
-        if ctx.nbranch == 1:
-            nv = 2 * V if ctx.symmetric else V
-            g_last = gz.reshape(nv, *((I, J, K, L)))
-            dws, dbs, gx0 = _stack_bwd(g_last, branches[0], ws, ctx.kinds, ctx.channels, need_dx0)
-        else:
-            n1 = V * R * Cc
-            g1 = gz[:n1].reshape(V, I, J, K, L)
-            g2 = gz[n1:].reshape(V, K, L, I, J)
-            dws1, dbs1, gxa = _stack_bwd(g1, branches[0], ws, ctx.kinds, ctx.channels, need_dx0)
-            dws2, dbs2, gxb = _stack_bwd(g2, branches[1], ws, ctx.kinds, ctx.channels, need_dx0)
-            dws = [a + b for a, b in zip(dws1, dws2)]
-            dbs = [a + b for a, b in zip(dbs1, dbs2)]
-            gx0 = None if gxa is None else torch.cat((gxa.reshape(-1), gxb.reshape(-1)))
-        gx = None
-        if need_dx0 and gx0 is not None:
-            gx0 = gx0.reshape(-1)
+        branches = []
+        pos = 0
+        for lay in ctx.layout:
+            br = []
+            for n in lay:
+                br.append(flat[pos] if n == 1 else tuple(flat[pos:pos + n]))
+                pos += n
+            branches.append(br)
+        if cl == 1:
+            gy3 = gy.reshape(V, R, Cc).float().contiguous()
             if ctx.symmetric:
-                n1 = V * R * Cc
-                ga = gx0[:n1].reshape(V, R, Cc)
-                gb = _swap_flat(gx0[n1:].reshape(V, Cc, R), (K, L, I, J))
-                gx = (ga + gb).reshape(V, 1, I, J, K, L)
+                gz = torch.empty(z.numel(), dtype=torch.bfloat16, device=gy.device)
+                _ext.ext().combine_bwd(gy3, z, gz, R, Cc)
             else:
-                gx = gx0.reshape(V, 1, I, J, K, L)
+                gz = (gy3.reshape(-1) * (z.reshape(-1) > 0)).to(torch.bfloat16)
+            n1 = V * R * Cc
+            if ctx.nbranch == 1:
+                nv = 2 * V if ctx.symmetric else V
+                gl = [gz.reshape(nv, I, J, K, L)]
+            else:
+                gl = [gz[:n1].reshape(V, I, J, K, L), gz[n1:].reshape(V, K, L, I, J)]
+        else:
+            g1 = gy.float().transpose(0, 1)                        # planar [C, V, I, J, K, L]
+            if ctx.symmetric:
+                g2 = g1.permute(0, 1, 4, 5, 2, 3)                  # [C, V, K, L, I, J]
+                zz = z.reshape(cl, -1)
+                n1 = V * R * Cc
+                gz1 = g1.reshape(cl, -1) * (zz[:, :n1] > 0)
+                gz2 = g2.reshape(cl, -1) * (zz[:, n1:] > 0)
+                if ctx.nbranch == 1:
+                    gl = [planar_to_blocks(torch.cat((gz1, gz2), 1).reshape(cl, 2 * V, I, J, K, L))]
+                else:
+                    gl = [planar_to_blocks(gz1.reshape(cl, V, I, J, K, L)),
+                          planar_to_blocks(gz2.reshape(cl, V, K, L, I, J))]
+            else:
+                gl = [planar_to_blocks(g1 * (z > 0))]
+        res = [_stack_bwd(g, br, ws, ctx.kinds, ctx.channels, need_dx0) for g, br in zip(gl, branches)]
+        dws = [sum(r[0][i] for r in res) for i in range(len(ws))]
+        dbs = [sum(r[1][i] for r in res) for i in range(len(ws))]
+        gx = None
+        if need_dx0:
+            if ctx.symmetric:
+                if len(res) == 1:
+                    g0 = res[0][2].reshape(-1)
+                    ga, gbt = g0[:V * R * Cc], g0[V * R * Cc:]
+                else:
+                    ga, gbt = res[0][2].reshape(-1), res[1][2].reshape(-1)
+                gb = _swap_flat(gbt.reshape(V, Cc, R), (K, L, I, J))
+                gx = (ga.reshape(V, R, Cc) + gb).reshape(V, 1, I, J, K, L)
+            else:
+                gx = res[0][2].reshape(V, 1, I, J, K, L)
         grads = []
         for dw, db in zip(dws, dbs):
             grads += [dw, db]
@@ -548,33 +595,24 @@ def _stack_fwd_fp8(x0: torch.Tensor, ws, bs, kinds) -> torch.Tensor:
     for li, (w_ref, b, kind) in enumerate(zip(ws, bs, kinds)):
         ks = w_ref.shape[0]
         w = _std(w_ref)
-        if kind == "1in" and USE_KL:
-            y = torch.empty((V, I, J, K, L, 16), dtype=FP8, device=x0.device)
-            C.conv1to16_kl(h, pack_kl_in(w), _pad_bias(b, 16), None, y, ks, 1)
-        elif kind == "1in":
+        if kind == "1in":
             G = ij_groups(ks)
             xs = torch.empty((G, V, I, J, K, L, 16), dtype=FP8, device=x0.device)
             C.ijpack(h, xs, ks, 1)
             wq, osc = _fp8_weights(pack_w16_planes(ij_in_weights(w)))
             y = torch.empty((V, I, J, K, L, 16), dtype=FP8, device=x0.device)
-            C.conv16f8_fwd(xs, wq, _pad_bias(b, 16), y, ks, 1, 0, osc)
+            C.conv16f8_fwd(xs, wq, _pad_bias(b, 16), y, ks, 1, osc)
         elif kind == "16":
             wq, osc = _fp8_weights(pack_w16(w))
             y = torch.empty((V, I, J, K, L, 16), dtype=FP8, device=x0.device)
-            C.conv16f8_fwd(h, wq, _pad_bias(b, 16), y, ks, 1, 0, osc)
-        elif USE_KL:  # "1out"
-            wq, osc = _fp8_weights(pack_kl_out(w))
-            y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
-            C.conv16to1_kl(h, wq, _pad_bias(b, 1), y, ks, 1, osc)
-            if li != len(kinds) - 1:
-                raise RuntimeError("fp8 NC path: the 1-channel output layer must be last")
+            C.conv16f8_fwd(h, wq, _pad_bias(b, 16), y, ks, 1, osc)
         else:  # "1out"
             G, nq = ij_groups(ks), ks * ks
             wq, osc = _fp8_weights(pack_w16_planes(ij_out_weights(w)))
             z = torch.empty((nq, V, I, J, K, L), dtype=torch.float32, device=x0.device)
             hx = h.unsqueeze(0)
             for gi in range(G):
-                C.conv16f8_fwd(hx, wq[gi:gi + 1], None, z[16 * gi:min(nq, 16 * gi + 16)], ks, 4, 0, osc)
+                C.conv16f8_fwd(hx, wq[gi:gi + 1], None, z[16 * gi:min(nq, 16 * gi + 16)], ks, 4, osc)
             y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x0.device)
             C.ijsum(z, _pad_bias(b, 1), y, ks, 1, 1)
             del z
@@ -683,27 +721,41 @@ def neigh_consensus_fused(x: torch.Tensor, weights, biases, symmetric: bool = Tr
     return y.reshape(V, 1, I, J, K, L)
 
 
-def _fused_ok(kinds, kernel_sizes, x) -> bool:
-    return (FUSED and not torch.is_grad_enabled() and list(kinds) == ["1in", "1out"]
+def _fused_ok(kinds, kernel_sizes, channels, x) -> bool:
+    return (FUSED and not torch.is_grad_enabled() and list(kinds) == ["1in", "1out"] and channels[0] <= 16
             and list(kernel_sizes) == [3, 3] and x.shape[2] * x.shape[3] * x.shape[4] * x.shape[5] < 2 ** 31)
+
+
+def fp8_ok(kinds, channels) -> bool:
+    """fp8 NC kernels cover 1 -> (<=16 ->)* -> 1 stacks (one channel block)."""
+    return (len(kinds) >= 2 and kinds[0] == "1in" and kinds[-1] == "1out" and all(k == "16" for k in kinds[1:-1])
+            and max(channels) <= 16)
 
 
 def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool = True, fp8: bool = False) -> torch.Tensor:
     """x: [V,1,I,J,K,L] fp32; weights in checkpoint layout [k, out, in, k, k, k].
+    Returns [V, C_last, I, J, K, L] fp32.
 
-    Inference of the InLoc (3,3)/(16,1) stack runs on the fused kernel (bf16
-    operands, hidden layer kept on chip) whatever ``fp8`` says.  ``fp8``:
-    inference of other 1-in/1-out stacks through the fp8 MFMA kernels (ignored
-    when gradients are required or the stack shape has no fp8 kernels)."""
+    On the GPU: the (3,3)/(<=16,1) inference stack runs on the fused kernel
+    (hidden layer in LDS); ``fp8`` (inference, ``fp8_ok`` stacks) on the fp8
+    MFMA Conv4d kernels; everything else with odd kernel sizes <= 7 and any
+    channel counts on the bf16 autograd stack.  ``_ext.DISPATCH`` records
+    which path ran."""
     kernel_sizes = [w.shape[0] for w in weights]
     kinds = layer_kinds(channels, kernel_sizes)
-    if _ext.use_hip(x) and kinds is not None:
-        if _fused_ok(kinds, kernel_sizes, x):
-            return neigh_consensus_fused(x.float().contiguous(), weights, biases, symmetric)
-        if fp8 and not torch.is_grad_enabled() and kinds[0] == "1in" and kinds[-1] == "1out":
-            return neigh_consensus_fp8(x.float().contiguous(), weights, biases, kinds, symmetric)
-        params = []
-        for w, b in zip(weights, biases):
-            params += [w, b]
-        return NeighConsensusFn.apply(x.float().contiguous(), symmetric, tuple(kinds), tuple(channels), *params)
+    if _ext.use_hip(x):
+        if kinds is None:
+            _ext.torch_fallback(f"NeighConsensus kernel sizes {kernel_sizes}")
+        else:
+            if _fused_ok(kinds, kernel_sizes, channels, x) and not fp8:
+                _ext.count("nc_fused_k3")
+                return neigh_consensus_fused(x.float().contiguous(), weights, biases, symmetric)
+            if fp8 and not torch.is_grad_enabled() and fp8_ok(kinds, channels):
+                _ext.count("nc_fp8")
+                return neigh_consensus_fp8(x.float().contiguous(), weights, biases, kinds, symmetric)
+            _ext.count("nc_bf16")
+            params = []
+            for w, b in zip(weights, biases):
+                params += [w, b]
+            return NeighConsensusFn.apply(x.float().contiguous(), symmetric, tuple(kinds), tuple(channels), *params)
     return ref.neigh_consensus(x.float(), [w.float() for w in weights], [b.float() for b in biases], symmetric)

@@ -5,13 +5,9 @@ Weights arrive in the standard layout ``[Cout, Cin, k, k, k, k]`` (see
 Packing is a single gather with cached index tensors, done once per forward
 (the tensors are <= 320 KB), in bf16.
 
-* ``pack_w16``   Cin=16, Cout=16 -> [k*k, ceil(k*k/2), 64, 8]
-                 lane l of pair q: W[co=l&15, ci=8((l>>4)&1)+j, di, dj, tap=2q+(l>>5)]
-* ``pack_w1in``  Cin=1,  Cout=16 -> [k*k, ceil(k/4), 64, 8]
-                 lane l of MFMA m: W[co=l&15, 0, di, dj, dk=4m+(l>>4), dl=j]
-* ``pack_w1out`` Cin=16, Cout=1  -> [k*k, ceil((k+3)^2/2), 64, 8]
-                 lane l of pair p: W'[tau=2p+(l>>5), s=l&15] for ci=8((l>>4)&1)+j
-                 with W'[tau, s] = W[0, ci, di, dj, tau - s] (4x4 shift grid)
+* ``pack_w16``        Cin=16, Cout=16 -> [k*k, ceil(k*k/2), 64, 8]
+                      lane l of pair q: W[co=l&15, ci=8((l>>4)&1)+j, di, dj, tap=2q+(l>>5)]
+* ``pack_w16_planes`` the same per group plane (ij encoding, channel blocks)
 
 ``transpose_for_dgrad`` gives the weights of the data-gradient convolution
 (swap in/out channels, flip all four kernel axes).
@@ -42,38 +38,6 @@ def _idx16(ks: int):
     return co, ci, tap, valid
 
 
-@functools.lru_cache(maxsize=None)
-def _idx1in(ks: int):
-    nm = (ks + 3) // 4
-    m = torch.arange(nm).view(nm, 1, 1)
-    lane = torch.arange(64).view(1, 64, 1)
-    j = torch.arange(8).view(1, 1, 8)
-    dk = 4 * m + (lane >> 4)
-    dl = j
-    valid = ((dk < ks) & (dl < ks)).expand(nm, 64, 8)
-    tap = (torch.clamp(dk, max=ks - 1) * ks + torch.clamp(dl, max=ks - 1)).expand(nm, 64, 8)
-    co = (lane & 15).expand(nm, 64, 8)
-    return co, tap, valid
-
-
-@functools.lru_cache(maxsize=None)
-def _idx1out(ks: int):
-    ts = ks + 3
-    npair = (ts * ts + 1) // 2
-    p = torch.arange(npair).view(npair, 1, 1)
-    lane = torch.arange(64).view(1, 64, 1)
-    j = torch.arange(8).view(1, 1, 8)
-    tau = 2 * p + (lane >> 5)
-    s = lane & 15
-    sk, sl = s // 4, s % 4
-    tk, tl = tau // ts, tau % ts
-    dk, dl = tk - sk, tl - sl
-    valid = ((tau < ts * ts) & (dk >= 0) & (dk < ks) & (dl >= 0) & (dl < ks)).expand(npair, 64, 8)
-    tap = (torch.clamp(dk, 0, ks - 1) * ks + torch.clamp(dl, 0, ks - 1)).expand(npair, 64, 8)
-    ci = (8 * ((lane >> 4) & 1) + j).expand(npair, 64, 8)
-    return ci, tap, valid
-
-
 def _as_std(w_std: torch.Tensor, cout: int, cin: int) -> torch.Tensor:
     """Zero-pad [co, ci, k^4] channels up to (cout, cin)."""
     co, ci = w_std.shape[:2]
@@ -91,60 +55,6 @@ def pack_w16(w_std: torch.Tensor) -> torch.Tensor:
     vals = w[co, ci, :, tap]                      # [nq, 64, 8, k*k]
     vals = vals * valid.unsqueeze(-1).to(vals.dtype)
     return vals.permute(3, 0, 1, 2).contiguous().to(torch.bfloat16)
-
-
-def pack_w1in(w_std: torch.Tensor) -> torch.Tensor:
-    ks = w_std.shape[-1]
-    assert w_std.shape[1] == 1
-    w = _as_std(w_std, 16, 1).reshape(16, ks * ks, ks * ks)
-    co, tap, valid = (t.to(w.device) for t in _idx1in(ks))
-    vals = w[co, :, tap]                           # [nm, 64, 8, k*k]
-    vals = vals * valid.unsqueeze(-1).to(vals.dtype)
-    return vals.permute(3, 0, 1, 2).contiguous().to(torch.bfloat16)
-
-
-def pack_w1out(w_std: torch.Tensor) -> torch.Tensor:
-    ks = w_std.shape[-1]
-    assert w_std.shape[0] == 1
-    w = _as_std(w_std, 1, 16).reshape(16, ks * ks, ks * ks)
-    ci, tap, valid = (t.to(w.device) for t in _idx1out(ks))
-    vals = w[ci, :, tap]                           # [npair, 64, 8, k*k]
-    vals = vals * valid.unsqueeze(-1).to(vals.dtype)
-    return vals.permute(3, 0, 1, 2).contiguous().to(torch.bfloat16)
-
-
-# ---------------------------------------------------------------------------
-# j-offset <-> channel encoding of the 1-channel layers (see csrc/jshift.hip).
-# A Cin=1 layer W1 [co,1,k^4] becomes a 16->16 conv over jpack(X0) whose kernel
-# lives on the dj=P plane only; a Cout=1 layer W3 [1,ci,k^4] becomes a 16->16
-# conv (channels = dj) followed by jsum.
-
-def jc_in_weights(w_std: torch.Tensor) -> torch.Tensor:
-    """[co, 1, k^4] -> [16, 16, k^4]: out[co][c][di][P][dk][dl] = w[co][0][di][c][dk][dl]."""
-    co, ks = w_std.shape[0], w_std.shape[-1]
-    out = w_std.new_zeros((16, 16) + (ks,) * 4)
-    out[:co, :ks, :, ks // 2] = w_std[:, 0].permute(0, 2, 1, 3, 4)
-    return out
-
-
-def jc_out_weights(w_std: torch.Tensor) -> torch.Tensor:
-    """[1, ci, k^4] -> [16, 16, k^4]: out[c][ci][di][P][dk][dl] = w[0][ci][di][c][dk][dl]."""
-    ci, ks = w_std.shape[1], w_std.shape[-1]
-    out = w_std.new_zeros((16, 16) + (ks,) * 4)
-    out[:ks, :ci, :, ks // 2] = w_std[0].permute(2, 0, 1, 3, 4)
-    return out
-
-
-def jc_in_grad(s5: torch.Tensor, cout: int) -> torch.Tensor:
-    """dW of the dj=P slice [co, c, di, dk, dl] -> [co, 1, di, dj=c, dk, dl]."""
-    ks = s5.shape[-1]
-    return s5[:cout, :ks].permute(0, 2, 1, 3, 4).unsqueeze(1).contiguous()
-
-
-def jc_out_grad(s5: torch.Tensor, cin: int) -> torch.Tensor:
-    """dW of the dj=P slice [c, ci, di, dk, dl] -> [1, ci, di, dj=c, dk, dl]."""
-    ks = s5.shape[-1]
-    return s5[:ks, :cin].permute(1, 2, 0, 3, 4).unsqueeze(0).contiguous()
 
 
 # ---------------------------------------------------------------------------
@@ -204,38 +114,3 @@ def ij_out_grad(s: torch.Tensor, cin: int) -> torch.Tensor:
     ks = int(round(nt ** 0.5))
     d = s.permute(2, 0, 3, 1).reshape(16, G * 16, nt)[:cin, :nt]      # [ci, q, tap]
     return d.reshape(1, cin, ks, ks, ks, ks).contiguous()
-
-
-# ---------------------------------------------------------------------------
-# kl kernels (csrc/conv4d_kl.hip): in-plane (dk, dl) shifts resolved in LDS.
-
-def pack_kl_in(w_std: torch.Tensor) -> torch.Tensor:
-    """Cin=1 -> Cout<=16 weights [co, 1, k, k, k, k] -> [ceil(k^4/32), 64, 8] bf16.
-
-    Lane l of K step s holds W[co=l&15, tap=32s+8(l>>4)+j] with the taps in
-    (di, dj, dk, dl) row-major order (zero past k^4 and for co >= Cout)."""
-    cout, ks = w_std.shape[0], w_std.shape[2]
-    nk = ks ** 4
-    ns = (nk + 31) // 32
-    wf = w_std.new_zeros((16, ns * 32), dtype=torch.float32)
-    wf[:cout, :nk] = w_std.reshape(cout, nk).float()
-    return wf.reshape(16, ns, 4, 8).permute(1, 2, 0, 3).reshape(ns, 64, 8).to(torch.bfloat16).contiguous()
-
-
-def kl_dgrad_in_weights(w_std: torch.Tensor) -> torch.Tensor:
-    """Data gradient of a Cout=1 layer as a 1 -> Cin conv: [1, ci, k^4] -> [ci, 1, k^4 flipped]."""
-    return transpose_for_dgrad(w_std)
-
-
-def pack_kl_out(w_std: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
-    """Cin<=16 -> Cout=1 weights [1, ci, k, k, k, k] -> [k*k + 1, ceil(k*k/16), 16, 16].
-
-    Entry [p=(di,dj), ct, r, c] = W[0, c, di, dj, dk, dl] for the in-plane combo
-    16*ct + r = dk*k + dl (zero past k*k, for c >= Cin and on the extra
-    all-zero plane k*k used to pad odd plane counts)."""
-    cin, ks = w_std.shape[1], w_std.shape[2]
-    nt = ks * ks
-    nct = (nt + 15) // 16
-    out = w_std.new_zeros((nt + 1, nct * 16, 16), dtype=torch.float32)
-    out[:nt, :nt, :cin] = w_std[0].float().permute(1, 2, 3, 4, 0).reshape(nt, nt, cin)
-    return out.reshape(nt + 1, nct, 16, 16).to(dtype).contiguous()

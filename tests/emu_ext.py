@@ -1,0 +1,145 @@
+"""A CPU stand-in for the HIP extension's Conv4d kernels (``ncnet_amd/_C.so``).
+
+Each function has the binding's signature and buffer contract (packed MFMA
+weight fragments in, bf16/fp32 buffers written in place) and computes the
+kernel's math exactly in float64 from the packed operands: conv16_fwd
+(full 4D or group-plane mode, epilogues 0/1/2/4), wgrad16 (full / plane-only
+partial layout), ijpack / ijsum, combine and transpose.  It lets the CPU suite
+check the Python orchestration of the HIP path (channel blocks, the ij
+encoding, weight packing, symmetric branches, every gradient) against
+autograd of the fp64 oracle, with bf16 rounding exactly where the GPU path
+stores bf16.  The packed-weight decode inverts ``packing._idx16``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ncnet_amd.ops import reference as ref
+from ncnet_amd.ops.packing import _idx16
+
+
+def _unpack16(wp: torch.Tensor, ks: int) -> torch.Tensor:
+    """[NPL, nq, 64, 8] packed fragments -> [NPL, 16 co, 16 ci, ks*ks taps] fp64."""
+    co, ci, tap, valid = _idx16(ks)
+    npl = wp.shape[0]
+    w = torch.zeros(npl, 16, 16, ks * ks, dtype=torch.float64)
+    src = wp.double()
+    for pl in range(npl):
+        w[pl, co[valid], ci[valid], tap[valid]] = src[pl][valid]
+    return w
+
+
+def _plane_conv(x, w, ks):
+    """x [N, 16, K, L] fp64, w [16, 16, ks*ks] -> [N, 16, K, L] ("same" 2D conv)."""
+    return F.conv2d(x, w.reshape(16, 16, ks, ks), padding=ks // 2)
+
+
+def conv16_fwd(X, Wp, bias, M, Y, ks, epi):
+    grp = X.dim() == 7
+    xs = X.double()
+    w = _unpack16(Wp, ks)
+    if grp:
+        G, V, I, J, K, L, _ = xs.shape
+        acc = 0
+        for s in range(G):
+            xx = xs[s].permute(0, 1, 2, 5, 3, 4).reshape(V * I * J, 16, K, L)
+            acc = acc + _plane_conv(xx, w[s], ks)
+        out = acc.reshape(V, I, J, 16, K, L).permute(0, 1, 2, 4, 5, 3)      # [V,I,J,K,L,16]
+    else:
+        V, I, J, K, L, _ = xs.shape
+        wstd = w.reshape(ks, ks, 16, 16, ks, ks).permute(2, 3, 0, 1, 4, 5)  # [co, ci, di, dj, dk, dl]
+        out = ref.conv4d(xs.permute(0, 5, 1, 2, 3, 4), ref.conv4d_weight_from_std(wstd))
+        out = out.permute(0, 2, 3, 4, 5, 1)
+    if epi == 4:
+        Y.copy_(out[..., :Y.shape[0]].permute(5, 0, 1, 2, 3, 4))
+        return
+    if epi == 1:
+        out = torch.relu(out + bias.double())
+    elif epi == 2:
+        out = out * (M.double() > 0)
+    Y.copy_(out)
+
+
+def wgrad16(X, G, part, partb, ks, mode, variant):
+    with torch.enable_grad():      # called from inside autograd backward passes
+        _wgrad16(X, G, part, partb, ks, mode)
+
+
+def _wgrad16(X, G, part, partb, ks, mode):
+    xs = X.double().permute(0, 5, 1, 2, 3, 4)           # [V,16,I,J,K,L]
+    gs = G.double().permute(0, 5, 1, 2, 3, 4)
+    part.zero_()
+    partb.zero_()
+    if mode == 2:
+        V, _, I, J, K, L = xs.shape
+        xx = xs.permute(0, 2, 3, 1, 4, 5).reshape(V * I * J, 16, K, L).requires_grad_(False)
+        gg = gs.permute(0, 2, 3, 1, 4, 5).reshape(V * I * J, 16, K, L)
+        w = torch.zeros(16, 16, ks, ks, dtype=torch.float64, requires_grad=True)
+        (F.conv2d(xx, w, padding=ks // 2) * gg).sum().backward()
+        part[0, 0] = w.grad.permute(2, 3, 1, 0).reshape(ks * ks, 16, 16).float()   # [tap, ci, co]
+    else:
+        w = torch.zeros(16, 16, ks, ks, ks, ks, dtype=torch.float64, requires_grad=True)
+        (ref.conv4d(xs, ref.conv4d_weight_from_std(w)) * gs).sum().backward()
+        # [co, ci, di, dj, dk, dl] -> [dd = di*ks+dj, tap = dk*ks+dl, ci, co]
+        part[0] = w.grad.permute(2, 3, 4, 5, 1, 0).reshape(ks * ks, ks * ks, 16, 16).float()
+    partb[0] = gs.sum(dim=(0, 2, 3, 4, 5)).float()
+
+
+def _shift_ij(x, si, sj):
+    """out[:, i, j] = x[:, i + si, j + sj] (zero outside), x [V, I, J, ...]."""
+    I, J = x.shape[1], x.shape[2]
+    out = torch.zeros_like(x)
+    ilo, ihi, jlo, jhi = max(0, -si), min(I, I - si), max(0, -sj), min(J, J - sj)
+    if ilo < ihi and jlo < jhi:
+        out[:, ilo:ihi, jlo:jhi] = x[:, ilo + si:ihi + si, jlo + sj:jhi + sj]
+    return out
+
+
+def ijpack(X, S, ks, sgn):
+    x = X.double()
+    P = ks // 2
+    S.zero_()
+    for q in range(ks * ks):
+        S[q // 16, ..., q % 16] = _shift_ij(x, sgn * (q // ks - P), sgn * (q % ks - P)).to(S.dtype)
+
+
+def ijsum(Z, bias, y, ks, relu, sgn):
+    P = ks // 2
+    acc = torch.zeros(y.shape, dtype=torch.float64)
+    for q in range(ks * ks):
+        acc += _shift_ij(Z[q].double(), sgn * (q // ks - P), sgn * (q % ks - P))
+    if bias is not None:
+        acc += float(bias[0])
+    y.copy_(torch.relu(acc) if relu else acc)
+
+
+def combine_fwd(z, y, R, C):
+    z = z.reshape(-1)
+    Vh = y.numel() // (R * C)
+    z1, z2 = z[:Vh * R * C].view(Vh, R, C), z[Vh * R * C:].view(Vh, C, R)
+    y.view(Vh, R, C).copy_(z1 + z2.transpose(1, 2))
+
+
+def combine_bwd(g, z, gz, R, C):
+    z = z.reshape(-1)
+    Vh = g.numel() // (R * C)
+    z1, z2 = z[:Vh * R * C].view(Vh, R, C), z[Vh * R * C:].view(Vh, C, R)
+    g3 = g.view(Vh, R, C)
+    gz[:Vh * R * C].view(Vh, R, C).copy_(g3 * (z1 > 0))
+    gz[Vh * R * C:].view(Vh, C, R).copy_(g3.transpose(1, 2) * (z2 > 0))
+
+
+def transpose(x, y):
+    y.copy_(x.transpose(1, 2))
+
+
+class EmuExt:
+    """Namespace with the binding names used by ops/neigh_consensus.py and ops/conv4d.py."""
+    conv16_fwd = staticmethod(conv16_fwd)
+    wgrad16 = staticmethod(wgrad16)
+    ijpack = staticmethod(ijpack)
+    ijsum = staticmethod(ijsum)
+    combine_fwd = staticmethod(combine_fwd)
+    combine_bwd = staticmethod(combine_bwd)
+    transpose = staticmethod(transpose)

@@ -35,13 +35,13 @@ def test_extension_loaded():
     import ncnet_amd._C as C  # noqa: F401
 
 
-@pytest.mark.parametrize("variant", ["3", "2"])
 @pytest.mark.parametrize("ks,shape", [(5, (2, 25, 25, 25, 25)), (3, (1, 7, 9, 11, 13)), (3, (1, 3, 2, 30, 27)),
-                                      (5, (1, 6, 5, 26, 29)), (5, (1, 4, 12, 9, 7))])
-def test_conv16_fwd(ks, shape, variant, monkeypatch):
-    """conv16 forward (v3: X reused over 5 output j-planes; v2: one plane per workgroup)."""
+                                      (5, (1, 6, 5, 26, 29)), (5, (1, 4, 12, 9, 7)), (7, (1, 9, 8, 25, 25)),
+                                      (7, (1, 4, 5, 30, 28)), (1, (2, 5, 6, 25, 25))])
+def test_conv16_fwd(ks, shape):
+    """conv16 forward: v3 (X reused over 5 output j-planes, KS 3/5) and v2
+    (one plane per workgroup, KS 1/7), multi-tile K, L."""
     from ncnet_amd.ops.packing import pack_w16
-    monkeypatch.setenv("NCNET_CONV16_VARIANT", variant)
     torch.manual_seed(0)
     V, I, J, K, L = shape
     x = torch.rand(V, 16, I, J, K, L, device=DEV)
@@ -49,50 +49,25 @@ def test_conv16_fwd(ks, shape, variant, monkeypatch):
     b = torch.randn(16, device=DEV) * 0.1
     xcl = x.permute(0, 2, 3, 4, 5, 1).contiguous().to(torch.bfloat16)
     y = torch.empty_like(xcl)
-    _ext.ext().conv16_fwd(xcl, pack_w16(w), b, None, y, ks, 1, 0)
+    _ext.ext().conv16_fwd(xcl, pack_w16(w), b, None, y, ks, 1)
     yr = torch.relu(ref.conv4d(bf(x), ref.conv4d_weight_from_std(bf(w)), b.double()))
     assert relerr(y.permute(0, 5, 1, 2, 3, 4), yr) < 1e-2
 
 
-@pytest.mark.parametrize("ks,shape", [(5, (2, 25, 25, 25, 25)), (3, (1, 9, 8, 30, 26))])
-def test_conv1in_fwd(ks, shape):
-    from ncnet_amd.ops.packing import pack_w1in
-    torch.manual_seed(1)
-    V, I, J, K, L = shape
-    x = torch.rand(V, I, J, K, L, device=DEV)
-    w = torch.randn(16, 1, ks, ks, ks, ks, device=DEV) * 0.1
-    b = torch.randn(16, device=DEV) * 0.1
-    y = torch.empty(V, I, J, K, L, 16, device=DEV, dtype=torch.bfloat16)
-    _ext.ext().conv1in_fwd(x.to(torch.bfloat16).contiguous(), pack_w1in(w), b, None, y, ks, 1)
-    yr = torch.relu(ref.conv4d(bf(x).unsqueeze(1), ref.conv4d_weight_from_std(bf(w)), b.double()))
-    assert relerr(y.permute(0, 5, 1, 2, 3, 4), yr) < 1e-2
-
-
-@pytest.mark.parametrize("ks,shape", [(5, (2, 25, 25, 25, 25)), (3, (1, 9, 8, 30, 26)), (5, (1, 5, 6, 7, 9))])
-def test_conv1out_fwd(ks, shape):
-    from ncnet_amd.ops.packing import pack_w1out
-    torch.manual_seed(2)
-    V, I, J, K, L = shape
-    x = torch.rand(V, 16, I, J, K, L, device=DEV)
-    w = torch.randn(1, 16, ks, ks, ks, ks, device=DEV) * 0.05
-    b = torch.randn(1, device=DEV) * 0.1
-    xcl = x.permute(0, 2, 3, 4, 5, 1).contiguous().to(torch.bfloat16)
-    y = torch.empty(V, I, J, K, L, device=DEV)
-    _ext.ext().conv1out_fwd(xcl, pack_w1out(w), b, y, ks, 1)
-    yr = torch.relu(ref.conv4d(bf(x), ref.conv4d_weight_from_std(bf(w)), b.double()))[:, 0]
-    assert relerr(y, yr) < 5e-3
-
-
 @pytest.mark.parametrize("cin,cout,ks", [(16, 16, 5), (1, 16, 5), (16, 1, 5), (16, 16, 3), (1, 16, 3), (16, 1, 3),
-                                         (10, 10, 3)])
+                                         (10, 10, 3), (32, 16, 3), (1, 40, 3), (24, 1, 5), (16, 16, 7), (1, 16, 7),
+                                         (16, 16, 1), (1, 1, 3), (20, 33, 3)])
 def test_conv4d_autograd(cin, cout, ks):
+    """The Conv4d module on the HIP path for any channel counts / kernel sizes 1-7."""
     from ncnet_amd.ops.conv4d import conv4d
     torch.manual_seed(3)
     shape = (2, cin, 9, 8, 11, 10)
     x = torch.rand(shape, device=DEV).to(torch.bfloat16).float().requires_grad_(True)
     w = (torch.randn(ks, cout, cin, ks, ks, ks, device=DEV) * 0.05).to(torch.bfloat16).float().requires_grad_(True)
     b = (torch.randn(cout, device=DEV) * 0.1).requires_grad_(True)
+    before = _ext.DISPATCH["conv4d_hip"]
     y = conv4d(x, w, b, permute_filters=False)
+    assert _ext.DISPATCH["conv4d_hip"] == before + 1
     g = torch.randn_like(y).to(torch.bfloat16).float()
     (y * g).sum().backward()
     xr, wr, br = (t.detach().double().requires_grad_(True) for t in (x, w, b))
@@ -104,9 +79,23 @@ def test_conv4d_autograd(cin, cout, ks):
     assert relerr(b.grad, br.grad) < 1e-3
 
 
+def test_conv4d_even_kernel_raises_without_opt_in(monkeypatch):
+    """No silent fallback: k = 4 has no HIP kernel, so the GPU op raises unless
+    NCNET_ALLOW_TORCH_FALLBACK=1 opts into the PyTorch reference."""
+    from ncnet_amd.ops.conv4d import conv4d
+    x = torch.rand(1, 16, 4, 4, 4, 4, device=DEV)
+    w = torch.randn(4, 16, 16, 4, 4, 4, device=DEV) * 0.05
+    monkeypatch.delenv("NCNET_ALLOW_TORCH_FALLBACK", raising=False)
+    with pytest.raises(NotImplementedError):
+        conv4d(x, w, None, permute_filters=False)
+
+
 @pytest.mark.parametrize("ks,ch,shape", [((5, 5, 5), (16, 16, 1), (2, 1, 12, 12, 12, 12)),
                                          ((3, 3), (16, 1), (2, 1, 10, 11, 10, 11)),
-                                         ((3, 3), (16, 1), (1, 1, 8, 10, 9, 7))])
+                                         ((3, 3), (16, 1), (1, 1, 8, 10, 9, 7)),
+                                         ((3, 3, 3), (10, 10, 1), (2, 1, 9, 9, 9, 9)),
+                                         ((5, 5), (32, 1), (1, 1, 10, 9, 10, 9)),
+                                         ((7, 3), (16, 1), (1, 1, 9, 10, 9, 10))])
 def test_neigh_consensus_autograd(ks, ch, shape):
     from ncnet_amd.ops.neigh_consensus import neigh_consensus
     torch.manual_seed(4)
@@ -119,7 +108,9 @@ def test_neigh_consensus_autograd(ks, ch, shape):
         # gradient a sum of ~100 terms where one bf16-induced ReLU flip moves it by 10-30%
         bs.append((0.5 + torch.rand(c, device=DEV) * 0.1).requires_grad_(True))
         cin = c
+    before = _ext.DISPATCH["nc_bf16"]
     y = neigh_consensus(x, ws, bs, list(ch), symmetric=True)
+    assert _ext.DISPATCH["nc_bf16"] == before + 1     # the HIP autograd stack, not a fallback
     g = torch.randn_like(y)
     (y * g).sum().backward()
     xr = x.detach().double().requires_grad_(True)
@@ -245,19 +236,21 @@ def test_immatchnet_volumes_and_grads_match_reference_algorithm():
     assert max(errs) < 0.3, errs
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [2, 3])
 @pytest.mark.parametrize("ks,shape", [(5, (2, 6, 5, 25, 25)), (5, (1, 5, 4, 30, 27)), (3, (1, 4, 5, 9, 33)),
-                                      (5, (1, 2, 3, 7, 6))])
-def test_wgrad16_kernel(variant, ks, shape, monkeypatch):
+                                      (5, (1, 2, 3, 7, 6)), (7, (1, 3, 4, 25, 25)), (1, (1, 3, 4, 25, 26))])
+def test_wgrad16_kernel(variant, ks, shape):
     """Weight / bias gradient of a 16->16 Conv4d straight from the wgrad16
-    kernel (both variants; multi-tile K, L exercise the per-item halo), full
-    and dj-centre modes, vs autograd of the fp64 oracle."""
+    kernels (v3 sliding ring for KS 3/5 when the row fits, v2 per plane
+    offset; multi-tile K, L exercise the per-item halo), full and plane-only
+    modes, vs autograd of the fp64 oracle."""
     import importlib
     nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
-    monkeypatch.setattr(nc, "WGRAD_VARIANT", variant)
     C = _ext.ext()
     torch.manual_seed(11)
     V, I, J, K, L = shape
+    if variant == 3 and not nc.wgrad_v3_ok(shape, ks):
+        pytest.skip("wgrad16v3 needs KS 3/5 and L + KS - 1 <= 32")
     x = torch.rand(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
     g = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
     xr = x.double().permute(0, 5, 1, 2, 3, 4)
@@ -265,15 +258,20 @@ def test_wgrad16_kernel(variant, ks, shape, monkeypatch):
     yr = ref.conv4d(xr, wr, None)
     (yr * g.double().permute(0, 5, 1, 2, 3, 4)).sum().backward()
     dstd = ref.conv4d_weight_to_std(wr.grad)           # [co, ci, di, dj, dk, dl]
-    ng = nc.wgrad_groups(ks, V * I * J * ((K + 24) // 25) * ((L + 24) // 25))
-    s, sb = nc.wgrad16_partials(C, x, g, ks, ng, False)
-    dw = nc._reduce_wgrad16(s, ks, 16, 16)
+    if variant == 3:
+        ng = nc.wgrad_v3_groups(shape, ks)
+    else:
+        ng = nc.wgrad_groups(ks, nc._nitems(shape))
+    part = torch.empty((2 * ng, ks * ks, ks * ks, 16, 16), device=DEV)
+    partb = torch.empty((2 * ng, 16), device=DEV)
+    C.wgrad16(x, g, part, partb, ks, 0, variant)
+    dw = nc._reduce_wgrad16(part.sum(0), ks, 16, 16)
     assert relerr(dw, dstd) < 1e-3
-    assert relerr(sb, g.double().sum(dim=(0, 1, 2, 3, 4))) < 1e-3
-    sc, sbc = nc.wgrad16_partials(C, x, g, ks, ng, True)
-    dwc = nc._reduce_wgrad16_center(sc, ks)            # [co, ci, di, dk, dl]
-    assert relerr(dwc, dstd[:, :, :, ks // 2]) < 1e-3
-    assert relerr(sbc, sb) < 1e-5
+    assert relerr(partb.sum(0), g.double().sum(dim=(0, 1, 2, 3, 4))) < 1e-3
+    sp, sbp = nc.wgrad16_partials(C, x, g, ks, True)     # plane-only: the (P, P) offset
+    P = ks // 2
+    assert relerr(sp[0].permute(2, 1, 0).reshape(16, 16, ks, ks), dstd[:, :, P, P]) < 1e-3
+    assert relerr(sbp, partb.sum(0)) < 1e-5
 
 
 @pytest.mark.parametrize("flags", ["0", "1"])
@@ -281,7 +279,6 @@ def test_wgrad16v3_priority_flag(flags, monkeypatch):
     """wgrad16v3 with the waves-4..7 s_setprio tuning bit: same sums as the oracle."""
     import importlib
     nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
-    monkeypatch.setattr(nc, "WGRAD_VARIANT", 3)
     monkeypatch.setenv("NCNET_WGRAD_FLAGS", flags)
     torch.manual_seed(12)
     V, I, J, K, L, ks = 2, 6, 5, 25, 25, 5
@@ -289,22 +286,22 @@ def test_wgrad16v3_priority_flag(flags, monkeypatch):
     g = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
     wr = torch.zeros(ks, 16, 16, ks, ks, ks, device=DEV, dtype=torch.float64, requires_grad=True)
     (ref.conv4d(x.double().permute(0, 5, 1, 2, 3, 4), wr, None) * g.double().permute(0, 5, 1, 2, 3, 4)).sum().backward()
-    s, sb = nc.wgrad16_partials(_ext.ext(), x, g, ks, 1, False)
+    s, sb = nc.wgrad16_partials(_ext.ext(), x, g, ks, False)
     assert relerr(nc._reduce_wgrad16(s, ks, 16, 16), ref.conv4d_weight_to_std(wr.grad)) < 1e-3
     assert relerr(sb, g.double().sum(dim=(0, 1, 2, 3, 4))) < 1e-3
 
 
-@pytest.mark.parametrize("version", ["1", "2", "3", "4"])
 @pytest.mark.parametrize("ks,sgn,shape,dtype", [(5, 1, (2, 6, 7, 25, 25), torch.bfloat16),
                                                 (5, -1, (1, 5, 4, 9, 11), torch.float32),
                                                 (3, 1, (1, 4, 5, 30, 26), torch.bfloat16),
                                                 (3, -1, (2, 3, 3, 7, 5), torch.bfloat16),
-                                                (5, 1, (1, 3, 4, 40, 30), torch.bfloat16)])
-def test_ijpack_kernel(version, ks, sgn, shape, dtype, monkeypatch):
-    """ijpack (both kernel versions) vs the torch emulation of the ij encoding:
+                                                (5, 1, (1, 3, 4, 40, 30), torch.bfloat16),
+                                                (7, 1, (1, 8, 9, 6, 7), torch.bfloat16),
+                                                (1, -1, (1, 3, 4, 6, 7), torch.float32)])
+def test_ijpack_kernel(ks, sgn, shape, dtype):
+    """ijpack vs the torch emulation of the ij encoding:
     S[g][v,i,j,k,l,c] = X[v, i+sgn*(di-P), j+sgn*(dj-P), k, l], q = 16g + c."""
     from tests.test_kernel_emulation import _ijpack
-    monkeypatch.setenv("NCNET_IJPACK_V", version)
     torch.manual_seed(13)
     x = torch.randn(shape, device=DEV).to(dtype)
     G = (ks * ks + 15) // 16
@@ -410,7 +407,7 @@ def test_conv16_fp8_kernel(ks, shape):
     xr = x.double().permute(0, 5, 1, 2, 3, 4)
     yr = ref.conv4d(xr, ref.conv4d_weight_from_std(wr), b.double())
     y = torch.empty((V, I, J, K, L, 16), dtype=F8, device=DEV)
-    C.conv16f8_fwd(x, wq, b, y, ks, 1, 0, 1.0 / wsc)
+    C.conv16f8_fwd(x, wq, b, y, ks, 1, 1.0 / wsc)
     y_ref = torch.relu(yr).permute(0, 2, 3, 4, 5, 1)
     assert rel_l2(y.float(), y_ref) < 0.04          # e4m3 output rounding (3 mantissa bits)
     # planar fp32, group-plane mode with 2 groups at the (i, j) plane
@@ -419,7 +416,7 @@ def test_conv16_fp8_kernel(ks, shape):
     wpr = (wp * wsc).to(F8).double() / wsc
     x2 = (torch.rand(2, V, I, J, K, L, 16, device=DEV) * 2).to(F8)
     z = torch.empty((16, V, I, J, K, L), dtype=torch.float32, device=DEV)
-    C.conv16f8_fwd(x2, wpq, None, z, ks, 4, 0, 1.0 / wsc)
+    C.conv16f8_fwd(x2, wpq, None, z, ks, 4, 1.0 / wsc)
     xx = x2.double().permute(0, 1, 2, 3, 6, 4, 5).reshape(2, V * I * J, 16, K, L)
     zr = sum(torch.nn.functional.conv2d(xx[g], wpr[g], padding=ks // 2) for g in range(2))
     zr = zr.reshape(V, I, J, 16, K, L).permute(3, 0, 1, 2, 4, 5)
@@ -427,7 +424,8 @@ def test_conv16_fp8_kernel(ks, shape):
 
 
 def test_immatchnet_fp8_nc_path():
-    """corr_dtype='fp8' (fp8 correlation + fp8 NC) vs the bf16 path."""
+    """corr_dtype='fp8' (fp8 correlation + fp8 Conv4d NC kernels) vs the bf16
+    path; the dispatch counters prove which NC implementation ran."""
     from ncnet_amd.models import ImMatchNet
     torch.manual_seed(0)
     m = ImMatchNet(use_cuda=True, ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1],
@@ -438,9 +436,12 @@ def test_immatchnet_fp8_nc_path():
     batch = {"source_image": torch.randn(1, 3, 256, 320, device=DEV),
              "target_image": torch.randn(1, 3, 256, 320, device=DEV)}
     with torch.inference_mode():
+        n_fused, n_fp8 = _ext.DISPATCH["nc_fused_k3"], _ext.DISPATCH["nc_fp8"]
         c16, _ = m(batch)
+        assert _ext.DISPATCH["nc_fused_k3"] == n_fused + 1          # bf16: the fused InLoc kernel
         m.corr_dtype = "fp8"
         c8, _ = m(batch)
+        assert _ext.DISPATCH["nc_fp8"] == n_fp8 + 1                # fp8: the fp8 MFMA Conv4d path
     assert c8.shape == c16.shape
     assert rel_l2(c8, c16) < 0.15
 
@@ -465,10 +466,10 @@ def test_nc_forward_deterministic_and_fully_written():
     xs = torch.rand(2, 9, 11, 30, 27, 16, device=DEV).to(torch.bfloat16)
     w = pack_w16(torch.randn(16, 16, 5, 5, 5, 5, device=DEV) * 0.05)
     y = torch.full_like(xs, float("nan"))
-    C.conv16_fwd(xs, w, torch.zeros(16, device=DEV), None, y, 5, 1, 0)
+    C.conv16_fwd(xs, w, torch.zeros(16, device=DEV), None, y, 5, 1)
     assert torch.isfinite(y.float()).all()
-    z = torch.full((5, 2, 9, 11, 30, 27), float("nan"), device=DEV)
-    C.conv16_fwd(xs, w, None, None, z, 5, 3, 1)
+    z = torch.full((16, 2, 9, 11, 30, 27), float("nan"), device=DEV)
+    C.conv16_fwd(xs, w, None, None, z, 5, 4)
     assert torch.isfinite(z).all()
 
 
@@ -524,11 +525,11 @@ def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch):
     for tpw in ("1", "5", "3"):
         monkeypatch.setenv("NCNET_GP_TPW", tpw)
         y1 = torch.full(shape + (16,), float("nan"), device=DEV, dtype=torch.bfloat16)
-        C.conv16_fwd(xs, wp, b, None, y1, ks, 1, 0)
+        C.conv16_fwd(xs, wp, b, None, y1, ks, 1)
         y2 = torch.full(shape + (16,), float("nan"), device=DEV, dtype=torch.bfloat16)
-        C.conv16_fwd(xs, wp, None, m, y2, ks, 2, 0)
+        C.conv16_fwd(xs, wp, None, m, y2, ks, 2)
         z = torch.full((16,) + shape, float("nan"), device=DEV)
-        C.conv16_fwd(xs, wp, None, None, z, ks, 4, 0)
+        C.conv16_fwd(xs, wp, None, None, z, ks, 4)
         outs[tpw] = (y1, y2, z)
     for tpw in ("5", "3"):
         for a, r in zip(outs[tpw], outs["1"]):
@@ -541,24 +542,24 @@ def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch):
 def test_nontemporal_epilogue_stores_bitwise(monkeypatch):
     """NCNET_NT_STORE=1 (streaming epilogue stores) writes the same bytes as the
     default stores for the v3 16->16 conv, the ReLU-mask data gradient and the
-    planar fp32 dj-centre epilogue."""
-    from ncnet_amd.ops.packing import jc_out_weights, pack_w16
+    planar fp32 epilogue (ij-encoded Cout=1 partials)."""
+    from ncnet_amd.ops.packing import ij_out_weights, pack_w16, pack_w16_planes
     torch.manual_seed(16)
     C = _ext.ext()
     shape = (2, 6, 7, 25, 25)
     x = torch.rand(shape + (16,), device=DEV).to(torch.bfloat16)
     w = pack_w16(torch.randn(16, 16, 5, 5, 5, 5, device=DEV) * 0.05)
-    wz = pack_w16(jc_out_weights(torch.randn(1, 16, 5, 5, 5, 5, device=DEV) * 0.05))
+    wz = pack_w16_planes(ij_out_weights(torch.randn(1, 16, 5, 5, 5, 5, device=DEV) * 0.05))[:1]
     b = torch.randn(16, device=DEV) * 0.1
     outs = {}
     for nt in ("0", "1"):
         monkeypatch.setenv("NCNET_NT_STORE", nt)
         y = torch.full_like(x, float("nan"))
-        C.conv16_fwd(x, w, b, None, y, 5, 1, 0)
+        C.conv16_fwd(x, w, b, None, y, 5, 1)
         yd = torch.full_like(x, float("nan"))
-        C.conv16_fwd(x, w, None, x, yd, 5, 2, 0)
-        z = torch.full((5,) + shape, float("nan"), device=DEV)
-        C.conv16_fwd(x, wz, None, None, z, 5, 3, 1)
+        C.conv16_fwd(x, w, None, x, yd, 5, 2)
+        z = torch.full((16,) + shape, float("nan"), device=DEV)
+        C.conv16_fwd(x.unsqueeze(0), wz, None, None, z, 5, 4)
         outs[nt] = (y, yd, z)
     for a, r in zip(outs["1"], outs["0"]):
         assert not torch.isnan(a).any() and torch.equal(a, r)

@@ -8,7 +8,7 @@ import torch
 
 from ncnet_amd.ops import _ext
 from ncnet_amd.ops import reference as ref
-from ncnet_amd.ops.neigh_consensus import _stack_bwd, _stack_fwd, layer_kinds
+from ncnet_amd.ops.neigh_consensus import _stack_bwd, _stack_fwd, blocks_to_ncl, layer_kinds, planar_to_blocks
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -34,7 +34,8 @@ def grads(x, w_std, g):
     return x.grad, w.grad
 
 
-@pytest.mark.parametrize("ks,ch", [((5, 5, 5), (16, 16, 1)), ((3, 3), (16, 1))])
+@pytest.mark.parametrize("ks,ch", [((5, 5, 5), (16, 16, 1)), ((3, 3), (16, 1)), ((3, 3, 3), (10, 10, 1)),
+                                   ((5, 5), (32, 1)), ((7, 3), (16, 1)), ((1, 3), (16, 1)), ((3, 3), (20, 24))])
 def test_stack_stages_vs_quantized_oracle(ks, ch):
     torch.manual_seed(11)
     V, I, J, K, L = 3, 9, 8, 10, 11
@@ -56,14 +57,16 @@ def test_stack_stages_vs_quantized_oracle(ks, ch):
         pre = conv_fwd(hs[-1], w) + b.double().view(1, -1, 1, 1, 1, 1)
         act = torch.relu(pre)
         hs.append(act if li == len(ks) - 1 else q(act))
-    errs = {"z": rl2(z, hs[-1][:, 0])}
+    zl = z.unsqueeze(1) if ch[-1] == 1 else z.transpose(0, 1)      # [V, C, I, J, K, L]
+    errs = {"z": rl2(zl, hs[-1])}
     for li in range(1, len(ks)):
-        errs[f"h{li}"] = rl2(saved[li].permute(0, 5, 1, 2, 3, 4)[:, :ch[li - 1]], hs[li])
+        errs[f"h{li}"] = rl2(blocks_to_ncl(saved[li], ch[li - 1]), hs[li])
     # backward from a random gradient on z
-    gz = torch.randn_like(z)
-    g_last = (gz * (z > 0)).to(torch.bfloat16)
+    gz = torch.randn_like(zl)
+    gm = gz * (zl > 0)
+    g_last = gm[:, 0].to(torch.bfloat16) if ch[-1] == 1 else planar_to_blocks(gm.transpose(0, 1))
     dws, dbs, gx0 = _stack_bwd(g_last, saved, ws_ref, kinds, list(ch), True)
-    g = q(gz.double() * (hs[-1][:, 0] > 0)).unsqueeze(1)
+    g = q(gz.double() * (hs[-1] > 0))
     for li in range(len(ks) - 1, -1, -1):
         gx, gw = grads(hs[li], ws_std[li], g)
         errs[f"dw{li}"] = rl2(ref.conv4d_weight_to_std(dws[li]), gw)

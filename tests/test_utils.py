@@ -45,10 +45,9 @@ def test_plot_roundtrip(tmp_path):
 
 def test_runtime_config_from_env():
     from ncnet_amd.config import RuntimeConfig
-    c = RuntimeConfig.from_env({"NCNET_NC_ENC": "jc", "NCNET_WGRAD_VARIANT": "2", "NCNET_TRUNK_GRAPH": "0"})
-    assert c.nc_encoding == "jc" and c.wgrad_variant == 2 and not c.trunk_graph and c.trunk_plan
-    assert RuntimeConfig.from_env({"NCNET_NC_JC": "0"}).nc_encoding == "direct"
-    assert set(c.as_dict()) >= {"nc_encoding", "wgrad_variant", "conv16_variant"}
+    c = RuntimeConfig.from_env({"NCNET_TRUNK_GRAPH": "0", "NCNET_BWD_OVERLAP": "0"})
+    assert c.nc_encoding == "ij" and not c.trunk_graph and c.trunk_plan and not c.bwd_overlap
+    assert set(c.as_dict()) >= {"nc_encoding", "trunk_prefetch", "allow_torch_fallback"}
 
 
 def test_segment_timer_cpu():
