@@ -17,21 +17,21 @@ int ncnet_conv16f8_fwd(const void*, const void*, const float*, void*, int, int, 
 int ncnet_ijsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_bias_act(void*, const float*, long long, int, int, hipStream_t);
 int ncnet_conv2d_nhwc(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, hipStream_t);
+int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, void*, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
 int ncnet_corr_gemm(const void*, const void*, void*, const int*, const int*, int, int, int, int, long long, long long,
                     long long, int, float, hipStream_t);
 int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, int, int, int, int, long long, long long,
                           float, hipStream_t);
-int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, hipStream_t);
-int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, float*, int, hipStream_t);
+int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, int, hipStream_t);
+int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, float*, int, int, hipStream_t);
 int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, hipStream_t);
 int ncnet_mm_bwd(const float*, const float*, const float*, const int*, const float*, const int*, float*, float*, float*,
                  int, int, int, float, hipStream_t);
 int ncnet_combine_fwd(const float*, float*, int, int, int, hipStream_t);
 int ncnet_combine_bwd(const float*, const float*, void*, int, int, int, hipStream_t);
 int ncnet_softmax_max_bwd(const float*, const float*, const int*, const float*, const float*, const int*, const float*,
-                          const float*, const float*, float*, int, int, int, hipStream_t);
+                          const float*, const float*, float*, int, int, int, int, float, hipStream_t);
 int ncnet_maxpool4d(const void*, int, float*, uint8_t*, int, int, int, int, int, int, hipStream_t);
 int ncnet_transpose(const void*, void*, int, int, int, int, hipStream_t);
 int ncnet_nonfinite_count(const float*, long long, int*, hipStream_t);
@@ -151,8 +151,9 @@ void ijsum(Tensor Z, c10::optional<Tensor> bias, Tensor y, int64_t ks, int64_t r
                  Z.size(4), Z.size(5), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z)), "ijsum");
 }
 
-// y: bf16, or OCP fp8 e4m3 holding fp8_scale * x / ||x|| (fp8_scale > 0)
-void l2norm_rows(Tensor x, Tensor y, c10::optional<Tensor> inv, double fp8_scale) {
+// y: bf16, or OCP fp8 e4m3 holding fp8_scale * x / ||x|| (fp8_scale > 0);
+// y_lo (bf16 y only): the rounding residual bf16(x / ||x|| - y) (bf16x3 mode)
+void l2norm_rows(Tensor x, Tensor y, c10::optional<Tensor> inv, double fp8_scale, c10::optional<Tensor> y_lo) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.is_cuda() && x.is_contiguous());
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat);
@@ -161,9 +162,14 @@ void l2norm_rows(Tensor x, Tensor y, c10::optional<Tensor> inv, double fp8_scale
   TORCH_CHECK(!f8 || fp8_scale > 0, "fp8 output needs fp8_scale > 0");
   TORCH_CHECK(x.dim() == 2 && y.sizes() == x.sizes(), "x,y must be [rows, C]");
   if (inv.has_value()) { check(*inv, "inv", at::kFloat); check_shape(*inv, "inv", {x.size(0)}); }
+  if (y_lo.has_value()) {
+    TORCH_CHECK(!f8, "l2norm_rows: y_lo needs bf16 y");
+    check(*y_lo, "y_lo", at::kBFloat16); check_shape(*y_lo, "y_lo", y.sizes().vec());
+  }
   ok(ncnet_l2norm_rows(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(),
                        inv.has_value() ? (float*)inv->data_ptr() : nullptr, x.size(0), x.size(1),
-                       f8 ? (float)fp8_scale : 0.f, cur_stream(x)), "l2norm");
+                       f8 ? (float)fp8_scale : 0.f, y_lo.has_value() ? y_lo->data_ptr() : nullptr, cur_stream(x)),
+     "l2norm");
 }
 
 void l2norm_rows_bwd(Tensor x, Tensor g, Tensor inv, Tensor gx) {
@@ -220,8 +226,9 @@ void corr_gemm_pool2(Tensor A, Tensor B, Tensor val, Tensor idx, int64_t hA, int
      "corr_gemm_pool2");
 }
 
-// x [V,R,C] fp32 -> per-row (dim 2) stats [V,R]
-void stats_rows(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Tensor> se) {
+// x [V,R,C] fp32 -> per-row (dim 2) stats [V,R]: max, first argmax, and se =
+// sum exp(x - max) (sum_kind 1) or the plain sum (sum_kind 2)
+void stats_rows(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Tensor> se, int64_t sum_kind) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check(x, "x", at::kFloat); check(mx, "mx", at::kFloat);
   TORCH_CHECK(x.dim() == 3);
@@ -229,12 +236,13 @@ void stats_rows(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Te
   if (arg.has_value()) { check(*arg, "arg", at::kInt); check_shape(*arg, "arg", {x.size(0), x.size(1)}); }
   if (se.has_value()) { check(*se, "se", at::kFloat); check_shape(*se, "se", {x.size(0), x.size(1)}); }
   ok(ncnet_stats_rows((float*)x.data_ptr(), (float*)mx.data_ptr(), arg.has_value() ? (int*)arg->data_ptr() : nullptr,
-                      se.has_value() ? (float*)se->data_ptr() : nullptr, x.size(0) * x.size(1), x.size(2), cur_stream(x)),
+                      se.has_value() ? (float*)se->data_ptr() : nullptr, x.size(0) * x.size(1), x.size(2),
+                      (int)sum_kind, cur_stream(x)),
      "stats_rows");
 }
 
-// x [V,R,C] fp32 -> per-column (dim 1) stats [V,C]
-void stats_cols(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Tensor> se) {
+// x [V,R,C] fp32 -> per-column (dim 1) stats [V,C] (sum_kind as stats_rows)
+void stats_cols(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Tensor> se, int64_t sum_kind) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check(x, "x", at::kFloat); check(mx, "mx", at::kFloat);
   TORCH_CHECK(x.dim() == 3);
@@ -250,7 +258,7 @@ void stats_cols(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Te
   if (nchunk > 1) work = at::empty({3 * V * nchunk * C}, x.options());
   ok(ncnet_stats_cols((float*)x.data_ptr(), (float*)mx.data_ptr(), arg.has_value() ? (int*)arg->data_ptr() : nullptr,
                       se.has_value() ? (float*)se->data_ptr() : nullptr, V, R, C,
-                      nchunk > 1 ? (float*)work.data_ptr() : nullptr, (int)nchunk, cur_stream(x)),
+                      nchunk > 1 ? (float*)work.data_ptr() : nullptr, (int)nchunk, (int)sum_kind, cur_stream(x)),
      "stats_cols");
 }
 
@@ -303,11 +311,13 @@ void combine_bwd(Tensor g, Tensor z, Tensor gz, int64_t R, int64_t C) {
   ok(ncnet_combine_bwd((float*)g.data_ptr(), (float*)z.data_ptr(), gz.data_ptr(), Vh, R, C, cur_stream(z)), "combine_bwd");
 }
 
+// norm: 1 'softmax', 2 'l1' (eps), 0 None -- rse / cse from stats with the matching sum_kind
 void softmax_max_bwd(Tensor x, Tensor rmax, Tensor rarg, Tensor rse, Tensor cmax, Tensor carg, Tensor cse, Tensor wr,
-                     Tensor wc, Tensor gx) {
+                     Tensor wc, Tensor gx, int64_t norm, double eps) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check(x, "x", at::kFloat); check(gx, "gx", at::kFloat);
   TORCH_CHECK(x.dim() == 3 && gx.sizes() == x.sizes());
+  TORCH_CHECK(norm >= 0 && norm <= 2, "softmax_max_bwd: norm must be 0 (None), 1 (softmax) or 2 (l1)");
   const int64_t V = x.size(0), R = x.size(1), C = x.size(2);
   check(rmax, "rmax", at::kFloat); check(rse, "rse", at::kFloat); check(rarg, "rarg", at::kInt);
   check(cmax, "cmax", at::kFloat); check(cse, "cse", at::kFloat); check(carg, "carg", at::kInt);
@@ -317,7 +327,8 @@ void softmax_max_bwd(Tensor x, Tensor rmax, Tensor rarg, Tensor rse, Tensor cmax
   check_shape(wr, "wr", {V}); check_shape(wc, "wc", {V});
   ok(ncnet_softmax_max_bwd((float*)x.data_ptr(), (float*)rmax.data_ptr(), (int*)rarg.data_ptr(), (float*)rse.data_ptr(),
                            (float*)cmax.data_ptr(), (int*)carg.data_ptr(), (float*)cse.data_ptr(), (float*)wr.data_ptr(),
-                           (float*)wc.data_ptr(), (float*)gx.data_ptr(), V, R, C, cur_stream(x)), "softmax_max_bwd");
+                           (float*)wc.data_ptr(), (float*)gx.data_ptr(), V, R, C, (int)norm, (float)eps,
+                           cur_stream(x)), "softmax_max_bwd");
 }
 
 void maxpool4d(Tensor x, Tensor y, Tensor code, int64_t ks) {

@@ -2,7 +2,9 @@
 //
 // l2norm_rows: y = x / sqrt(sum_c x^2 + 1e-6) over the contiguous channel axis
 //   of a channels-last feature map (lib/model.py:14-17), written as bf16 in the
-//   [B, H*W, C] layout the correlation GEMM consumes (one pass, one wave/row).
+//   [B, H*W, C] layout the correlation GEMM consumes (one pass, one wave/row);
+//   optionally also y_lo = bf16(y - y_hi) (the fp32-accurate "bf16x3" mode:
+//   A.B ~ Ahi.Bhi + Ahi.Blo + Alo.Bhi on three bf16 GEMMs, ~16 mantissa bits).
 //
 // corr_gemm: C[b] = A[amap[b]] . B[bmap[b]]^T, A:[M,K], B:[N,K] bf16 row-major,
 //   fp32 accumulate, fp32 or bf16 output (lib/model.py:106-115, '4D' mode).
@@ -22,7 +24,7 @@ namespace ncnet {
 template <typename TIN, bool FP8>
 __global__ __launch_bounds__(256) void l2norm_rows_kernel(const TIN* __restrict__ x, void* __restrict__ yv,
                                                           float* __restrict__ inv_norm, int rows, int C,
-                                                          float out_scale) {
+                                                          float out_scale, bf16* __restrict__ ylo) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -63,14 +65,24 @@ __global__ __launch_bounds__(256) void l2norm_rows_kernel(const TIN* __restrict_
     return;
   }
   bf16* yr = (bf16*)yv + (size_t)row * C;
+  bf16* lr = ylo ? ylo + (size_t)row * C : nullptr;
   for (int c = lane * 8; c < C; c += 512) {
     if (c + 8 <= C) {
-      bf16x8 o;
+      bf16x8 o, lo;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf((float)xr[c + e] * inv);
+      for (int e = 0; e < 8; ++e) {
+        const float v = (float)xr[c + e] * inv;
+        o[e] = f2bf(v);
+        lo[e] = f2bf(v - (float)o[e]);
+      }
       *(bf16x8*)(yr + c) = o;
+      if (lr) *(bf16x8*)(lr + c) = lo;
     } else {
-      for (int e = 0; c + e < C; ++e) yr[c + e] = f2bf((float)xr[c + e] * inv);
+      for (int e = 0; c + e < C; ++e) {
+        const float v = (float)xr[c + e] * inv;
+        yr[c + e] = f2bf(v);
+        if (lr) lr[c + e] = f2bf(v - (float)yr[c + e]);
+      }
     }
   }
 }
@@ -276,17 +288,18 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
 
 using namespace ncnet;
 
-// y dtype: bf16 (fp8_scale == 0) or OCP fp8 e4m3 scaled by fp8_scale.
+// y dtype: bf16 (fp8_scale == 0; ylo: optional low half) or OCP fp8 e4m3 scaled by fp8_scale.
 extern "C" int ncnet_l2norm_rows(const void* x, int x_is_bf16, void* y, float* inv_norm, int rows, int C,
-                                 float fp8_scale, hipStream_t stream) {
+                                 float fp8_scale, void* ylo, hipStream_t stream) {
+  bf16* lo = (bf16*)ylo;
   dim3 grid((unsigned)cdiv(rows, 4)), block(256);
   const bool f8 = fp8_scale != 0.f;
   if (x_is_bf16) {
-    if (f8) hipLaunchKernelGGL((l2norm_rows_kernel<bf16, true>), grid, block, 0, stream, (const bf16*)x, y, inv_norm, rows, C, fp8_scale);
-    else hipLaunchKernelGGL((l2norm_rows_kernel<bf16, false>), grid, block, 0, stream, (const bf16*)x, y, inv_norm, rows, C, 1.f);
+    if (f8) hipLaunchKernelGGL((l2norm_rows_kernel<bf16, true>), grid, block, 0, stream, (const bf16*)x, y, inv_norm, rows, C, fp8_scale, nullptr);
+    else hipLaunchKernelGGL((l2norm_rows_kernel<bf16, false>), grid, block, 0, stream, (const bf16*)x, y, inv_norm, rows, C, 1.f, lo);
   } else {
-    if (f8) hipLaunchKernelGGL((l2norm_rows_kernel<float, true>), grid, block, 0, stream, (const float*)x, y, inv_norm, rows, C, fp8_scale);
-    else hipLaunchKernelGGL((l2norm_rows_kernel<float, false>), grid, block, 0, stream, (const float*)x, y, inv_norm, rows, C, 1.f);
+    if (f8) hipLaunchKernelGGL((l2norm_rows_kernel<float, true>), grid, block, 0, stream, (const float*)x, y, inv_norm, rows, C, fp8_scale, nullptr);
+    else hipLaunchKernelGGL((l2norm_rows_kernel<float, false>), grid, block, 0, stream, (const float*)x, y, inv_norm, rows, C, 1.f, lo);
   }
   return (int)hipGetLastError();
 }

@@ -2,7 +2,8 @@
 // [V, R = I*J (A positions), C = K*L (B positions)] of fp32.
 //
 //  * stats_rows / stats_cols: max, first-argmax and (optionally) sum exp(x-max)
-//    per row / column in one pass (online softmax).  Used by MutualMatching
+//    (online softmax) or the plain sum (the weak loss's 'l1' normalisation)
+//    per row / column in one pass.  Used by MutualMatching
 //    (lib/model.py:163-166), the weak loss (train.py:125-134) and
 //    corr_to_matches (lib/point_tnf.py:32-57).
 //  * mm_apply: MutualMatching output c*((c/(maxB+eps))*(c/(maxA+eps))); can
@@ -11,7 +12,8 @@
 //  * mm_bwd: gradient of MutualMatching including the max-routed terms.
 //  * combine: y = z1 + z2^T (the symmetric-branch un-swap + add) and its
 //    backward fused with the last Conv4d's ReLU mask.
-//  * softmax_max_bwd: backward of the weak-loss score (closed form).
+//  * softmax_max_bwd: backward of the weak-loss score (closed form) for the
+//    'softmax', 'l1' and None normalisations (train.py:111-116).
 //  * maxpool4d: stride = kernel = ks 4D max pool + packed 2-bit offsets.
 #include "common.h"
 
@@ -19,24 +21,28 @@ namespace ncnet {
 
 struct Stat { float m; float s; int idx; };
 
-__device__ __forceinline__ Stat stat_merge(Stat a, Stat b, bool want_sum) {
+// sum kind: 0 none, 1 sum exp(x - max) (online softmax), 2 plain sum
+__device__ __forceinline__ Stat stat_merge(Stat a, Stat b, int want_sum) {
   Stat r;
   bool take_b = (b.m > a.m) || (b.m == a.m && b.idx < a.idx);
   r.m = take_b ? b.m : a.m;
   r.idx = take_b ? b.idx : a.idx;
-  if (want_sum) {
+  if (want_sum == 1) {
     float sa = (a.s == 0.f) ? 0.f : a.s * __expf(a.m - r.m);
     float sb = (b.s == 0.f) ? 0.f : b.s * __expf(b.m - r.m);
     r.s = sa + sb;
+  } else if (want_sum == 2) {
+    r.s = a.s + b.s;
   } else r.s = 0.f;
   return r;
 }
 
-__device__ __forceinline__ Stat stat_push(Stat a, float x, int idx, bool want_sum) {
+__device__ __forceinline__ Stat stat_push(Stat a, float x, int idx, int want_sum) {
+  if (want_sum == 2) a.s += x;
   if (x > a.m) {
-    if (want_sum) a.s = a.s * __expf(a.m - x) + 1.f;
+    if (want_sum == 1) a.s = a.s * __expf(a.m - x) + 1.f;
     a.m = x; a.idx = idx;
-  } else if (want_sum) {
+  } else if (want_sum == 1) {
     a.s += __expf(x - a.m);
   }
   return a;
@@ -45,12 +51,12 @@ __device__ __forceinline__ Stat stat_push(Stat a, float x, int idx, bool want_su
 // One wave per row.
 __global__ __launch_bounds__(256) void stats_rows_kernel(const float* __restrict__ x, float* __restrict__ mx,
                                                          int* __restrict__ arg, float* __restrict__ se,
-                                                         long long rows, int C) {
+                                                         long long rows, int C, int sum_kind) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const float* xr = x + row * C;
-  const bool ws = se != nullptr;
+  const int ws = se != nullptr ? sum_kind : 0;
   Stat st{-INFINITY, 0.f, 0x7fffffff};
   for (int c = lane; c < C; c += 64) st = stat_push(st, xr[c], c, ws);
 #pragma unroll
@@ -74,7 +80,7 @@ __global__ __launch_bounds__(256) void stats_rows_kernel(const float* __restrict
 // so a short-and-wide volume (InLoc: V = 1, C = 7500) still fills the chip.
 __global__ __launch_bounds__(256) void stats_cols_kernel(const float* __restrict__ x, float* __restrict__ mx,
                                                          int* __restrict__ arg, float* __restrict__ se,
-                                                         int R, int C, int nchunk, int rpc) {
+                                                         int R, int C, int nchunk, int rpc, int sum_kind) {
   __shared__ float sm[4][64], ss[4][64];
   __shared__ int si[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -82,7 +88,7 @@ __global__ __launch_bounds__(256) void stats_cols_kernel(const float* __restrict
   const int chunk = blockIdx.x % nchunk, rest = blockIdx.x / nchunk;
   const int v = rest / ncb, cb = rest % ncb;
   const int c = cb * 64 + lane;
-  const bool ws = se != nullptr;
+  const int ws = se != nullptr ? sum_kind : 0;
   const int r0 = chunk * rpc, r1 = min(R, r0 + rpc);
   Stat st{-INFINITY, 0.f, 0x7fffffff};
   if (c < C) {
@@ -105,11 +111,11 @@ __global__ __launch_bounds__(256) void stats_cols_kernel(const float* __restrict
 __global__ __launch_bounds__(256) void stats_cols_merge_kernel(const float* __restrict__ pm, const int* __restrict__ pi,
                                                                const float* __restrict__ ps, float* __restrict__ mx,
                                                                int* __restrict__ arg, float* __restrict__ se, int V,
-                                                               int C, int nchunk) {
+                                                               int C, int nchunk, int sum_kind) {
   const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
   if (e >= (long long)V * C) return;
   const int v = (int)(e / C), c = (int)(e % C);
-  const bool ws = se != nullptr;
+  const int ws = se != nullptr ? sum_kind : 0;
   Stat a{-INFINITY, 0.f, 0x7fffffff};
   for (int k = 0; k < nchunk; ++k) {
     const size_t o = ((size_t)v * nchunk + k) * C + c;
@@ -287,27 +293,40 @@ __global__ __launch_bounds__(256) void combine_bwd_kernel(const float* __restric
 // Weak-loss score backward (softmax normalisation):
 //   s = max softmax = 1/sumexp; ds/dx_j = s (delta_{j,argmax} - softmax_j)
 // g = wr[v] * ds_row/dx + wc[v] * ds_col/dx
+// norm 1 'softmax': s = 1 / sum exp(x - max), ds/dx_j = s (delta_{j,argmax} - softmax_j)
+// norm 2 'l1':      s = max / (sum + eps),     ds/dx_j = delta_{j,argmax} / D - max / D^2
+// norm 0 None:      s = max,                   ds/dx_j = delta_{j,argmax}
+// (rse / cse hold the row / column sum exp for 'softmax', the plain sum for 'l1')
 __global__ __launch_bounds__(256) void softmax_max_bwd_kernel(const float* __restrict__ x,
                                                               const float* __restrict__ rmax, const int* __restrict__ rarg,
                                                               const float* __restrict__ rse,
                                                               const float* __restrict__ cmax, const int* __restrict__ carg,
                                                               const float* __restrict__ cse,
                                                               const float* __restrict__ wr, const float* __restrict__ wc,
-                                                              float* __restrict__ gx, long long total, int R, int C) {
+                                                              float* __restrict__ gx, long long total, int R, int C,
+                                                              int norm, float eps) {
   long long e = (long long)blockIdx.x * 256 + threadIdx.x;
   if (e >= total) return;
   const int k = (int)(e % C);
   const long long row = e / C;
   const int r = (int)(row % R);
   const int v = (int)(row / R);
-  const float xv = x[e];
-  const float sr = 1.f / rse[row];
   const size_t ci = (size_t)v * C + k;
-  const float sc = 1.f / cse[ci];
-  const float pr = __expf(xv - rmax[row]) * sr;
-  const float pc = __expf(xv - cmax[ci]) * sc;
-  float gr = wr[v] * sr * (((rarg[row] == k) ? 1.f : 0.f) - pr);
-  gr += wc[v] * sc * (((carg[ci] == r) ? 1.f : 0.f) - pc);
+  const float dr = (rarg[row] == k) ? 1.f : 0.f, dc = (carg[ci] == r) ? 1.f : 0.f;
+  float gr;
+  if (norm == 1) {
+    const float xv = x[e];
+    const float sr = 1.f / rse[row];
+    const float sc = 1.f / cse[ci];
+    const float pr = __expf(xv - rmax[row]) * sr;
+    const float pc = __expf(xv - cmax[ci]) * sc;
+    gr = wr[v] * sr * (dr - pr) + wc[v] * sc * (dc - pc);
+  } else if (norm == 2) {
+    const float ir = 1.f / (rse[row] + eps), ic = 1.f / (cse[ci] + eps);
+    gr = wr[v] * ir * (dr - rmax[row] * ir) + wc[v] * ic * (dc - cmax[ci] * ic);
+  } else {
+    gr = wr[v] * dr + wc[v] * dc;
+  }
   gx[e] = gr;
 }
 
@@ -368,24 +387,27 @@ using namespace ncnet;
 
 static unsigned tiles64(int V, int R, int C) { return (unsigned)((long long)V * cdiv(R, 64) * cdiv(C, 64)); }
 
-extern "C" int ncnet_stats_rows(const float* x, float* mx, int* arg, float* se, long long rows, int C, hipStream_t s) {
-  hipLaunchKernelGGL(stats_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, mx, arg, se, rows, C);
+// sum_kind: 1 sum exp(x - max), 2 plain sum (only when se != nullptr)
+extern "C" int ncnet_stats_rows(const float* x, float* mx, int* arg, float* se, long long rows, int C, int sum_kind,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(stats_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, mx, arg, se, rows, C,
+                     sum_kind);
   return (int)hipGetLastError();
 }
 // work: nullptr (nchunk = 1) or 3 * V * nchunk * C floats of partials.
 extern "C" int ncnet_stats_cols(const float* x, float* mx, int* arg, float* se, int V, int R, int C, float* work,
-                                int nchunk, hipStream_t s) {
+                                int nchunk, int sum_kind, hipStream_t s) {
   if (nchunk <= 1 || work == nullptr) {
-    hipLaunchKernelGGL(stats_cols_kernel, dim3((unsigned)(V * cdiv(C, 64))), dim3(256), 0, s, x, mx, arg, se, R, C, 1, R);
+    hipLaunchKernelGGL(stats_cols_kernel, dim3((unsigned)(V * cdiv(C, 64))), dim3(256), 0, s, x, mx, arg, se, R, C, 1, R, sum_kind);
     return (int)hipGetLastError();
   }
   const size_t n = (size_t)V * nchunk * C;
   float* pm = work; int* pi = (int*)(work + n); float* ps = work + 2 * n;
   const int rpc = cdiv(R, nchunk);
   hipLaunchKernelGGL(stats_cols_kernel, dim3((unsigned)(V * cdiv(C, 64) * nchunk)), dim3(256), 0, s, x, pm, pi,
-                     se ? ps : nullptr, R, C, nchunk, rpc);
+                     se ? ps : nullptr, R, C, nchunk, rpc, sum_kind);
   hipLaunchKernelGGL(stats_cols_merge_kernel, dim3((unsigned)cdiv(V * C, 256)), dim3(256), 0, s, pm, pi,
-                     se ? ps : nullptr, mx, arg, se, V, C, nchunk);
+                     se ? ps : nullptr, mx, arg, se, V, C, nchunk, sum_kind);
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_mm_apply(const float* c, const float* rmax, const float* cmax, float* out_f32, void* out_x,
@@ -417,10 +439,11 @@ extern "C" int ncnet_combine_bwd(const float* g, const float* z, void* gz, int V
 }
 extern "C" int ncnet_softmax_max_bwd(const float* x, const float* rmax, const int* rarg, const float* rse,
                                      const float* cmax, const int* carg, const float* cse, const float* wr,
-                                     const float* wc, float* gx, int V, int R, int C, hipStream_t s) {
+                                     const float* wc, float* gx, int V, int R, int C, int norm, float eps,
+                                     hipStream_t s) {
   long long total = (long long)V * R * C;
   hipLaunchKernelGGL(softmax_max_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, rmax, rarg, rse,
-                     cmax, carg, cse, wr, wc, gx, total, R, C);
+                     cmax, carg, cse, wr, wc, gx, total, R, C, norm, eps);
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_maxpool4d(const void* x, int x_is_bf16, float* y, uint8_t* code, int V, int I, int J, int K,

@@ -156,3 +156,58 @@ def synthetic_batch(batch: int, image_size=(400, 400), device="cpu", seed: int =
     src = torch.randn(batch, 3, h, w, generator=g, device=device)
     tgt = torch.randn(batch, 3, h, w, generator=g, device=device)
     return {"source_image": src, "target_image": tgt}
+
+
+def _smooth_texture(n: int, size: int, g: torch.Generator, device) -> torch.Tensor:
+    """[n, 3, size, size] smooth random colour textures (sum of upsampled noise
+    octaves), roughly ImageNet-normalised."""
+    out = torch.zeros(n, 3, size, size, device=device)
+    for cells, amp in ((6, 1.0), (12, 0.6), (24, 0.35), (48, 0.2)):
+        noise = torch.randn(n, 3, cells, cells, generator=g, device=device)
+        out += amp * torch.nn.functional.interpolate(noise, size=(size, size), mode="bicubic", align_corners=True)
+    return out / out.flatten(1).std(1).view(n, 1, 1, 1)
+
+
+def synthetic_correspondence_batch(batch: int, size: int, device="cpu", seed: int = 0, n_points: int = 20,
+                                   max_shift: float = 0.15, max_rot_deg: float = 10.0, scale_range=(0.9, 1.1)):
+    """Image pairs with a KNOWN dense correspondence (training-quality checks).
+
+    A smooth texture is drawn on a 1.5x canvas; the source is its centre crop and
+    the target samples the canvas through a random similarity transform
+    (rotation, scale, shift), so target pixel p_t shows source pixel
+    p_s = A (p_t - c) + c + t.  Keypoints are drawn in the target where p_s
+    lands inside the source (PF-Pascal layout: [b, 2, n_points], -1 padded;
+    ``L_pck`` = image size).  Everything is generated on ``device``."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    canvas = int(round(1.5 * size))
+    tex = _smooth_texture(batch, canvas, g, device)
+    off = (canvas - size) / 2.0
+    src = tex[:, :, int(off):int(off) + size, int(off):int(off) + size]
+    u = lambda *s: torch.rand(*s, generator=g, device=device)  # noqa: E731
+    ang = (u(batch) * 2 - 1) * max_rot_deg * 3.141592653589793 / 180
+    sc = scale_range[0] + u(batch) * (scale_range[1] - scale_range[0])
+    sh = (u(batch, 2) * 2 - 1) * max_shift * size
+    A = torch.stack([torch.stack([sc * torch.cos(ang), -sc * torch.sin(ang)], -1),
+                     torch.stack([sc * torch.sin(ang), sc * torch.cos(ang)], -1)], 1)      # [b, 2, 2] on (x, y)
+    c = (size - 1) / 2.0
+    ys, xs = torch.meshgrid(torch.arange(size, device=device, dtype=torch.float32),
+                            torch.arange(size, device=device, dtype=torch.float32), indexing="ij")
+    pt = torch.stack((xs, ys), -1).view(1, -1, 2) - c                                    # target pixels, centred
+    ps = torch.einsum("bij,bnj->bni", A, pt.expand(batch, -1, -1)) + c + sh.view(batch, 1, 2)
+    grid = (ps + off) / (canvas - 1) * 2 - 1                                               # canvas coords (align_corners)
+    tgt = torch.nn.functional.grid_sample(tex, grid.view(batch, size, size, 2), mode="bilinear",
+                                          padding_mode="border", align_corners=True)
+    # keypoints: target points whose source correspondence is inside the source image
+    cand = u(batch, 4 * n_points, 2) * (size - 1)
+    cs = torch.einsum("bij,bnj->bni", A, cand - c) + c + sh.view(batch, 1, 2)
+    ok = ((cs >= 0) & (cs <= size - 1)).all(-1)
+    tp = torch.full((batch, 2, n_points), -1.0, device=device)
+    sp = torch.full((batch, 2, n_points), -1.0, device=device)
+    for i in range(batch):
+        idx = torch.nonzero(ok[i]).view(-1)[:n_points]
+        tp[i, :, :idx.numel()] = cand[i, idx].t()
+        sp[i, :, :idx.numel()] = cs[i, idx].t()
+    sz = torch.tensor([float(size), float(size), 3.0], device=device).expand(batch, 3)
+    return {"source_image": src.contiguous(), "target_image": tgt.contiguous(), "source_points": sp,
+            "target_points": tp, "source_im_size": sz, "target_im_size": sz,
+            "L_pck": torch.full((batch, 1), float(size), device=device)}

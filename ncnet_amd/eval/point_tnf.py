@@ -32,9 +32,9 @@ def _best(mat: torch.Tensor, dim: int, do_softmax: bool):
         arg = torch.empty((b, n), dtype=torch.int32, device=x.device)
         se = torch.empty((b, n), dtype=torch.float32, device=x.device) if do_softmax else None
         if dim == 1:
-            _ext.ext().stats_cols(x, mx, arg, se)
+            _ext.ext().stats_cols(x, mx, arg, se, 1)
         else:
-            _ext.ext().stats_rows(x, mx, arg, se)
+            _ext.ext().stats_rows(x, mx, arg, se, 1)
         score = (1.0 / se) if do_softmax else mx
         return score, arg.long()
     v = torch.softmax(mat, dim=dim) if do_softmax else mat

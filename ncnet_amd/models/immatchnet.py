@@ -23,7 +23,8 @@ import torch.nn.functional as F
 
 from ..ops import reference as ref
 from ..ops.conv4d import Conv4d
-from ..ops.correlation import correlation, correlation_pool2, l2norm_pack, l2norm_pack_fp8, maxpool4d as _maxpool4d
+from ..ops.correlation import (correlation, correlation_pool2, correlation_x3, l2norm_pack, l2norm_pack_fp8,
+                               l2norm_pack_split, maxpool4d as _maxpool4d)
 from ..ops.mutual import mutual_matching
 from ..ops.neigh_consensus import neigh_consensus
 from ..utils.timing import segment
@@ -153,7 +154,7 @@ class NeighConsensus(nn.Module):
         ws = [m.weight_ref() for m in layers]
         bs = [m.bias if m.bias is not None else torch.zeros(m.out_channels, device=x.device) for m in layers]
         return neigh_consensus(x, ws, bs, self.channels, symmetric=self.symmetric_mode,
-                               fp8=getattr(self, "fp8", False))
+                               fp8=getattr(self, "fp8", False), precision=getattr(self, "precision", "bf16"))
 
 
 def _load_reference_checkpoint(path: str):
@@ -201,10 +202,12 @@ class ImMatchNet(nn.Module):
         self.half_precision = half_precision
         self.compute_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype]
         self.fold_bn = fold_bn
-        if corr_dtype not in ("bf16", "fp8"):
-            raise ValueError("corr_dtype must be 'bf16' or 'fp8'")
+        if corr_dtype not in ("bf16", "fp8", "fp32"):
+            raise ValueError("corr_dtype must be 'bf16', 'fp8' or 'fp32'")
         # fp8: OCP e4m3 correlation operands on the MX-fp8 MFMA and fp8
-        # NeighConsensus (fp8 MFMA Conv4d) -- inference only
+        # NeighConsensus (fp8 MFMA Conv4d) -- inference only.
+        # fp32: fp32-accurate correlation + NeighConsensus (bf16x3 split on the
+        # bf16 MFMA kernels), the reference's evaluation precision -- inference only
         self.corr_dtype = corr_dtype
         self.FeatureExtraction = FeatureExtraction(train_fe=train_fe, feature_extraction_cnn=feature_extraction_cnn,
                                                    feature_extraction_model_file=feature_extraction_model_file or "",
@@ -244,6 +247,10 @@ class ImMatchNet(nn.Module):
             if torch.is_grad_enabled() and self.training:
                 raise RuntimeError("corr_dtype='fp8' is an inference path (no autograd)")
             return l2norm_pack_fp8(f), tuple(f.shape[-2:])
+        if self.corr_dtype == "fp32":
+            if torch.is_grad_enabled() and self.training:
+                raise RuntimeError("corr_dtype='fp32' is an inference path (no autograd)")
+            return l2norm_pack_split(f), tuple(f.shape[-2:])
         return l2norm_pack(f), tuple(f.shape[-2:])
 
     def process_correlation(self, corr4d: torch.Tensor) -> torch.Tensor:
@@ -251,6 +258,7 @@ class ImMatchNet(nn.Module):
         with segment("mutual_matching"):
             corr4d = MutualMatching(corr4d)
         self.NeighConsensus.fp8 = self.corr_dtype == "fp8"
+        self.NeighConsensus.precision = "fp32" if self.corr_dtype == "fp32" else "bf16"
         with segment("neigh_consensus"):
             corr4d = self.NeighConsensus(corr4d)
         with segment("mutual_matching"):
@@ -261,18 +269,25 @@ class ImMatchNet(nn.Module):
         b = src.shape[0]
         if src.shape == tgt.shape:
             f, (h, w) = self.extract(torch.cat((src, tgt), 0))
-            fa, fb = f[:b], f[b:]
+            if isinstance(f, tuple):           # corr_dtype='fp32': (hi, lo) split operands
+                fa, fb = (f[0][:b], f[1][:b]), (f[0][b:], f[1][b:])
+            else:
+                fa, fb = f[:b], f[b:]
             ha, wa, hb, wb = h, w, h, w
         else:
             fa, (ha, wa) = self.extract(src)
             fb, (hb, wb) = self.extract(tgt)
         k = self.relocalization_k_size
-        if k > 1:
+        if isinstance(fa, tuple):
+            corr4d = correlation_x3(fa, fb).view(b, 1, ha, wa, hb, wb)
+            if k > 1:
+                corr4d, delta = _maxpool4d(corr4d, k)
+        elif k > 1:
             if k == 2 and ha % 2 == 0 and wa % 2 == 0 and hb % 2 == 0 and wb % 2 == 0:
                 corr4d, delta = correlation_pool2(fa, fb, ha, wa, hb, wb)
             else:
                 corr4d = correlation(fa, fb).view(b, 1, ha, wa, hb, wb)
-                corr4d, delta = maxpool4d(corr4d, k)
+                corr4d, delta = _maxpool4d(corr4d, k)
         else:
             corr4d = correlation(fa, fb).view(b, 1, ha, wa, hb, wb)
         corr4d = self.process_correlation(corr4d)

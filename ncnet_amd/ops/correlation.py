@@ -9,6 +9,10 @@
 * ``correlation_pool2``: the InLoc relocalization path; GEMM with a fused
   2x2x2x2 max-pool epilogue (lib/model.py:177-191) -- only the pooled volume
   and packed argmax offsets are written.
+* fp32-accurate inference ("bf16x3", ``corr_dtype='fp32'``): the L2-norm
+  kernel also writes the bf16 rounding residual and the correlation is three
+  bf16 GEMMs (hi.hi + hi.lo + lo.hi), matching the reference's fp32 bmm
+  (lib/model.py:110-113) to ~16 mantissa bits.
 * fp8 inference path (BASELINE config 5): ``l2norm_pack_fp8`` writes OCP
   e4m3 operands scaled by ``FP8_FEAT_SCALE`` (unit rows have entries ~1/sqrt(C),
   the scale keeps them out of the e4m3 subnormals) and both correlation entry
@@ -35,7 +39,7 @@ class L2NormPackFn(torch.autograd.Function):
         x2 = x.reshape(n * h * w, c)
         y = torch.empty((n * h * w, c), dtype=torch.bfloat16, device=feat.device)
         inv = torch.empty((n * h * w,), dtype=torch.float32, device=feat.device)
-        _ext.ext().l2norm_rows(x2, y, inv, 0.0)
+        _ext.ext().l2norm_rows(x2, y, inv, 0.0, None)
         ctx.save_for_backward(x2, inv)
         ctx.shape = (n, c, h, w)
         ctx.in_dtype = feat.dtype
@@ -75,8 +79,53 @@ def l2norm_pack_fp8(feat: torch.Tensor) -> torch.Tensor:
     if x.dtype not in (torch.bfloat16, torch.float32):
         x = x.float()
     y = torch.empty((n * h * w, c), dtype=FP8, device=feat.device)
-    _ext.ext().l2norm_rows(x.reshape(n * h * w, c), y, None, FP8_FEAT_SCALE)
+    _ext.ext().l2norm_rows(x.reshape(n * h * w, c), y, None, FP8_FEAT_SCALE, None)
     return y.reshape(n, h * w, c)
+
+
+def l2norm_pack_split(feat: torch.Tensor):
+    """[N, C, H, W] -> (hi, lo) bf16 [N, H*W, C] with hi + lo = the L2-normalised
+    rows to ~16 mantissa bits (fp32-accurate "bf16x3" inference mode)."""
+    n, c, h, w = feat.shape
+    x = feat.permute(0, 2, 3, 1)
+    if not x.is_contiguous():
+        x = x.contiguous()
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        x = x.float()
+    if not _ext.use_hip(feat):
+        y = ref.feature_l2norm(feat.float()).permute(0, 2, 3, 1).reshape(n, h * w, c)
+        hi = y.to(torch.bfloat16)
+        return hi, (y - hi.float()).to(torch.bfloat16)
+    hi = torch.empty((n * h * w, c), dtype=torch.bfloat16, device=feat.device)
+    lo = torch.empty_like(hi)
+    _ext.ext().l2norm_rows(x.reshape(n * h * w, c), hi, None, 0.0, lo)
+    return hi.reshape(n, h * w, c), lo.reshape(n, h * w, c)
+
+
+def correlation_x3(fa, fb, amap: torch.Tensor | None = None, bmap: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32-accurate correlation of split operands (``l2norm_pack_split``):
+    A.B^T ~ Ahi.Bhi^T + Ahi.Blo^T + Alo.Bhi^T on three bf16 MFMA GEMMs with
+    fp32 accumulation (the dropped Alo.Blo^T term is ~2^-16 relative).
+    Inference only.  fa = (hi, lo) [Na, M, C], fb = (hi, lo) [Nb, N, C]."""
+    (ah, al), (bh, bl) = fa, fb
+    if amap is None:
+        amap = torch.arange(ah.shape[0], device=ah.device, dtype=torch.int32)
+    if bmap is None:
+        bmap = torch.arange(bh.shape[0], device=bh.device, dtype=torch.int32)
+    if not _ext.use_hip(ah):
+        a = ah.float() + al.float()
+        b = bh.float() + bl.float()
+        return torch.bmm(a[amap.long()], b[bmap.long()].transpose(1, 2))
+    C = _ext.ext()
+    am, bm = amap.to(torch.int32), bmap.to(torch.int32)
+    out = torch.empty((am.numel(), ah.shape[1], bh.shape[1]), dtype=torch.float32, device=ah.device)
+    part = torch.empty_like(out)
+    C.corr_gemm(ah.contiguous(), bh.contiguous(), out, am, bm, 1.0)
+    C.corr_gemm(ah.contiguous(), bl.contiguous(), part, am, bm, 1.0)
+    out += part
+    C.corr_gemm(al.contiguous(), bh.contiguous(), part, am, bm, 1.0)
+    out += part
+    return out
 
 
 def _fp8_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:

@@ -1,10 +1,15 @@
 """Weak-supervision score (train.py:110-156) with a fused HIP forward/backward.
 
-For the default ``'softmax'`` normalisation, ``max_j softmax(x)_j =
-1 / sum_j exp(x_j - max x)``: the forward needs only the online-softmax row /
-column statistics and the backward has the closed form
-``ds/dx_j = s (delta_{j, argmax} - softmax_j)``.  ``None`` and ``'l1'``
-normalisations use the PyTorch oracle path.
+All three normalisations of the reference (train.py:111-116) run on the same
+single-pass HIP statistics (max, first argmax, and a sum) plus one
+closed-form backward kernel:
+
+* ``'softmax'`` (default): ``max_j softmax(x)_j = 1 / sum_j exp(x_j - max x)``,
+  ``ds/dx_j = s (delta_{j, argmax} - softmax_j)``;
+* ``'l1'``: ``max_j x_j / (sum x + eps) = max x / (sum x + eps)`` (eps 1e-4;
+  the volumes are non-negative -- ReLU'd NC outputs after MutualMatching -- so
+  the positive denominator keeps the argmax), ``ds/dx_j = delta_{j, argmax} / D - max / D^2``;
+* ``None``: ``max x``, ``ds/dx_j = delta_{j, argmax}``.
 """
 from __future__ import annotations
 
@@ -14,7 +19,10 @@ from . import _ext
 from . import reference as ref
 
 
-def _row_col_stats(x3: torch.Tensor):
+_NORM = {"softmax": 1, "l1": 2, None: 0}
+
+
+def _row_col_stats(x3: torch.Tensor, norm: int):
     C = _ext.ext()
     V, R, Cc = x3.shape
     f = dict(dtype=torch.float32, device=x3.device)
@@ -22,20 +30,34 @@ def _row_col_stats(x3: torch.Tensor):
     cmax, cse = torch.empty((V, Cc), **f), torch.empty((V, Cc), **f)
     rarg = torch.empty((V, R), dtype=torch.int32, device=x3.device)
     carg = torch.empty((V, Cc), dtype=torch.int32, device=x3.device)
-    C.stats_rows(x3, rmax, rarg, rse)
-    C.stats_cols(x3, cmax, carg, cse)
+    sum_kind = {1: 1, 2: 2, 0: 0}[norm]
+    C.stats_rows(x3, rmax, rarg, rse if sum_kind else None, sum_kind)
+    C.stats_cols(x3, cmax, carg, cse if sum_kind else None, sum_kind)
+    if not sum_kind:
+        rse.zero_()
+        cse.zero_()
     return rmax, rarg, rse, cmax, carg, cse
 
 
+def _scores(norm: int, mx: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    if norm == 1:
+        return 1.0 / s
+    if norm == 2:
+        return mx / (s + ref.L1_EPS)
+    return mx
+
+
 class SoftmaxMaxScoreFn(torch.autograd.Function):
-    """sum_v wr[v] * sum_rows s_row + wc[v] * sum_cols s_col (s = max softmax)."""
+    """sum_v wr[v] * sum_rows s_row + wc[v] * sum_cols s_col, s = the max of the
+    normalised row / column (norm 1 softmax, 2 l1, 0 None)."""
 
     @staticmethod
-    def forward(ctx, x3, wr, wc):
+    def forward(ctx, x3, wr, wc, norm=1):
         x3 = x3.float().contiguous()
-        st = _row_col_stats(x3)
+        st = _row_col_stats(x3, norm)
         rmax, rarg, rse, cmax, carg, cse = st
-        val = (wr.view(-1, 1) / rse).sum() + (wc.view(-1, 1) / cse).sum()
+        val = (wr.view(-1, 1) * _scores(norm, rmax, rse)).sum() + (wc.view(-1, 1) * _scores(norm, cmax, cse)).sum()
+        ctx.norm = norm
         ctx.save_for_backward(x3, wr, wc, *st)
         return val
 
@@ -44,8 +66,8 @@ class SoftmaxMaxScoreFn(torch.autograd.Function):
         x3, wr, wc, rmax, rarg, rse, cmax, carg, cse = ctx.saved_tensors
         gx = torch.empty_like(x3)
         _ext.ext().softmax_max_bwd(x3, rmax, rarg, rse, cmax, carg, cse, wr.float().contiguous(),
-                                   wc.float().contiguous(), gx)
-        return gx * g, None, None
+                                   wc.float().contiguous(), gx, ctx.norm, ref.L1_EPS)
+        return gx * g, None, None, None
 
 
 _WEIGHTS: dict = {}
@@ -74,10 +96,12 @@ def weak_loss_from_corr(corr4d: torch.Tensor, n_pos: int, normalization: str | N
     assert V == 2 * b
     i, j, k, l = corr4d.shape[2:]
     R, Cc = i * j, k * l
-    if _ext.use_hip(corr4d) and normalization == "softmax":
+    if normalization not in _NORM:
+        raise ValueError(f"normalization must be 'softmax', 'l1' or None, got {normalization!r}")
+    if _ext.use_hip(corr4d):
         x3 = corr4d.reshape(V, R, Cc)
         wr, wc = _loss_weights(b, R, Cc, corr4d.device)
-        return SoftmaxMaxScoreFn.apply(x3, wr, wc)
+        return SoftmaxMaxScoreFn.apply(x3, wr, wc, _NORM[normalization])
     pos = ref.match_score(corr4d[:b], normalization)
     neg = ref.match_score(corr4d[b:], normalization)
     return neg - pos
@@ -88,8 +112,10 @@ def match_score(corr4d: torch.Tensor, normalization: str | None = "softmax") -> 
     V = corr4d.shape[0]
     i, j, k, l = corr4d.shape[2:]
     R, Cc = i * j, k * l
-    if _ext.use_hip(corr4d) and normalization == "softmax":
+    if normalization not in _NORM:
+        raise ValueError(f"normalization must be 'softmax', 'l1' or None, got {normalization!r}")
+    if _ext.use_hip(corr4d):
         wr = torch.full((V,), 1.0 / (2.0 * V * R), device=corr4d.device)
         wc = torch.full((V,), 1.0 / (2.0 * V * Cc), device=corr4d.device)
-        return SoftmaxMaxScoreFn.apply(corr4d.reshape(V, R, Cc), wr, wc)
+        return SoftmaxMaxScoreFn.apply(corr4d.reshape(V, R, Cc), wr, wc, _NORM[normalization])
     return ref.match_score(corr4d, normalization)

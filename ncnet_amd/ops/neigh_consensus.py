@@ -573,6 +573,58 @@ class NeighConsensusFn(torch.autograd.Function):
 
 
 # ---------------------------------------------------------------------------
+# fp32-accurate inference ("bf16x3"): every Conv4d is three bf16 MFMA convs,
+# conv(h, w) ~ conv(h_hi, w_hi) + conv(h_hi, w_lo) + conv(h_lo, w_hi), where
+# x_hi = bf16(x) and x_lo = bf16(x - x_hi), summed in fp32; the activations
+# stay fp32 between layers (split again for the next layer).  This is the
+# reference's fp32 NeighConsensus (lib/conv4d.py:23-24, lib/model.py:110-113)
+# to ~16 mantissa bits, at 3x the bf16 cost; used by ImMatchNet(corr_dtype='fp32').
+
+def _split(t: torch.Tensor):
+    hi = t.to(torch.bfloat16)
+    return hi, (t - hi.float()).to(torch.bfloat16)
+
+
+def _stack_fwd_x3(x0: torch.Tensor, ws, bs, channels) -> torch.Tensor:
+    """x0 fp32 [V,I,J,K,L] -> last layer ReLU output fp32 ([V,...] or planar [C, V, ...])."""
+    h = x0
+    cin = 1
+    for w_ref, b, cout in zip(ws, bs, channels):
+        w = _std(w_ref)
+        w_hi = w.to(torch.bfloat16).float()
+        w_lo = w - w_hi
+        if cin == 1:
+            h_hi, h_lo = _split(h)
+        else:
+            hh, hl = _split(h)                  # planar fp32 [cin, V, ...] -> blocks
+            h_hi, h_lo = planar_to_blocks(hh.float()), planar_to_blocks(hl.float())
+        z = conv_layer(h_hi, w_hi, cin, cout, relu=False, f32=True)
+        z = z + conv_layer(h_hi, w_lo, cin, cout, relu=False, f32=True)
+        z = z + conv_layer(h_lo, w_hi, cin, cout, relu=False, f32=True)
+        bb = b.float().view(-1, *([1] * (z.dim() - 1))) if cout > 1 else b.float().view(1)
+        h = torch.relu(z + bb)
+        cin = cout
+    return h
+
+
+def neigh_consensus_x3(x: torch.Tensor, weights, biases, channels, symmetric: bool = True) -> torch.Tensor:
+    """fp32-accurate inference NeighConsensus on the bf16 MFMA kernels (no autograd)."""
+    V, _, I, J, K, L = x.shape
+    cl = channels[-1]
+    xf = x.reshape(V, I, J, K, L).float().contiguous()
+
+    def as_out(z, shape):
+        return z.reshape((V, 1) + shape) if cl == 1 else z.transpose(0, 1).reshape((V, cl) + shape)
+
+    y = as_out(_stack_fwd_x3(xf, weights, biases, channels), (I, J, K, L))
+    if symmetric:
+        xt = xf.permute(0, 3, 4, 1, 2).contiguous()
+        y2 = as_out(_stack_fwd_x3(xt, weights, biases, channels), (K, L, I, J))
+        y = y + y2.permute(0, 1, 4, 5, 2, 3)
+    return y.contiguous()
+
+
+# ---------------------------------------------------------------------------
 # fp8 inference path (BASELINE config 5): OCP e4m3 activations and weights on
 # the fp8 MFMA conv kernel, ij encoding for the 1-channel layers.
 
@@ -732,14 +784,16 @@ def fp8_ok(kinds, channels) -> bool:
             and max(channels) <= 16)
 
 
-def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool = True, fp8: bool = False) -> torch.Tensor:
+def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool = True, fp8: bool = False,
+                    precision: str = "bf16") -> torch.Tensor:
     """x: [V,1,I,J,K,L] fp32; weights in checkpoint layout [k, out, in, k, k, k].
     Returns [V, C_last, I, J, K, L] fp32.
 
     On the GPU: the (3,3)/(<=16,1) inference stack runs on the fused kernel
     (hidden layer in LDS); ``fp8`` (inference, ``fp8_ok`` stacks) on the fp8
-    MFMA Conv4d kernels; everything else with odd kernel sizes <= 7 and any
-    channel counts on the bf16 autograd stack.  ``_ext.DISPATCH`` records
+    MFMA Conv4d kernels; ``precision='fp32'`` (inference) on the bf16x3
+    kernels (fp32-accurate); everything else with odd kernel sizes <= 7 and
+    any channel counts on the bf16 autograd stack.  ``_ext.DISPATCH`` records
     which path ran."""
     kernel_sizes = [w.shape[0] for w in weights]
     kinds = layer_kinds(channels, kernel_sizes)
@@ -747,6 +801,11 @@ def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool 
         if kinds is None:
             _ext.torch_fallback(f"NeighConsensus kernel sizes {kernel_sizes}")
         else:
+            if precision == "fp32":
+                if torch.is_grad_enabled() and x.requires_grad:
+                    raise RuntimeError("precision='fp32' NeighConsensus is an inference path")
+                _ext.count("nc_x3")
+                return neigh_consensus_x3(x, weights, biases, channels, symmetric)
             if _fused_ok(kinds, kernel_sizes, channels, x) and not fp8:
                 _ext.count("nc_fused_k3")
                 return neigh_consensus_fused(x.float().contiguous(), weights, biases, symmetric)
