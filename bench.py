@@ -45,6 +45,30 @@ def _baseline():
         return None
 
 
+def _inloc_secondary():
+    """BASELINE configs 3-5 (InLoc dense matching, NC 3,3/16,1, k=2), measured
+    after the headline window on rank 0 so the driver's run records them:
+    ms/pair at 1600 px and 3200 px (bf16) and 3200 px (fp8 correlation + NC)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_inloc
+    from ncnet_amd.models import ImMatchNet
+    out = {}
+    try:
+        torch.manual_seed(0)
+        model = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], half_precision=True,
+                           relocalization_k_size=2).cuda().eval()
+        for name, size, fp8, pairs in (("inloc_1600_bf16", 1600, False, 5), ("inloc_3200_bf16", 3200, False, 3),
+                                       ("inloc_3200_fp8", 3200, True, 3)):
+            r = bench_inloc.run_single(size, fp8, pairs=pairs, warmup=1, model=model)
+            out[name] = {"ms_per_pair": r["value"], "stages_ms": r["stages_ms"], "volume": r["config"]["volume"],
+                         "dtype": r["dtype"]}
+        del model
+    except Exception as e:  # the headline record must still print
+        out["error"] = repr(e)
+    torch.cuda.empty_cache()
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -55,6 +79,9 @@ def main(argv=None):
     ap.add_argument("--impl", choices=["hip", "reference"], default="hip")
     ap.add_argument("--ref-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--profile", type=str, default="", help="write a torch.profiler trace to this dir")
+    ap.add_argument("--inloc", type=int, default=1,
+                    help="1: after the timed training steps, rank 0 also times the InLoc inference configs "
+                         "(BASELINE configs 3-5: 1600 px bf16, 3200 px bf16, 3200 px fp8) into config.secondary")
     args = ap.parse_args(argv)
 
     from ncnet_amd.config import RuntimeConfig
@@ -145,6 +172,9 @@ def main(argv=None):
     vs = None
     if base:
         vs = pairs_per_s / base
+    secondary = None
+    if args.inloc and ctx.is_main and dev.type == "cuda" and args.impl == "hip":
+        secondary = _inloc_secondary()
     if ctx.is_main:
         rec = {
             "metric": "image-pairs/sec fwd+bwd, ResNet-101+NC-Net(5,5,5) 400x400 bf16",
@@ -166,7 +196,8 @@ def main(argv=None):
                        "comm": comm_info(ctx), "optimizer": type(opt).__name__,
                        "hbm_peak_gb": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
                                        if dev.type == "cuda" else None),
-                       "runtime": RuntimeConfig.from_env().as_dict()},
+                       "runtime": RuntimeConfig.from_env().as_dict(),
+                       "secondary": secondary},
         }
         print(json.dumps(rec), flush=True)
     from ncnet_amd.parallel.dist import destroy

@@ -35,6 +35,91 @@ from ncnet_amd.models import ImMatchNet  # noqa: E402
 from ncnet_amd.ops.correlation import correlation, correlation_pool2  # noqa: E402
 
 
+def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup: int = 2, k: int = 2,
+               ncons_kernel_sizes=(3, 3), ncons_channels=(16, 1), src_hw=(3024, 4032), no_matches: bool = False,
+               impl: str = "hip", model=None) -> dict:
+    """One InLoc query/pano pair per forward on one GPU; returns the JSON record."""
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    if model is None:
+        model = ImMatchNet(use_cuda=True, ncons_kernel_sizes=list(ncons_kernel_sizes),
+                           ncons_channels=list(ncons_channels), half_precision=True, relocalization_k_size=k,
+                           corr_dtype="fp8" if fp8 else "bf16").to(dev).eval()
+    model.corr_dtype = "fp8" if fp8 else "bf16"
+    h, w = target_size(src_hw[0], src_hw[1], image_size, k)
+    src = torch.randn(1, 3, h, w, device=dev)
+    tgt = torch.randn(1, 3, h, w, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    stages = {"backbone": 0.0, "corr_pool": 0.0, "mm_nc_mm": 0.0, "matches": 0.0}
+    nmatch = 0
+
+    if impl == "reference":
+        from ncnet_amd.engine.reference_impl import ReferenceAlgorithm, reference_inloc_forward
+        alg = ReferenceAlgorithm(model, torch.float32)
+
+    def one_ref(timed: bool):
+        nonlocal nmatch
+        with torch.inference_mode():
+            ev[0].record()
+            corr4d, delta = reference_inloc_forward(alg, src, tgt, k)
+            ev[3].record()
+            if not no_matches:
+                m = pair_matches(corr4d.float(), tuple(d.long() for d in delta) if delta else None, k, True, True)
+                nmatch = int(m.shape[0])
+            ev[4].record()
+        if timed:
+            torch.cuda.synchronize()
+            stages["mm_nc_mm"] += ev[0].elapsed_time(ev[3])
+            stages["matches"] += ev[3].elapsed_time(ev[4])
+
+    def one(timed: bool):
+        if impl == "reference":
+            return one_ref(timed)
+        nonlocal nmatch
+        with torch.inference_mode():
+            ev[0].record()
+            f, (fh, fw) = model.extract(torch.cat((src, tgt), 0))
+            fa, fb = f[:1], f[1:]
+            ev[1].record()
+            if k == 2:
+                corr4d, delta = correlation_pool2(fa, fb, fh, fw, fh, fw)
+            else:
+                corr4d, delta = correlation(fa, fb).view(1, 1, fh, fw, fh, fw), None
+            ev[2].record()
+            corr4d = model.process_correlation(corr4d)
+            ev[3].record()
+            if not no_matches:
+                m = pair_matches(corr4d, delta, k, True, True)
+                nmatch = int(m.shape[0])
+            ev[4].record()
+        if timed:
+            torch.cuda.synchronize()
+            for i, kk in enumerate(stages):
+                stages[kk] += ev[i].elapsed_time(ev[i + 1])
+
+    for _ in range(warmup):
+        one(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(pairs):
+        one(True)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / pairs
+    fs = (h // 16 // k, w // 16 // k)
+    return {
+        "metric": "InLoc dense matching latency per pair (fwd, k=%d relocalization)" % k,
+        "value": round(ms, 3), "unit": "ms/pair", "higher_is_better": False,
+        "pairs_per_s": round(1e3 / ms, 3), "n_gpus": 1, "pairs": pairs, "warmup": warmup,
+        "impl": impl,
+        "dtype": ("fp32-backbone/fp16-volume" if impl == "reference" else ("fp8-corr+fp8-nc" if fp8 else "bf16")),
+        "data": "synthetic (random 4:3 images, random-init weights)",
+        "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,
+                   "ncons": [list(ncons_kernel_sizes), list(ncons_channels)], "k": k},
+        "stages_ms": {kk: round(v / pairs, 3) for kk, v in stages.items()},
+        "matches": nmatch, "matches_contract": n_matches(image_size, k, True),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--image-size", type=int, default=1600)
@@ -45,90 +130,15 @@ def main():
     ap.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 1])
     ap.add_argument("--src-hw", type=int, nargs=2, default=[3024, 4032], help="raw query size (iPhone7)")
     ap.add_argument("--no-matches", action="store_true")
-    ap.add_argument("--fp8", action="store_true", help="OCP fp8 correlation operands (MX-fp8 MFMA)")
+    ap.add_argument("--fp8", action="store_true", help="OCP fp8 correlation operands (MX-fp8 MFMA) + fp8 NC")
     ap.add_argument("--impl", choices=["hip", "reference"], default="hip",
                     help="reference: the reference algorithm in plain PyTorch-ROCm (fp32 backbone, fp16 volume)")
     ap.add_argument("--volume-parallel", action="store_true")
     a = ap.parse_args()
     if a.volume_parallel:
         return bench_volume_parallel(a)
-    dev = torch.device("cuda")
-    torch.manual_seed(0)
-    model = ImMatchNet(use_cuda=True, ncons_kernel_sizes=a.ncons_kernel_sizes, ncons_channels=a.ncons_channels,
-                       half_precision=True, relocalization_k_size=a.k,
-                       corr_dtype="fp8" if a.fp8 else "bf16").to(dev).eval()
-    h, w = target_size(a.src_hw[0], a.src_hw[1], a.image_size, a.k)
-    src = torch.randn(1, 3, h, w, device=dev)
-    tgt = torch.randn(1, 3, h, w, device=dev)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-    stages = {"backbone": 0.0, "corr_pool": 0.0, "mm_nc_mm": 0.0, "matches": 0.0}
-    nmatch = 0
-
-    if a.impl == "reference":
-        from ncnet_amd.engine.reference_impl import ReferenceAlgorithm, reference_inloc_forward
-        alg = ReferenceAlgorithm(model, torch.float32)
-
-    def one_ref(timed: bool):
-        nonlocal nmatch
-        with torch.inference_mode():
-            ev[0].record()
-            corr4d, delta = reference_inloc_forward(alg, src, tgt, a.k)
-            ev[3].record()
-            if not a.no_matches:
-                m = pair_matches(corr4d.float(), tuple(d.long() for d in delta) if delta else None, a.k, True, True)
-                nmatch = int(m.shape[0])
-            ev[4].record()
-        if timed:
-            torch.cuda.synchronize()
-            stages["mm_nc_mm"] += ev[0].elapsed_time(ev[3])
-            stages["matches"] += ev[3].elapsed_time(ev[4])
-
-    def one(timed: bool):
-        if a.impl == "reference":
-            return one_ref(timed)
-        nonlocal nmatch
-        with torch.inference_mode():
-            ev[0].record()
-            f, (fh, fw) = model.extract(torch.cat((src, tgt), 0))
-            fa, fb = f[:1], f[1:]
-            ev[1].record()
-            if a.k == 2:
-                corr4d, delta = correlation_pool2(fa, fb, fh, fw, fh, fw)
-            else:
-                corr4d, delta = correlation(fa, fb).view(1, 1, fh, fw, fh, fw), None
-            ev[2].record()
-            corr4d = model.process_correlation(corr4d)
-            ev[3].record()
-            if not a.no_matches:
-                m = pair_matches(corr4d, delta, a.k, True, True)
-                nmatch = int(m.shape[0])
-            ev[4].record()
-        if timed:
-            torch.cuda.synchronize()
-            for i, k in enumerate(stages):
-                stages[k] += ev[i].elapsed_time(ev[i + 1])
-
-    for _ in range(a.warmup):
-        one(False)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.pairs):
-        one(True)
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3 / a.pairs
-    fs = (h // 16 // a.k, w // 16 // a.k)
-    print(json.dumps({
-        "metric": "InLoc dense matching latency per pair (fwd, k=%d relocalization)" % a.k,
-        "value": round(ms, 3), "unit": "ms/pair", "higher_is_better": False,
-        "pairs_per_s": round(1e3 / ms, 3), "n_gpus": 1, "pairs": a.pairs, "warmup": a.warmup,
-        "impl": a.impl,
-        "dtype": ("fp32-backbone/fp16-volume" if a.impl == "reference" else ("fp8-corr/bf16" if a.fp8 else "bf16")),
-        "data": "synthetic (random 4:3 images, random-init weights)",
-        "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,
-                   "ncons": [a.ncons_kernel_sizes, a.ncons_channels], "k": a.k},
-        "stages_ms": {k: round(v / a.pairs, 3) for k, v in stages.items()},
-        "matches": nmatch, "matches_contract": n_matches(a.image_size, a.k, True),
-    }))
+    print(json.dumps(run_single(a.image_size, a.fp8, a.pairs, a.warmup, a.k, a.ncons_kernel_sizes, a.ncons_channels,
+                                a.src_hw, a.no_matches, a.impl)))
 
 
 def bench_volume_parallel(a):

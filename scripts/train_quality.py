@@ -72,7 +72,8 @@ def recalibrate_bn(model, size, dev, batches=4, batch=8):
 def run(args):
     dev = torch.device("cuda")
     torch.manual_seed(args.seed)
-    m_h = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1]).to(dev)
+    m_h = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1],
+                     feature_extraction_last_layer=args.last_layer).to(dev)
     recalibrate_bn(m_h, args.image_size, dev)
     # non-degenerate NC start: at the reference init (biases ~U(+-1/sqrt(fan_in))) a
     # negative last-layer bias on these weak random-trunk volumes zeroes the whole NC
@@ -108,8 +109,8 @@ def run(args):
         loss_r = reference_weak_loss(alg, batch)
         loss_r.backward()
         opt_r.step()
-        lh.append(float(loss))
-        lr_.append(float(loss_r))
+        lh.append(float(loss.detach()))
+        lr_.append(float(loss_r.detach()))
         if step % 20 == 0 or step == args.steps - 1:
             print(f"step {step}: hip {lh[-1]:.5f} ref {lr_[-1]:.5f} ({time.time() - t0:.0f}s)", flush=True)
     m_h.eval()
@@ -132,6 +133,7 @@ def main(argv=None):
     ap.add_argument("--lr", type=float, default=5e-4)
     ap.add_argument("--eval-batches", type=int, default=8)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--last-layer", type=str, default="", help="trunk cut (default layer3, the reference's)")
     ap.add_argument("--out", type=str, default="")
     a = ap.parse_args(argv)
     res = run(a)

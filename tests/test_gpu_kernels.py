@@ -207,38 +207,6 @@ def test_maxpool4d_and_fused_pool():
     assert agree == 4
 
 
-def test_immatchnet_volumes_and_grads_match_reference_algorithm():
-    """Positive/negative volumes of the fused HIP path (feature reuse, bf16 NC)
-    vs the pure-torch reference algorithm (two full forwards, conv3d-loop
-    Conv4d, fp32), and NC gradients of a random linear functional of them.
-    (The weak loss itself is ~1e-7 at random init -- a cancellation -- so the
-    volumes are compared instead; the loss op is tested separately.)"""
-    import numpy as np
-    from ncnet_amd.engine.reference_impl import ReferenceAlgorithm
-    from ncnet_amd.models import ImMatchNet
-    torch.manual_seed(10)
-    m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], dtype="fp32").cuda()
-    src = torch.randn(3, 3, 160, 160, device=DEV)
-    tgt = torch.randn(3, 3, 160, 160, device=DEV)
-    vols = m.weak_loss_volumes(src, tgt)
-    g = torch.randn_like(vols)
-    (vols * g).sum().backward()
-    g_hip = [p.grad.clone() for p in m.NeighConsensus.parameters()]
-    m.zero_grad()
-    alg = ReferenceAlgorithm(m, torch.float32)
-    pos = alg({"source_image": src, "target_image": tgt})
-    neg = alg({"source_image": src[np.roll(np.arange(3), -1)], "target_image": tgt})
-    ref_vols = torch.cat((pos, neg))
-    (ref_vols * g).sum().backward()
-    g_ref = [p.grad.clone() for p in m.NeighConsensus.parameters()]
-    assert rel_l2(vols, ref_vols) < 2e-2
-    errs = [rel_l2(a, b) for a, b in zip(g_hip, g_ref)]
-    # bf16 features + bf16 NC vs an fp32 reference: near-tied row/column maxima in
-    # MutualMatching route their gradient to different elements, so the end-to-end
-    # gradient agrees to ~10-20% here; every op is pinned tightly by its own test.
-    assert max(errs) < 0.3, errs
-
-
 @pytest.mark.parametrize("variant", [2, 3])
 @pytest.mark.parametrize("ks,shape", [(5, (2, 6, 5, 25, 25)), (5, (1, 5, 4, 30, 27)), (3, (1, 4, 5, 9, 33)),
                                       (5, (1, 2, 3, 7, 6)), (7, (1, 3, 4, 25, 25)), (1, (1, 3, 4, 25, 26))])

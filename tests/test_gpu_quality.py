@@ -60,3 +60,79 @@ def test_training_tracks_fp32_reference():
     assert drop_h > 0 and drop_r > 0, s
     assert abs(drop_h - drop_r) < 0.25 * drop_r, s
     assert abs(res["pck_final_hip"] - res["pck_final_ref"]) < 0.05, res
+
+
+def _nc_std(m):
+    from ncnet_amd.ops import reference as ref
+    layers = m.NeighConsensus.conv_layers()
+    return [ref.conv4d_weight_to_std(l.weight_ref()).detach() for l in layers], [l.bias.detach() for l in layers]
+
+
+@pytest.mark.parametrize("fe_finetune", [0, 1])
+def test_training_grads_vs_quantized_oracle(fe_finetune):
+    """End-to-end gradients of the fused training path (features reused for the
+    rolled negatives, HIP correlation / MutualMatching / ij-encoded NC with the
+    side-stream weight gradients) against its own math in float64 with bf16
+    rounding at exactly the stored-bf16 points (engine/quantized_oracle.py), at
+    a non-degenerate operating point (known-correspondence pairs, after three
+    Adam steps).  fe_finetune=1 unfreezes the last layer3 bottleneck
+    (train.py:60-63): the L2-norm, correlation and first-MutualMatching
+    backward and the NC input gradient are then checked too, as the gradient
+    w.r.t. the raw trunk features."""
+    from ncnet_amd.data.datasets import synthetic_correspondence_batch
+    from ncnet_amd.engine import quantized_oracle as qo
+    from ncnet_amd.engine.trainer import make_adam, weak_loss
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.ops.correlation import l2norm_pack
+    torch.manual_seed(0)
+    m = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1]).to(DEV)
+    for p in m.NeighConsensus.parameters():
+        if p.dim() == 1:
+            p.data.uniform_(0.0, 0.05)
+    if fe_finetune:
+        for p in m.FeatureExtraction.model[-1][-1].parameters():
+            p.requires_grad = True
+    m.train()
+    params = [p for p in m.parameters() if p.requires_grad]
+    opt = make_adam(params, 5e-4)
+    for s in range(3):
+        b = synthetic_correspondence_batch(2, 240, DEV, seed=s)
+        opt.zero_grad(set_to_none=True)
+        weak_loss(m, {"source_image": b["source_image"], "target_image": b["target_image"]}).backward()
+        opt.step()
+    b = synthetic_correspondence_batch(2, 240, DEV, seed=7)
+    imgs = torch.cat((b["source_image"], b["target_image"]))
+    opt.zero_grad(set_to_none=True)
+    if fe_finetune:
+        raw = m.FeatureExtraction.trunk_forward(imgs, torch.bfloat16).detach().requires_grad_(True)
+        f, hw = l2norm_pack(raw), tuple(raw.shape[-2:])
+    else:
+        with torch.no_grad():
+            f, hw = m.extract(imgs)
+    vols = m.weak_loss_volumes_from_features(f, hw, 2)
+    G = torch.randn_like(vols)
+    (vols * G).sum().backward()
+    g_hip = [p.grad.detach().double().clone() for p in m.NeighConsensus.parameters()]
+    ws, bs = _nc_std(m)
+    ws = [w.double().requires_grad_(True) for w in ws]
+    bs = [x.double().requires_grad_(True) for x in bs]
+    if fe_finetune:
+        raw64 = raw.detach().double().requires_grad_(True)
+        ovols = qo.weak_loss_volumes(raw64, hw, 2, ws, bs, normalize=True)
+    else:
+        ovols = qo.weak_loss_volumes(f.detach(), hw, 2, ws, bs, normalize=False)
+    (ovols * G.double()).sum().backward()
+    errs = {"vols": rl2(vols, ovols)}
+    o_grads = []
+    for w, x in zip(ws, bs):
+        o_grads += [w.grad, x.grad]
+    # NC parameters are (weight, bias) per layer in module order; the oracle's are std-layout weights
+    from ncnet_amd.ops import reference as ref
+    for i, (gh, go) in enumerate(zip(g_hip, o_grads)):
+        if gh.dim() == 6:
+            go = ref.conv4d_weight_from_std(go)
+        errs[f"nc{i}"] = rl2(gh, go)
+    if fe_finetune:
+        errs["d_raw_features"] = rl2(raw.grad, raw64.grad)
+    assert errs["vols"] < 2e-3, errs
+    assert max(v for k, v in errs.items() if k != "vols") < 1e-2, errs
