@@ -45,15 +45,16 @@ def _worker(rank, world, port, out_dir):
     destroy(ctx)
 
 
-def test_dp_gradients_equal_mean_of_shards(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_gradients_equal_mean_of_shards(tmp_path, world):
     port = _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     res = [torch.load(str(tmp_path / f"r{r}.pt"), weights_only=True) for r in range(world)]
-    for a, b in zip(res[0]["params"], res[1]["params"]):
-        assert torch.equal(a, b)  # broadcast from rank 0
-    for a, b in zip(res[0]["grads"], res[1]["grads"]):
-        assert torch.allclose(a, b)
+    for r in range(1, world):
+        for a, b in zip(res[0]["params"], res[r]["params"]):
+            assert torch.equal(a, b)  # broadcast from rank 0
+        for a, b in zip(res[0]["grads"], res[r]["grads"]):
+            assert torch.allclose(a, b)
     # single-process reference with rank 0's parameters
     from ncnet_amd.engine.trainer import weak_loss
     from ncnet_amd.models import ImMatchNet
@@ -68,9 +69,10 @@ def test_dp_gradients_equal_mean_of_shards(tmp_path):
             a += p.grad / world
     for a, g in zip(acc, res[0]["grads"]):
         assert torch.allclose(a, g, rtol=1e-4, atol=1e-8)
-    # disjoint shards covering the data
-    s0, s1 = res[0]["shard"], res[1]["shard"]
-    assert not set(s0) & set(s1) and len(s0) == len(s1) == 5
+    # disjoint, equal-size shards (drop_last: 10 // world pairs per rank, as DistributedSampler)
+    shards = [set(r["shard"]) for r in res]
+    assert sum(len(x) for x in shards) == len(set().union(*shards)) == world * (10 // world)
+    assert all(len(r["shard"]) == 10 // world for r in res)
 
 
 def test_bench_torchrun_two_ranks_cpu(tmp_path):
@@ -156,3 +158,43 @@ def test_volume_parallel_matches_single_process(tmp_path, world, k_size, ks):
     else:
         assert res["out"].shape == ref.shape
         assert torch.allclose(res["out"], ref, rtol=1e-4, atol=1e-6)
+
+
+def _hang_worker(rank, world, port, out_dir):
+    """Rank 1 never joins the all-reduce (a hung or dead peer); rank 0 must get
+    an error from the process-group timeout instead of blocking forever."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import time
+    from ncnet_amd.parallel.dist import init_distributed
+    ctx = init_distributed(device="cpu", timeout_s=5)
+    if rank == 1:
+        time.sleep(30)           # stays alive but silent past the timeout
+        return
+    import torch.distributed as dist
+    t0 = time.time()
+    err = ""
+    try:
+        dist.all_reduce(torch.ones(4))
+    except Exception as e:        # gloo: RuntimeError "... Timed out ..."
+        err = repr(e)
+    with open(os.path.join(out_dir, "hang.txt"), "w") as f:
+        f.write(f"{time.time() - t0:.1f}\n{err}")
+    os._exit(0)                   # do not wait for the silent peer in destroy()
+
+
+def test_rank_failure_detected_by_pg_timeout(tmp_path):
+    """SURVEY 5.3 failure detection: with NCNET_PG_TIMEOUT_S-style timeouts a
+    collective that a peer never joins raises on the surviving rank within the
+    timeout (parallel/dist.py init_distributed)."""
+    port = _free_port()
+    ctx = mp.spawn(_hang_worker, args=(2, port, str(tmp_path)), nprocs=2, join=False)
+    ctx.processes[0].join(120)
+    assert not ctx.processes[0].is_alive(), "rank 0 blocked past the process-group timeout"
+    for p in ctx.processes:
+        if p.is_alive():
+            p.terminate()
+            p.join(10)
+    elapsed, err = (tmp_path / "hang.txt").read_text().split("\n", 1)
+    assert err, "the all-reduce with a silent peer did not raise"
+    assert float(elapsed) < 60
