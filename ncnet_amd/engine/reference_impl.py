@@ -25,11 +25,15 @@ from ..ops import reference as ref
 
 
 class ReferenceAlgorithm(nn.Module):
-    def __init__(self, model, dtype: torch.dtype = torch.float32):
-        """``model`` is an ImMatchNet; its parameters are shared."""
+    def __init__(self, model, dtype: torch.dtype = torch.float32, conv=None):
+        """``model`` is an ImMatchNet; its parameters are shared.  ``conv``:
+        the Conv4d implementation -- default the reference's per-slice conv3d
+        loop (what the baseline times); ``ops.reference.conv4d`` computes the
+        same sums with k conv3d calls per layer (numerics checks)."""
         super().__init__()
         self.m = model
         self.dtype = dtype
+        self.conv = conv or ref.conv4d_sliced
 
     def _fe(self, img):
         with torch.autocast("cuda", dtype=self.dtype, enabled=img.is_cuda and self.dtype != torch.float32):
@@ -46,7 +50,7 @@ class ReferenceAlgorithm(nn.Module):
             layers = self.m.NeighConsensus.conv_layers()
             ws = [l.weight_ref() for l in layers]
             bs = [l.bias for l in layers]
-            corr = ref.neigh_consensus(corr, ws, bs, symmetric=True, conv=ref.conv4d_sliced)
+            corr = ref.neigh_consensus(corr, ws, bs, symmetric=True, conv=self.conv)
             corr = ref.mutual_matching(corr)
         return corr.float()
 

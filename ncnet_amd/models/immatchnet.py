@@ -186,7 +186,7 @@ class ImMatchNet(nn.Module):
                  ncons_kernel_sizes=(3, 3, 3), ncons_channels=(10, 10, 1), normalize_features: bool = True,
                  train_fe: bool = False, use_cuda: bool = True, relocalization_k_size: int = 0,
                  half_precision: bool = False, checkpoint: str | None = None, dtype: str = "bf16",
-                 fold_bn: bool = True, corr_dtype: str = "bf16"):
+                 fold_bn: bool = True, corr_dtype: str = "bf16", nc_precision: str = "bf16"):
         super().__init__()
         ck = None
         if checkpoint:
@@ -209,6 +209,15 @@ class ImMatchNet(nn.Module):
         # fp32: fp32-accurate correlation + NeighConsensus (bf16x3 split on the
         # bf16 MFMA kernels), the reference's evaluation precision -- inference only
         self.corr_dtype = corr_dtype
+        # nc_precision='fp32': NeighConsensus forward AND backward as bf16x3 splits
+        # (fp32-accurate training at 3x the NC cost; ops/neigh_consensus.py NeighConsensusX3Fn)
+        if nc_precision not in ("bf16", "fp32"):
+            raise ValueError("nc_precision must be 'bf16' or 'fp32'")
+        self.nc_precision = nc_precision
+        if nc_precision == "fp32":
+            # fp32-accurate training: fp32 trunk, split (bf16x3) correlation when the
+            # trunk is frozen, bf16x3 NeighConsensus forward and backward
+            self.compute_dtype = torch.float32
         self.FeatureExtraction = FeatureExtraction(train_fe=train_fe, feature_extraction_cnn=feature_extraction_cnn,
                                                    feature_extraction_model_file=feature_extraction_model_file or "",
                                                    last_layer=feature_extraction_last_layer,
@@ -247,9 +256,11 @@ class ImMatchNet(nn.Module):
             if torch.is_grad_enabled() and self.training:
                 raise RuntimeError("corr_dtype='fp8' is an inference path (no autograd)")
             return l2norm_pack_fp8(f), tuple(f.shape[-2:])
-        if self.corr_dtype == "fp32":
-            if torch.is_grad_enabled() and self.training:
-                raise RuntimeError("corr_dtype='fp32' is an inference path (no autograd)")
+        if self.corr_dtype == "fp32" or self.nc_precision == "fp32":
+            if f.requires_grad:
+                if self.corr_dtype == "fp32":
+                    raise RuntimeError("corr_dtype='fp32' is an inference path (no autograd)")
+                return l2norm_pack(f), tuple(f.shape[-2:])     # trainable trunk: bf16 correlation operands
             return l2norm_pack_split(f), tuple(f.shape[-2:])
         return l2norm_pack(f), tuple(f.shape[-2:])
 
@@ -258,7 +269,7 @@ class ImMatchNet(nn.Module):
         with segment("mutual_matching"):
             corr4d = MutualMatching(corr4d)
         self.NeighConsensus.fp8 = self.corr_dtype == "fp8"
-        self.NeighConsensus.precision = "fp32" if self.corr_dtype == "fp32" else "bf16"
+        self.NeighConsensus.precision = "fp32" if "fp32" in (self.corr_dtype, self.nc_precision) else "bf16"
         with segment("neigh_consensus"):
             corr4d = self.NeighConsensus(corr4d)
         with segment("mutual_matching"):
@@ -312,6 +323,11 @@ class ImMatchNet(nn.Module):
         2B images [source; target] (engine/trainer.py TrunkPrefetcher runs it
         one step ahead on a side stream when the trunk is frozen)."""
         h, w = hw
+        if isinstance(f, tuple):               # split operands (nc_precision / corr_dtype 'fp32')
+            amap, bmap = _pair_maps(b, f[0].device)
+            with segment("correlation"):
+                corr = correlation_x3((f[0][:b], f[1][:b]), (f[0][b:], f[1][b:]), amap, bmap)
+            return self.process_correlation(corr.view(2 * b, 1, h, w, h, w))
         fa, fb = f[:b], f[b:]
         amap, bmap = _pair_maps(b, f.device)
         with segment("correlation"):

@@ -35,6 +35,7 @@ from ncnet_amd.eval.point_tnf import (PointsToPixelCoords, PointsToUnitCoords, b
                                       corr_to_matches)
 from ncnet_amd.models import ImMatchNet  # noqa: E402
 from ncnet_amd.ops import _ext  # noqa: E402
+from ncnet_amd.ops import reference as ref  # noqa: E402
 
 
 def pck_of(forward, pairs, alpha=0.1):
@@ -82,7 +83,10 @@ def run(args):
         if p.dim() == 1:
             p.data.uniform_(0.0, 0.05)
     m_r = copy.deepcopy(m_h)
-    alg = ReferenceAlgorithm(m_r, torch.float32)
+    if args.nc_precision == "fp32":      # fp32-accurate HIP training: fp32 trunk, bf16x3 correlation + NC
+        m_h.nc_precision = "fp32"
+        m_h.compute_dtype = torch.float32
+    alg = ReferenceAlgorithm(m_r, torch.float32, conv=ref.conv4d)   # same fp32 sums, k conv3d per layer
     p_h = [p for p in m_h.parameters() if p.requires_grad]
     p_r = [p for p in m_r.parameters() if p.requires_grad]
     opt_h = make_adam(p_h, args.lr)
@@ -111,7 +115,7 @@ def run(args):
         opt_r.step()
         lh.append(float(loss.detach()))
         lr_.append(float(loss_r.detach()))
-        if step % 20 == 0 or step == args.steps - 1:
+        if step % 5 == 0 or step == args.steps - 1:
             print(f"step {step}: hip {lh[-1]:.5f} ref {lr_[-1]:.5f} ({time.time() - t0:.0f}s)", flush=True)
     m_h.eval()
     m_r.eval()
@@ -125,7 +129,21 @@ def run(args):
     return res
 
 
+def _heartbeat(period=60):
+    """MIOpen compiles its conv3d kernels (the reference run) on first use,
+    minutes of silence on a fresh box: keep the log alive."""
+    import threading
+
+    def beat():
+        t0 = time.time()
+        while True:
+            time.sleep(period)
+            print(f"[alive {time.time() - t0:.0f}s]", flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main(argv=None):
+    _heartbeat()
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--batch", type=int, default=4)
@@ -134,6 +152,8 @@ def main(argv=None):
     ap.add_argument("--eval-batches", type=int, default=8)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--last-layer", type=str, default="", help="trunk cut (default layer3, the reference's)")
+    ap.add_argument("--nc-precision", choices=["bf16", "fp32"], default="bf16",
+                    help="HIP run's NeighConsensus precision (fp32: bf16x3 forward+backward)")
     ap.add_argument("--out", type=str, default="")
     a = ap.parse_args(argv)
     res = run(a)

@@ -139,3 +139,32 @@ def test_nc_x3_fp32_accurate(emu, ks, ch):
         y = neigh_consensus_x3(x, [w.detach() for w in ws], [b.detach() for b in bs], list(ch), True)
         yr = ref.neigh_consensus(x.double(), [w.detach().double() for w in ws], [b.detach().double() for b in bs], True)
     assert rl2(y, yr) < 3e-4
+
+
+@pytest.mark.parametrize("ks,ch", [((5, 5, 5), (16, 16, 1)), ((3, 3), (16, 1)), ((3, 3), (20, 24))])
+def test_nc_x3_training_gradients(emu, ks, ch):
+    """The fp32-accurate training NC (bf16x3 forward, data and weight gradients)
+    matches autograd of the fp64 oracle to ~1e-4 (mixed-sign weights)."""
+    from ncnet_amd.ops.neigh_consensus import NeighConsensusX3Fn
+    torch.manual_seed(4)
+    ws, bs = _params(ks, ch, "mixed")
+    x = torch.rand(2, 1, 4, 5, 4, 5)
+    xa = x.clone().requires_grad_(True)
+    params = []
+    for w, b in zip(ws, bs):
+        params += [w, b]
+    y = NeighConsensusX3Fn.apply(xa, True, tuple(layer_kinds(list(ch), list(ks))), tuple(ch), *params)
+    gy = torch.randn_like(y)
+    (y * gy).sum().backward()
+    got = [xa.grad] + [p.grad.clone() for p in params]
+    xr = x.double().requires_grad_(True)
+    wd = [w.detach().double().requires_grad_(True) for w in ws]
+    bd = [b.detach().double().requires_grad_(True) for b in bs]
+    yr = ref.neigh_consensus(xr, wd, bd, True)
+    (yr * gy.double()).sum().backward()
+    want = [xr.grad]
+    for w, b in zip(wd, bd):
+        want += [w.grad, b.grad]
+    errs = {"y": rl2(y, yr)}
+    errs.update({f"g{i}": rl2(a, b) for i, (a, b) in enumerate(zip(got, want))})
+    assert max(errs.values()) < 1e-3, errs

@@ -63,6 +63,8 @@ def build_parser():
     p.add_argument("--max_steps", type=int, default=0)
     p.add_argument("--metrics", type=str, default="")
     p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--nc_precision", type=str, default="bf16", choices=["bf16", "fp32"],
+                   help="fp32: fp32-accurate NeighConsensus training (bf16x3 splits, 3x NC cost)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--segment_timing", action="store_true")
     p.add_argument("--profile", type=str, default="")
@@ -99,7 +101,7 @@ def main(argv=None):
     # --resume rebuilds the NC architecture from the checkpoint's args, like --checkpoint
     model = ImMatchNet(use_cuda=ctx.device.type == "cuda", checkpoint=(args.resume or args.checkpoint) or None,
                        ncons_kernel_sizes=args.ncons_kernel_sizes, ncons_channels=args.ncons_channels,
-                       dtype=args.dtype).to(ctx.device)
+                       dtype=args.dtype, nc_precision=args.nc_precision).to(ctx.device)
     # the saved Namespace must describe the architecture actually built
     args.ncons_kernel_sizes = list(model.NeighConsensus.kernel_sizes)
     args.ncons_channels = list(model.NeighConsensus.channels)
