@@ -69,6 +69,40 @@ def _inloc_secondary():
     return out
 
 
+def _fe_finetune_secondary(batch: int, size: int, steps: int = 5, warmup: int = 2):
+    """train.py --fe_finetune_params 1 (last layer3 bottleneck trainable,
+    train.py:60-63): the trunk runs under autograd and the L2-norm,
+    correlation and MutualMatching backward and the NC input gradient join the
+    step; one GPU, same config as the headline."""
+    from ncnet_amd.engine.trainer import Trainer, make_adam
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.parallel.dist import DistContext
+    dev = torch.device("cuda")
+    torch.manual_seed(2)
+    model = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1], dtype="bf16").to(dev)
+    for p in model.FeatureExtraction.model[-1][-1].parameters():
+        p.requires_grad = True
+    model.train()
+    params = [p for p in model.parameters() if p.requires_grad]
+    trainer = Trainer(model, make_adam(params, 5e-4), DistContext(device=dev))
+    g = torch.Generator(device=dev).manual_seed(99)
+    pool = [{"source_image": torch.randn(batch, 3, size, size, device=dev, generator=g),
+             "target_image": torch.randn(batch, 3, size, size, device=dev, generator=g)} for _ in range(2)]
+    for w in range(warmup):
+        trainer.train_step(pool[w % 2])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = trainer.train_step(pool[i % 2])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"pairs_per_s": round(batch * steps / dt, 3), "ms_per_step": round(1e3 * dt / steps, 3),
+           "trainable_params": sum(p.numel() for p in params), "final_loss": float(loss.detach())}
+    del trainer, model
+    torch.cuda.empty_cache()
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,6 +209,11 @@ def main(argv=None):
     secondary = None
     if args.inloc and ctx.is_main and dev.type == "cuda" and args.impl == "hip":
         secondary = _inloc_secondary()
+        if ctx.world_size == 1:
+            try:
+                secondary["fe_finetune_1"] = _fe_finetune_secondary(args.batch, s)
+            except Exception as e:  # the headline record must still print
+                secondary["fe_finetune_1"] = {"error": repr(e)}
     if ctx.is_main:
         rec = {
             "metric": "image-pairs/sec fwd+bwd, ResNet-101+NC-Net(5,5,5) 400x400 bf16",

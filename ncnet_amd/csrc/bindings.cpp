@@ -38,6 +38,7 @@ int ncnet_nonfinite_count(const float*, long long, int*, hipStream_t);
 int ncnet_adam_masked(float*, float*, float*, float*, long long, const int*, const float*, float, float, float, float,
                       float, float, hipStream_t);
 int ncnet_adam_finalize(float*, int*, int*, hipStream_t);
+int ncnet_resize_norm_u8(const void*, const long long*, float*, int, int, int, const float*, const float*, hipStream_t);
 int ncnet_nc_fused_k3(const void*, const void*, const float*, const void*, const float*, float*, int, int, int, int,
                       int, int, int, int, int, hipStream_t);
 }
@@ -479,6 +480,24 @@ void adam_finalize(Tensor step, Tensor count, Tensor skipped) {
      "adam_finalize");
 }
 
+// Batched resize + normalise of packed HWC uint8 images (csrc/dataprep.hip).
+// src uint8 [bytes] (device), meta int64 [B, 3] = (byte offset, H, W) (device;
+// validated against src by the caller before its host->device copy),
+// out fp32 [B, 3, oh, ow]; mean / std: 3 floats each.
+void resize_norm_u8(Tensor src, Tensor meta, Tensor out, std::vector<double> mean, std::vector<double> stdv) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
+  check(src, "src", at::kByte); check(meta, "meta", at::kLong); check(out, "out", at::kFloat);
+  TORCH_CHECK(src.dim() == 1, "src must be a flat byte buffer");
+  TORCH_CHECK(meta.dim() == 2 && meta.size(1) == 3, "meta must be [B, 3]");
+  TORCH_CHECK(out.dim() == 4 && out.size(0) == meta.size(0) && out.size(1) == 3, "out must be [B, 3, oh, ow]");
+  TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "mean / std need 3 values");
+  const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  const float sd[3] = {(float)stdv[0], (float)stdv[1], (float)stdv[2]};
+  ok(ncnet_resize_norm_u8(src.data_ptr(), (const long long*)meta.data_ptr(), (float*)out.data_ptr(), (int)out.size(0),
+                          (int)out.size(2), (int)out.size(3), m, sd, cur_stream(src)),
+     "resize_norm_u8");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for ncnet_amd";
   m.def("conv16_fwd", &conv16_fwd);
@@ -502,6 +521,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool4d", &maxpool4d);
   m.def("transpose", &transpose);
   m.def("nc_fused_k3", &nc_fused_k3);
+  m.def("resize_norm_u8", &resize_norm_u8);
   m.def("nonfinite_count", &nonfinite_count);
   m.def("adam_masked", &adam_masked);
   m.def("adam_finalize", &adam_finalize);

@@ -25,8 +25,13 @@ class ImagePairDataset(Dataset):
     """Weakly supervised image pairs (lib/im_pair_dataset.py:11-93)."""
 
     def __init__(self, dataset_csv_path, dataset_csv_file, dataset_image_path, dataset_size=0,
-                 output_size=(240, 240), transform=None, random_crop=False):
+                 output_size=(240, 240), transform=None, random_crop=False, gpu_resize=False):
+        """``gpu_resize``: return the decoded (cropped / flipped) images as
+        uint8 CHW tensors of their own size and let the consumer resize +
+        normalise the batch on the GPU (``gpu_pair_batch``; collate with
+        ``collate_uint8_pairs``) -- the DataLoader workers then only decode."""
         self.random_crop = random_crop
+        self.gpu_resize = gpu_resize
         self.out_h, self.out_w = output_size
         data = pd.read_csv(os.path.join(dataset_csv_path, dataset_csv_file))
         if dataset_size:
@@ -53,6 +58,8 @@ class ImagePairDataset(Dataset):
         if flip:
             image = np.flip(image, 1)
         im_size = torch.tensor(image.shape, dtype=torch.float32)
+        if self.gpu_resize:          # HWC uint8 as decoded; packed per batch by collate_uint8_pairs
+            return torch.from_numpy(np.ascontiguousarray(image)), im_size
         img = resize_bilinear(to_chw_float(image), self.out_h, self.out_w)
         return img, im_size
 
@@ -61,10 +68,60 @@ class ImagePairDataset(Dataset):
         b, sb = self.get_image(self.img_B_names[idx], self.flip[idx])
         sample = {"source_image": a, "target_image": b, "source_im_size": sa, "target_im_size": sb,
                   "set": int(self.set[idx])}
-        if self.transform:
+        if self.transform and not self.gpu_resize:
             sample = self.transform(sample)
         return sample
 
+
+def collate_uint8_pairs(samples):
+    """Batch of ``gpu_resize`` samples (runs in the DataLoader workers): the
+    decoded HWC uint8 pixels of all 2B images are packed into ONE byte buffer
+    ``pixels`` with a table ``pixel_meta`` [2B, 3] = (byte offset, H, W)
+    (sources first, then targets) -- one pinned tensor, one host->device copy;
+    everything else is stacked."""
+    imgs = [s["source_image"] for s in samples] + [s["target_image"] for s in samples]
+    sizes = [int(x.numel()) for x in imgs]
+    offs = np.concatenate(([0], np.cumsum(sizes)[:-1])).astype(np.int64)
+    meta = torch.tensor([[o, x.shape[0], x.shape[1]] for o, x in zip(offs, imgs)], dtype=torch.int64)
+    out = {"pixels": torch.cat([x.reshape(-1) for x in imgs]), "pixel_meta": meta}
+    for k in samples[0]:
+        if k in ("source_image", "target_image"):
+            continue
+        vals = [s[k] for s in samples]
+        out[k] = torch.stack(vals) if torch.is_tensor(vals[0]) else torch.tensor(vals)
+    return out
+
+
+def gpu_pair_batch(batch, device, out_h: int, out_w: int):
+    """Move a ``collate_uint8_pairs`` batch to ``device`` (uint8 pixels: 4x
+    fewer bytes than float, one non-blocking copy) and resize + normalise all
+    images there in one HIP launch (csrc/dataprep.hip): bilinear with
+    align_corners=True as the reference's identity AffineTnf
+    (lib/transformation.py), then ImageNet normalisation
+    (lib/normalization.py).  On CPU the same math runs through torch."""
+    from .transforms import IMAGENET_MEAN, IMAGENET_STD, gpu_normalize_resize
+    from ..ops import _ext
+    pix, meta = batch["pixels"], batch["pixel_meta"]
+    n = meta.shape[0]
+    ends = meta[:, 0] + meta[:, 1] * meta[:, 2] * 3
+    if int(ends.max()) > pix.numel() or int(meta[:, 1:].min()) < 1:
+        raise ValueError("malformed pixel table")
+    res = {k: (v.to(device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()
+           if k not in ("pixels", "pixel_meta")}
+    dev = torch.device(device)
+    if dev.type == "cuda" and _ext.use_hip(pix.to(dev, non_blocking=True)[:1]):
+        out = torch.empty((n, 3, out_h, out_w), dtype=torch.float32, device=dev)
+        _ext.ext().resize_norm_u8(pix.to(dev, non_blocking=True), meta.to(dev, non_blocking=True), out,
+                                  list(IMAGENET_MEAN), list(IMAGENET_STD))
+    else:
+        ims = []
+        for o, h, w in meta.tolist():
+            x = pix[o:o + h * w * 3].view(h, w, 3).permute(2, 0, 1).unsqueeze(0).to(dev)
+            ims.append(gpu_normalize_resize(x, out_h, out_w))
+        out = torch.cat(ims)
+    b = n // 2
+    res["source_image"], res["target_image"] = out[:b], out[b:]
+    return res
 
 class PFPascalDataset(Dataset):
     """PF-Pascal keypoint pairs (lib/pf_dataset.py:11-112)."""

@@ -118,6 +118,11 @@ class TrunkPrefetcher:
             main.wait_event(done)
             f.record_stream(main)
             return f, hw, b
+        if self.enabled:                        # batch may have been moved on the prefetch stream
+            main = torch.cuda.current_stream(self.stream.device)
+            main.wait_stream(self.stream)
+            for t in (batch["source_image"], batch["target_image"]):
+                t.record_stream(main)
         with segment("backbone"):
             return self._extract(batch)
 
@@ -137,10 +142,24 @@ class Trainer:
         self.global_step = 0
         self.fault_step = fault_step if fault_step is not None else int(os.environ.get("NCNET_FAULT_STEP", "-1"))
         self.prefetch = TrunkPrefetcher(model)
+        self.batch_to_device = None       # optional hook: host batch -> device batch (train.py: GPU resize)
 
-    def to_device(self, batch):
+    def _move(self, batch):
+        if self.batch_to_device is not None:
+            return self.batch_to_device(batch)
         dev = self.ctx.device
         return {k: (v.to(dev, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()}
+
+    def to_device(self, batch):
+        """Host batch -> device.  With the trunk prefetcher the copies (and a
+        ``batch_to_device`` hook such as train.py's GPU resize + normalise) are
+        queued on the prefetch stream, in front of that batch's backbone, so they
+        overlap the current step instead of delaying it on the main stream."""
+        st = self.prefetch.stream if self.prefetch.enabled else None
+        if st is None:
+            return self._move(batch)
+        with torch.cuda.stream(st):
+            return self._move(batch)
 
     def train_step(self, batch, next_batch=None) -> torch.Tensor:
         """One step on ``batch``; ``next_batch`` (already on the device) gets
@@ -182,6 +201,8 @@ class Trainer:
 
     @torch.inference_mode()
     def eval_step(self, batch) -> torch.Tensor:
+        if self.prefetch.enabled:               # the batch was moved on the prefetch stream
+            torch.cuda.current_stream(self.prefetch.stream.device).wait_stream(self.prefetch.stream)
         return weak_loss(self.model, batch, self.normalization).detach()
 
     def _log(self, rec: dict):

@@ -578,3 +578,24 @@ def test_pipelined_step_equals_serial(monkeypatch):
     assert torch.equal(l_ser, l_pip), (l_ser, l_pip)
     for a, b in zip(p_ser, p_pip):
         assert torch.equal(a, b)
+
+
+def test_resize_norm_u8_kernel():
+    """One-launch batched resize + normalise of packed HWC uint8 images of
+    different sizes (csrc/dataprep.hip) vs torch bilinear (align_corners=True)
+    + ImageNet normalisation."""
+    from ncnet_amd.data.datasets import collate_uint8_pairs, gpu_pair_batch
+    from ncnet_amd.data.transforms import gpu_normalize_resize
+    g = torch.Generator().manual_seed(5)
+    samples = []
+    for (h1, w1), (h2, w2) in (((375, 500), (500, 333)), ((300, 300), (481, 322)), ((17, 9), (400, 400))):
+        samples.append({"source_image": torch.randint(0, 256, (h1, w1, 3), generator=g, dtype=torch.uint8),
+                        "target_image": torch.randint(0, 256, (h2, w2, 3), generator=g, dtype=torch.uint8),
+                        "set": 1})
+    batch = collate_uint8_pairs(samples)
+    out = gpu_pair_batch(batch, DEV, 400, 400)
+    for k in ("source_image", "target_image"):
+        want = torch.cat([gpu_normalize_resize(s[k].permute(2, 0, 1).unsqueeze(0).to(DEV), 400, 400)
+                          for s in samples])
+        assert out[k].shape == want.shape
+        assert (out[k] - want).abs().max() < 2e-4

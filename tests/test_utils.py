@@ -132,3 +132,34 @@ def test_fetch_assets_dry_run(capsys):
     out = capsys.readouterr().out
     assert "PF-dataset-PASCAL.zip" in out and "ncnet_ivd.pth.tar" in out
     assert len(m.read_pairs_file(m.DATASETS / "ivd" / "urls.txt")) == 3708
+
+
+def test_gpu_resize_path_matches_cpu_resize(tmp_path):
+    """The uint8 decode-only dataset + batched resize/normalise (train.py's GPU
+    path, run here on CPU tensors) equals the reference-style per-sample CPU
+    resize + NormalizeImageDict."""
+    import sys
+
+    import torch
+
+    sys.path.insert(0, str(tmp_path.parent))
+    from ncnet_amd.data.datasets import ImagePairDataset, collate_uint8_pairs, gpu_pair_batch
+    from ncnet_amd.data.transforms import NormalizeImageDict
+    import importlib.util
+    import os
+    p = os.path.join(os.path.dirname(__file__), "..", "scripts", "make_jpeg_pairs.py")
+    spec = importlib.util.spec_from_file_location("mkj", p)
+    mkj = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mkj)
+    mkj.main(["--out", str(tmp_path), "--pairs", "6"])
+    csv = str(tmp_path / "image_pairs")
+    norm = NormalizeImageDict(["source_image", "target_image"])
+    a = ImagePairDataset(csv, "train_pairs.csv", str(tmp_path), output_size=(64, 80), transform=norm)
+    b = ImagePairDataset(csv, "train_pairs.csv", str(tmp_path), output_size=(64, 80), transform=norm, gpu_resize=True)
+    sa = [a[i] for i in range(3)]
+    batch = gpu_pair_batch(collate_uint8_pairs([b[i] for i in range(3)]), "cpu", 64, 80)
+    for k in ("source_image", "target_image"):
+        want = torch.stack([s[k] for s in sa])
+        assert batch[k].shape == want.shape == (3, 3, 64, 80)
+        assert torch.allclose(batch[k], want, atol=1e-4)
+    assert torch.equal(batch["source_im_size"], torch.stack([s["source_im_size"] for s in sa]))

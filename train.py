@@ -33,6 +33,7 @@ from torch.utils.data import DataLoader, Subset
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from ncnet_amd.data import ImagePairDataset, NormalizeImageDict, SyntheticPairDataset  # noqa: E402
+from ncnet_amd.data.datasets import collate_uint8_pairs, gpu_pair_batch  # noqa: E402
 from ncnet_amd.engine.checkpoint import capture_rng, load_checkpoint, restore_rng, save_checkpoint  # noqa: E402
 from ncnet_amd.engine.trainer import Trainer, make_adam  # noqa: E402
 from ncnet_amd.models import ImMatchNet  # noqa: E402
@@ -57,7 +58,10 @@ def build_parser():
     p.add_argument("--fe_finetune_params", type=int, default=0, help="number of layers to finetune")
     # extensions
     p.add_argument("--synthetic", type=int, default=0)
-    p.add_argument("--num_workers", type=int, default=0)
+    p.add_argument("--num_workers", type=int, default=-1,
+                   help="DataLoader decode workers per rank (-1: min(8, cpus per rank) on GPU, 0 on CPU)")
+    p.add_argument("--cpu_resize", action="store_true",
+                   help="resize/normalise in the workers (reference behaviour) instead of on the GPU")
     p.add_argument("--log_interval", type=int, default=1)
     p.add_argument("--resume", type=str, default="")
     p.add_argument("--max_steps", type=int, default=0)
@@ -118,22 +122,31 @@ def main(argv=None):
     optimizer = make_adam(params, args.lr)
 
     size = (args.image_size, args.image_size)
+    gpu_resize = ctx.device.type == "cuda" and not args.cpu_resize
     if args.synthetic:
         train_set = SyntheticPairDataset(args.synthetic, size, seed=1)
         test_set = SyntheticPairDataset(max(2 * args.batch_size, args.synthetic // 8), size, seed=2)
     else:
         norm = NormalizeImageDict(["source_image", "target_image"])
         train_set = ImagePairDataset(args.dataset_csv_path, "train_pairs.csv", args.dataset_image_path,
-                                     output_size=size, transform=norm)
+                                     output_size=size, transform=norm, gpu_resize=gpu_resize)
         test_set = ImagePairDataset(args.dataset_csv_path, "val_pairs.csv", args.dataset_image_path,
-                                    output_size=size, transform=norm)
+                                    output_size=size, transform=norm, gpu_resize=gpu_resize)
     tr_sampler = _Shard(len(train_set), ctx, True, args.seed)
     te_sampler = _Shard(len(test_set), ctx, True, args.seed + 7)
     pin = ctx.device.type == "cuda"
-    train_loader = DataLoader(train_set, batch_size=args.batch_size, sampler=tr_sampler, num_workers=args.num_workers,
-                              pin_memory=pin, drop_last=True)
-    test_loader = DataLoader(test_set, batch_size=args.batch_size, sampler=te_sampler, num_workers=args.num_workers,
-                             pin_memory=pin, drop_last=True)
+    nw = args.num_workers
+    if nw < 0:
+        nw = min(8, max(1, (os.cpu_count() or 2) // max(1, ctx.world_size) - 1)) if pin else 0
+    lkw = dict(batch_size=args.batch_size, num_workers=nw, pin_memory=pin, drop_last=True,
+               collate_fn=collate_uint8_pairs if (gpu_resize and not args.synthetic) else None,
+               persistent_workers=nw > 0, prefetch_factor=4 if nw > 0 else None)
+    train_loader = DataLoader(train_set, sampler=tr_sampler, **lkw)
+    test_loader = DataLoader(test_set, sampler=te_sampler, **lkw)
+    if gpu_resize and not args.synthetic:
+        trainer_to_device = lambda batch: gpu_pair_batch(batch, ctx.device, size[0], size[1])  # noqa: E731
+    else:
+        trainer_to_device = None
 
     checkpoint_name = os.path.join(args.result_model_dir,
                                    datetime.datetime.now().strftime("%Y-%m-%d_%H:%M") + "_" + args.result_model_fn +
@@ -160,6 +173,7 @@ def main(argv=None):
     timer = SegmentTimer(device=ctx.device) if args.segment_timing else None
     set_active(timer)
     trainer = Trainer(model, optimizer, ctx, metrics_path=args.metrics or None)
+    trainer.batch_to_device = trainer_to_device
     if args.max_steps:
         # bounded run (smoke / profiling)
         model.train()
@@ -171,18 +185,30 @@ def main(argv=None):
             prof = torch.profiler.profile(activities=acts)
             prof.__enter__()
         t0 = time.perf_counter()
+        t_warm, warm = None, min(10, max(0, args.max_steps - 1))
         steps = 0
+
+        def batches():
+            while True:
+                for b in train_loader:
+                    yield b
+        it = batches()
+        nxt = trainer.to_device(next(it))
         while steps < args.max_steps:
-            for batch in train_loader:
-                loss = trainer.train_step(trainer.to_device(batch))
-                steps += 1
-                if ctx.is_main and (steps % max(1, args.log_interval) == 0):
-                    msg = f"step {steps} loss {float(loss):.6f}"
-                    if timer is not None:
-                        msg += " " + " ".join(f"{k}={v:.2f}ms" for k, v in timer.collect().items())
-                    print(msg, flush=True)
-                if steps >= args.max_steps:
-                    break
+            batch = nxt
+            # one batch of lookahead, as Trainer.process_epoch: its backbone overlaps this step
+            nxt = trainer.to_device(next(it)) if steps + 1 < args.max_steps else None
+            loss = trainer.train_step(batch, nxt)
+            steps += 1
+            if steps == warm:
+                if ctx.device.type == "cuda":
+                    torch.cuda.synchronize()
+                t_warm = time.perf_counter()
+            if ctx.is_main and (steps % max(1, args.log_interval) == 0):
+                msg = f"step {steps} loss {float(loss):.6f}"
+                if timer is not None:
+                    msg += " " + " ".join(f"{k}={v:.2f}ms" for k, v in timer.collect().items())
+                print(msg, flush=True)
         if ctx.device.type == "cuda":
             torch.cuda.synchronize()
         if prof is not None:
@@ -193,8 +219,14 @@ def main(argv=None):
                 f.write(prof.key_averages().table(sort_by=sort, row_limit=60))
             prof.export_chrome_trace(os.path.join(args.profile, "train_trace.json"))
         if ctx.is_main:
-            dt = time.perf_counter() - t0
-            print(f"{steps} steps in {dt:.2f}s ({steps * args.batch_size * ctx.world_size / dt:.1f} pairs/s)")
+            t1 = time.perf_counter()
+            dt = t1 - t0
+            msg = f"{steps} steps in {dt:.2f}s ({steps * args.batch_size * ctx.world_size / dt:.1f} pairs/s)"
+            if t_warm is not None and steps > warm:
+                # steady state: excludes DataLoader worker start-up and the first (graph-capturing) steps
+                msg += (f"; steady state after {warm} steps: "
+                        f"{(steps - warm) * args.batch_size * ctx.world_size / (t1 - t_warm):.1f} pairs/s")
+            print(msg)
         set_active(None)
         destroy(ctx)
         return
