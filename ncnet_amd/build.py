@@ -1,5 +1,17 @@
 """In-tree build of the gfx950 HIP extension ``ncnet_amd/_C.so``.
 
+Variants (the sanitizer tier):
+* ``release`` (default): ``-O3`` -> ``_C.so``;
+* ``debug``: ``-O1 -g -DNCNET_DEBUG=1`` -> ``_C_debug.so``: device-side bounds
+  checks (``NCNET_CHECK`` in csrc/common.h) print the failing condition with
+  file:line from the kernel instead of silently reading out of range;
+* ``asan``: host code (pybind bindings and every launcher) built with
+  AddressSanitizer by clang (``-Xarch_host -fsanitize=address``; device code
+  unsanitized, GPU ASan is not available here) -> ``_C_asan.so``; run with
+  ``LD_PRELOAD=<libclang_rt.asan-x86_64.so> ASAN_OPTIONS=detect_leaks=0``
+  (``asan_runtime()`` returns the path).
+``NCNET_EXT=debug|asan`` makes ``ops._ext`` import that variant.
+
 Each ``csrc/*.hip`` file is compiled by hipcc for gfx950 only (no torch
 headers, so kernels rebuild in seconds); ``bindings.cpp`` is the only
 translation unit that includes torch.  Objects are relinked into one shared
@@ -56,27 +68,58 @@ def _run(cmd):
     return r.stdout
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
-    BUILD.mkdir(exist_ok=True)
+VARIANTS = ("release", "debug", "asan")
+CLANGXX = os.path.join(ROCM, "lib", "llvm", "bin", "clang++")
+
+
+def asan_runtime() -> str:
+    """The clang AddressSanitizer runtime matching hipcc (LD_PRELOAD it)."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(ROCM, "lib", "llvm", "lib", "clang", "*", "lib", "linux",
+                                         "libclang_rt.asan-x86_64.so")))
+    if not hits:
+        raise FileNotFoundError("libclang_rt.asan-x86_64.so not found under ROCm's LLVM")
+    return hits[-1]
+
+
+def target_for(variant: str) -> Path:
+    return TARGET if variant == "release" else PKG / f"_C_{variant}.so"
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False, variant: str = "release") -> Path:
+    if variant not in VARIANTS:
+        raise ValueError(f"variant must be one of {VARIANTS}")
+    bdir = BUILD if variant == "release" else PKG / f"_build_{variant}"
+    target = target_for(variant)
+    modname = target.stem
+    bdir.mkdir(exist_ok=True)
     headers = sorted(CSRC.glob("*.h"))
     hip_srcs = sorted(CSRC.glob("*.hip"))
     inc, libdir, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
+    hip_flags = list(HIP_FLAGS)
+    if variant == "debug":
+        hip_flags = [f for f in hip_flags if f != "-O3"] + ["-O1", "-g", "-DNCNET_DEBUG=1"]
+    elif variant == "asan":
+        hip_flags = [f for f in hip_flags if f != "-O3"] + ["-O1", "-g", "-Xarch_host", "-fsanitize=address",
+                                                             "-Xarch_host", "-fno-omit-frame-pointer"]
 
     steps = []
     objs = []
     for src in hip_srcs:
-        obj = BUILD / (src.stem + ".o")
+        obj = bdir / (src.stem + ".o")
         objs.append(obj)
         if force or _newer(src, obj, headers):
-            steps.append([HIPCC, *HIP_FLAGS, "-I", str(CSRC), "-c", str(src), "-o", str(obj)])
+            steps.append([HIPCC, *hip_flags, "-I", str(CSRC), "-c", str(src), "-o", str(obj)])
     bsrc = CSRC / "bindings.cpp"
-    bobj = BUILD / "bindings.o"
+    bobj = bdir / "bindings.o"
     objs.append(bobj)
     if force or _newer(bsrc, bobj):
-        cmd = ["g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-               "-DTORCH_EXTENSION_NAME=_C", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I", py_inc,
-               "-I", os.path.join(ROCM, "include"), "-Wno-deprecated-declarations"]
+        cxx = ["g++", "-O2"] if variant != "asan" else [CLANGXX, "-O1", "-g", "-fsanitize=address",
+                                                        "-fno-omit-frame-pointer"]
+        cmd = cxx + ["-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+                     f"-DTORCH_EXTENSION_NAME={modname}", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I", py_inc,
+                     "-I", os.path.join(ROCM, "include"), "-Wno-deprecated-declarations"]
         for p in inc:
             cmd += ["-I", p]
         cmd += ["-c", str(bsrc), "-o", str(bobj)]
@@ -88,13 +131,15 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
             for out in ex.map(_run, steps):
                 if verbose and out.strip():
                     print(out)
-    if force or steps or not TARGET.exists() or any(o.stat().st_mtime > TARGET.stat().st_mtime for o in objs):
-        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(TARGET) + ".tmp",
+    if force or steps or not target.exists() or any(o.stat().st_mtime > target.stat().st_mtime for o in objs):
+        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(target) + ".tmp",
                 "-L", libdir, "-Wl,-rpath," + libdir, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
                 "-ltorch_hip", "-ltorch_python", "-L", os.path.join(ROCM, "lib"), "-lamdhip64"]
+        if variant == "asan":
+            link += ["-shared-libasan", "-fsanitize=address"]
         _run(link)
-        os.replace(str(TARGET) + ".tmp", TARGET)
-    return TARGET
+        os.replace(str(target) + ".tmp", target)
+    return target
 
 
 def main(argv=None):
@@ -102,8 +147,12 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("-v", action="store_true")
+    ap.add_argument("--variant", choices=VARIANTS, default="release")
+    ap.add_argument("--debug", action="store_true", help="same as --variant debug")
+    ap.add_argument("--asan", action="store_true", help="same as --variant asan")
     a = ap.parse_args(argv)
-    out = build(force=a.force, jobs=a.j, verbose=a.v)
+    variant = "debug" if a.debug else "asan" if a.asan else a.variant
+    out = build(force=a.force, jobs=a.j, verbose=a.v, variant=variant)
     print(f"built {out}")
 
 

@@ -39,6 +39,7 @@ int ncnet_adam_masked(float*, float*, float*, float*, long long, const int*, con
                       float, float, hipStream_t);
 int ncnet_adam_finalize(float*, int*, int*, hipStream_t);
 int ncnet_resize_norm_u8(const void*, const long long*, float*, int, int, int, const float*, const float*, hipStream_t);
+int ncnet_debug_selftest(int*, hipStream_t);
 int ncnet_nc_fused_k3(const void*, const void*, const float*, const void*, const float*, float*, int, int, int, int,
                       int, int, int, int, int, hipStream_t);
 }
@@ -484,6 +485,13 @@ void adam_finalize(Tensor step, Tensor count, Tensor skipped) {
 // src uint8 [bytes] (device), meta int64 [B, 3] = (byte offset, H, W) (device;
 // validated against src by the caller before its host->device copy),
 // out fp32 [B, 3, oh, ow]; mean / std: 3 floats each.
+// 1 from a release build; 0 (after printing an NCNET_CHECK line) from the debug build.
+int64_t debug_selftest(Tensor out) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kInt && out.numel() >= 1, "debug_selftest: int32 cuda");
+  ok(ncnet_debug_selftest((int*)out.data_ptr(), cur_stream(out)), "debug_selftest");
+  return out.cpu().item<int>();
+}
+
 void resize_norm_u8(Tensor src, Tensor meta, Tensor out, std::vector<double> mean, std::vector<double> stdv) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
   check(src, "src", at::kByte); check(meta, "meta", at::kLong); check(out, "out", at::kFloat);
@@ -522,6 +530,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose", &transpose);
   m.def("nc_fused_k3", &nc_fused_k3);
   m.def("resize_norm_u8", &resize_norm_u8);
+  m.def("debug_selftest", &debug_selftest);
   m.def("nonfinite_count", &nonfinite_count);
   m.def("adam_masked", &adam_masked);
   m.def("adam_finalize", &adam_finalize);

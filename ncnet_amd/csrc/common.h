@@ -96,3 +96,21 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblocks) {
 }
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Debug-build bounds checks (python -m ncnet_amd.build --debug -> _C_debug.so).
+// NCNET_OK(cond) is `cond` in the debug build -- printing the failed condition
+// with file:line and the block / thread, so the guarded access is skipped
+// instead of faulting -- and `true` (compiled away) in release.  Used on every
+// global-memory address a kernel forms from runtime geometry (LDS-DMA sources
+// and destinations, gathers, stores); tests/conftest.py fails any GPU test
+// whose output contains "NCNET_CHECK" when run with NCNET_EXT=debug.
+#ifdef NCNET_DEBUG
+__device__ __noinline__ bool ncnet_check_fail(const char* cond, const char* file, int line) {
+  printf("NCNET_CHECK failed %s:%d: %s (block %d,%d,%d thread %d)\n", file, line, cond, (int)blockIdx.x,
+         (int)blockIdx.y, (int)blockIdx.z, (int)threadIdx.x);
+  return false;
+}
+#define NCNET_OK(cond) ((cond) ? true : ncnet_check_fail(#cond, __FILE__, __LINE__))
+#else
+#define NCNET_OK(cond) true
+#endif

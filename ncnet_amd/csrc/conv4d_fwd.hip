@@ -69,6 +69,7 @@ template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
                                         const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0,
                                         int nco = 16, bool nt = false) {
+  if (!NCNET_OK(vox_index < nvox_all && co0 >= 0 && co0 + 4 <= 16)) return;
   if (EPI == EPI_F32X16) {
     // channel-planar fp32 [nco][nvox_all] (only the channels a consumer reads):
     // 16 lanes write 16 consecutive voxels of one channel
@@ -169,6 +170,8 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
   const int nchunk = 2 * (lend - lstart);
   const int col0 = lstart - (t.l0 - P);
 
+  const size_t xext = g.npg > 0 ? (size_t)g.npg * g.gstride : (size_t)g.V * g.I * g.J * g.K * g.L * 16;
+  (void)xext;
   // plane s of output j-tile t.j + jt (jt > 0 only in multi-tile group-plane mode)
   auto issue_x = [&](int jt, int s, char* buf) {
     const bf16* xp;
@@ -182,15 +185,18 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
       const int kg = t.k0 - P + r;
       if (kg >= 0 && kg < g.K && lane < nchunk) {
         const bf16* src = xp + ((size_t)kg * g.L + lstart) * 16 + lane * 8;
-        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(void, buf + (r * g.RS + col0) * 32), 16, 0, 0);
+        if (NCNET_OK((size_t)(src - X) + 8 <= xext) &&
+            NCNET_OK((r * g.RS + col0) * 32 + lane * 16 + 16 <= plane_bytes))
+          __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(void, buf + (r * g.RS + col0) * 32), 16, 0, 0);
       }
     }
   };
   auto issue_w = [&](int s) {
     const int wplane = g.npg > 0 ? s : (di_lo + s / ndj) * KS + dj_lo + s % ndj;
     const u32x4* wp = Wp + (size_t)wplane * (NQ * 64);
-    for (int q = wave; q < NQ; q += NW)
-      __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + q * 1024), 16, 0, 0);
+    if (NCNET_OK(wplane >= 0 && wplane < (g.npg > 0 ? g.npg : NT)))
+      for (int q = wave; q < NQ; q += NW)
+        __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + q * 1024), 16, 0, 0);
   };
 
   const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
@@ -339,18 +345,23 @@ __global__ __launch_bounds__(512, 1) void conv16v3_fwd_kernel(const bf16* __rest
   const int nchunk = 2 * (lend - lstart);
   const int col0 = lstart - (l0 - P);
 
+  const size_t xext = (size_t)g.V * g.I * g.J * g.K * g.L * 16;
+  (void)xext;
   auto issue_x = [&](int di, int jp, char* buf) {
     const bf16* xp = X + plane_offset(g, tv, ti + di - P, jp, 16);
     for (int r = wave; r < g.PR; r += NW) {
       const int kg = k0 - P + r;
       if (kg >= 0 && kg < g.K && lane < nchunk) {
         const bf16* src = xp + ((size_t)kg * g.L + lstart) * 16 + lane * 8;
-        __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(void, buf + (r * g.RS + col0) * 32), 16, 0, 0);
+        if (NCNET_OK(src >= X && (size_t)(src - X) + 8 <= xext) &&
+            NCNET_OK((r * g.RS + col0) * 32 + lane * 16 + 16 <= plane_bytes))
+          __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(void, buf + (r * g.RS + col0) * 32), 16, 0, 0);
       }
     }
   };
   auto issue_w = [&](int di, int dj) {
     const u32x4* wp = Wp + (size_t)(di * KS + dj) * (NQ * 64);
+    if (NCNET_OK(di >= 0 && di < KS && dj >= 0 && dj < KS))
     for (int q = wave; q < NQ; q += NW)
       __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + (dj * NQ + q) * 1024),
                                        16, 0, 0);

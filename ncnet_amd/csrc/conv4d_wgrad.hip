@@ -134,6 +134,8 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
     // with ds_write (tile positions differ per item, so no stale halo survives).
     const bf16* xp = X + plane_off(g, r.v, ii, jj, 16);
     const bf16* gp = G + plane_off(g, r.v, r.i, r.j, 16);
+    const size_t ext = (size_t)g.V * g.I * g.J * g.K * g.L * 16;
+    (void)ext;
     {
       const int ls = max(0, r.l0 - P), le = min(g.L, r.l0 - P + g.RW);
       const int c0 = 2 * (ls - (r.l0 - P)), c1 = c0 + 2 * (le - ls);
@@ -141,7 +143,8 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
         const int kg = r.k0 - P + row;
         const bool in_k = kg >= 0 && kg < g.K;
         if (in_k) {
-          if (lane < c1 - c0)
+          if (lane < c1 - c0 && NCNET_OK((size_t)(xp - X) + ((size_t)kg * g.L + ls) * 16 + lane * 8 + 8 <= ext) &&
+              NCNET_OK(row * g.RS * 32 + c0 * 16 + lane * 16 + 16 <= g.PR * g.RS * 32))
             __builtin_amdgcn_global_load_lds((const void*)(xp + ((size_t)kg * g.L + ls) * 16 + lane * 8),
                                              LDS_PTR(void, plane + row * g.RS * 32 + c0 * 16), 16, 0, 0);
         }
@@ -150,7 +153,8 @@ __global__ __launch_bounds__(512, 2) void wgrad16v2_kernel(const bf16* __restric
       }
       const int tl = min(g.TL, g.L - r.l0), tk = min(g.TK, g.K - r.k0);
       for (int row = wave; row < g.TK; row += NW) {
-        if (row < tk && lane < 2 * tl)
+        if (row < tk && lane < 2 * tl &&
+            NCNET_OK((size_t)(gp - G) + ((size_t)(r.k0 + row) * g.L + r.l0) * 16 + lane * 8 + 8 <= ext))
           __builtin_amdgcn_global_load_lds((const void*)(gp + ((size_t)(r.k0 + row) * g.L + r.l0) * 16 + lane * 8),
                                            LDS_PTR(void, gt + row * g.TL * 32), 16, 0, 0);
         else if (lane < 2 * g.TL)
@@ -307,13 +311,16 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
     return c;
   };
 
+  const size_t ext = (size_t)g.V * g.I * g.J * g.K * g.L * 16;
+  (void)ext;
   // Stage the X rows kf-P .. kf-P+PR-1 of plane (ii, jj), full width, col 0 <-> l = -P.
   auto stage_x = [&](const Col& r, int ii, char* buf) {
     const bf16* xp = X + ((((size_t)r.v * g.I + ii) * g.J + r.jj) * (size_t)g.K * g.L) * 16;
     for (int row = wave; row < g.PR; row += NW) {
       const int kg = r.kf - P + row;
       const bool in_k = kg >= 0 && kg < g.K;
-      if (in_k && lane < 2 * g.L)
+      if (in_k && lane < 2 * g.L && NCNET_OK((size_t)(xp - X) + (size_t)kg * g.L * 16 + lane * 8 + 8 <= ext) &&
+          NCNET_OK(row * g.RS * 32 + P * 32 + lane * 16 + 16 <= g.PR * g.RS * 32))
         __builtin_amdgcn_global_load_lds((const void*)(xp + (size_t)kg * g.L * 16 + lane * 8),
                                          LDS_PTR(void, buf + row * g.RS * 32 + P * 32), 16, 0, 0);
       if (lane < 2 * g.RW && (!in_k || lane < 2 * P || lane >= 2 * P + 2 * g.L))
@@ -326,7 +333,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
     const bf16* gp = G + ((((size_t)r.v * g.I + gi) * g.J + gj) * (size_t)g.K * g.L + r.a) * 16;
     for (int q = wave; q * 64 < 2 * g.VT; q += NW) {
       const int ci = q * 64 + lane;
-      if (ci < 2 * r.nv)
+      if (ci < 2 * r.nv && NCNET_OK((size_t)(gp - G) + ci * 8 + 8 <= ext))
         __builtin_amdgcn_global_load_lds((const void*)(gp + ci * 8), LDS_PTR(void, buf + q * 1024), 16, 0, 0);
       else
         *(u32x4*)(buf + ci * 16) = u32x4{0u, 0u, 0u, 0u};

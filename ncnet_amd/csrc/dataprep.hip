@@ -36,6 +36,7 @@ __global__ __launch_bounds__(256) void resize_norm_u8_kernel(const uint8_t* __re
   const int y0 = min((int)sy, H - 1), x0 = min((int)sx, W - 1);
   const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
   const float fy = sy - (float)y0, fx = sx - (float)x0;
+  if (!NCNET_OK(off >= 0 && H > 0 && W > 0 && (b == 0 || off >= meta[3 * (b - 1)]))) return;
   const uint8_t* im = src + off;
   const uint8_t* a = im + ((size_t)y0 * W + x0) * 3;
   const uint8_t* bb = im + ((size_t)y0 * W + x1) * 3;

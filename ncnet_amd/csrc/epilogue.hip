@@ -28,9 +28,20 @@ __global__ __launch_bounds__(256) void bias_act_kernel(bf16* __restrict__ Y, con
   *(bf16x8*)(Y + e * 8) = v;
 }
 
+// Sanitizer-tier self test: out[0] = 1 in release; in the debug build the
+// check fails on purpose (n >= 0), prints its NCNET_CHECK line and out[0] = 0.
+__global__ void debug_selftest_kernel(int* out, int n) {
+  if (threadIdx.x == 0) out[0] = NCNET_OK(n < 0) ? 1 : 0;
+}
+
 }  // namespace ncnet
 
 using namespace ncnet;
+
+extern "C" int ncnet_debug_selftest(int* out, hipStream_t stream) {
+  hipLaunchKernelGGL(debug_selftest_kernel, dim3(1), dim3(64), 0, stream, out, 1);
+  return (int)hipGetLastError();
+}
 
 extern "C" int ncnet_bias_act(void* Y, const float* b, long long rows, int C, int relu, hipStream_t stream) {
   if (C % 8) return -1;

@@ -31,6 +31,7 @@ __global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, vo
   const int j = (int)(blockIdx.x % J);
   const int i = (int)((blockIdx.x / J) % I);
   const long long e = plane * KL + kl;
+  if (!NCNET_OK(e < nvox)) return;
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     float vals[16];
@@ -40,7 +41,8 @@ __global__ __launch_bounds__(256) void ijpack_kernel(const T* __restrict__ X, vo
       float v = 0.f;
       if (q < NQ) {
         const int ii = i + sgn * (q / KS - P), jj = j + sgn * (q % KS - P);
-        if (ii >= 0 && ii < I && jj >= 0 && jj < J) v = (float)X[(plane + (long long)(ii - i) * J + (jj - j)) * KL + kl];
+        const long long src = (plane + (long long)(ii - i) * J + (jj - j)) * KL + kl;
+        if (ii >= 0 && ii < I && jj >= 0 && jj < J && NCNET_OK(src >= 0 && src < nvox)) v = (float)X[src];
       }
       vals[c] = v;
     }
@@ -86,8 +88,8 @@ __global__ __launch_bounds__(256) void ijsum_kernel(const float* __restrict__ Z,
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int ii = i + sgn * (q / KS - P), jj = j + sgn * (q % KS - P);
-    if (ii >= 0 && ii < I && jj >= 0 && jj < J)
-      s += Z[(long long)q * nvox + e + ((long long)(ii - i) * J + (jj - j)) * KL];
+    const long long src = e + ((long long)(ii - i) * J + (jj - j)) * KL;
+    if (ii >= 0 && ii < I && jj >= 0 && jj < J && NCNET_OK(src >= 0 && src < nvox)) s += Z[(long long)q * nvox + src];
   }
   y[e] = relu ? fmaxf(s, 0.f) : s;
 }

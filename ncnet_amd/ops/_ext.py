@@ -24,9 +24,11 @@ def load():
     if _C is not None or _ERR is not None:
         return _C
     try:
-        from ncnet_amd import _C as mod  # noqa: N813
+        import importlib
 
-        _C = mod
+        variant = os.environ.get("NCNET_EXT", "release")   # build variants: ncnet_amd/build.py
+        name = "ncnet_amd._C" if variant in ("", "release") else f"ncnet_amd._C_{variant}"
+        _C = importlib.import_module(name)
     except Exception as e:  # pragma: no cover - depends on the build state
         _ERR = e
     return _C

@@ -21,3 +21,21 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _ncnet_debug_kernel_checks(request):
+    """With NCNET_EXT=debug (the bounds-checked kernel build, ncnet_amd/build.py
+    --debug) a GPU test fails if any kernel printed an NCNET_CHECK line."""
+    if os.environ.get("NCNET_EXT") != "debug" or "gpu" not in request.keywords or not torch.cuda.is_available():
+        yield
+        return
+    capfd = request.getfixturevalue("capfd")
+    yield
+    torch.cuda.synchronize()
+    out, err = capfd.readouterr()
+    sys.stdout.write(out)
+    sys.stderr.write(err)
+    if "NCNET_CHECK failed" in out + err and "selftest" not in request.node.name:
+        pytest.fail("device bounds check failed:\n" + "\n".join(
+            ln for ln in (out + err).splitlines() if "NCNET_CHECK" in ln)[:4000])

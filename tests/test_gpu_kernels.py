@@ -4,6 +4,7 @@ Inputs are rounded to bf16 first and the oracle runs in fp64 on those values,
 so the remaining differences are fp32 accumulation order and the bf16 rounding
 of stored activations.
 """
+import os
 import pytest
 import torch
 
@@ -599,3 +600,18 @@ def test_resize_norm_u8_kernel():
                           for s in samples])
         assert out[k].shape == want.shape
         assert (out[k] - want).abs().max() < 2e-4
+
+
+def test_debug_build_selftest(capfd):
+    """Sanitizer tier: the debug build (NCNET_EXT=debug) reports a failed
+    device-side bounds check by printing it (and skipping the access); the
+    release build compiles the checks away."""
+    from ncnet_amd.ops._ext import ext
+    out = torch.zeros(1, dtype=torch.int32, device=DEV)
+    r = ext().debug_selftest(out)
+    torch.cuda.synchronize()
+    text = capfd.readouterr().out
+    if os.environ.get("NCNET_EXT") == "debug":
+        assert r == 0 and "NCNET_CHECK failed" in text
+    else:
+        assert r == 1 and "NCNET_CHECK" not in text

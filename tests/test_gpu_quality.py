@@ -95,17 +95,22 @@ def test_training_grads_vs_quantized_oracle(fe_finetune):
     for p in m.NeighConsensus.parameters():
         if p.dim() == 1:
             p.data.uniform_(0.0, 0.05)
-    if fe_finetune:
-        for p in m.FeatureExtraction.model[-1][-1].parameters():
-            p.requires_grad = True
     m.train()
-    params = [p for p in m.parameters() if p.requires_grad]
-    opt = make_adam(params, 5e-4)
+    opt = make_adam([p for p in m.parameters() if p.requires_grad], 5e-4)
+    # the operating point: three NC Adam steps with the trunk frozen.  (Training
+    # the trunk here too makes the point itself run-dependent -- MIOpen's
+    # backward-weight convolutions are not bitwise deterministic -- and with it
+    # how many MutualMatching argmax near-ties the bf16 path and the oracle
+    # resolve differently: measured 2.6e-3 .. 2.7e-2 NC gradient error over
+    # runs of one build, profiles/r2_sanitizers/README.md.)
     for s in range(3):
         b = synthetic_correspondence_batch(2, 240, DEV, seed=s)
         opt.zero_grad(set_to_none=True)
         weak_loss(m, {"source_image": b["source_image"], "target_image": b["target_image"]}).backward()
         opt.step()
+    if fe_finetune:
+        for p in m.FeatureExtraction.model[-1][-1].parameters():
+            p.requires_grad = True
     b = synthetic_correspondence_batch(2, 240, DEV, seed=7)
     imgs = torch.cat((b["source_image"], b["target_image"]))
     opt.zero_grad(set_to_none=True)
@@ -140,6 +145,7 @@ def test_training_grads_vs_quantized_oracle(fe_finetune):
         errs[f"nc{i}"] = rl2(gh, go)
     if fe_finetune:
         errs["d_raw_features"] = rl2(raw.grad, raw64.grad)
+    print("quantized-oracle errors:", {k: f"{v:.2e}" for k, v in errs.items()})
     assert errs["vols"] < 2e-3, errs
     assert max(v for k, v in errs.items() if k.startswith("nc")) < 1e-2, errs
     assert errs.get("d_raw_features", 0.0) < 2.5e-2, errs
