@@ -125,11 +125,17 @@ def main(argv=None):
             matches = np.zeros((1, args.n_panos, N, 5))
             src = prepare_image(read_image(os.path.join(args.query_path, queries[q])), args.image_size, args.k_size,
                                 ctx.device)
+            # the query's features are extracted once for its n_panos pairs (the
+            # reference re-runs its backbone per pair; identical features)
+            fq = model.extract(src) if vp is None else None
             for idx in range(min(args.n_panos, len(panos[q]))):
                 tgt = prepare_image(read_image(os.path.join(args.pano_path, panos[q][idx])), args.image_size,
                                     args.k_size, ctx.device)
-                pair = {"source_image": src, "target_image": tgt}
-                out = vp.forward(pair) if vp is not None else model(pair)
+                if vp is not None:
+                    out = vp.forward({"source_image": src, "target_image": tgt})
+                else:
+                    fp = model.extract(tgt)
+                    out = model.match_features(fq[0], fq[1], fp[0], fp[1])
                 corr4d, delta4d = out if args.k_size > 1 else (out, None)
                 m = pair_matches(corr4d, delta4d, args.k_size, args.softmax, args.matching_both_directions,
                                  args.flip_matching_direction).double().cpu().numpy()

@@ -284,6 +284,171 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
   }
 }
 
+// ===========================================================================
+// corr_gemm_v2 (bf16, large grids: the InLoc volumes): the correlation GEMM
+// fed by LDS-DMA through a 4-stage ring, as conv2d_nhwc_v2 (csrc/conv2d.hip):
+// 256 x 128 tile, 8 waves of 64 x 64, BK = 32 (64-byte LDS rows, swizzled
+// DMA source), one barrier per k-step with a compile-time vmcnt, global loads
+// three k-steps ahead of the MFMAs (v1: register double buffer, the k-step's
+// compute shorter than the load latency).  Rows past M / N read a 16-byte zero
+// block.  Tile order: GM consecutive row tiles per column sweep, so the ~32
+// workgroups an XCD runs at once share 4 A and 8 B tiles in its L2 instead of
+// 1 A and 32 B.  Epilogues as v1 (plain fp32 / bf16 store, fused 2x2x2x2
+// max-pool with packed argmax offsets).
+// ===========================================================================
+__device__ const uint4 g_corr_zero16 = {0u, 0u, 0u, 0u};
+
+namespace cg2 {
+constexpr int BM = 256, BN = 128, NW = 8, BK = 32, GM = 4;
+constexpr int APW = BM / (16 * NW), BPW = BN / (16 * NW), PER = APW + BPW;
+constexpr int STAGE = (BM + BN) * 64;
+__device__ __forceinline__ int swz(int r) { return (r & 1) ^ ((r >> 1) & 2); }
+__device__ __forceinline__ uint32_t roff(int row, int chunk) { return (uint32_t)(row * 64 + ((chunk ^ swz(row)) << 4)); }
+}  // namespace cg2
+
+template <int N>
+__device__ __forceinline__ void cg2_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <bool OUT_BF16, bool POOL, int NS>
+__global__ __launch_bounds__(512, NS <= 3 ? 2 : 1) void corr_gemm_v2_kernel(GemmArgs p) {
+  constexpr int BM = cg2::BM, BN = cg2::BN, BK = cg2::BK, GM = cg2::GM;
+  constexpr int APW = cg2::APW, BPW = cg2::BPW, PER = cg2::PER, STAGE = cg2::STAGE;
+  using cg2::swz;
+  using cg2::roff;
+  constexpr int TM = 4, TN = 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_b = p.tiles_m * p.tiles_n;
+  const int b = bid / per_b;
+  int t = bid - b * per_b;
+  const int grp = t / (GM * p.tiles_n), first = grp * GM;
+  const int gsz = min(GM, p.tiles_m - first);
+  t -= grp * GM * p.tiles_n;
+  const int tm = first + t % gsz, tn = t / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const bf16* A = (const bf16*)p.A + (size_t)(p.amap ? p.amap[b] : b) * p.sA;
+  const bf16* B = (const bf16*)p.B + (size_t)(p.bmap ? p.bmap[b] : b) * p.sB;
+  const bf16* zero = (const bf16*)&g_corr_zero16;
+  const int pos = lane & 3;
+
+  const bf16* a_ptr[APW];
+  bool a_ok[APW];
+#pragma unroll
+  for (int m = 0; m < APW; ++m) {
+    const int row = 16 * (wave * APW + m) + (lane >> 2);
+    a_ok[m] = m0 + row < p.M;
+    a_ptr[m] = A + (size_t)(a_ok[m] ? m0 + row : 0) * p.K + (pos ^ swz(row)) * 8;
+  }
+  const bf16* b_ptr[BPW];
+  bool b_ok[BPW];
+#pragma unroll
+  for (int m = 0; m < BPW; ++m) {
+    const int row = 16 * (wave * BPW + m) + (lane >> 2);
+    b_ok[m] = n0 + row < p.N;
+    b_ptr[m] = B + (size_t)(b_ok[m] ? n0 + row : 0) * p.K + (pos ^ swz(row)) * 8;
+  }
+  const int nk = p.K / BK;
+  auto issue = [&](int ks, int buf) {
+    char* sb = smem + buf * STAGE;
+    const int kk = ks * BK;
+#pragma unroll
+    for (int m = 0; m < APW; ++m)
+      __builtin_amdgcn_global_load_lds((const void*)(a_ok[m] ? a_ptr[m] + kk : zero),
+                                       LDS_PTR(void, sb + (wave * APW + m) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int m = 0; m < BPW; ++m)
+      __builtin_amdgcn_global_load_lds((const void*)(b_ok[m] ? b_ptr[m] + kk : zero),
+                                       LDS_PTR(void, sb + BM * 64 + (wave * BPW + m) * 1024), 16, 0, 0);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+  const int fr = lane & 15, fq = lane >> 4;
+  int buf = 0;
+  for (int ks = 0; ks < nk; ++ks) {
+    const int after = min(NS - 2, nk - 1 - ks);
+    if (after >= 2) cg2_wait_barrier<2 * PER>();
+    else if (after >= 1) cg2_wait_barrier<PER>();
+    else cg2_wait_barrier<0>();
+    if (ks + NS - 1 < nk) issue(ks + NS - 1, (buf + NS - 1) % NS);
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * 64;
+    bf16x8 af[TM], bfv[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = lds_read16(As, roff(wm * 64 + i * 16 + fr, fq));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfv[j] = lds_read16(Bs, roff(wn * 64 + j * 16 + fr, fq));
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfv[j], acc[i][j]);
+    buf = (buf + 1 == NS) ? 0 : buf + 1;
+  }
+
+  if (!POOL) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gm = m0 + wm * 64 + i * 16 + 4 * fq + r, gn = n0 + wn * 64 + j * 16 + fr;
+          if (gm < p.M && gn < p.N) {
+            const size_t o = (size_t)b * p.sC + (size_t)gm * p.N + gn;
+            if (OUT_BF16) ((bf16*)p.C)[o] = f2bf(acc[i][j][r]);
+            else ((float*)p.C)[o] = acc[i][j][r];
+          }
+        }
+  } else {
+    // rows / columns in 2x2-block order: a lane's 4 accumulator rows are one A
+    // block, the 4 columns of a B block sit in lanes fr&~3 .. fr|3 (as v1)
+    const int pa_w = p.wA >> 1, pb_w = p.wB >> 1;
+    const size_t vol = (size_t)(p.hA >> 1) * pa_w * (p.hB >> 1) * pb_w;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float best = acc[i][j][0];
+        int bidx = 0;
+#pragma unroll
+        for (int r = 1; r < 4; ++r)
+          if (acc[i][j][r] > best) { best = acc[i][j][r]; bidx = r * 4; }
+        bidx += (fr & 3);
+#pragma unroll
+        for (int o = 1; o < 4; o <<= 1) {
+          const float ob = __shfl_xor(best, o, 64);
+          const int oi = __shfl_xor(bidx, o, 64);
+          const bool take = (ob > best) || (ob == best && oi < bidx);
+          best = take ? ob : best;
+          bidx = take ? oi : bidx;
+        }
+        const int gm = m0 + wm * 64 + i * 16 + 4 * fq, gn = n0 + wn * 64 + j * 16 + (fr & ~3);
+        if ((fr & 3) == 0 && gm < p.M && gn < p.N) {
+          const int ba = gm >> 2, bb = gn >> 2;
+          const int ai = ba / pa_w, aj = ba - ai * pa_w, bi = bb / pb_w, bj = bb - bi * pb_w;
+          const int ra_ = bidx >> 2, rb_ = bidx & 3;
+          const uint8_t code = (uint8_t)(((ra_ >> 1) << 6) | ((ra_ & 1) << 4) | ((rb_ >> 1) << 2) | (rb_ & 1));
+          const size_t o = (size_t)b * vol + (((size_t)ai * pa_w + aj) * (p.hB >> 1) + bi) * pb_w + bj;
+          if (NCNET_OK(o < (size_t)(b + 1) * vol)) {
+            p.pool_val[o] = best;
+            p.pool_idx[o] = code;
+          }
+        }
+      }
+  }
+}
+
 }  // namespace ncnet
 
 using namespace ncnet;
@@ -311,6 +476,22 @@ extern "C" int ncnet_l2norm_rows_bwd(const float* x, const float* g, const float
   return (int)hipGetLastError();
 }
 
+// v2 (LDS-DMA ring, 256 x 128 tiles) for bf16 GEMMs whose grid still gives
+// >= 2 workgroups per CU (InLoc volumes); v1 for the small training GEMMs and
+// fp8.  NCNET_CORR_V2=0 / 1 forces v1 / v2 (where legal: K % 32 == 0).
+static bool use_v2(bool f8, int batch, int M, int N, int K) {
+  if (f8 || K % cg2::BK != 0) return false;
+  static const int force = [] { const char* e = getenv("NCNET_CORR_V2"); return e ? atoi(e) : -1; }();
+  if (force >= 0) return force == 1;
+  return (long long)batch * cdiv(M, cg2::BM) * cdiv(N, cg2::BN) >= 512;
+}
+
+// ring depth: 4 stages (96 KB, one workgroup per CU) or 3 (72 KB, two per CU); NCNET_CORR_NS
+static int cg2_stages() {
+  static const int ns = [] { const char* e = getenv("NCNET_CORR_NS"); return e && atoi(e) == 4 ? 4 : 3; }();
+  return ns;
+}
+
 // C[b] = A[amap[b]] . B[bmap[b]]^T ; out_bf16 selects the output dtype.
 // fp8_out_scale != 0: A, B are OCP fp8 e4m3 and C = fp8_out_scale * (A . B^T).
 extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int* amap, const int* bmap, int batch,
@@ -322,6 +503,18 @@ extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int*
   p.A = A; p.B = B; p.C = C; p.amap = amap; p.bmap = bmap;
   p.M = M; p.N = N; p.K = K; p.sA = sA; p.sB = sB; p.sC = sC;
   p.out_scale = fp8_out_scale;
+  if (use_v2(f8, batch, M, N, K)) {
+    p.tiles_m = cdiv(M, cg2::BM); p.tiles_n = cdiv(N, cg2::BN);
+    dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);
+    if (cg2_stages() == 3) {
+      if (out_bf16) hipLaunchKernelGGL((corr_gemm_v2_kernel<true, false, 3>), grid, block, 3 * cg2::STAGE, stream, p);
+      else hipLaunchKernelGGL((corr_gemm_v2_kernel<false, false, 3>), grid, block, 3 * cg2::STAGE, stream, p);
+    } else {
+      if (out_bf16) hipLaunchKernelGGL((corr_gemm_v2_kernel<true, false, 4>), grid, block, 4 * cg2::STAGE, stream, p);
+      else hipLaunchKernelGGL((corr_gemm_v2_kernel<false, false, 4>), grid, block, 4 * cg2::STAGE, stream, p);
+    }
+    return (int)hipGetLastError();
+  }
   p.tiles_m = cdiv(M, BM); p.tiles_n = cdiv(N, BN);
   dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(256);
   size_t lds = (size_t)(BM + BN) * 128;
@@ -346,9 +539,16 @@ extern "C" int ncnet_corr_gemm_pool2(const void* A, const void* B, float* pool_v
   p.A = A; p.B = B; p.C = nullptr;
   p.M = hA * wA; p.N = hB * wB; p.K = K; p.sA = sA; p.sB = sB;
   p.out_scale = fp8_out_scale;
-  p.tiles_m = cdiv(p.M, BM); p.tiles_n = cdiv(p.N, BN);
   p.pool_ks = 2; p.pool_val = pool_val; p.pool_idx = pool_idx;
   p.hA = hA; p.wA = wA; p.hB = hB; p.wB = wB;
+  if (use_v2(f8, batch, p.M, p.N, K)) {
+    p.tiles_m = cdiv(p.M, cg2::BM); p.tiles_n = cdiv(p.N, cg2::BN);
+    dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);
+    if (cg2_stages() == 3) hipLaunchKernelGGL((corr_gemm_v2_kernel<false, true, 3>), grid, block, 3 * cg2::STAGE, stream, p);
+    else hipLaunchKernelGGL((corr_gemm_v2_kernel<false, true, 4>), grid, block, 4 * cg2::STAGE, stream, p);
+    return (int)hipGetLastError();
+  }
+  p.tiles_m = cdiv(p.M, BM); p.tiles_n = cdiv(p.N, BN);
   dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(256);
   size_t lds = (size_t)(BM + BN) * 128;
   if (f8) hipLaunchKernelGGL((corr_gemm_kernel<false, true, true>), grid, block, lds, stream, p);

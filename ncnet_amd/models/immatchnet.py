@@ -288,6 +288,16 @@ class ImMatchNet(nn.Module):
         else:
             fa, (ha, wa) = self.extract(src)
             fb, (hb, wb) = self.extract(tgt)
+        return self.match_features(fa, (ha, wa), fb, (hb, wb))
+
+    def match_features(self, fa, hwa, fb, hwb):
+        """Everything after the backbone: correlation (+ k x k max-pool when
+        relocalizing), MutualMatching, NeighConsensus, MutualMatching.  ``fa`` /
+        ``fb`` come from ``extract`` -- eval_inloc.py extracts a query once and
+        matches it against its 10 panos (the reference re-runs the query
+        backbone per pano, eval_inloc.py:124-132; the features are identical)."""
+        (ha, wa), (hb, wb) = hwa, hwb
+        b = (fa[0] if isinstance(fa, tuple) else fa).shape[0]
         k = self.relocalization_k_size
         if isinstance(fa, tuple):
             corr4d = correlation_x3(fa, fb).view(b, 1, ha, wa, hb, wb)

@@ -37,8 +37,13 @@ from ncnet_amd.ops.correlation import correlation, correlation_pool2  # noqa: E4
 
 def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup: int = 2, k: int = 2,
                ncons_kernel_sizes=(3, 3), ncons_channels=(16, 1), src_hw=(3024, 4032), no_matches: bool = False,
-               impl: str = "hip", model=None) -> dict:
-    """One InLoc query/pano pair per forward on one GPU; returns the JSON record."""
+               impl: str = "hip", model=None, panos_per_query: int = 1) -> dict:
+    """One InLoc query/pano pair per forward on one GPU; returns the JSON record.
+
+    panos_per_query > 1: eval_inloc.py's schedule -- the query's features are
+    extracted once and reused for that many consecutive pairs (the reference
+    recomputes them per pair; the matches are identical), so ``pairs`` should
+    be a multiple of it.  1: both backbones per pair."""
     dev = torch.device("cuda")
     torch.manual_seed(0)
     if model is None:
@@ -72,14 +77,23 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
             stages["mm_nc_mm"] += ev[0].elapsed_time(ev[3])
             stages["matches"] += ev[3].elapsed_time(ev[4])
 
-    def one(timed: bool):
+    fq = None
+
+    def one(timed: bool, new_query: bool = True):
         if impl == "reference":
             return one_ref(timed)
-        nonlocal nmatch
+        nonlocal nmatch, fq
         with torch.inference_mode():
             ev[0].record()
-            f, (fh, fw) = model.extract(torch.cat((src, tgt), 0))
-            fa, fb = f[:1], f[1:]
+            if panos_per_query <= 1:
+                f, (fh, fw) = model.extract(torch.cat((src, tgt), 0))
+                fa, fb = f[:1], f[1:]
+            else:
+                # eval_inloc.py: the query's features are extracted once for its panos
+                if new_query or fq is None:
+                    fq = model.extract(src)
+                fa, (fh, fw) = fq
+                fb, _ = model.extract(tgt)
             ev[1].record()
             if k == 2:
                 corr4d, delta = correlation_pool2(fa, fb, fh, fw, fh, fw)
@@ -97,12 +111,12 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
             for i, kk in enumerate(stages):
                 stages[kk] += ev[i].elapsed_time(ev[i + 1])
 
-    for _ in range(warmup):
-        one(False)
+    for i in range(warmup):
+        one(False, True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(pairs):
-        one(True)
+    for i in range(pairs):
+        one(True, i % max(1, panos_per_query) == 0)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / pairs
     fs = (h // 16 // k, w // 16 // k)
@@ -114,7 +128,8 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
         "dtype": ("fp32-backbone/fp16-volume" if impl == "reference" else ("fp8-corr+fp8-nc" if fp8 else "bf16")),
         "data": "synthetic (random 4:3 images, random-init weights)",
         "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,
-                   "ncons": [list(ncons_kernel_sizes), list(ncons_channels)], "k": k},
+                   "ncons": [list(ncons_kernel_sizes), list(ncons_channels)], "k": k,
+                   "panos_per_query": panos_per_query},
         "stages_ms": {kk: round(v / pairs, 3) for kk, v in stages.items()},
         "matches": nmatch, "matches_contract": n_matches(image_size, k, True),
     }
@@ -130,6 +145,8 @@ def main():
     ap.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 1])
     ap.add_argument("--src-hw", type=int, nargs=2, default=[3024, 4032], help="raw query size (iPhone7)")
     ap.add_argument("--no-matches", action="store_true")
+    ap.add_argument("--panos-per-query", type=int, default=1,
+                    help="eval_inloc.py schedule: query features extracted once per this many pairs (10 in InLoc)")
     ap.add_argument("--fp8", action="store_true", help="OCP fp8 correlation operands (MX-fp8 MFMA) + fp8 NC")
     ap.add_argument("--impl", choices=["hip", "reference"], default="hip",
                     help="reference: the reference algorithm in plain PyTorch-ROCm (fp32 backbone, fp16 volume)")
@@ -138,7 +155,7 @@ def main():
     if a.volume_parallel:
         return bench_volume_parallel(a)
     print(json.dumps(run_single(a.image_size, a.fp8, a.pairs, a.warmup, a.k, a.ncons_kernel_sizes, a.ncons_channels,
-                                a.src_hw, a.no_matches, a.impl)))
+                                a.src_hw, a.no_matches, a.impl, panos_per_query=a.panos_per_query)))
 
 
 def bench_volume_parallel(a):

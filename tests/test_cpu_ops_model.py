@@ -87,6 +87,11 @@ def test_relocalization_forward_cpu():
         out, delta = m(batch)
     assert out.shape == (1, 1, 6, 8, 6, 8) and len(delta) == 4
     assert all(d.shape == out.shape and d.max() <= 1 and d.min() >= 0 for d in delta)
+    # eval_inloc.py's query-feature reuse: extract once, match per pano == forward of the pair
+    with torch.no_grad():
+        fq, fp = m.extract(batch["source_image"]), m.extract(batch["target_image"])
+        out2, delta2 = m.match_features(fq[0], fq[1], fp[0], fp[1])
+    assert torch.equal(out, out2) and all(torch.equal(a, b) for a, b in zip(delta, delta2))
 
 
 def test_state_dict_keys_match_reference_layout():

@@ -208,6 +208,28 @@ def test_maxpool4d_and_fused_pool():
     assert agree == 4
 
 
+def test_correlation_v2_large_grids():
+    """The LDS-DMA-ring correlation GEMM (corr_gemm_v2, chosen for >= 512
+    workgroups: InLoc volumes) with ragged M / N edges and batch maps: plain
+    store vs an fp64 GEMM, fused 2x2x2x2 max-pool vs pooling the full volume."""
+    from ncnet_amd.ops.correlation import correlation, correlation_pool2, maxpool4d
+    torch.manual_seed(10)
+    hA, wA, hB, wB = 66, 70, 58, 74
+    fa = torch.nn.functional.normalize(torch.randn(2, hA * wA, 1024, device=DEV), dim=-1).to(torch.bfloat16).float()
+    fb = torch.nn.functional.normalize(torch.randn(2, hB * wB, 1024, device=DEV), dim=-1).to(torch.bfloat16).float()
+    amap = torch.tensor([1, 0], device=DEV, dtype=torch.int32)
+    bmap = torch.tensor([0, 0], device=DEV, dtype=torch.int32)
+    c = correlation(fa, fb, amap, bmap)
+    cr = torch.bmm(fa.double()[amap.long()], fb.double()[bmap.long()].transpose(1, 2))
+    assert relerr(c, cr) < 1e-5
+    pv, po = correlation_pool2(fa, fb, hA, wA, hB, wB)
+    full = correlation(fa, fb).view(2, 1, hA, wA, hB, wB)
+    rv, ro = maxpool4d(full, 2)
+    assert relerr(pv, rv) < 1e-6
+    for a, b in zip(po, ro):
+        assert (a.long() == b.long()).float().mean() > 0.999
+
+
 @pytest.mark.parametrize("variant", [2, 3])
 @pytest.mark.parametrize("ks,shape", [(5, (2, 6, 5, 25, 25)), (5, (1, 5, 4, 30, 27)), (3, (1, 4, 5, 9, 33)),
                                       (5, (1, 2, 3, 7, 6)), (7, (1, 3, 4, 25, 25)), (1, (1, 3, 4, 25, 26))])
