@@ -48,7 +48,8 @@ def _baseline():
 def _inloc_secondary():
     """BASELINE configs 3-5 (InLoc dense matching, NC 3,3/16,1, k=2), measured
     after the headline window on rank 0 so the driver's run records them:
-    ms/pair at 1600 px and 3200 px (bf16) and 3200 px (fp8 correlation + NC)."""
+    ms/pair at 1600 px and 3200 px (bf16) and 3200 px (fp8 correlation; fused bf16 NC or, in
+    inloc_3200_fp8_nc_fp8, the fp8 Conv4d NC kernels)."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import bench_inloc
     from ncnet_amd.models import ImMatchNet
@@ -65,6 +66,14 @@ def _inloc_secondary():
             out[name] = {"ms_per_pair": r["value"], "stages_ms": r["stages_ms"], "panos_per_query": 10,
                          "ms_per_pair_both_backbones": r1["value"], "volume": r["config"]["volume"],
                          "dtype": r["dtype"]}
+        # the all-fp8 pipeline (fp8 Conv4d NC kernels instead of the fused bf16 stack)
+        os.environ["NCNET_NC_FP8"] = "1"
+        try:
+            r = bench_inloc.run_single(3200, True, pairs=10, warmup=2, model=model, panos_per_query=10)
+            out["inloc_3200_fp8_nc_fp8"] = {"ms_per_pair": r["value"], "stages_ms": r["stages_ms"],
+                                            "panos_per_query": 10, "dtype": r["dtype"]}
+        finally:
+            os.environ.pop("NCNET_NC_FP8", None)
         del model
     except Exception as e:  # the headline record must still print
         out["error"] = repr(e)

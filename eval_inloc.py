@@ -125,17 +125,25 @@ def main(argv=None):
             matches = np.zeros((1, args.n_panos, N, 5))
             src = prepare_image(read_image(os.path.join(args.query_path, queries[q])), args.image_size, args.k_size,
                                 ctx.device)
-            # the query's features are extracted once for its n_panos pairs (the
-            # reference re-runs its backbone per pair; identical features)
-            fq = model.extract(src) if vp is None else None
-            for idx in range(min(args.n_panos, len(panos[q]))):
-                tgt = prepare_image(read_image(os.path.join(args.pano_path, panos[q][idx])), args.image_size,
-                                    args.k_size, ctx.device)
-                if vp is not None:
-                    out = vp.forward({"source_image": src, "target_image": tgt})
+            npq = min(args.n_panos, len(panos[q]))
+            tgts = [prepare_image(read_image(os.path.join(args.pano_path, panos[q][idx])), args.image_size,
+                                  args.k_size, ctx.device) for idx in range(npq)]
+            if vp is None:
+                # the query's features are extracted once for its n_panos pairs and
+                # the panos' trunk runs as one batch when their sizes agree (the
+                # reference re-runs both backbones per pair; identical features)
+                fq = model.extract(src)
+                if npq > 1 and all(t.shape == tgts[0].shape for t in tgts):
+                    fpb, hwp = model.extract(torch.cat(tgts, 0))
+                    fps = [(tuple(t[i:i + 1] for t in fpb) if isinstance(fpb, tuple) else fpb[i:i + 1], hwp)
+                           for i in range(npq)]
                 else:
-                    fp = model.extract(tgt)
-                    out = model.match_features(fq[0], fq[1], fp[0], fp[1])
+                    fps = [model.extract(t) for t in tgts]
+            for idx in range(npq):
+                if vp is not None:
+                    out = vp.forward({"source_image": src, "target_image": tgts[idx]})
+                else:
+                    out = model.match_features(fq[0], fq[1], fps[idx][0], fps[idx][1])
                 corr4d, delta4d = out if args.k_size > 1 else (out, None)
                 m = pair_matches(corr4d, delta4d, args.k_size, args.softmax, args.matching_both_directions,
                                  args.flip_matching_direction).double().cpu().numpy()

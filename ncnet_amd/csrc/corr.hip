@@ -311,6 +311,65 @@ __device__ __forceinline__ void cg2_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// Epilogue of the v2 kernels for one wave's TM x TN 16 x 16 sub-tiles at
+// (row0, col0): plain fp32 / bf16 store, or the fused 2x2x2x2 max-pool.
+template <int TM, int TN, bool OUT_BF16, bool POOL>
+__device__ __forceinline__ void corr_v2_epilogue(const f32x4 (&acc)[TM][TN], const GemmArgs& p, int b, int row0,
+                                                 int col0, int lane) {
+  const int fr = lane & 15, fq = lane >> 4;
+  if (!POOL) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gm = row0 + i * 16 + 4 * fq + r, gn = col0 + j * 16 + fr;
+          if (gm < p.M && gn < p.N) {
+            const size_t o = (size_t)b * p.sC + (size_t)gm * p.N + gn;
+            if (OUT_BF16) ((bf16*)p.C)[o] = f2bf(acc[i][j][r]);
+            else ((float*)p.C)[o] = acc[i][j][r];
+          }
+        }
+  } else {
+    // rows / columns in 2x2-block order: a lane's 4 accumulator rows are one A
+    // block, the 4 columns of a B block sit in lanes fr&~3 .. fr|3 (as v1)
+    const int pa_w = p.wA >> 1, pb_w = p.wB >> 1;
+    const size_t vol = (size_t)(p.hA >> 1) * pa_w * (p.hB >> 1) * pb_w;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float best = acc[i][j][0];
+        int bidx = 0;
+#pragma unroll
+        for (int r = 1; r < 4; ++r)
+          if (acc[i][j][r] > best) { best = acc[i][j][r]; bidx = r * 4; }
+        bidx += (fr & 3);
+#pragma unroll
+        for (int o = 1; o < 4; o <<= 1) {
+          const float ob = __shfl_xor(best, o, 64);
+          const int oi = __shfl_xor(bidx, o, 64);
+          const bool take = (ob > best) || (ob == best && oi < bidx);
+          best = take ? ob : best;
+          bidx = take ? oi : bidx;
+        }
+        const int gm = row0 + i * 16 + 4 * fq, gn = col0 + j * 16 + (fr & ~3);
+        if ((fr & 3) == 0 && gm < p.M && gn < p.N) {
+          const int ba = gm >> 2, bb = gn >> 2;
+          const int ai = ba / pa_w, aj = ba - ai * pa_w, bi = bb / pb_w, bj = bb - bi * pb_w;
+          const int ra_ = bidx >> 2, rb_ = bidx & 3;
+          const uint8_t code = (uint8_t)(((ra_ >> 1) << 6) | ((ra_ & 1) << 4) | ((rb_ >> 1) << 2) | (rb_ & 1));
+          const size_t o = (size_t)b * vol + (((size_t)ai * pa_w + aj) * (p.hB >> 1) + bi) * pb_w + bj;
+          if (NCNET_OK(o < (size_t)(b + 1) * vol)) {
+            p.pool_val[o] = best;
+            p.pool_idx[o] = code;
+          }
+        }
+      }
+  }
+}
+
 template <bool OUT_BF16, bool POOL, int NS>
 __global__ __launch_bounds__(512, NS <= 3 ? 2 : 1) void corr_gemm_v2_kernel(GemmArgs p) {
   constexpr int BM = cg2::BM, BN = cg2::BN, BK = cg2::BK, GM = cg2::GM;
@@ -384,69 +443,141 @@ __global__ __launch_bounds__(512, NS <= 3 ? 2 : 1) void corr_gemm_v2_kernel(Gemm
     if (ks + NS - 1 < nk) issue(ks + NS - 1, (buf + NS - 1) % NS);
     const char* As = smem + buf * STAGE;
     const char* Bs = As + BM * 64;
-    bf16x8 af[TM], bfv[TN];
+    bf16x8 af[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) af[i] = lds_read16(As, roff(wm * 64 + i * 16 + fr, fq));
+    bf16x8 bcur = lds_read16(Bs, roff(wn * 64 + fr, fq));
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bfv[j] = lds_read16(Bs, roff(wn * 64 + j * 16 + fr, fq));
+    for (int j = 0; j < TN; ++j) {
+      bf16x8 bnext = bcur;
+      if (j + 1 < TN) bnext = lds_read16(Bs, roff(wn * 64 + (j + 1) * 16 + fr, fq));
+      __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of these MFMAs (counted lgkmcnt)
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfv[j], acc[i][j]);
+      for (int i = 0; i < TM; ++i) acc[i][j] = mfma16(af[i], bcur, acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      bcur = bnext;
+    }
     buf = (buf + 1 == NS) ? 0 : buf + 1;
   }
 
-  if (!POOL) {
+  corr_v2_epilogue<TM, TN, OUT_BF16, POOL>(acc, p, b, m0 + wm * 64, n0 + wn * 64, lane);
+}
+
+
+// ---------------------------------------------------------------------------
+// corr_gemm_f8v2: the MX-fp8 (OCP e4m3) correlation GEMM on the same LDS-DMA
+// ring: 256 x 128 tile, 8 waves of 64 x 64, one K = 128 stage (a 128-byte LDS
+// row) per v_mfma_scale_f32_16x16x128_f8f6f4 k-step, 3 stages (144 KB, one
+// workgroup per CU).  A lane's 32 operand bytes are two ds_read_b128 of
+// chunks 2fq, 2fq + 1; chunk c of row r sits at 16-byte slot c ^ h(r),
+// h(r) = bit1(r) | bit3(r) << 2 (searched offline: both reads conflict-free
+// for all four ds_read_b128 lane groups; rows r, r+1 alternate 128-byte
+// halves of the 256-byte bank period).  The DMA source is swizzled instead.
+// ---------------------------------------------------------------------------
+namespace cf2 {
+constexpr int BM = 256, BN = 128, NW = 8, NS = 3, GM = 4;
+constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW), PER = APW + BPW;   // 8 rows per DMA instruction
+constexpr int STAGE = (BM + BN) * 128;
+__device__ __forceinline__ int h(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ uint32_t roff(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ h(row)) << 4)); }
+}  // namespace cf2
+
+template <bool OUT_BF16, bool POOL>
+__global__ __launch_bounds__(512, 1) void corr_gemm_f8v2_kernel(GemmArgs p) {
+  constexpr int BM = cf2::BM, BN = cf2::BN, NS = cf2::NS, GM = cf2::GM;
+  constexpr int APW = cf2::APW, BPW = cf2::BPW, PER = cf2::PER, STAGE = cf2::STAGE;
+  constexpr int TM = 4, TN = 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_b = p.tiles_m * p.tiles_n;
+  const int b = bid / per_b;
+  int t = bid - b * per_b;
+  const int grp = t / (GM * p.tiles_n), first = grp * GM;
+  const int gsz = min(GM, p.tiles_m - first);
+  t -= grp * GM * p.tiles_n;
+  const int tm = first + t % gsz, tn = t / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const uint8_t* A = (const uint8_t*)p.A + (size_t)(p.amap ? p.amap[b] : b) * p.sA;
+  const uint8_t* B = (const uint8_t*)p.B + (size_t)(p.bmap ? p.bmap[b] : b) * p.sB;
+  const uint8_t* zero = (const uint8_t*)&g_corr_zero16;
+  const int pos = lane & 7;
+
+  const uint8_t* a_ptr[APW];
+  bool a_ok[APW];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gm = m0 + wm * 64 + i * 16 + 4 * fq + r, gn = n0 + wn * 64 + j * 16 + fr;
-          if (gm < p.M && gn < p.N) {
-            const size_t o = (size_t)b * p.sC + (size_t)gm * p.N + gn;
-            if (OUT_BF16) ((bf16*)p.C)[o] = f2bf(acc[i][j][r]);
-            else ((float*)p.C)[o] = acc[i][j][r];
-          }
-        }
-  } else {
-    // rows / columns in 2x2-block order: a lane's 4 accumulator rows are one A
-    // block, the 4 columns of a B block sit in lanes fr&~3 .. fr|3 (as v1)
-    const int pa_w = p.wA >> 1, pb_w = p.wB >> 1;
-    const size_t vol = (size_t)(p.hA >> 1) * pa_w * (p.hB >> 1) * pb_w;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float best = acc[i][j][0];
-        int bidx = 0;
-#pragma unroll
-        for (int r = 1; r < 4; ++r)
-          if (acc[i][j][r] > best) { best = acc[i][j][r]; bidx = r * 4; }
-        bidx += (fr & 3);
-#pragma unroll
-        for (int o = 1; o < 4; o <<= 1) {
-          const float ob = __shfl_xor(best, o, 64);
-          const int oi = __shfl_xor(bidx, o, 64);
-          const bool take = (ob > best) || (ob == best && oi < bidx);
-          best = take ? ob : best;
-          bidx = take ? oi : bidx;
-        }
-        const int gm = m0 + wm * 64 + i * 16 + 4 * fq, gn = n0 + wn * 64 + j * 16 + (fr & ~3);
-        if ((fr & 3) == 0 && gm < p.M && gn < p.N) {
-          const int ba = gm >> 2, bb = gn >> 2;
-          const int ai = ba / pa_w, aj = ba - ai * pa_w, bi = bb / pb_w, bj = bb - bi * pb_w;
-          const int ra_ = bidx >> 2, rb_ = bidx & 3;
-          const uint8_t code = (uint8_t)(((ra_ >> 1) << 6) | ((ra_ & 1) << 4) | ((rb_ >> 1) << 2) | (rb_ & 1));
-          const size_t o = (size_t)b * vol + (((size_t)ai * pa_w + aj) * (p.hB >> 1) + bi) * pb_w + bj;
-          if (NCNET_OK(o < (size_t)(b + 1) * vol)) {
-            p.pool_val[o] = best;
-            p.pool_idx[o] = code;
-          }
-        }
-      }
+  for (int m = 0; m < APW; ++m) {
+    const int row = 8 * (wave * APW + m) + (lane >> 3);
+    a_ok[m] = m0 + row < p.M;
+    a_ptr[m] = A + (size_t)(a_ok[m] ? m0 + row : 0) * p.K + (pos ^ cf2::h(row)) * 16;
   }
+  const uint8_t* b_ptr[BPW];
+  bool b_ok[BPW];
+#pragma unroll
+  for (int m = 0; m < BPW; ++m) {
+    const int row = 8 * (wave * BPW + m) + (lane >> 3);
+    b_ok[m] = n0 + row < p.N;
+    b_ptr[m] = B + (size_t)(b_ok[m] ? n0 + row : 0) * p.K + (pos ^ cf2::h(row)) * 16;
+  }
+  const int nk = p.K / 128;
+  auto issue = [&](int ks, int buf) {
+    char* sb = smem + buf * STAGE;
+    const int kk = ks * 128;
+#pragma unroll
+    for (int m = 0; m < APW; ++m)
+      __builtin_amdgcn_global_load_lds((const void*)(a_ok[m] ? a_ptr[m] + kk : zero),
+                                       LDS_PTR(void, sb + (wave * APW + m) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int m = 0; m < BPW; ++m)
+      __builtin_amdgcn_global_load_lds((const void*)(b_ok[m] ? b_ptr[m] + kk : zero),
+                                       LDS_PTR(void, sb + BM * 128 + (wave * BPW + m) * 1024), 16, 0, 0);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+  const int fr = lane & 15, fq = lane >> 4;
+  int buf = 0;
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk) cg2_wait_barrier<PER>();
+    else cg2_wait_barrier<0>();
+    if (ks + NS - 1 < nk) issue(ks + NS - 1, (buf + NS - 1) % NS);
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * 128;
+    auto frag = [&](const char* base, int r) {
+      const u32x4 lo = *(const u32x4*)(base + cf2::roff(r, 2 * fq)), hi = *(const u32x4*)(base + cf2::roff(r, 2 * fq + 1));
+      return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    };
+    // column fragments stream one ahead of their MFMAs, so the matrix cores
+    // start after the A fragments and the first B fragment have landed
+    i32x8 af[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = frag(As, wm * 64 + i * 16 + fr);
+    i32x8 bcur = frag(Bs, wn * 64 + fr);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      i32x8 bnext = bcur;
+      if (j + 1 < TN) bnext = frag(Bs, wn * 64 + (j + 1) * 16 + fr);
+      __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of these MFMAs (counted lgkmcnt)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[i][j] = mfma_fp8_k128(af[i], bcur, acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      bcur = bnext;
+    }
+    buf = (buf + 1 == NS) ? 0 : buf + 1;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] * p.out_scale;
+  corr_v2_epilogue<TM, TN, OUT_BF16, POOL>(acc, p, b, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
 }  // namespace ncnet
@@ -476,11 +607,12 @@ extern "C" int ncnet_l2norm_rows_bwd(const float* x, const float* g, const float
   return (int)hipGetLastError();
 }
 
-// v2 (LDS-DMA ring, 256 x 128 tiles) for bf16 GEMMs whose grid still gives
-// >= 2 workgroups per CU (InLoc volumes); v1 for the small training GEMMs and
-// fp8.  NCNET_CORR_V2=0 / 1 forces v1 / v2 (where legal: K % 32 == 0).
+// v2 (LDS-DMA ring, 256 x 128 tiles; bf16 and MX-fp8) for GEMMs whose grid
+// still gives >= 2 workgroups per CU (InLoc volumes); v1 for the small
+// training GEMMs.  NCNET_CORR_V2=0 / 1 forces v1 / v2 (where legal: K % 32 ==
+// 0 for bf16, K % 128 == 0 for fp8).
 static bool use_v2(bool f8, int batch, int M, int N, int K) {
-  if (f8 || K % cg2::BK != 0) return false;
+  if (K % (f8 ? 128 : cg2::BK) != 0) return false;
   static const int force = [] { const char* e = getenv("NCNET_CORR_V2"); return e ? atoi(e) : -1; }();
   if (force >= 0) return force == 1;
   return (long long)batch * cdiv(M, cg2::BM) * cdiv(N, cg2::BN) >= 512;
@@ -503,6 +635,14 @@ extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int*
   p.A = A; p.B = B; p.C = C; p.amap = amap; p.bmap = bmap;
   p.M = M; p.N = N; p.K = K; p.sA = sA; p.sB = sB; p.sC = sC;
   p.out_scale = fp8_out_scale;
+  if (f8 && use_v2(f8, batch, M, N, K)) {
+    p.tiles_m = cdiv(M, cf2::BM); p.tiles_n = cdiv(N, cf2::BN);
+    dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);
+    const size_t lds = cf2::NS * cf2::STAGE;
+    if (out_bf16) hipLaunchKernelGGL((corr_gemm_f8v2_kernel<true, false>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((corr_gemm_f8v2_kernel<false, false>), grid, block, lds, stream, p);
+    return (int)hipGetLastError();
+  }
   if (use_v2(f8, batch, M, N, K)) {
     p.tiles_m = cdiv(M, cg2::BM); p.tiles_n = cdiv(N, cg2::BN);
     dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);
@@ -541,6 +681,12 @@ extern "C" int ncnet_corr_gemm_pool2(const void* A, const void* B, float* pool_v
   p.out_scale = fp8_out_scale;
   p.pool_ks = 2; p.pool_val = pool_val; p.pool_idx = pool_idx;
   p.hA = hA; p.wA = wA; p.hB = hB; p.wB = wB;
+  if (f8 && use_v2(f8, batch, p.M, p.N, K)) {
+    p.tiles_m = cdiv(p.M, cf2::BM); p.tiles_n = cdiv(p.N, cf2::BN);
+    dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);
+    hipLaunchKernelGGL((corr_gemm_f8v2_kernel<false, true>), grid, block, cf2::NS * cf2::STAGE, stream, p);
+    return (int)hipGetLastError();
+  }
   if (use_v2(f8, batch, p.M, p.N, K)) {
     p.tiles_m = cdiv(p.M, cg2::BM); p.tiles_n = cdiv(p.N, cg2::BN);
     dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);

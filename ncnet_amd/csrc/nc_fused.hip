@@ -22,7 +22,8 @@
 //        weights of 2 taps x 16 combos, B = S at the tap shift), + b1, ReLU,
 //        zero outside the volume (layer 2's "same" padding), bf16 into LDS.
 //     C  layer 2: z_q(ih, j'') for the 9 plane combos q = (di2, dj2) over the
-//        tile (MFMA rows = combos, K = taps x 16 channels of h), accumulated
+//        tile (MFMA rows = combos, row 4 dj2 + di2, so a lane's 4 rows share
+//        dj2 and the output plane; K = taps x 16 channels of h), accumulated
 //        into an LDS ring of 3 output rows x R planes at
 //        (ih - di2 + 1, j'' - dj2 + 1).
 //   output row ih-1 is complete after hidden row ih: + b2, ReLU, store fp32.
@@ -75,7 +76,12 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   const int R = min(g.R, g.J - j0);
   const size_t KL = (size_t)g.K * g.L;
   const int KLi = g.K * g.L;
-  const uint16_t* xv = (const uint16_t*)(X + (size_t)v * g.I * g.J * KL);   // one volume < 2^31 elements
+  // this volume's x0 through a buffer resource: a lane whose S voxel lies
+  // outside the (k, l) volume reads with an out-of-range offset and gets 0,
+  // the plane offset is a scalar (one buffer_load_ushort per combo, no
+  // per-lane address arithmetic); one volume < 2^31 bytes (host-checked)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(X + (size_t)v * g.I * g.J * KL), (short)0, (int)((size_t)g.I * g.J * KL * 2), 0x00020000);
 
   // ---- static maps --------------------------------------------------------
   // the S voxel owned by this thread (phase A): (TK+4)(TL+4) <= 512
@@ -87,7 +93,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     const int kg = k0 - 2 + r, lg = l0 - 2 + c;
     s_lds = (e < SR * SW) ? (r * g.SRS + c) * 32 : -1;
     s_in = e < SR * SW && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
-    s_goff = s_in ? kg * g.L + lg : 0;
+    s_goff = s_in ? (kg * g.L + lg) * 2 : 0x7ffffff0;   // byte offset in the plane / out of range
   }
   // layer-1 tiles: h ext voxels e = tile*16 + (lane & 15) over HR x HW
   const int nt1 = (HR * HW + 15) >> 4;
@@ -129,6 +135,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   }
   for (int o = threadIdx.x; o < NQ * 64; o += 512) { wl[o] = W1p[o]; wl[NQ * 64 + o] = W2p[o]; }
   const int co0 = 4 * (lane >> 4);
+  const int dj2 = lane >> 4;                 // layer-2 combo column of this lane's MFMA rows
   float bias1[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) bias1[r] = b1[co0 + r];
@@ -150,8 +157,8 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
 #pragma unroll
     for (int c = 0; c < 9; ++c) {
       const int ii = ih + c / 3 - 1, jj = jh + c % 3 - 1;
-      const bool pin = ii >= 0 && ii < g.I && jj >= 0 && jj < g.J;
-      raw[c] = (pin && s_in) ? (uint32_t)xv[(ii * g.J + jj) * KLi + s_goff] : 0u;
+      const bool pin = ii >= 0 && ii < g.I && jj >= 0 && jj < g.J;   // wave-uniform
+      raw[c] = pin ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(xr, s_goff, (ii * g.J + jj) * KLi * 2, 0) : 0u;
     }
   };
   auto write_s = [&](const uint32_t (&raw)[9]) {
@@ -204,6 +211,8 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     }
     __syncthreads();                   // h complete
     // ---- C: layer 2 combos -> ring ----
+    const int p2 = jh - dj2 + 1 - j0;         // output plane of this lane's combos
+    const bool p_ok = dj2 < 3 && p2 >= 0 && p2 < R;
 #pragma unroll 2
     for (int u = 0; u < NCF_MAXT2; ++u) {
       if (wave + NCF_NW * u >= nt2) continue;
@@ -211,14 +220,14 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
         acc = mfma16u(wl[(NQ + q) * 64 + lane], *(const u32x4*)(H + b2off[u] + toff2[q]), acc);
-      if (vo[u] < 0) continue;
+      if (vo[u] < 0 || !p_ok) continue;
+      // MFMA row 4 * dj2 + di2 <-> combo (di2, dj2): this lane's rows r share
+      // one output plane p2 and differ in the output row ih - r + 1 (uniform)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = co0 + r;               // combo (di2, dj2)
-        if (c >= 9) continue;
-        const int io = ih - c / 3 + 1, p = jh - (c % 3) + 1 - j0;
-        if (io < i0 || io >= i1 || p < 0 || p >= R) continue;
-        ring[((io % 3) * g.R + p) * nvox + vo[u]] += acc[r];
+      for (int r = 0; r < 3; ++r) {
+        const int io = ih - r + 1;
+        if (io < i0 || io >= i1) continue;
+        ring[((io % 3) * g.R + p2) * nvox + vo[u]] += acc[r];
       }
     }
     // hidden row ih done: output row ih - 1 has all three contributions
@@ -257,7 +266,7 @@ extern "C" int ncnet_nc_fused_k3(const void* X, const void* W1p, const float* b1
   g.nkt = cdiv(K, TK); g.nlt = cdiv(L, TL); g.njb = cdiv(J, R); g.nib = cdiv(I, IR);
   g.SRS = TL + 10;   // S rows: a layer-1 tile wrapping from column TL+1 to 0 jumps 9 voxels (one 256-B bank period + 1)
   g.HRS = TL + 8;    // h rows: a layer-2 tile wrapping from column TL-1 to 0 jumps 9 voxels
-  if ((long long)I * J * K * L >= (1ll << 31)) return -4;
+  if ((long long)I * J * K * L * 2 >= (1ll << 31)) return -4;   // buffer-resource byte offsets
   size_t lds = (size_t)(TK + 4) * g.SRS * 32 + (size_t)(TK + 2) * g.HRS * 32 + (size_t)3 * R * TK * TL * 4 +
                2 * 5 * 64 * 16;
   if (lds > 160 * 1024) return -3;

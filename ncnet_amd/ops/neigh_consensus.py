@@ -856,7 +856,14 @@ def fused_tiles(V: int, I: int, J: int, K: int, L: int):
 def _fused_weights(weights, biases):
     w1, w2 = _std(weights[0]), _std(weights[1])
     W1p = pack_w16_planes(ij_in_weights(w1))[0].contiguous()
-    W2p = pack_w16_planes(ij_out_weights(w2))[0].contiguous()
+    # layer-2 MFMA rows: row 4 * dj + di <- ij combo di * 3 + dj (nc_fused.hip: a
+    # lane's four rows then share dj and one output plane); other rows zero
+    wo = ij_out_weights(w2)
+    wr = torch.zeros_like(wo)
+    for di in range(3):
+        for dj in range(3):
+            wr[:, 4 * dj + di] = wo[:, 3 * di + dj]
+    W2p = pack_w16_planes(wr)[0].contiguous()
     return W1p, _pad_bias(biases[0], 16), W2p, _pad_bias(biases[1], 1)
 
 
@@ -888,7 +895,7 @@ def neigh_consensus_fused(x: torch.Tensor, weights, biases, symmetric: bool = Tr
 
 def _fused_ok(kinds, kernel_sizes, channels, x) -> bool:
     return (FUSED and not torch.is_grad_enabled() and list(kinds) == ["1in", "1out"] and channels[0] <= 16
-            and list(kernel_sizes) == [3, 3] and x.shape[2] * x.shape[3] * x.shape[4] * x.shape[5] < 2 ** 31)
+            and list(kernel_sizes) == [3, 3] and x.shape[2] * x.shape[3] * x.shape[4] * x.shape[5] < 2 ** 30)
 
 
 def fp8_ok(kinds, channels) -> bool:
@@ -903,8 +910,8 @@ def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool 
     Returns [V, C_last, I, J, K, L] fp32.
 
     On the GPU: the (3,3)/(<=16,1) inference stack runs on the fused kernel
-    (hidden layer in LDS); ``fp8`` (inference, ``fp8_ok`` stacks) on the fp8
-    MFMA Conv4d kernels; ``precision='fp32'`` (inference) on the bf16x3
+    (hidden layer in LDS; also in fp8 mode unless NCNET_NC_FP8=1); ``fp8``
+    (inference, other ``fp8_ok`` stacks) on the fp8 MFMA Conv4d kernels; ``precision='fp32'`` (inference) on the bf16x3
     kernels (fp32-accurate); everything else with odd kernel sizes <= 7 and
     any channel counts on the bf16 autograd stack.  ``_ext.DISPATCH`` records
     which path ran."""
@@ -923,7 +930,11 @@ def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool 
                     return NeighConsensusX3Fn.apply(x.float().contiguous(), symmetric, tuple(kinds),
                                                     tuple(channels), *params)
                 return neigh_consensus_x3(x, weights, biases, channels, symmetric)
-            if _fused_ok(kinds, kernel_sizes, channels, x) and not fp8:
+            # fp8 mode: the fp8 Conv4d kernels, except where the fused bf16 stack
+            # applies -- measured faster at InLoc 3200 px (5.5 vs 7.3 ms per pair:
+            # the fused kernel never writes the hidden volume) -- unless
+            # NCNET_NC_FP8=1 asks for the all-fp8 pipeline
+            if _fused_ok(kinds, kernel_sizes, channels, x) and not (fp8 and _os.environ.get("NCNET_NC_FP8") == "1"):
                 _ext.count("nc_fused_k3")
                 return neigh_consensus_fused(x.float().contiguous(), weights, biases, symmetric)
             if fp8 and not torch.is_grad_enabled() and fp8_ok(kinds, channels):

@@ -41,9 +41,10 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
     """One InLoc query/pano pair per forward on one GPU; returns the JSON record.
 
     panos_per_query > 1: eval_inloc.py's schedule -- the query's features are
-    extracted once and reused for that many consecutive pairs (the reference
-    recomputes them per pair; the matches are identical), so ``pairs`` should
-    be a multiple of it.  1: both backbones per pair."""
+    extracted once and reused for that many consecutive pairs, and the panos'
+    trunk runs as one batch (the reference runs both backbones per pair; the
+    matches are identical), so ``pairs`` should be a multiple of it.  1: both
+    backbones per pair."""
     dev = torch.device("cuda")
     torch.manual_seed(0)
     if model is None:
@@ -78,6 +79,7 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
             stages["matches"] += ev[3].elapsed_time(ev[4])
 
     fq = None
+    fpano = {}
 
     def one(timed: bool, new_query: bool = True):
         if impl == "reference":
@@ -89,11 +91,15 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
                 f, (fh, fw) = model.extract(torch.cat((src, tgt), 0))
                 fa, fb = f[:1], f[1:]
             else:
-                # eval_inloc.py: the query's features are extracted once for its panos
+                # eval_inloc.py: the query's features are extracted once for its
+                # panos, and the panos' trunk runs as one batch
                 if new_query or fq is None:
                     fq = model.extract(src)
+                    fpano["f"] = model.extract(tgt.expand(panos_per_query, -1, -1, -1).contiguous())[0]
+                    fpano["i"] = 0
                 fa, (fh, fw) = fq
-                fb, _ = model.extract(tgt)
+                fb = fpano["f"][fpano["i"]:fpano["i"] + 1]
+                fpano["i"] += 1
             ev[1].record()
             if k == 2:
                 corr4d, delta = correlation_pool2(fa, fb, fh, fw, fh, fw)
@@ -125,7 +131,9 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
         "value": round(ms, 3), "unit": "ms/pair", "higher_is_better": False,
         "pairs_per_s": round(1e3 / ms, 3), "n_gpus": 1, "pairs": pairs, "warmup": warmup,
         "impl": impl,
-        "dtype": ("fp32-backbone/fp16-volume" if impl == "reference" else ("fp8-corr+fp8-nc" if fp8 else "bf16")),
+        "dtype": ("fp32-backbone/fp16-volume" if impl == "reference" else
+                  (("fp8-corr+fp8-nc" if os.environ.get("NCNET_NC_FP8") == "1" else "fp8-corr+bf16-fused-nc")
+                   if fp8 else "bf16")),
         "data": "synthetic (random 4:3 images, random-init weights)",
         "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,
                    "ncons": [list(ncons_kernel_sizes), list(ncons_channels)], "k": k,

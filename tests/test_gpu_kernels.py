@@ -228,6 +228,18 @@ def test_correlation_v2_large_grids():
     assert relerr(pv, rv) < 1e-6
     for a, b in zip(po, ro):
         assert (a.long() == b.long()).float().mean() > 0.999
+    # the MX-fp8 v2 kernel (corr_gemm_f8v2): same grids on e4m3 operands vs fp64 on the same values
+    from ncnet_amd.ops.correlation import FP8, FP8_FEAT_SCALE
+    qa, qb = (fa * FP8_FEAT_SCALE).to(FP8), (fb * FP8_FEAT_SCALE).to(FP8)
+    c8 = correlation(qa, qb, amap, bmap)
+    cr8 = torch.bmm(qa.double()[amap.long()], qb.double()[bmap.long()].transpose(1, 2)) / FP8_FEAT_SCALE ** 2
+    assert relerr(c8, cr8) < 1e-4   # fp32 accumulation order (near-zero random correlations)
+    pv8, po8 = correlation_pool2(qa, qb, hA, wA, hB, wB)
+    full8 = correlation(qa, qb).view(2, 1, hA, wA, hB, wB)
+    rv8, ro8 = maxpool4d(full8, 2)
+    assert relerr(pv8, rv8) < 1e-6
+    for a, b in zip(po8, ro8):
+        assert (a.long() == b.long()).float().mean() > 0.999
 
 
 @pytest.mark.parametrize("variant", [2, 3])
@@ -417,9 +429,12 @@ def test_conv16_fp8_kernel(ks, shape):
     assert relerr(z, zr) < 1e-4
 
 
-def test_immatchnet_fp8_nc_path():
-    """corr_dtype='fp8' (fp8 correlation + fp8 Conv4d NC kernels) vs the bf16
-    path; the dispatch counters prove which NC implementation ran."""
+def test_immatchnet_fp8_nc_path(monkeypatch):
+    """corr_dtype='fp8' (fp8 correlation + fp8 Conv4d NC kernels, forced with
+    NCNET_NC_FP8=1: by default this (3,3)/(16,1) stack takes the faster fused
+    bf16 NC kernel) vs the bf16 path; the dispatch counters prove which NC
+    implementation ran."""
+    monkeypatch.setenv("NCNET_NC_FP8", "1")
     from ncnet_amd.models import ImMatchNet
     torch.manual_seed(0)
     m = ImMatchNet(use_cuda=True, ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1],
@@ -438,6 +453,12 @@ def test_immatchnet_fp8_nc_path():
         assert _ext.DISPATCH["nc_fp8"] == n_fp8 + 1                # fp8: the fp8 MFMA Conv4d path
     assert c8.shape == c16.shape
     assert rel_l2(c8, c16) < 0.15
+    monkeypatch.delenv("NCNET_NC_FP8")
+    with torch.inference_mode():
+        n_fused = _ext.DISPATCH["nc_fused_k3"]
+        c8f, _ = m(batch)                                         # default fp8 mode: fp8 correlation + fused NC
+        assert _ext.DISPATCH["nc_fused_k3"] == n_fused + 1
+    assert rel_l2(c8f, c16) < 0.15
 
 
 def test_nc_forward_deterministic_and_fully_written():
@@ -637,3 +658,30 @@ def test_debug_build_selftest(capfd):
         assert r == 0 and "NCNET_CHECK failed" in text
     else:
         assert r == 1 and "NCNET_CHECK" not in text
+
+
+@pytest.mark.parametrize("cfg", [None, (3, 4, 6, 7), (2, 3, 16, 20), (5, 2, 9, 11)])
+def test_nc_fused_k3_vs_quantized_oracle(cfg):
+    """The fused InLoc NeighConsensus kernel (csrc/nc_fused.hip: 1 -> 16 -> 1,
+    k = 3, hidden layer in LDS) against the fp64 oracle with bf16 rounding of
+    x0, the weights and the hidden activation; cfg = (R, IR, TK, TL) forces
+    multi-workgroup splits along j, i and the (k, l) tile (None: the
+    production choice, fused_tiles)."""
+    import importlib
+    from ncnet_amd.engine import quantized_oracle as qo
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    torch.manual_seed(21)
+    V, I, J, K, L = 2, 9, 13, 11, 14
+    w1 = torch.randn(16, 1, 3, 3, 3, 3, device=DEV) * 0.2
+    w2 = torch.randn(1, 16, 3, 3, 3, 3, device=DEV) * 0.1
+    b1, b2 = torch.rand(16, device=DEV) * 0.1 - 0.03, torch.rand(1, device=DEV) * 0.1
+    ws = [ref.conv4d_weight_from_std(w1), ref.conv4d_weight_from_std(w2)]
+    x0 = torch.rand(V, I, J, K, L, device=DEV).to(torch.bfloat16)
+    wts = nc._fused_weights(ws, [b1, b2])
+    y = torch.full((V, I, J, K, L), float("nan"), device=DEV)
+    tk, tl, R, IR = nc.fused_tiles(V, I, J, K, L) if cfg is None else (cfg[2], cfg[3], cfg[0], cfg[1])
+    _ext.ext().nc_fused_k3(x0, *wts, y, R, IR, tk, tl)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    yr = qo.nc_stack(x0.double().unsqueeze(1), [w1.double(), w2.double()], [b1.double(), b2.double()])
+    assert relerr(y, yr.squeeze(1)) < 2e-3
