@@ -198,7 +198,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     advance(gih, gpj);
     __syncthreads();                   // S complete
     // ---- B: layer 1 -> h (bf16, zero outside the volume) ----
-#pragma unroll 2
+#pragma unroll
     for (int u = 0; u < NCF_MAXT1; ++u) {
       if (wave + NCF_NW * u >= nt1) continue;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     // ---- C: layer 2 combos -> ring ----
     const int p2 = jh - dj2 + 1 - j0;         // output plane of this lane's combos
     const bool p_ok = dj2 < 3 && p2 >= 0 && p2 < R;
-#pragma unroll 2
+#pragma unroll
     for (int u = 0; u < NCF_MAXT2; ++u) {
       if (wave + NCF_NW * u >= nt2) continue;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
