@@ -314,9 +314,14 @@ class FrozenResNetPlan(nn.Module):
         import os
         self.use_graphs = os.environ.get("NCNET_TRUNK_GRAPH", "1") != "0"
         # "native": NHWC implicit-GEMM HIP kernels with fused bias/residual/ReLU
-        # (csrc/conv2d.hip); "blas": hipBLASLt 1x1 GEMMs + MIOpen 3x3 + bias_act
-        self.conv_mode = os.environ.get("NCNET_TRUNK_CONV", "native")
+        # (csrc/conv2d.hip); "blas": hipBLASLt 1x1 GEMMs + MIOpen 3x3 + bias_act;
+        # "auto" (default): native, except each bottleneck's first 1x1 conv
+        # (bias + ReLU, no residual) goes to hipBLASLt's fused-epilogue GEMM
+        # where that measured faster for this input shape (timed once per shape
+        # in the eager warm-up before the graph capture)
+        self.conv_mode = os.environ.get("NCNET_TRUNK_CONV", "auto")
         self._graphs = {}
+        self._tuned = {}
 
     @staticmethod
     def _bias_act(y: torch.Tensor, b: torch.Tensor, relu: bool) -> torch.Tensor:
@@ -384,17 +389,53 @@ class FrozenResNetPlan(nn.Module):
         graph.replay()
         return static_out.clone(memory_format=torch.channels_last)
 
+    def _n1_blas(self, x: torch.Tensor, p) -> torch.Tensor:
+        n, _, h, w = x.shape
+        return self._nchw(torch._addmm_activation(p["b1"], self._rows(x), p["w1t"]), n, h, w)
+
+    def _n1(self, x: torch.Tensor, p, bi: int) -> torch.Tensor:
+        """First 1x1 conv of bottleneck ``bi`` (bias + ReLU): the native kernel or
+        hipBLASLt, whichever measured faster at this shape (tuned outside graph
+        capture; until tuned, and on any tie, native)."""
+        key = (tuple(x.shape), bi)
+        choice = self._tuned.get(key)
+        if choice is None:
+            if torch.cuda.is_current_stream_capturing():
+                choice = "native"
+            else:
+                def t(fn):
+                    fn()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(3):
+                        fn()
+                    e1.record()
+                    e1.synchronize()
+                    return e0.elapsed_time(e1)
+                tn = t(lambda: self._nconv(x, p["n1"], True))
+                tb = t(lambda: self._n1_blas(x, p))
+                choice = "blas" if tb < 0.95 * tn else "native"
+                self._tuned[key] = choice
+        return self._n1_blas(x, p) if choice == "blas" else self._nconv(x, p["n1"], True)
+
+    def tuned_choices(self) -> dict:
+        """{(input shape, bottleneck index): 'native' | 'blas'} picked so far."""
+        return dict(self._tuned)
+
     def _run(self, x: torch.Tensor) -> torch.Tensor:
         x = x.to(self.dtype).contiguous(memory_format=torch.channels_last)
+        bi = -1
         for kind, p in self.steps:
+            if kind == "bottleneck":
+                bi += 1
             if kind == "conv":
                 w, b, stride, pad, relu = p
                 x = self._bias_act(F.conv2d(x, w, None, stride, pad).contiguous(memory_format=torch.channels_last),
                                    b, relu)
             elif kind == "maxpool":
                 x = F.max_pool2d(x, *p).contiguous(memory_format=torch.channels_last)
-            elif self.conv_mode == "native" and x.is_cuda and self.dtype == torch.bfloat16:
-                y1 = self._nconv(x, p["n1"], True)
+            elif self.conv_mode in ("native", "auto") and x.is_cuda and self.dtype == torch.bfloat16:
+                y1 = self._n1(x, p, bi) if self.conv_mode == "auto" else self._nconv(x, p["n1"], True)
                 y2 = self._nconv(y1, p["n2"], True)
                 idt = x if p["nd"] is None else self._nconv(x, p["nd"], False)
                 x = self._nconv(y2, p["n3"], True, idt)

@@ -32,6 +32,7 @@ def timeit(fn, reps=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--res", type=int, default=3200)
+    ap.add_argument("--n", type=int, default=0, help="images (default: 2 at 3200 px, 32 at 400 px)")
     a = ap.parse_args()
     C = _ext.ext()
     dev = torch.device("cuda")
@@ -40,6 +41,7 @@ def main():
         n, hw = 2, {1: (600, 800), 2: (300, 400), 3: (150, 200)}
     else:
         n, hw = 32, {1: (100, 100), 2: (50, 50), 3: (25, 25)}
+    n = a.n or n
     # (name, layer, cin, cout, k, stride, input hw layer)
     shapes = [("l1.n1", 1, 256, 64, 1, 1, 1), ("l1.n2", 1, 64, 64, 3, 1, 1), ("l1.n3", 1, 64, 256, 1, 1, 1),
               ("l2.n1", 2, 512, 128, 1, 1, 2), ("l2.n2", 2, 128, 128, 3, 1, 2), ("l2.n3", 2, 128, 512, 1, 1, 2),
