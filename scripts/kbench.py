@@ -106,6 +106,7 @@ def main():
         "ij_1in_conv_tpw1": (with_env("NCNET_GP_TPW", "1", lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1)), fl1),
         "ij_out_dgrad": (lambda: C.conv16_fwd(xs, wij, None, x16, y16, ks, 2), fl1),
         "ij_out_fwd_total": (ij_out_fwd, fl1),
+        "ijsum": (lambda: C.ijsum(zq, b1, y1, ks, 1, 1), None),
         "wgrad16v2_plane": (lambda: C.wgrad16(xs[0], g16, pp, ppb, ks, 2, 2), fl1 / G),
     }
     only = set(a.only.split(",")) if a.only else None
