@@ -126,7 +126,7 @@ def main(argv=None):
     ap.add_argument("--ref-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--profile", type=str, default="", help="write a torch.profiler trace to this dir")
     ap.add_argument("--inloc", type=int, default=1,
-                    help="1: after the timed training steps, rank 0 also times the InLoc inference configs "
+                    help="1: after the timed training steps of a 1-GPU run, also time the InLoc inference configs "
                          "(BASELINE configs 3-5: 1600 px bf16, 3200 px bf16, 3200 px fp8) into config.secondary")
     args = ap.parse_args(argv)
 
@@ -219,13 +219,15 @@ def main(argv=None):
     if base:
         vs = pairs_per_s / base
     secondary = None
-    if args.inloc and ctx.is_main and dev.type == "cuda" and args.impl == "hip":
+    # the secondary records are single-GPU measurements: taken in the 1-GPU run
+    # only, so the multi-GPU scaling runs stay short and rank 0 never works on
+    # alone while its peers tear the process group down
+    if args.inloc and ctx.world_size == 1 and dev.type == "cuda" and args.impl == "hip":
         secondary = _inloc_secondary()
-        if ctx.world_size == 1:
-            try:
-                secondary["fe_finetune_1"] = _fe_finetune_secondary(args.batch, s)
-            except Exception as e:  # the headline record must still print
-                secondary["fe_finetune_1"] = {"error": repr(e)}
+        try:
+            secondary["fe_finetune_1"] = _fe_finetune_secondary(args.batch, s)
+        except Exception as e:  # the headline record must still print
+            secondary["fe_finetune_1"] = {"error": repr(e)}
     if ctx.is_main:
         rec = {
             "metric": "image-pairs/sec fwd+bwd, ResNet-101+NC-Net(5,5,5) 400x400 bf16",
