@@ -153,12 +153,17 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   // Loads land in a register set that is only read (packed into the S tile)
   // two planes later: the set of plane t+2 is issued right after plane t's
   // set was written out, so no plane waits for its own gather.
+  // plane byte offsets: one multiply per gather, the 9 combos differ by constants
+  const int pstride = KLi * 2, rstride = g.J * KLi * 2;
   auto gather = [&](int ih, int jh, uint32_t (&raw)[9]) {
+    const int base = (ih * g.J + jh) * pstride;
+    const bool iok[3] = {ih >= 1, true, ih + 1 < g.I}, jok[3] = {jh >= 1, true, jh + 1 < g.J};   // wave-uniform
 #pragma unroll
     for (int c = 0; c < 9; ++c) {
-      const int ii = ih + c / 3 - 1, jj = jh + c % 3 - 1;
-      const bool pin = ii >= 0 && ii < g.I && jj >= 0 && jj < g.J;   // wave-uniform
-      raw[c] = pin ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(xr, s_goff, (ii * g.J + jj) * KLi * 2, 0) : 0u;
+      const int di = c / 3, dj = c % 3;
+      raw[c] = (iok[di] && jok[dj])
+                   ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(xr, s_goff, base + (di - 1) * rstride + (dj - 1) * pstride, 0)
+                   : 0u;
     }
   };
   auto write_s = [&](const uint32_t (&raw)[9]) {
