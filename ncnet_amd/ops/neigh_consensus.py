@@ -880,14 +880,21 @@ def neigh_consensus_fused(x: torch.Tensor, weights, biases, symmetric: bool = Tr
     V, _, I, J, K, L = x.shape
     R, Cc = I * J, K * L
     wts = _fused_weights(weights, biases)
+    if symmetric and (I, J) == (K, L):
+        # both branches in one launch: the cast and the transpose write straight
+        # into the halves of one [2V, ...] input (no concatenation pass)
+        x2 = torch.empty((2 * V, I, J, K, L), dtype=torch.bfloat16, device=x.device)
+        x2[:V].copy_(x.reshape(V, I, J, K, L))
+        _ext.ext().transpose(x2[:V].reshape(V, R, Cc), x2[V:].reshape(V, Cc, R))
+        z = _run_fused(x2, wts)
+        y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x.device)
+        _ext.ext().combine_fwd(z, y, R, Cc)
+        return y.reshape(V, 1, I, J, K, L)
     xb = x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous()
     if not symmetric:
         return _run_fused(xb, wts).reshape(V, 1, I, J, K, L)
     xt = _swap_flat(xb.reshape(V, R, Cc), (I, J, K, L)).reshape(V, K, L, I, J)
-    if (I, J) == (K, L):
-        z = _run_fused(torch.cat((xb, xt), 0), wts)
-    else:
-        z = torch.cat((_run_fused(xb, wts).reshape(-1), _run_fused(xt, wts).reshape(-1)))
+    z = torch.cat((_run_fused(xb, wts).reshape(-1), _run_fused(xt, wts).reshape(-1)))
     y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x.device)
     _ext.ext().combine_fwd(z, y, R, Cc)
     return y.reshape(V, 1, I, J, K, L)

@@ -685,3 +685,22 @@ def test_nc_fused_k3_vs_quantized_oracle(cfg):
     assert torch.isfinite(y).all()
     yr = qo.nc_stack(x0.double().unsqueeze(1), [w1.double(), w2.double()], [b1.double(), b2.double()])
     assert relerr(y, yr.squeeze(1)) < 2e-3
+
+
+def test_neigh_consensus_fused_symmetric_wrapper():
+    """The symmetric InLoc NC (both branches through the fused kernel in one
+    launch: cast + transpose into one [2V, ...] input, then the combine)
+    against the quantized fp64 oracle of the whole symmetric stack."""
+    import importlib
+    from ncnet_amd.engine import quantized_oracle as qo
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    torch.manual_seed(22)
+    w1 = torch.randn(16, 1, 3, 3, 3, 3, device=DEV) * 0.2
+    w2 = torch.randn(1, 16, 3, 3, 3, 3, device=DEV) * 0.1
+    b1, b2 = torch.rand(16, device=DEV) * 0.1, torch.rand(1, device=DEV) * 0.1
+    x = torch.rand(2, 1, 7, 9, 7, 9, device=DEV).to(torch.bfloat16).float()
+    with torch.inference_mode():
+        y = nc.neigh_consensus_fused(x, [ref.conv4d_weight_from_std(w1), ref.conv4d_weight_from_std(w2)],
+                                     [b1, b2], symmetric=True)
+    yr = qo.neigh_consensus(x.double(), [w1.double(), w2.double()], [b1.double(), b2.double()], symmetric=True)
+    assert relerr(y, yr) < 2e-3
