@@ -410,13 +410,13 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
             dw, db = _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout)
         if li > 0 or need_dx0:
             if kind == "1out":                       # reuses ijpack(g, -1) of the weight gradient
-                gi_ = []
+                # each input block's gradient is written straight into its slot
+                # (no stacking copy of the [NB, V,I,J,K,L,16] result)
+                gn = torch.empty((nblocks(cin),) + tuple(hin.shape[1:]), dtype=torch.bfloat16, device=g.device)
                 for a in range(nblocks(cin)):
                     wp = pack_w16_planes(plane_dgrad_weights(ij_out_weights(w[:, 16 * a:16 * a + 16])))
-                    y = torch.empty(tuple(hin.shape[1:]), dtype=torch.bfloat16, device=g.device)
-                    C.conv16_fwd(gs, wp, None, hin[a], y, ks, 2)
-                    gi_.append(y)
-                g = torch.stack(gi_)
+                    C.conv16_fwd(gs, wp, None, hin[a], gn[a], ks, 2)
+                g = gn
             elif cin == 1:                           # gradient w.r.t. a 1-channel input (fp32)
                 gx = conv_layer(g, transpose_for_dgrad(w), cout, 1, relu=False)
                 if li == 0:

@@ -23,8 +23,15 @@ def transpose_for_dgrad(w_std: torch.Tensor) -> torch.Tensor:
     return w_std.transpose(0, 1).flip(2, 3, 4, 5)
 
 
+def _idx16(ks: int, device=None):
+    """Gather indices of the fragment order, cached per (ks, device): packing
+    runs every step, and re-uploading CPU index tensors cost four pageable
+    host-to-device copies per packed weight."""
+    return _idx16_dev(ks, str(torch.device(device)) if device is not None else "cpu")
+
+
 @functools.lru_cache(maxsize=None)
-def _idx16(ks: int):
+def _idx16_dev(ks: int, device: str):
     nt = ks * ks
     nq = (nt + 1) // 2
     q = torch.arange(nq).view(nq, 1, 1)
@@ -35,7 +42,7 @@ def _idx16(ks: int):
     ci = (8 * ((lane >> 4) & 1) + j).expand(nq, 64, 8)
     valid = (tap < nt).expand(nq, 64, 8)
     tap = torch.clamp(tap, max=nt - 1).expand(nq, 64, 8)
-    return co, ci, tap, valid
+    return tuple(t.contiguous().to(device) for t in (co, ci, tap, valid))
 
 
 def _as_std(w_std: torch.Tensor, cout: int, cin: int) -> torch.Tensor:
@@ -51,7 +58,7 @@ def _as_std(w_std: torch.Tensor, cout: int, cin: int) -> torch.Tensor:
 def pack_w16(w_std: torch.Tensor) -> torch.Tensor:
     ks = w_std.shape[-1]
     w = _as_std(w_std, 16, 16).reshape(16, 16, ks * ks, ks * ks)
-    co, ci, tap, valid = (t.to(w.device) for t in _idx16(ks))
+    co, ci, tap, valid = _idx16(ks, w.device)
     vals = w[co, ci, :, tap]                      # [nq, 64, 8, k*k]
     vals = vals * valid.unsqueeze(-1).to(vals.dtype)
     return vals.permute(3, 0, 1, 2).contiguous().to(torch.bfloat16)
@@ -72,7 +79,7 @@ def pack_w16_planes(wp: torch.Tensor) -> torch.Tensor:
     """[NPL, 16 co, 16 ci, k, k] -> [NPL, ceil(k*k/2), 64, 8] (pack_w16 per plane)."""
     npl, ks = wp.shape[0], wp.shape[-1]
     w = wp.reshape(npl, 16, 16, ks * ks)
-    co, ci, tap, valid = (t.to(w.device) for t in _idx16(ks))
+    co, ci, tap, valid = _idx16(ks, w.device)
     vals = w[:, co, ci, tap] * valid.to(w.dtype)      # [npl, nq, 64, 8]
     return vals.contiguous().to(torch.bfloat16)
 

@@ -39,6 +39,17 @@ def main():
             tr.train_step(pool[i % 2], pool[(i + 1) % 2])
         torch.cuda.synchronize()
     lines = []
+    # framework ops (not ncnet kernels) by input shapes: where the small copies come from
+    agg = {}
+    for e in prof.key_averages(group_by_input_shape=True):
+        if e.key.startswith("aten::") and e.device_time_total > 0 and e.key in (
+                "aten::cat", "aten::copy_", "aten::sum", "aten::add_", "aten::mul", "aten::clone", "aten::index",
+                "aten::to", "aten::_to_copy", "aten::contiguous", "aten::zero_", "aten::fill_", "aten::stack",
+                "aten::add", "aten::where", "aten::sub", "aten::div", "aten::mean", "aten::flip", "aten::zeros"):
+            agg[(e.key, str(e.input_shapes)[:150])] = (e.device_time_total / a.steps, e.count / a.steps)
+    lines.append("per-step device time (us) / calls of framework ops by input shape:")
+    for (k, shp), (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:40]:
+        lines.append(f"{t:9.1f} us {c:5.1f}x  {k:18s} {shp}")
     t = prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=a.top)
     lines.append(t)
     t2 = prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=a.top)
