@@ -197,7 +197,10 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   };
   auto step = [&](uint32_t (&raw)[9]) {
     const int jh = jh_lo + pj;
-    __syncthreads();                   // S and h of the previous plane fully consumed (and ring zeroed)
+    // no barrier here: every wave already passed the previous step's "h
+    // complete" barrier, i.e. all layer-1 reads of S are done, and h is next
+    // written only after the "S complete" barrier below, i.e. after all
+    // layer-2 reads of the previous plane (ring entries are wave-private)
     write_s(raw);
     if (gih < ih_hi) gather(gih, jh_lo + gpj, raw);
     advance(gih, gpj);
@@ -240,6 +243,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     advance(ih, pj);
   };
 
+  __syncthreads();                     // weights in LDS and the zeroed ring visible to every wave
   uint32_t rawA[9], rawB[9];
   gather(gih, jh_lo + gpj, rawA);
   advance(gih, gpj);
