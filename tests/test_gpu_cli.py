@@ -1,0 +1,65 @@
+"""The command lines end to end on the MI355X (the CPU suite runs the same
+flows on the torch oracles): train.py on synthetic pairs with checkpoint and
+resume, eval_pf_pascal.py, eval_inloc.py (bf16 and fp8, the query-once /
+batched-pano schedule) with the .mat contract, and the keypoint-transfer demo.
+Every NC-Net op must dispatch to a HIP kernel: no torch fallback."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from ncnet_amd.ops import _ext
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def workdir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("gpucli")
+    old = os.getcwd()
+    os.chdir(d)
+    yield d
+    os.chdir(old)
+
+
+def test_train_resume_eval_gpu(workdir):
+    import eval_pf_pascal
+    import train
+    before = _ext.DISPATCH["torch_fallback"]
+    train.main(["--synthetic", "8", "--batch_size", "4", "--image_size", "128", "--num_epochs", "1",
+                "--result-model-dir", "models"])
+    cks = sorted(glob.glob("models/2*_checkpoint_adam.pth.tar"))
+    assert cks
+    train.main(["--synthetic", "8", "--batch_size", "4", "--image_size", "128", "--num_epochs", "2",
+                "--resume", cks[0]])
+    from ncnet_amd.engine.checkpoint import load_checkpoint
+    assert load_checkpoint(cks[0])["epoch"] == 2
+    stats = eval_pf_pascal.main(["--synthetic", "4", "--image_size", "128", "--checkpoint", cks[0]])
+    assert stats["point_tnf"]["pck"].shape[0] == 4
+    assert _ext.DISPATCH["torch_fallback"] == before
+    assert _ext.DISPATCH["nc_bf16"] > 0
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_inloc_export_gpu(workdir, fp8):
+    import eval_inloc
+    from scipy.io import loadmat
+    before = _ext.DISPATCH["nc_fused_k3"]
+    args = ["--synthetic_queries", "1", "--n_panos", "3", "--image_size", "640", "--k_size", "2",
+            "--output_dir", "m8" if fp8 else "m16"]
+    out = eval_inloc.main(args + (["--fp8"] if fp8 else []))
+    assert _ext.DISPATCH["nc_fused_k3"] == before + 3           # one fused NC per pair
+    m = loadmat(os.path.join(out, "1.mat"))["matches"]
+    assert m.shape[:2] == (1, 3) and m.dtype == np.float64
+    used = m[0, 0, :, 4] > 0
+    assert used.sum() > 0
+    xy = m[0, 0, used, :4]
+    assert (xy > 0).all() and (xy < 1).all()
+
+
+def test_point_transfer_demo_gpu(workdir):
+    import point_transfer_demo
+    out = os.path.join(workdir, "demo_gpu.png")
+    acc = point_transfer_demo.main(["--synthetic", "--image_size", "240", "--out", out])
+    assert os.path.exists(out) and 0.0 <= acc <= 1.0
