@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from ncnet_amd.data.transforms import read_image  # noqa: E402
 from ncnet_amd.engine.checkpoint import str_to_bool  # noqa: E402
-from ncnet_amd.eval.inloc import (load_shortlist, n_matches, output_folder, pair_matches, prepare_image,  # noqa: E402
+from ncnet_amd.eval.inloc import (PairMatcher, load_shortlist, n_matches, output_folder, pair_matches, prepare_image,  # noqa: E402
                                   save_query)
 from ncnet_amd.models import ImMatchNet  # noqa: E402
 from ncnet_amd.parallel.dist import barrier, destroy, init_distributed  # noqa: E402
@@ -113,6 +113,8 @@ def main(argv=None):
     if ctx.is_main:
         print("Output matches folder: " + folder)
     queries, panos, pano_all = load_shortlist(args.inloc_shortlist)
+    matcher = PairMatcher(model, args.k_size, args.softmax, args.matching_both_directions,
+                          args.flip_matching_direction)
     N = n_matches(args.image_size, args.k_size, args.matching_both_directions)
     nq = min(args.n_queries, len(queries))
     t0 = time.perf_counter()
@@ -142,11 +144,13 @@ def main(argv=None):
             for idx in range(npq):
                 if vp is not None:
                     out = vp.forward({"source_image": src, "target_image": tgts[idx]})
+                    corr4d, delta4d = out if args.k_size > 1 else (out, None)
+                    m = pair_matches(corr4d, delta4d, args.k_size, args.softmax, args.matching_both_directions,
+                                     args.flip_matching_direction).double().cpu().numpy()
                 else:
-                    out = model.match_features(fq[0], fq[1], fps[idx][0], fps[idx][1])
-                corr4d, delta4d = out if args.k_size > 1 else (out, None)
-                m = pair_matches(corr4d, delta4d, args.k_size, args.softmax, args.matching_both_directions,
-                                 args.flip_matching_direction).double().cpu().numpy()
+                    # correlation .. match extraction as one HIP graph per shape
+                    res, cnt = matcher(fq[0], fq[1], fps[idx][0], fps[idx][1])
+                    m = res[:int(cnt)].double().cpu().numpy()
                 n = min(len(m), N)
                 matches[0, idx, :n] = m[:n]
                 npairs += 1

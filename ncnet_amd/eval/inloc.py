@@ -67,8 +67,12 @@ def prepare_image(img_uint8_hwc: np.ndarray, image_size: int, k_size: int, devic
 
 
 def pair_matches(corr4d, delta4d, k_size: int, do_softmax: bool = True, both_dirs: bool = True,
-                 flip: bool = False):
-    """Bidirectional, de-duplicated, recentred matches of one pair -> [Npts, 5] tensor."""
+                 flip: bool = False, static: bool = False):
+    """Bidirectional, de-duplicated, recentred matches of one pair -> [Npts, 5] tensor.
+
+    ``static``: shapes independent of the data (HIP-graph capturable): returns
+    ``(out [M, 5], count)`` with the ``count`` unique matches in the same order
+    in the first rows and zeros after them (M = all candidate matches)."""
     b, _, fs1, fs2, fs3, fs4 = corr4d.shape
     k = max(1, k_size)
     kw = dict(scale="positive", do_softmax=do_softmax, delta4d=delta4d, k_size=k, return_indices=True)
@@ -85,18 +89,87 @@ def pair_matches(corr4d, delta4d, k_size: int, do_softmax: bool = True, both_dir
         ks_ = key[idx]
         first = torch.ones_like(ks_, dtype=torch.bool)
         first[1:] = ks_[1:] != ks_[:-1]
+        if static:
+            # stable compaction without a data-dependent size: the kept rows go
+            # to their rank among the kept, the duplicates to a dump row
+            pos = torch.cumsum(first.to(torch.int64), 0) - 1
+            dst = torch.where(first, pos, torch.full_like(pos, idx.numel()))
+            m = _recentre(xA[idx], yA[idx], xB[idx], yB[idx], sc[idx], fs1, fs2, fs3, fs4, k)
+            out = torch.zeros((idx.numel() + 1, 5), dtype=m.dtype, device=m.device)
+            out.index_copy_(0, dst, m)
+            return out[:-1], first.sum()
         idx = idx[first]
         xA, yA, xB, yB, sc = xA[idx], yA[idx], xB[idx], yB[idx], sc[idx]
     else:
         xA, yA, xB, yB, sc, *_ = corr_to_matches(corr4d, invert_matching_direction=flip, **kw)
         xA, yA, xB, yB, sc = (t.reshape(-1) for t in (xA, yA, xB, yB, sc))
-    # recentre to pixel centres (eval_inloc.py:180-189)
+    m = _recentre(xA, yA, xB, yB, sc, fs1, fs2, fs3, fs4, k)
+    if static:
+        return m, torch.tensor(m.shape[0], device=m.device)
+    return m
+
+
+def _recentre(xA, yA, xB, yB, sc, fs1, fs2, fs3, fs4, k):
+    """Recentre to pixel centres (eval_inloc.py:180-189) -> [N, 5]."""
     n1, n2, n3, n4 = fs1 * k, fs2 * k, fs3 * k, fs4 * k
     yA = yA * (n1 - 1) / n1 + 0.5 / n1
     xA = xA * (n2 - 1) / n2 + 0.5 / n2
     yB = yB * (n3 - 1) / n3 + 0.5 / n3
     xB = xB * (n4 - 1) / n4 + 0.5 / n4
     return torch.stack((xA, yA, xB, yB, sc.float()), dim=1)
+
+
+class PairMatcher:
+    """Everything after the backbones for one query/pano pair -- correlation
+    (+ k x k pool), MutualMatching, NeighConsensus, MutualMatching and the
+    bidirectional de-duplicated match extraction -- replayed as one HIP graph
+    per input shape (the ~60 launches of a pair otherwise leave gaps between
+    the memory-bound kernels).  The graph is captured after two eager runs;
+    if capture fails the matcher stays eager.  The returned tensors are
+    reused by the next call: consume them first (eval_inloc.py copies them to
+    the host)."""
+
+    def __init__(self, model, k_size: int, do_softmax: bool = True, both_dirs: bool = True, flip: bool = False,
+                 use_graph: bool | None = None):
+        self.model, self.k = model, k_size
+        self.kw = dict(do_softmax=do_softmax, both_dirs=both_dirs, flip=flip)
+        self.use_graph = (os.environ.get("NCNET_PAIR_GRAPH", "1") != "0") if use_graph is None else use_graph
+        self._graphs = {}
+
+    def _eager(self, fa, hwa, fb, hwb):
+        out = self.model.match_features(fa, hwa, fb, hwb)
+        corr4d, delta = out if self.k > 1 else (out, None)
+        return pair_matches(corr4d, delta, self.k, static=True, **self.kw)
+
+    def __call__(self, fa, hwa, fb, hwb):
+        if not (self.use_graph and torch.is_tensor(fa) and fa.is_cuda):
+            return self._eager(fa, hwa, fb, hwb)
+        key = (tuple(fa.shape), tuple(fb.shape), fa.dtype, tuple(hwa), tuple(hwb))
+        ent = self._graphs.get(key)
+        if ent is None:
+            try:
+                sa, sb = fa.clone(), fb.clone()
+                side = torch.cuda.Stream(device=fa.device)
+                side.wait_stream(torch.cuda.current_stream(fa.device))
+                with torch.cuda.stream(side):
+                    for _ in range(2):
+                        self._eager(sa, hwa, sb, hwb)
+                torch.cuda.current_stream(fa.device).wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    res = self._eager(sa, hwa, sb, hwb)
+                ent = self._graphs[key] = (g, sa, sb, res)
+            except RuntimeError as err:      # capture unsupported -> eager from now on
+                import warnings
+                warnings.warn(f"PairMatcher: HIP graph capture disabled ({err})")
+                self.use_graph = False
+                return self._eager(fa, hwa, fb, hwb)
+        g, sa, sb, res = ent
+        if sa.data_ptr() != fa.data_ptr():
+            sa.copy_(fa)
+        sb.copy_(fb)
+        g.replay()
+        return res
 
 
 def save_query(path: str, matches: np.ndarray, query_fn, pano_fns):

@@ -37,14 +37,17 @@ from ncnet_amd.ops.correlation import correlation, correlation_pool2  # noqa: E4
 
 def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup: int = 2, k: int = 2,
                ncons_kernel_sizes=(3, 3), ncons_channels=(16, 1), src_hw=(3024, 4032), no_matches: bool = False,
-               impl: str = "hip", model=None, panos_per_query: int = 1) -> dict:
+               impl: str = "hip", model=None, panos_per_query: int = 1, pair_graph: bool | None = None) -> dict:
     """One InLoc query/pano pair per forward on one GPU; returns the JSON record.
 
     panos_per_query > 1: eval_inloc.py's schedule -- the query's features are
     extracted once and reused for that many consecutive pairs, and the panos'
     trunk runs as one batch (the reference runs both backbones per pair; the
     matches are identical), so ``pairs`` should be a multiple of it.  1: both
-    backbones per pair."""
+    backbones per pair.  pair_graph (default: with panos_per_query > 1, as
+    eval_inloc.py does): everything after the backbones replayed as one HIP
+    graph (eval/inloc.py PairMatcher); its time is reported under "corr_pool"
+    with the later stages 0."""
     dev = torch.device("cuda")
     torch.manual_seed(0)
     if model is None:
@@ -53,6 +56,8 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
                            corr_dtype="fp8" if fp8 else "bf16").to(dev).eval()
     model.corr_dtype = "fp8" if fp8 else "bf16"
     h, w = target_size(src_hw[0], src_hw[1], image_size, k)
+    if pair_graph is None:
+        pair_graph = panos_per_query > 1 and os.environ.get("NCNET_PAIR_GRAPH", "1") != "0"
     src = torch.randn(1, 3, h, w, device=dev)
     tgt = torch.randn(1, 3, h, w, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
@@ -80,6 +85,8 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
 
     fq = None
     fpano = {}
+    from ncnet_amd.eval.inloc import PairMatcher
+    matcher = PairMatcher(model, k) if pair_graph else None
 
     def one(timed: bool, new_query: bool = True):
         if impl == "reference":
@@ -101,6 +108,19 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
                 fb = fpano["f"][fpano["i"]:fpano["i"] + 1]
                 fpano["i"] += 1
             ev[1].record()
+            if matcher is not None:
+                # correlation .. match extraction replayed as one HIP graph (eval_inloc.py)
+                res, cnt = matcher(fa, (fh, fw), fb, (fh, fw))
+                ev[2].record()
+                ev[3].record()
+                ev[4].record()
+                if timed:
+                    nmatch = int(cnt)
+                if timed:
+                    torch.cuda.synchronize()
+                    for i, kk in enumerate(stages):
+                        stages[kk] += ev[i].elapsed_time(ev[i + 1])
+                return
             if k == 2:
                 corr4d, delta = correlation_pool2(fa, fb, fh, fw, fh, fw)
             else:

@@ -49,7 +49,7 @@ def test_inloc_export_gpu(workdir, fp8):
     args = ["--synthetic_queries", "1", "--n_panos", "3", "--image_size", "640", "--k_size", "2",
             "--output_dir", "m8" if fp8 else "m16"]
     out = eval_inloc.main(args + (["--fp8"] if fp8 else []))
-    assert _ext.DISPATCH["nc_fused_k3"] == before + 3           # one fused NC per pair
+    assert _ext.DISPATCH["nc_fused_k3"] > before                # (replays of the pair graph are not counted)
     m = loadmat(os.path.join(out, "1.mat"))["matches"]
     assert m.shape[:2] == (1, 3) and m.dtype == np.float64
     used = m[0, 0, :, 4] > 0
@@ -63,3 +63,27 @@ def test_point_transfer_demo_gpu(workdir):
     out = os.path.join(workdir, "demo_gpu.png")
     acc = point_transfer_demo.main(["--synthetic", "--image_size", "240", "--out", out])
     assert os.path.exists(out) and 0.0 <= acc <= 1.0
+
+
+def test_pair_matcher_graph_equals_eager():
+    """eval/inloc.py PairMatcher: the HIP-graph replay of correlation .. match
+    extraction returns exactly the eager matches, for a fixed query and
+    changing panos (static inputs re-filled per replay)."""
+    import torch
+    from ncnet_amd.eval.inloc import PairMatcher, pair_matches
+    from ncnet_amd.models import ImMatchNet
+    torch.manual_seed(3)
+    m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], relocalization_k_size=2).cuda().eval()
+    src = torch.randn(1, 3, 320, 416, device="cuda")
+    panos = [torch.randn(1, 3, 320, 416, device="cuda") for _ in range(3)]
+    pm = PairMatcher(m, 2)
+    with torch.inference_mode():
+        fq = m.extract(src)
+        for t in panos:
+            fp = m.extract(t)
+            res, cnt = pm(fq[0], fq[1], fp[0], fp[1])
+            got = res[:int(cnt)].clone()
+            corr, delta = m.match_features(fq[0], fq[1], fp[0], fp[1])
+            want = pair_matches(corr, delta, 2)
+            assert torch.equal(got, want)
+    assert pm._graphs, "the pair graph was not captured"
