@@ -134,12 +134,19 @@ def main(argv=None):
                 # the query's features are extracted once for its n_panos pairs and
                 # the panos' trunk runs as one batch when their sizes agree (the
                 # reference re-runs both backbones per pair; identical features)
-                fq = model.extract(src)
-                if npq > 1 and all(t.shape == tgts[0].shape for t in tgts):
+                if all(t.shape == src.shape for t in tgts):
+                    # query and panos in one trunk batch (InLoc resizes both to the same size)
+                    fb_, hwp = model.extract(torch.cat([src] + tgts, 0))
+                    sl = lambda i: tuple(t[i:i + 1] for t in fb_) if isinstance(fb_, tuple) else fb_[i:i + 1]  # noqa: E731
+                    fq = (sl(0), hwp)
+                    fps = [(sl(i + 1), hwp) for i in range(npq)]
+                elif npq > 1 and all(t.shape == tgts[0].shape for t in tgts):
+                    fq = model.extract(src)
                     fpb, hwp = model.extract(torch.cat(tgts, 0))
                     fps = [(tuple(t[i:i + 1] for t in fpb) if isinstance(fpb, tuple) else fpb[i:i + 1], hwp)
                            for i in range(npq)]
                 else:
+                    fq = model.extract(src)
                     fps = [model.extract(t) for t in tgts]
             for idx in range(npq):
                 if vp is not None:

@@ -101,8 +101,10 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
                 # eval_inloc.py: the query's features are extracted once for its
                 # panos, and the panos' trunk runs as one batch
                 if new_query or fq is None:
-                    fq = model.extract(src)
-                    fpano["f"] = model.extract(tgt.expand(panos_per_query, -1, -1, -1).contiguous())[0]
+                    # the query and its panos in one trunk batch (eval_inloc.py)
+                    fall, hw_ = model.extract(torch.cat((src, tgt.expand(panos_per_query, -1, -1, -1)), 0))
+                    fq = (fall[:1], hw_)
+                    fpano["f"] = fall[1:]
                     fpano["i"] = 0
                 fa, (fh, fw) = fq
                 fb = fpano["f"][fpano["i"]:fpano["i"] + 1]
