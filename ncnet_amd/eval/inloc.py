@@ -137,7 +137,7 @@ class PairMatcher:
         self._graphs = {}
 
     def _eager(self, fa, hwa, fb, hwb):
-        out = self.model.match_features(fa, hwa, fb, hwb)
+        out = self.model.match_features(fa, hwa, fb, hwb, packed_offsets=True)
         corr4d, delta = out if self.k > 1 else (out, None)
         return pair_matches(corr4d, delta, self.k, static=True, **self.kw)
 

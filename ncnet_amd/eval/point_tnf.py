@@ -70,12 +70,18 @@ def corr_to_matches(corr4d, delta4d=None, k_size=1, do_softmax=False, scale="cen
         iB, jB = ib // fs4, ib % fs4
         iA, jA = idx // fs2, idx % fs2
     if delta4d is not None:
-        di, dj, dk, dl = (d.reshape(b, fs1, fs2, fs3, fs4) for d in delta4d)
         bi = torch.arange(b, device=dev).view(b, 1).expand_as(iA)
-        ddi = di[bi, iA, jA, iB, jB]
-        ddj = dj[bi, iA, jA, iB, jB]
-        ddk = dk[bi, iA, jA, iB, jB]
-        ddl = dl[bi, iA, jA, iB, jB]
+        if torch.is_tensor(delta4d):
+            # packed 2-bit offsets (ops/correlation.py decode_offsets layout), decoded
+            # only at the matched cells instead of over the whole volume
+            code = delta4d.reshape(b, fs1, fs2, fs3, fs4)[bi, iA, jA, iB, jB].long()
+            ddi, ddj, ddk, ddl = (code >> 6) & 3, (code >> 4) & 3, (code >> 2) & 3, code & 3
+        else:
+            di, dj, dk, dl = (d.reshape(b, fs1, fs2, fs3, fs4) for d in delta4d)
+            ddi = di[bi, iA, jA, iB, jB]
+            ddj = dj[bi, iA, jA, iB, jB]
+            ddk = dk[bi, iA, jA, iB, jB]
+            ddl = dl[bi, iA, jA, iB, jB]
         iA, jA = iA * k_size + ddi, jA * k_size + ddj
         iB, jB = iB * k_size + ddk, jB * k_size + ddl
     xA, yA = xa[jA], ya[iA]

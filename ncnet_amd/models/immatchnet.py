@@ -290,12 +290,15 @@ class ImMatchNet(nn.Module):
             fb, (hb, wb) = self.extract(tgt)
         return self.match_features(fa, (ha, wa), fb, (hb, wb))
 
-    def match_features(self, fa, hwa, fb, hwb):
+    def match_features(self, fa, hwa, fb, hwb, packed_offsets: bool = False):
         """Everything after the backbone: correlation (+ k x k max-pool when
         relocalizing), MutualMatching, NeighConsensus, MutualMatching.  ``fa`` /
         ``fb`` come from ``extract`` -- eval_inloc.py extracts a query once and
         matches it against its 10 panos (the reference re-runs the query
-        backbone per pano, eval_inloc.py:124-132; the features are identical)."""
+        backbone per pano, eval_inloc.py:124-132; the features are identical).
+        ``packed_offsets``: the k=2 max-pool offsets as one uint8 volume of 2-bit
+        codes (decoded at the matched cells by eval/point_tnf.py) instead of
+        four decoded volumes."""
         (ha, wa), (hb, wb) = hwa, hwb
         b = (fa[0] if isinstance(fa, tuple) else fa).shape[0]
         k = self.relocalization_k_size
@@ -305,7 +308,7 @@ class ImMatchNet(nn.Module):
                 corr4d, delta = _maxpool4d(corr4d, k)
         elif k > 1:
             if k == 2 and ha % 2 == 0 and wa % 2 == 0 and hb % 2 == 0 and wb % 2 == 0:
-                corr4d, delta = correlation_pool2(fa, fb, ha, wa, hb, wb)
+                corr4d, delta = correlation_pool2(fa, fb, ha, wa, hb, wb, packed=packed_offsets)
             else:
                 corr4d = correlation(fa, fb).view(b, 1, ha, wa, hb, wb)
                 corr4d, delta = _maxpool4d(corr4d, k)

@@ -201,10 +201,12 @@ def block_order_index(h: int, w: int, k: int, device) -> torch.Tensor:
     return perm  # new row r takes old row perm[r]
 
 
-def correlation_pool2(fa: torch.Tensor, fb: torch.Tensor, hA: int, wA: int, hB: int, wB: int):
+def correlation_pool2(fa: torch.Tensor, fb: torch.Tensor, hA: int, wA: int, hB: int, wB: int,
+                      packed: bool = False):
     """Fused correlation + maxpool4d(k=2). fa [V, hA*wA, C], fb [V, hB*wB, C]
     (natural row order).  Returns (pooled [V,1,hA/2,wA/2,hB/2,wB/2] fp32,
-    (di, dj, dk, dl) int64 offsets of the same shape)."""
+    (di, dj, dk, dl) uint8 offsets of the same shape) -- or, ``packed``, the
+    single uint8 volume of 2-bit codes (``decode_offsets``)."""
     V = fa.shape[0]
     fp8 = fa.dtype == FP8
     scale = 1.0 / (FP8_FEAT_SCALE * FP8_FEAT_SCALE) if fp8 else 1.0
@@ -222,6 +224,8 @@ def correlation_pool2(fa: torch.Tensor, fb: torch.Tensor, hA: int, wA: int, hB: 
     val = torch.empty(shape, dtype=torch.float32, device=fa.device)
     code = torch.empty(shape, dtype=torch.uint8, device=fa.device)
     _ext.ext().corr_gemm_pool2(a, b, val, code, hA, wA, hB, wB, scale)
+    if packed:
+        return val.unsqueeze(1), code.unsqueeze(1)
     return val.unsqueeze(1), decode_offsets(code.unsqueeze(1))
 
 
