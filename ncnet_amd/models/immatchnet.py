@@ -14,6 +14,7 @@ Compute policy (MI355X):
 """
 from __future__ import annotations
 
+import importlib
 import os
 from collections import OrderedDict
 
@@ -25,8 +26,13 @@ from ..ops import reference as ref
 from ..ops.conv4d import Conv4d
 from ..ops.correlation import (correlation, correlation_pool2, correlation_x3, l2norm_pack, l2norm_pack_fp8,
                                l2norm_pack_split, maxpool4d as _maxpool4d)
-from ..ops.mutual import mutual_matching
+from ..ops import _ext as _ext_mod
+from ..ops.mutual import mutual_matching, mutual_matching_nc_input as _mm_nc_input
 from ..ops.neigh_consensus import neigh_consensus
+
+# the module (the package re-exports the function under the same name)
+_nc_ops = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+_ext_count = _ext_mod.count
 from ..utils.timing import segment
 from .backbones import FrozenResNetPlan, build_trunk, fold_frozen_bn
 
@@ -266,10 +272,27 @@ class ImMatchNet(nn.Module):
 
     def process_correlation(self, corr4d: torch.Tensor) -> torch.Tensor:
         """MutualMatching -> NeighConsensus -> MutualMatching (lib/model.py:274-276)."""
-        with segment("mutual_matching"):
-            corr4d = MutualMatching(corr4d)
         self.NeighConsensus.fp8 = self.corr_dtype == "fp8"
         self.NeighConsensus.precision = "fp32" if "fp32" in (self.corr_dtype, self.nc_precision) else "bf16"
+        nc = self.NeighConsensus
+        if (not torch.is_grad_enabled() and nc.symmetric_mode and corr4d.is_cuda
+                and tuple(corr4d.shape[2:4]) == tuple(corr4d.shape[4:6])
+                and _nc_ops.fused_applies(corr4d, [m.weight_ref() for m in nc.conv_layers()], nc.channels,
+                                          nc.fp8, nc.precision)):
+            # inference on the fused NC stack: MutualMatching writes the bf16
+            # input of both symmetric branches directly
+            layers = nc.conv_layers()
+            with segment("mutual_matching"):
+                x2 = _mm_nc_input(corr4d)
+            _ext_count("nc_fused_k3")
+            with segment("neigh_consensus"):
+                corr4d = _nc_ops.neigh_consensus_fused_x2(
+                    x2, [m.weight_ref() for m in layers],
+                    [m.bias if m.bias is not None else torch.zeros(m.out_channels, device=x2.device) for m in layers])
+            with segment("mutual_matching"):
+                return MutualMatching(corr4d)
+        with segment("mutual_matching"):
+            corr4d = MutualMatching(corr4d)
         with segment("neigh_consensus"):
             corr4d = self.NeighConsensus(corr4d)
         with segment("mutual_matching"):

@@ -875,6 +875,25 @@ def _run_fused(xb: torch.Tensor, wts) -> torch.Tensor:
     return y
 
 
+def neigh_consensus_fused_x2(x2: torch.Tensor, weights, biases) -> torch.Tensor:
+    """Symmetric fused NC on a prepared [2V, I, J, K, L] bf16 input (x, then its
+    A<->B swap: ops/mutual.py mutual_matching_nc_input) -> [V, 1, I, J, K, L] fp32."""
+    V2, I, J, K, L = x2.shape
+    V = V2 // 2
+    z = _run_fused(x2, _fused_weights(weights, biases))
+    y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x2.device)
+    _ext.ext().combine_fwd(z, y, I * J, K * L)
+    return y.reshape(V, 1, I, J, K, L)
+
+
+def fused_applies(x: torch.Tensor, weights, channels, fp8: bool = False, precision: str = "bf16") -> bool:
+    """Would ``neigh_consensus`` run this input on the fused kernel?"""
+    kernel_sizes = [w.shape[0] for w in weights]
+    kinds = layer_kinds(channels, kernel_sizes)
+    return (x.is_cuda and _ext.use_hip(x) and kinds is not None and precision != "fp32"
+            and _fused_ok(kinds, kernel_sizes, channels, x) and not (fp8 and _os.environ.get("NCNET_NC_FP8") == "1"))
+
+
 def neigh_consensus_fused(x: torch.Tensor, weights, biases, symmetric: bool = True) -> torch.Tensor:
     """Inference NeighConsensus of a (3, 3) / (<=16, 1) stack on the fused kernel."""
     V, _, I, J, K, L = x.shape
