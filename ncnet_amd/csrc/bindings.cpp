@@ -10,6 +10,7 @@
 
 extern "C" {
 int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv16_blk_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad16v3(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_ijpack(const void*, int, void*, int, int, int, int, int, int, int, int, hipStream_t);
@@ -98,6 +99,22 @@ void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<T
   ok(ncnet_conv16_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), vs[0],
                       vs[1], vs[2], vs[3], vs[4], ks, epi, (int)npg, (int)nco, cur_stream(X)),
      "conv16_fwd");
+}
+
+// Cout = 1 layer (<= 16 input channels) in output-plane-block mode:
+// Y [V,I,J,K,L] fp32 = act(bias + conv); Wp [(ks+3)^2, nq, 64, 8] (packing.blk_out_weights).
+void conv16_blk_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t relu) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(Wp, "Wp", at::kBFloat16); check(Y, "Y", at::kFloat);
+  check_ks(ks);
+  TORCH_CHECK(X.dim() == 6 && X.size(-1) == 16, "X must be [V,I,J,K,L,16]");
+  std::vector<int64_t> vs(X.sizes().begin(), X.sizes().end() - 1);
+  check_shape(Y, "Y", vs);
+  check_shape(Wp, "Wp", {(ks + 3) * (ks + 3), conv_pairs16(ks), 64, 8});
+  if (bias.has_value()) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == 1, "bias must have 1 element"); }
+  ok(ncnet_conv16_blk_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), Y.data_ptr<float>(), vs[0], vs[1], vs[2],
+                          vs[3], vs[4], ks, (int)relu, cur_stream(X)),
+     "conv16_blk_fwd");
 }
 
 // Weight gradient partials.  mode 0: all KS*KS plane offsets (di, dj); mode 2:
@@ -509,6 +526,7 @@ void resize_norm_u8(Tensor src, Tensor meta, Tensor out, std::vector<double> mea
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for ncnet_amd";
   m.def("conv16_fwd", &conv16_fwd);
+  m.def("conv16_blk_fwd", &conv16_blk_fwd);
   m.def("wgrad16", &wgrad16);
   m.def("ijpack", &ijpack);
   m.def("conv16f8_fwd", &conv16f8_fwd);

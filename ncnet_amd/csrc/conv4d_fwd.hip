@@ -26,7 +26,10 @@ namespace ncnet {
 // EPI_F32X16: raw fp32 accumulators of the first nco channels, channel-planar
 // [nco][V,I,J,K,L] (ij-encoded Cout=1 partials summed by ijsum, or the per
 // input-block partials of a layer wider than 16 channels).
-enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32X16 = 4 };
+// EPI_BLK1: Cout = 1 layer in output-plane-block mode (conv16v2 only, below):
+// the 16 MFMA rows are a 4 x 4 block of output (i, j) planes; fp32 single-channel
+// output with bias (+ ReLU).
+enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32X16 = 4, EPI_BLK1 = 8 };
 
 struct ConvGeom {
   int V, I, J, K, L;  // volume dims
@@ -41,6 +44,8 @@ struct ConvGeom {
   int njb;            // output j-blocks per (v, i): J, or cdiv(J, R) (v3) / cdiv(J, tpw) (v2 group planes)
   int tpw;            // v2 group-plane mode: consecutive output j-tiles per workgroup (1 otherwise)
   int nt;             // v2 / v3 epilogues: non-temporal output stores (NCNET_NT_STORE)
+  int nib;            // EPI_BLK1: 4-plane output blocks along i (njb: along j)
+  int relu;           // EPI_BLK1: ReLU after the bias
 };
 
 // Decode the workgroup's output tile.
@@ -135,9 +140,25 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
   char* wbuf = smem + 2 * plane_bytes;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const TileId t = decode_tile(g);
-  const int di_lo = max(0, P - t.i), di_hi = min(KS, g.I + P - t.i);
-  const int dj_lo = max(0, P - t.j), dj_hi = min(KS, g.J + P - t.j);
+  constexpr bool BLK = EPI == EPI_BLK1;
+  constexpr int SP = KS + 3;   // EPI_BLK1: input planes per block side (4 + KS - 1)
+  TileId t;
+  if (BLK) {
+    uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int lt = bid % g.nlt; bid /= g.nlt;
+    const int kt = bid % g.nkt; bid /= g.nkt;
+    t.j = (bid % g.njb) * 4; bid /= g.njb;
+    t.i = (bid % g.nib) * 4; t.v = bid / g.nib;
+    t.k0 = kt * g.TK; t.l0 = lt * g.TL;
+  } else {
+    t = decode_tile(g);
+  }
+  // plane-offset ranges; EPI_BLK1: absolute input plane ranges of the block
+  // (i0 - P .. i0 + 3 + P clipped to the volume), every one feeding <= 16 rows
+  const int di_lo = BLK ? max(0, t.i - P) : max(0, P - t.i);
+  const int di_hi = BLK ? min(g.I, t.i + 4 + P) : min(KS, g.I + P - t.i);
+  const int dj_lo = BLK ? max(0, t.j - P) : max(0, P - t.j);
+  const int dj_hi = BLK ? min(g.J, t.j + 4 + P) : min(KS, g.J + P - t.j);
   const int ndj = dj_hi - dj_lo;
   const int nplanes = g.npg > 0 ? g.npg : (di_hi - di_lo) * ndj;
   const int nvox = g.TK * g.TL;
@@ -175,7 +196,9 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
   // plane s of output j-tile t.j + jt (jt > 0 only in multi-tile group-plane mode)
   auto issue_x = [&](int jt, int s, char* buf) {
     const bf16* xp;
-    if (g.npg > 0) {
+    if (BLK) {
+      xp = X + plane_offset(g, t.v, di_lo + s / ndj, dj_lo + s % ndj, 16);
+    } else if (g.npg > 0) {
       xp = X + s * g.gstride + plane_offset(g, t.v, t.i, t.j + jt, 16);
     } else {
       const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
@@ -192,15 +215,45 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
     }
   };
   auto issue_w = [&](int s) {
-    const int wplane = g.npg > 0 ? s : (di_lo + s / ndj) * KS + dj_lo + s % ndj;
+    const int wplane = BLK ? (di_lo + s / ndj - (t.i - P)) * SP + dj_lo + s % ndj - (t.j - P)
+                           : g.npg > 0 ? s : (di_lo + s / ndj) * KS + dj_lo + s % ndj;
     const u32x4* wp = Wp + (size_t)wplane * (NQ * 64);
-    if (NCNET_OK(wplane >= 0 && wplane < (g.npg > 0 ? g.npg : NT)))
+    if (NCNET_OK(wplane >= 0 && wplane < (BLK ? SP * SP : g.npg > 0 ? g.npg : NT)))
       for (int q = wave; q < NQ; q += NW)
         __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + q * 1024), 16, 0, 0);
   };
 
   const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
   auto store_tile = [&](int jt) {
+    if constexpr (BLK) {
+      // row co = 4 (lane >> 4) + r is output plane (i0 + (lane >> 4), j0 + r)
+      const int oi = t.i + (lane >> 4);
+      const float b0 = bias ? bias[0] : 0.f;
+#pragma unroll
+      for (int tt = 0; tt < MAXT; ++tt) {
+        int tile = wave + NW * tt;
+        if (tile < ntile) {
+          int vi = tile * 16 + (lane & 15);
+          int kk = vi / g.TL, ll = vi - kk * g.TL;
+          int kg = t.k0 + kk, lg = t.l0 + ll;
+          if (vi < nvox && kg < g.K && lg < g.L && oi < g.I) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (t.j + r < g.J) {
+                float x = acc[tt][r] + b0;
+                if (g.relu) x = fmaxf(x, 0.f);
+                const size_t o = plane_offset(g, t.v, oi, t.j + r, 1) + (size_t)kg * g.L + lg;
+                if (NCNET_OK(o < nvox_all)) {
+                  if (g.nt) __builtin_nontemporal_store(x, (float*)Y + o);
+                  else ((float*)Y)[o] = x;
+                }
+              }
+            }
+          }
+        }
+      }
+      return;
+    }
     const size_t vbase_out = plane_offset(g, t.v, t.i, t.j + jt, 1);
 #pragma unroll
     for (int tt = 0; tt < MAXT; ++tt) {
@@ -590,6 +643,7 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.RS = g.RW;
   g.npg = 0; g.gstride = 0; g.nco = 16; g.oscale = 1.f;
   g.njb = J; g.tpw = 1;
+  g.nib = I; g.relu = 0;
   {
     // default on: conv16v3 5.51 -> 5.31 ms at 64 x 25^4 (profiles/r1s3_kbench_nt.json)
     const char* e = getenv("NCNET_NT_STORE");   // read per launch: tests / kbench switch it in-process
@@ -669,6 +723,30 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
   KS_DISPATCH(L16V2, 0);
 #undef L16V2
 #undef L16V2E
+  return (int)hipGetLastError();
+}
+
+// Cout = 1 layer (16 input channels) in output-plane-block mode: Y fp32
+// [V,I,J,K,L] = act(bias + conv(X, W)); Wp [(KS+3)^2 relative planes][nq][64][8]
+// (ops/packing.py blk_out_weights): the 16 MFMA rows are a 4 x 4 block of output
+// planes, so every input plane staged in LDS feeds up to 16 output planes and
+// no combo-planar partials (ij encoding + ijsum) round-trip HBM.
+extern "C" int ncnet_conv16_blk_fwd(const void* X, const void* Wp, const float* bias, float* Y, int V, int I, int J,
+                                    int K, int L, int KS, int relu, hipStream_t stream) {
+  int tk, tl;
+  pick_tile(K, L, tk, tl);
+  ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl);
+  if (g.RW > 32) return -1;
+  g.RS = tl + ((KS - 1 + 7) / 8) * 8;
+  g.nib = cdiv(I, 4); g.njb = cdiv(J, 4);
+  g.relu = relu;
+  const int nq = (KS * KS + 1) / 2;
+  size_t lds2 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
+  dim3 grid((unsigned)(V * g.nib * g.njb * g.nkt * g.nlt)), block(512);
+  const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp;
+#define LBLK(KSV, _) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPI_BLK1, false>), grid, block, lds2, stream, x, w, bias, nullptr, (bf16*)Y, g)
+  KS_DISPATCH(LBLK, 0);
+#undef LBLK
   return (int)hipGetLastError();
 }
 

@@ -16,7 +16,9 @@ MI355X design:
 * every layer runs on the conv16 MFMA kernels (csrc/conv4d_fwd.hip): 16-channel
   blocks directly (one call per output block; input blocks beyond the first
   are summed as fp32 partials), 1-channel operands through the ij encoding
-  (csrc/jshift.hip: the (di, dj) plane offsets move into the channel axis);
+  (csrc/jshift.hip: the (di, dj) plane offsets move into the channel axis),
+  except the forward of a Cout=1 layer, whose MFMA rows are a 4x4 block of
+  output planes (conv16_blk_fwd);
   kernel sizes 1, 3, 5, 7 (reference: any size, lib/conv4d.py:58-82);
 * bias + ReLU are fused into each conv's epilogue; the backward runs the
   data-gradient convs with the previous layer's ReLU mask fused into their
@@ -38,10 +40,13 @@ import torch
 
 from . import _ext
 from . import reference as ref
-from .packing import (ij_groups, ij_in_grad, ij_in_weights, ij_out_grad, ij_out_weights, pack_w16, pack_w16_planes,
-                      plane_dgrad_weights, transpose_for_dgrad)
+from .packing import (blk_out_weights, ij_groups, ij_in_grad, ij_in_weights, ij_out_grad, ij_out_weights, pack_w16,
+                      pack_w16_planes, plane_dgrad_weights, transpose_for_dgrad)
 
 HIP_KS = (1, 3, 5, 7)
+# Cout=1 layers with <= 16 input channels run in output-plane-block mode
+# (conv16_blk_fwd); NCNET_BLK1OUT=0 selects the ij encoding + ijsum instead.
+BLK_1OUT = _os.environ.get("NCNET_BLK1OUT", "1") != "0"
 
 
 def nblocks(c: int) -> int:
@@ -200,6 +205,13 @@ def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=N
             wb = _ij_in_planes(w_std[_blk(w_std, b, cout)])
             outs.append(_epilogue_call(C, xs, wb, bias, b, cout, relu, mask, f32, shp, ks))
         return _gather(outs, f32, cout)
+    if cout == 1 and nbi == 1 and BLK_1OUT:
+        # output-plane blocks: the 16 MFMA rows are 4x4 output planes, no
+        # combo-planar partials (2.5 GB at the training shape) and no ijsum
+        y = torch.empty(shp, dtype=torch.float32, device=dev)
+        C.conv16_blk_fwd(h[0], pack_w16_planes(blk_out_weights(w_std)),
+                         None if bias is None else bias.float().reshape(1).contiguous(), y, ks, 1 if relu else 0)
+        return y
     if cout == 1:                          # ij encoding: combo-planar partials, shift-summed by ijsum
         G, nq = ij_groups(ks), ks * ks
         wz = _ij_out_planes(w_std, nbi)

@@ -102,6 +102,22 @@ def ij_out_weights(w_std: torch.Tensor) -> torch.Tensor:
     return tmp.view(G, 16, 16, ks, ks).contiguous()
 
 
+def blk_out_weights(w_std: torch.Tensor) -> torch.Tensor:
+    """[1, ci<=16, k^4] -> [(k+3)^2, 16 rows, 16 ci, k, k]: the output-plane-block
+    weights of a Cout=1 layer (csrc/conv4d_fwd.hip EPI_BLK1).  A workgroup owns
+    the 4x4 block of output planes (i0+a, j0+b), row r = 4a + b, and streams the
+    input planes (i0-P+pi, j0-P+qj), pi, qj in [0, k+3); relative plane
+    pi*(k+3)+qj holds, in row r, W[0, :, pi-a, qj-b] (zero outside the kernel)."""
+    ci, ks = w_std.shape[1], w_std.shape[-1]
+    sp = ks + 3
+    out = w_std.new_zeros((sp, sp, 16, 16, ks, ks))
+    w = w_std[0]                                   # [ci, di, dj, dk, dl]
+    for a in range(4):
+        for b in range(4):
+            out[a:a + ks, b:b + ks, 4 * a + b, :ci] = w.permute(1, 2, 0, 3, 4)
+    return out.reshape(sp * sp, 16, 16, ks, ks)
+
+
 def plane_dgrad_weights(wp: torch.Tensor) -> torch.Tensor:
     """Data-gradient weights of a (dk, dl)-only plane conv: swap channels, flip taps."""
     return wp.transpose(1, 2).flip(-2, -1)

@@ -79,10 +79,13 @@ def init_distributed(device: str | None = None, timeout_s: int | None = None) ->
     if wants_process_group(world):
         os.environ.setdefault("MASTER_PORT", "29500")
         backend = "nccl" if use_gpu else "gloo"
+        # NCNET_DIST_BACKEND=gloo: rehearse the multi-rank GPU path with several
+        # ranks on ONE card (RCCL refuses two ranks per device)
+        backend = os.environ.get("NCNET_DIST_BACKEND", backend)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
             kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-            if use_gpu:
+            if use_gpu and backend == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(**kw)
         backend = dist.get_backend()

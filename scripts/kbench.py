@@ -84,6 +84,8 @@ def main():
     pp = torch.empty((2 * npg, 1, ks * ks, 16, 16), device=dev)
     ppb = torch.empty((2 * npg, 16), device=dev)
     wz = pack_w16_planes(ij_out_weights(torch.randn(1, 16, ks, ks, ks, ks, device=dev) * 0.05))
+    from ncnet_amd.ops.packing import blk_out_weights
+    wblk = pack_w16_planes(blk_out_weights(torch.randn(1, 16, ks, ks, ks, ks, device=dev) * 0.05))
     nq = ks * ks
     zq = torch.empty((nq,) + shp, device=dev)
 
@@ -107,6 +109,7 @@ def main():
         "ij_out_dgrad": (lambda: C.conv16_fwd(xs, wij, None, x16, y16, ks, 2), fl1),
         "ij_out_fwd_total": (ij_out_fwd, fl1),
         "ijsum": (lambda: C.ijsum(zq, b1, y1, ks, 1, 1), None),
+        "blk_out_fwd": (lambda: C.conv16_blk_fwd(x16, wblk, b1, y1, ks, 1), fl1),
         "wgrad16v2_plane": (lambda: C.wgrad16(xs[0], g16, pp, ppb, ks, 2, 2), fl1 / G),
     }
     only = set(a.only.split(",")) if a.only else None

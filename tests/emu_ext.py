@@ -3,7 +3,8 @@
 Each function has the binding's signature and buffer contract (packed MFMA
 weight fragments in, bf16/fp32 buffers written in place) and computes the
 kernel's math exactly in float64 from the packed operands: conv16_fwd
-(full 4D or group-plane mode, epilogues 0/1/2/4), wgrad16 (full / plane-only
+(full 4D or group-plane mode, epilogues 0/1/2/4), conv16_blk_fwd (output-plane
+blocks of a Cout=1 layer), wgrad16 (full / plane-only
 partial layout), ijpack / ijsum, combine and transpose.  It lets the CPU suite
 check the Python orchestration of the HIP path (channel blocks, the ij
 encoding, weight packing, symmetric branches, every gradient) against
@@ -59,6 +60,31 @@ def conv16_fwd(X, Wp, bias, M, Y, ks, epi):
     elif epi == 2:
         out = out * (M.double() > 0)
     Y.copy_(out)
+
+
+def conv16_blk_fwd(X, Wp, bias, Y, ks, relu):
+    """Output-plane-block Cout=1 conv: block (i0, j0) streams input planes
+    (p, q) in [i0-P, i0+4+P) x [j0-P, j0+4+P); relative plane
+    (p-i0+P)*(ks+3) + (q-j0+P) of the packed weights gives row r = 4a+b, i.e.
+    output plane (i0+a, j0+b)."""
+    xs = X.double()
+    V, I, J, K, L, _ = xs.shape
+    P, sp = ks // 2, ks + 3
+    w = _unpack16(Wp, ks)                                     # [sp*sp, 16 rows, 16 ci, taps]
+    acc = torch.zeros((V, I, J, K, L), dtype=torch.float64)
+    for i0 in range(0, I, 4):
+        for j0 in range(0, J, 4):
+            for p in range(max(0, i0 - P), min(I, i0 + 4 + P)):
+                for q in range(max(0, j0 - P), min(J, j0 + 4 + P)):
+                    wp = w[(p - i0 + P) * sp + (q - j0 + P)]
+                    rows = _plane_conv(xs[:, p, q].permute(0, 3, 1, 2), wp, ks)     # [V, 16 rows, K, L]
+                    for r in range(16):
+                        i, j = i0 + r // 4, j0 + r % 4
+                        if i < I and j < J:
+                            acc[:, i, j] += rows[:, r]
+    if bias is not None:
+        acc += float(bias.reshape(-1)[0])
+    Y.copy_(torch.relu(acc) if relu else acc)
 
 
 def wgrad16(X, G, part, partb, ks, mode, variant):
@@ -137,6 +163,7 @@ def transpose(x, y):
 class EmuExt:
     """Namespace with the binding names used by ops/neigh_consensus.py and ops/conv4d.py."""
     conv16_fwd = staticmethod(conv16_fwd)
+    conv16_blk_fwd = staticmethod(conv16_blk_fwd)
     wgrad16 = staticmethod(wgrad16)
     ijpack = staticmethod(ijpack)
     ijsum = staticmethod(ijsum)

@@ -55,6 +55,31 @@ def test_conv16_fwd(ks, shape):
     assert relerr(y.permute(0, 5, 1, 2, 3, 4), yr) < 1e-2
 
 
+@pytest.mark.parametrize("ks,shape,cin,relu", [(5, (4, 25, 25, 25, 25), 16, 1), (5, (1, 6, 5, 26, 29), 16, 0),
+                                               (3, (2, 7, 9, 11, 13), 10, 1), (3, (1, 3, 2, 30, 27), 16, 1),
+                                               (7, (1, 9, 8, 25, 25), 16, 1), (1, (2, 5, 6, 25, 25), 16, 0),
+                                               (5, (1, 13, 11, 9, 7), 16, 1)])
+def test_conv16_blk_fwd(ks, shape, cin, relu):
+    """Cout=1 conv in output-plane-block mode (4x4 output planes per
+    workgroup = the 16 MFMA rows, partial blocks at the I/J edges, multi-tile
+    K, L) vs the fp64 Conv4d oracle."""
+    from ncnet_amd.ops.packing import blk_out_weights, pack_w16_planes
+    torch.manual_seed(1)
+    V, I, J, K, L = shape
+    x = torch.rand(V, cin, I, J, K, L, device=DEV)
+    w = torch.randn(1, cin, ks, ks, ks, ks, device=DEV) * 0.05
+    b = torch.randn(1, device=DEV) * 0.1 - (0.3 if relu else 0.0)
+    xcl = torch.zeros(V, I, J, K, L, 16, device=DEV, dtype=torch.bfloat16)
+    xcl[..., :cin] = x.permute(0, 2, 3, 4, 5, 1).to(torch.bfloat16)
+    y = torch.full((V, I, J, K, L), float("nan"), device=DEV)
+    _ext.ext().conv16_blk_fwd(xcl, pack_w16_planes(blk_out_weights(w)), b, y, ks, relu)
+    yr = ref.conv4d(bf(x), ref.conv4d_weight_from_std(bf(w)), b.double())[:, 0]
+    if relu:
+        yr = torch.relu(yr)
+    assert torch.isfinite(y).all()
+    assert relerr(y, yr) < 1e-4
+
+
 @pytest.mark.parametrize("cin,cout,ks", [(16, 16, 5), (1, 16, 5), (16, 1, 5), (16, 16, 3), (1, 16, 3), (16, 1, 3),
                                          (10, 10, 3), (32, 16, 3), (1, 40, 3), (24, 1, 5), (16, 16, 7), (1, 16, 7),
                                          (16, 16, 1), (1, 1, 3), (20, 33, 3)])
