@@ -230,7 +230,10 @@ __device__ __forceinline__ Col decode_col(const W3Geom& g, int c) {
   return r;
 }
 
-template <int KS>
+// NCH: 32-voxel chunks per half-tile (VT = 64 NCH), a compile-time constant so
+// the chunk loop is branch-free and the fragment prefetch of chunk u + 1 needs
+// no conservative LDS-counter drain at a control-flow merge.
+template <int KS, int NCH>
 __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ G,
                                                            float* __restrict__ part, float* __restrict__ partb,
                                                            W3Geom g) {
@@ -240,8 +243,9 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
   constexpr int TPG = (NT - 1) / 4;      // regular taps per tap group
   constexpr int EXP = (KS + 2) / 3;      // di values of the last tap per group 1..3
   constexpr int NW = 8;
-  constexpr int MAXC = 6;                // voxel chunks per half (VT <= 384)
+  constexpr int MAXC = NCH;              // voxel chunks per half (VT = 64 NCH <= 384)
   static_assert((NT - 1) % 4 == 0, "NT must be 1 mod 4");
+  static_assert(NCH >= 1 && NCH <= 6, "1..6 chunks per half");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int xbytes = g.PR * g.RS * 32, gbytes = g.VT * 32;
@@ -281,7 +285,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
   const u32x4 ones = {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};   // bf16 1.0 x 8
 
   const int c_lo = grp * g.cpg, c_hi = min(g.ncols, c_lo + g.cpg);
-  const int nch = (g.VT >> 6);            // chunks per half (VT multiple of 64)
+  constexpr int nch = NCH;                // chunks per half (VT multiple of 64)
   const int ch_lo = half * nch;
   const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
   const uint32_t ga_base = (ch_lo * 32 + gq * 4 + qq) * 32 + pp * 8;   // + u*1024 (+512 for the 2nd read)
@@ -424,9 +428,9 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
           }
 #pragma unroll
           for (int m = 0; m < TPG; ++m) {
-            u32x4 afn = afr;
-            if (m + 1 < TPG || tg > 0)
-              afn = cat4u(lds_read_tr16u(xc, pa0 + toff[m + 1]), lds_read_tr16u(xc, pa1 + toff[m + 1]));
+            // (m = TPG - 1: the last tap NT - 1, used by groups 1..3 only; group 0
+            // reads it too, which keeps this loop free of a wave-uniform branch)
+            const u32x4 afn = cat4u(lds_read_tr16u(xc, pa0 + toff[m + 1]), lds_read_tr16u(xc, pa1 + toff[m + 1]));
 #pragma unroll
             for (int d = 0; d < KS; ++d) acc[m][d] = mfma16u(afr, bfr[u & 1][d], acc[m][d]);
             afr = afn;
@@ -548,8 +552,14 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
   if (lds > 160 * 1024) return -1;
   dim3 grid((unsigned)(KS * ngroups)), block(512);
   const bf16* x = (const bf16*)X; const bf16* gg = (const bf16*)G;
-  if (KS == 5) hipLaunchKernelGGL((wgrad16v3_kernel<5>), grid, block, lds, stream, x, gg, part, partb, g);
-  else if (KS == 3) hipLaunchKernelGGL((wgrad16v3_kernel<3>), grid, block, lds, stream, x, gg, part, partb, g);
+  const int nch = g.VT / 64;
+#define W3N(KSV, N) hipLaunchKernelGGL((wgrad16v3_kernel<KSV, N>), grid, block, lds, stream, x, gg, part, partb, g)
+#define W3(KSV) do { switch (nch) { case 1: W3N(KSV, 1); break; case 2: W3N(KSV, 2); break; case 3: W3N(KSV, 3); break; \
+                                    case 4: W3N(KSV, 4); break; case 5: W3N(KSV, 5); break; default: W3N(KSV, 6); } } while (0)
+  if (KS == 5) W3(5);
+  else if (KS == 3) W3(3);
   else return -2;
+#undef W3
+#undef W3N
   return (int)hipGetLastError();
 }
