@@ -12,6 +12,8 @@ extern "C" {
 int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv16_blk_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_wgrad16p(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, int, long long,
+                   long long, hipStream_t);
 int ncnet_wgrad16v3(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_ijpack(const void*, int, void*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv16f8_fwd(const void*, const void*, const float*, void*, int, int, int, int, int, int, int, int, int, float, hipStream_t);
@@ -141,6 +143,27 @@ void wgrad16(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks, int64_t 
   }
   ok(ncnet_wgrad16(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(0), X.size(1),
                    X.size(2), X.size(3), X.size(4), ks, rows / 2, (int)mode, cur_stream(X)), "wgrad16");
+}
+
+// Plane-only weight gradient of the ij-encoded layers (whole-plane tiles, K, L <= 25):
+// X [nsets,V,I,J,K,L,16], G [ngg,V,I,J,K,L,16]; part [rows, nsets*ngg, ks*ks, 16, 16],
+// partb [rows, nsets*ngg, 16] (rows = 2 * workgroup groups); nsets * ngg <= 2.
+void wgrad16p(Tensor X, Tensor G, Tensor part, Tensor partb, int64_t ks) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(G, "G", at::kBFloat16); check(part, "part", at::kFloat); check(partb, "partb", at::kFloat);
+  check_ks(ks);
+  TORCH_CHECK(X.dim() == 7 && G.dim() == 7 && X.size(6) == 16, "X, G must be [n,V,I,J,K,L,16]");
+  const int64_t nsets = X.size(0), ngg = G.size(0);
+  TORCH_CHECK(nsets * ngg <= 2 && nsets >= 1 && ngg >= 1, "wgrad16p: nsets * ngg must be 1 or 2");
+  TORCH_CHECK(X.sizes().slice(1).vec() == G.sizes().slice(1).vec(), "wgrad16p: X and G volumes differ");
+  const int64_t rows = part.size(0);
+  TORCH_CHECK(rows > 0 && rows % 2 == 0, "wgrad16p needs an even number of partial rows");
+  check_shape(part, "part", {rows, nsets * ngg, ks * ks, 16, 16});
+  check_shape(partb, "partb", {rows, nsets * ngg, 16});
+  const int64_t vol = X[0].numel();
+  ok(ncnet_wgrad16p(X.data_ptr(), G.data_ptr(), (float*)part.data_ptr(), (float*)partb.data_ptr(), X.size(1), X.size(2),
+                    X.size(3), X.size(4), X.size(5), ks, rows / 2, (int)nsets, (int)ngg, vol, vol, cur_stream(X)),
+     "wgrad16p");
 }
 
 // X [V,I,J,K,L] (bf16/fp32) -> S [G,V,I,J,K,L,16] bf16 (ij encoding, G = ceil(ks*ks/16))
@@ -527,6 +550,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for ncnet_amd";
   m.def("conv16_fwd", &conv16_fwd);
   m.def("conv16_blk_fwd", &conv16_blk_fwd);
+  m.def("wgrad16p", &wgrad16p);
   m.def("wgrad16", &wgrad16);
   m.def("ijpack", &ijpack);
   m.def("conv16f8_fwd", &conv16f8_fwd);

@@ -18,8 +18,17 @@
 //   wgrad16v3 (the 16 -> 16 training layers): sliding G-plane ring, below.
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace ncnet {
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void wstatic_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    wstatic_for<B + 1, E>(f);
+  }
+}
 
 struct WGeom {
   int V, I, J, K, L;
@@ -399,14 +408,6 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
         const int sd = s0 - d < 0 ? s0 - d + NS : s0 - d;
         gslot[d] = (uint32_t)((d >= di_lo && d <= di_hi) ? sd : NS) * gbytes;
       }
-      // the last tap's extra di values of this tap group (groups 1..3), hoisted out of the chunk loop
-      uint32_t gsxv[EXP];
-#pragma unroll
-      for (int e = 0; e < EXP; ++e) {
-        const int d = xdi_lo + e;
-        const int sd = s0 - d < 0 ? s0 - d + NS : s0 - d;
-        gsxv[e] = (uint32_t)((d >= di_lo && d <= di_hi) ? sd : NS) * gbytes;
-      }
       // software pipeline: the next chunk's G fragments and the next tap's X
       // fragment are in flight while the current MFMAs run
       // fragments held as u32 vectors (see cat4u in common.h)
@@ -435,17 +436,19 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
             for (int d = 0; d < KS; ++d) acc[m][d] = mfma16u(afr, bfr[u & 1][d], acc[m][d]);
             afr = afn;
           }
-          if (tg > 0) {   // last tap (afr), this group's di range (B re-read from LDS)
-            const uint32_t ga = ga_base + u * 1024;
-#pragma unroll
-            for (int e = 0; e < EXP; ++e) {
-              const int d = xdi_lo + e;
-              if (d < xdi_hi) {
-                u32x4 bx = cat4u(lds_read_tr16u(gbuf, gsxv[e] + ga), lds_read_tr16u(gbuf, gsxv[e] + ga + 512));
-                accx[e] = mfma16u(afr, bx, accx[e]);
-              }
+          // last tap (afr) x this group's di range: the G fragments of those di
+          // are already in registers (bfr), selected by a wave-uniform branch
+          // on the group so every fragment index stays compile-time
+          wstatic_for<1, 4>([&](auto tc) {
+            constexpr int TGC = decltype(tc)::value;
+            if (tg == TGC) {
+              wstatic_for<0, EXP>([&](auto ec) {
+                constexpr int e = decltype(ec)::value;
+                constexpr int d = (TGC - 1) * EXP + e;
+                if constexpr (d < KS && d < TGC * EXP) accx[e] = mfma16u(afr, bfr[u & 1][d], accx[e]);
+              });
             }
-          }
+          });
           if (center_blk && tg == 0) accb = mfma16u(ones, bfr[u & 1][P], accb);
         }
       }
@@ -476,6 +479,140 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
     }
   }
   if (center_blk && tg == 0 && lane < 16) partb[row * 16 + lane] = accb[0];
+}
+
+
+// ===========================================================================
+// wgrad16p: plane-only weight gradient of the ij-encoded 1-channel layers
+// (same math as wgrad16v2 with dj_center = 2) for whole-plane tiles
+// (K, L <= 25), with the next item's X plane and G tiles streaming into the
+// second of two LDS buffers while the current item is computed (v2 exposes the
+// DMA latency of every item), and NGG G operands per X plane:
+//   NGG = 2: the Cout = 1 layer, X = layer input, G = both groups of
+//            ijpack(g, -1): every X fragment read feeds 2 MFMAs;
+//   NGG = 1 with nsets = 2: the Cin = 1 layer, X = both groups of ijpack(x0)
+//            (set = blockIdx-derived), G = the layer's output gradient.
+// Tiles sit at fixed positions, so the zero halo is written once.
+// part: [2 * ngroups][nsets * NGG][NT][16 ci][16 co]; partb [2 * ngroups][nsets * NGG][16].
+// ===========================================================================
+template <int KS, int NGG>
+__global__ __launch_bounds__(512, 1) void wgrad16p_kernel(const bf16* __restrict__ X, const bf16* __restrict__ G,
+                                                          float* __restrict__ part, float* __restrict__ partb, WGeom g,
+                                                          long long xstride, long long gstride, int nsets) {
+  constexpr int P = KS / 2;
+  constexpr int NT = KS * KS;
+  constexpr int TPW = (NT + 3) / 4;
+  constexpr int NW = 8;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nvox = g.K * g.L;
+  const int nv32 = (nvox + 31) & ~31;
+  const int xbytes = g.PR * g.RS * 32, gtb = nv32 * 32;
+  const int bufbytes = xbytes + NGG * gtb;
+  uint16_t* voff = (uint16_t*)(smem + 2 * bufbytes);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tg = wave & 3, half = wave >> 2;
+  const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int set = lb % nsets, grp = lb / nsets;
+  const bf16* Xs = X + (size_t)set * xstride;
+
+  for (int o = threadIdx.x * 16; o < 2 * bufbytes; o += NW * 64 * 16) *(u32x4*)(smem + o) = u32x4{0u, 0u, 0u, 0u};
+  for (int e = threadIdx.x; e < nv32; e += NW * 64) {
+    int kk = e / g.L, ll = e - kk * g.L;
+    voff[e] = (uint16_t)((e < nvox) ? (kk * g.RS + ll) * 32 : 0);
+  }
+  uint32_t toffw[TPW];
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) {
+    int tap = min(tg + 4 * tt, NT - 1);
+    int dk = tap / KS, dl = tap - dk * KS;
+    toffw[tt] = (uint32_t)((dk * g.RS + dl) * 32);
+  }
+  f32x4 acc[NGG][TPW];
+  f32x4 accb[NGG];
+#pragma unroll
+  for (int n = 0; n < NGG; ++n) {
+    accb[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) acc[n][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ones[q] = f2bf(1.f);
+
+  const int it_lo = grp * g.ipg, it_hi = min(g.nitems, it_lo + g.ipg);
+  const int nchunk = nv32 >> 5;
+  const int c_lo = half ? (nchunk + 1) / 2 : 0, c_hi = half ? nchunk : (nchunk + 1) / 2;
+  const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const size_t ext = (size_t)g.V * g.I * g.J * g.K * g.L * 16;
+  (void)ext;
+
+  // item = plane (v, i, j); X rows k = -P .. K+P-1 land at LDS row k + P, column P
+  auto stage = [&](int it, char* buf) {
+    const size_t po = (size_t)it * g.K * g.L * 16;
+    for (int row = wave; row < g.K; row += NW) {
+      if (lane < 2 * g.L && NCNET_OK(po + ((size_t)row * g.L) * 16 + lane * 8 + 8 <= ext))
+        __builtin_amdgcn_global_load_lds((const void*)(Xs + po + (size_t)row * g.L * 16 + lane * 8),
+                                         LDS_PTR(void, buf + ((row + P) * g.RS + P) * 32), 16, 0, 0);
+    }
+#pragma unroll
+    for (int n = 0; n < NGG; ++n) {
+      const bf16* gp = G + (size_t)n * gstride + po;
+      char* gb = buf + xbytes + n * gtb;
+      for (int q = wave; q * 64 < 2 * nvox; q += NW) {
+        const int ci = q * 64 + lane;
+        if (ci < 2 * nvox && NCNET_OK(po + ci * 8 + 8 <= ext))
+          __builtin_amdgcn_global_load_lds((const void*)(gp + ci * 8), LDS_PTR(void, gb + q * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  __syncthreads();  // zero fill and voff done before any DMA lands
+  if (it_lo < it_hi) stage(it_lo, smem);
+  for (int it = it_lo; it < it_hi; ++it) {
+    const int n0 = it - it_lo;
+    __syncthreads();  // vmcnt(0) + barrier: item it landed; item it-1's reads of the other buffer done
+    if (it + 1 < it_hi) stage(it + 1, smem + ((n0 + 1) & 1) * bufbytes);
+    const char* plane = smem + (n0 & 1) * bufbytes;
+    const char* gt = plane + xbytes;
+    for (int c = c_lo; c < c_hi; ++c) {
+      const int vb0 = c * 32 + gq * 4 + qq, vb1 = vb0 + 16;
+      bf16x8 bfr[NGG];
+#pragma unroll
+      for (int n = 0; n < NGG; ++n)
+        bfr[n] = cat8(lds_read_tr16(gt + n * gtb, vb0 * 32 + pp * 8), lds_read_tr16(gt + n * gtb, vb1 * 32 + pp * 8));
+      const uint32_t pa0 = voff[vb0] + pp * 8, pa1 = voff[vb1] + pp * 8;
+#pragma unroll
+      for (int tt = 0; tt < TPW; ++tt) {
+        if (tg + 4 * tt < NT) {
+          bf16x8 afr = cat8(lds_read_tr16(plane, pa0 + toffw[tt]), lds_read_tr16(plane, pa1 + toffw[tt]));
+#pragma unroll
+          for (int n = 0; n < NGG; ++n) acc[n][tt] = mfma16(afr, bfr[n], acc[n][tt]);
+        }
+      }
+      if (tg == 0) {
+#pragma unroll
+        for (int n = 0; n < NGG; ++n) accb[n] = mfma16(ones, bfr[n], accb[n]);
+      }
+    }
+  }
+
+  const int row = grp * 2 + half, nsl = nsets * NGG;
+#pragma unroll
+  for (int n = 0; n < NGG; ++n) {
+    float* pout = part + ((size_t)row * nsl + set * NGG + n) * NT * 256;
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      int tap = tg + 4 * tt;
+      if (tap < NT) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pout[tap * 256 + (4 * (lane >> 4) + r) * 16 + (lane & 15)] = acc[n][tt][r];
+      }
+    }
+    if (tg == 0 && lane < 16) partb[((size_t)row * nsl + set * NGG + n) * 16 + lane] = accb[n][0];
+  }
 }
 
 }  // namespace ncnet
@@ -524,6 +661,30 @@ extern "C" int ncnet_wgrad16(const void* X, const void* G, float* part, float* p
 #define WG2(KSV, _) hipLaunchKernelGGL((wgrad16v2_kernel<KSV>), grid, block, lds, stream, x, gg, part, partb, g)
   KS_DISPATCH(WG2, 0);
 #undef WG2
+  return (int)hipGetLastError();
+}
+
+// wgrad16p (plane-only, whole-plane tiles: K, L <= 25): X [nsets][V,I,J,K,L,16]
+// (set stride xstride elements), G [NGG][...] (stride gstride); grid = ngroups * nsets.
+extern "C" int ncnet_wgrad16p(const void* X, const void* G, float* part, float* partb, int V, int I, int J, int K,
+                              int L, int KS, int ngroups, int nsets, int ngg, long long xstride, long long gstride,
+                              hipStream_t stream) {
+  if (K > 25 || L > 25) return -1;
+  if (ngg != 1 && ngg != 2) return -3;
+  WGeom g = make_wgeom(V, I, J, K, L, KS, ngroups);
+  g.RS = L + ((KS - 1 + 7) / 8) * 8;        // row wrap jumps 256 B (conflict-free transposed reads)
+  g.PR = K + KS - 1;
+  if (L + KS - 1 > g.RS || g.PR * g.RS * 32 > 65535) return -1;
+  const int nv32 = (K * L + 31) & ~31;
+  const size_t buf = (size_t)g.PR * g.RS * 32 + (size_t)ngg * nv32 * 32;
+  const size_t lds = 2 * buf + (size_t)nv32 * 2;
+  if (lds > 160 * 1024) return -1;
+  dim3 grid((unsigned)(ngroups * nsets)), block(512);
+  const bf16* x = (const bf16*)X; const bf16* gg = (const bf16*)G;
+#define WGP(KSV, _) do { if (ngg == 2) hipLaunchKernelGGL((wgrad16p_kernel<KSV, 2>), grid, block, lds, stream, x, gg, part, partb, g, xstride, gstride, nsets); \
+                         else hipLaunchKernelGGL((wgrad16p_kernel<KSV, 1>), grid, block, lds, stream, x, gg, part, partb, g, xstride, gstride, nsets); } while (0)
+  KS_DISPATCH(WGP, 0);
+#undef WGP
   return (int)hipGetLastError();
 }
 

@@ -124,6 +124,36 @@ def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, plane_onl
     return part.sum(0), partb.sum(0)
 
 
+# Plane-only weight gradient of the Cout=1 layer on wgrad16p (double-buffered
+# items, both ij groups of ijpack(g, -1) against one staged X plane: 0.81 ms vs
+# 2 x 0.44 ms at the training shape) when the (k, l) plane is one tile;
+# NCNET_WGRAD_P=0 selects the per-group wgrad16v2 calls.  The Cin=1 layer stays
+# on wgrad16v2: with one G operand every X fragment feeds a single MFMA, the
+# kernel is LDS-bound and v2's 2-3 workgroups per CU hide more (1.18 vs 0.89 ms).
+WGRAD_P = _os.environ.get("NCNET_WGRAD_P", "1") != "0"
+
+
+def wgrad_p_ok(shape) -> bool:
+    return WGRAD_P and shape[3] <= 25 and shape[4] <= 25
+
+
+def wgrad16p_partials(C, x7: torch.Tensor, g7: torch.Tensor, ks: int):
+    """x7 [nx, V,I,J,K,L,16], g7 [ng, ...] bf16 with nx == 1 or ng == 1:
+    plane-only partials of every (x, g) pair -> (s [nx*ng, tap, ci, co], sb [nx*ng, 16])."""
+    nx, ng = x7.shape[0], g7.shape[0]
+    if nx * ng > 2:                       # the kernel pairs at most two operands
+        if nx > 1:
+            outs = [wgrad16p_partials(C, x7[i:i + 2], g7, ks) for i in range(0, nx, 2)]
+        else:
+            outs = [wgrad16p_partials(C, x7, g7[i:i + 2], ks) for i in range(0, ng, 2)]
+        return torch.cat([o[0] for o in outs]), torch.cat([o[1] for o in outs])
+    groups = max(1, min(1024 // (nx * ng), _nitems(x7.shape[1:6])))
+    part = torch.empty((2 * groups, nx * ng, ks * ks, 16, 16), dtype=torch.float32, device=x7.device)
+    partb = torch.empty((2 * groups, nx * ng, 16), dtype=torch.float32, device=x7.device)
+    C.wgrad16p(x7, g7, part, partb, ks)
+    return part.sum(0), partb.sum(0)
+
+
 def _reduce_wgrad16(s: torch.Tensor, ks: int, cout: int, cin: int) -> torch.Tensor:
     # s [dd, tap, ci, co] -> std [co, ci, di, dj, dk, dl]
     return s.permute(3, 2, 0, 1).reshape(16, 16, ks, ks, ks, ks)[:cout, :cin]
@@ -376,6 +406,12 @@ def _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout):
         db = None
         for a in range(nblocks(cin)):
             si = slice(16 * a, min(cin, 16 * a + 16))
+            if wgrad_p_ok(gs.shape[1:6]):
+                s, sb = wgrad16p_partials(C, xin[a:a + 1], gs, ks)
+                dw[:, si] = ij_out_grad(s, si.stop - si.start)
+                if a == 0:
+                    db = sb[qc // 16][qc % 16].reshape(1)
+                continue
             parts = [wgrad16_partials(C, xin[a], gs[gi], ks, True) for gi in range(G)]
             dw[:, si] = ij_out_grad(torch.stack([p[0][0] for p in parts]), si.stop - si.start)
             if a == 0:

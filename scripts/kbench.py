@@ -86,6 +86,8 @@ def main():
     wz = pack_w16_planes(ij_out_weights(torch.randn(1, 16, ks, ks, ks, ks, device=dev) * 0.05))
     from ncnet_amd.ops.packing import blk_out_weights
     wblk = pack_w16_planes(blk_out_weights(torch.randn(1, 16, ks, ks, ks, ks, device=dev) * 0.05))
+    pq = torch.empty((1024, G, ks * ks, 16, 16), device=dev)
+    pqb = torch.empty((1024, G, 16), device=dev)
     nq = ks * ks
     zq = torch.empty((nq,) + shp, device=dev)
 
@@ -111,6 +113,8 @@ def main():
         "ijsum": (lambda: C.ijsum(zq, b1, y1, ks, 1, 1), None),
         "blk_out_fwd": (lambda: C.conv16_blk_fwd(x16, wblk, b1, y1, ks, 1), fl1),
         "wgrad16v2_plane": (lambda: C.wgrad16(xs[0], g16, pp, ppb, ks, 2, 2), fl1 / G),
+        "wgrad16p_1out": (lambda: C.wgrad16p(x16.unsqueeze(0), xs, pq, pqb, ks), fl1),
+        "wgrad16p_1in": (lambda: C.wgrad16p(xs, g16.unsqueeze(0), pq, pqb, ks), fl1),
     }
     only = set(a.only.split(",")) if a.only else None
     res = {}

@@ -112,6 +112,20 @@ def _wgrad16(X, G, part, partb, ks, mode):
     partb[0] = gs.sum(dim=(0, 2, 3, 4, 5)).float()
 
 
+def wgrad16p(X, G, part, partb, ks):
+    """Plane-only partials of every (X set, G operand) pair (one of them single)."""
+    nx, ng = X.shape[0], G.shape[0]
+    part.zero_()
+    partb.zero_()
+    for i in range(nx):
+        for n in range(ng):
+            p1 = torch.zeros((2, 1, ks * ks, 16, 16))
+            pb = torch.zeros((2, 16))
+            wgrad16(X[i], G[n], p1, pb, ks, 2, 2)
+            part[0, i * ng + n] = p1[0, 0]
+            partb[0, i * ng + n] = pb[0]
+
+
 def _shift_ij(x, si, sj):
     """out[:, i, j] = x[:, i + si, j + sj] (zero outside), x [V, I, J, ...]."""
     I, J = x.shape[1], x.shape[2]
@@ -165,6 +179,7 @@ class EmuExt:
     conv16_fwd = staticmethod(conv16_fwd)
     conv16_blk_fwd = staticmethod(conv16_blk_fwd)
     wgrad16 = staticmethod(wgrad16)
+    wgrad16p = staticmethod(wgrad16p)
     ijpack = staticmethod(ijpack)
     ijsum = staticmethod(ijsum)
     combine_fwd = staticmethod(combine_fwd)

@@ -80,6 +80,33 @@ def test_conv16_blk_fwd(ks, shape, cin, relu):
     assert relerr(y, yr) < 1e-4
 
 
+@pytest.mark.parametrize("ks,shape,nx,ng", [(5, (2, 25, 25, 25, 25), 1, 2), (5, (2, 25, 25, 25, 25), 2, 1),
+                                            (3, (2, 7, 9, 11, 13), 1, 1), (7, (1, 9, 8, 25, 25), 1, 2),
+                                            (1, (2, 5, 6, 20, 25), 2, 1)])
+def test_wgrad16p(ks, shape, nx, ng):
+    """Double-buffered plane-only weight gradient (both ij groups per launch)
+    vs the fp64 plane-conv definition: dW[tap][ci][co] = sum X[vox + tap] G[vox]."""
+    import torch.nn.functional as F
+    torch.manual_seed(2)
+    V, I, J, K, L = shape
+    x = (torch.rand((nx,) + shape + (16,), device=DEV) - 0.3).to(torch.bfloat16)
+    g = torch.randn((ng,) + shape + (16,), device=DEV).to(torch.bfloat16)
+    part = torch.full((64, nx * ng, ks * ks, 16, 16), float("nan"), device=DEV)
+    partb = torch.full((64, nx * ng, 16), float("nan"), device=DEV)
+    _ext.ext().wgrad16p(x, g, part, partb, ks)
+    s, sb = part.sum(0), partb.sum(0)
+    for a in range(nx):
+        for n in range(ng):
+            xx = x[a].double().reshape(V * I * J, K, L, 16).permute(0, 3, 1, 2)
+            gg = g[n].double().reshape(V * I * J, K, L, 16).permute(0, 3, 1, 2)
+            P = ks // 2
+            xp = F.pad(xx, (P, P, P, P))
+            want = torch.stack([torch.einsum("nckl,nokl->co", xp[:, :, dk:dk + K, dl:dl + L], gg)
+                                for dk in range(ks) for dl in range(ks)])   # [tap, ci, co]
+            assert relerr(s[a * ng + n], want) < 1e-4
+            assert relerr(sb[a * ng + n], gg.sum(dim=(0, 2, 3))) < 1e-4
+
+
 @pytest.mark.parametrize("cin,cout,ks", [(16, 16, 5), (1, 16, 5), (16, 1, 5), (16, 16, 3), (1, 16, 3), (16, 1, 3),
                                          (10, 10, 3), (32, 16, 3), (1, 40, 3), (24, 1, 5), (16, 16, 7), (1, 16, 7),
                                          (16, 16, 1), (1, 1, 3), (20, 33, 3)])
