@@ -73,6 +73,8 @@ def main():
     n3 = wgrad_v3_groups(shp, ks)
     p3 = torch.empty((2 * n3, ks ** 2, ks ** 2, 16, 16), device=dev)
     p3b = torch.empty((2 * n3, 16), device=dev)
+    p3g = {n: (torch.empty((2 * n, ks ** 2, ks ** 2, 16, 16), device=dev), torch.empty((2 * n, 16), device=dev))
+           for n in (51, 204, 306)}
     ng2 = wgrad_groups(ks, V * S * S * ((S + 24) // 25) ** 2)
     p2 = torch.empty((2 * ng2, ks ** 2, ks ** 2, 16, 16), device=dev)
     p2b = torch.empty((2 * ng2, 16), device=dev)
@@ -104,6 +106,8 @@ def main():
         "conv16_f32": (lambda: C.conv16_fwd(x16, w16, None, None, torch.empty((16,) + shp, device=dev), ks, 4), fl16),
         "wgrad16v3": (lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3), fl16),
         "wgrad16v2": (lambda: C.wgrad16(x16, g16, p2, p2b, ks, 0, 2), fl16),
+        **{f"wgrad16v3_g{n}": ((lambda n=n: C.wgrad16(x16, g16, p3g[n][0], p3g[n][1], ks, 0, 3)), fl16)
+           for n in (51, 204, 306)},
         "wgrad16v3_prio": (with_env("NCNET_WGRAD_FLAGS", "1", lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3)), fl16),
         "ijpack": (lambda: C.ijpack(x1, xs, ks, 1), None),
         "ij_1in_conv": (lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1), fl1),
