@@ -110,12 +110,25 @@ def blk_out_weights(w_std: torch.Tensor) -> torch.Tensor:
     pi*(k+3)+qj holds, in row r, W[0, :, pi-a, qj-b] (zero outside the kernel)."""
     ci, ks = w_std.shape[1], w_std.shape[-1]
     sp = ks + 3
-    out = w_std.new_zeros((sp, sp, 16, 16, ks, ks))
-    w = w_std[0]                                   # [ci, di, dj, dk, dl]
-    for a in range(4):
-        for b in range(4):
-            out[a:a + ks, b:b + ks, 4 * a + b, :ci] = w.permute(1, 2, 0, 3, 4)
-    return out.reshape(sp * sp, 16, 16, ks, ks)
+    # one gather (cached index, zero slot ks*ks) instead of 16 slice copies per step
+    planes = torch.cat((w_std[0].permute(1, 2, 0, 3, 4).reshape(ks * ks, ci, ks, ks),
+                        w_std.new_zeros((1, ci, ks, ks))))
+    if ci < 16:
+        planes = torch.cat((planes, planes.new_zeros((ks * ks + 1, 16 - ci, ks, ks))), 1)
+    return planes[_blk_index(ks, str(w_std.device))].reshape(sp * sp, 16, 16, ks, ks)
+
+
+@functools.lru_cache(maxsize=None)
+def _blk_index(ks: int, device: str) -> torch.Tensor:
+    """[(ks+3)^2 * 16] plane index of blk_out_weights: (pi, qj, row 4a+b) ->
+    di*ks + dj with di = pi - a, dj = qj - b, or the zero slot ks*ks."""
+    sp = ks + 3
+    pi = torch.arange(sp).view(sp, 1, 1)
+    qj = torch.arange(sp).view(1, sp, 1)
+    r = torch.arange(16).view(1, 1, 16)
+    di, dj = pi - r // 4, qj - r % 4
+    ok = (di >= 0) & (di < ks) & (dj >= 0) & (dj < ks)
+    return torch.where(ok, di * ks + dj, torch.full_like(di, ks * ks)).reshape(-1).to(device)
 
 
 def plane_dgrad_weights(wp: torch.Tensor) -> torch.Tensor:
