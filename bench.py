@@ -22,10 +22,17 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
+# RCCL / CUDA-tensor sharing across processes: the ROCm driver only supports
+# dmabuf IPC (tests/test_gpu_dist_optim.py, scripts/gpu_job.sh); set before any
+# HIP initialisation, inherited by the torchrun children below.
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402  (importing torch does not initialise HIP)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -115,7 +122,49 @@ def _fe_finetune_secondary(batch: int, size: int, steps: int = 5, warmup: int = 
     return out
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(args, argv) -> int:
+    """``python bench.py --gpus N`` (N > 1) without a launcher: run the same
+    command under ``torch.distributed.run --nproc-per-node N`` as a CHILD
+    process (never an exec: this process has not touched the GPU and stays
+    that way), relay rank 0's JSON record, and fail loudly when the child fails
+    or reports another world size.  Decided from argv/env only, before any
+    torch.cuda call."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ, NCNET_BENCH_SELF_LAUNCHED="1")
+    print(f"bench.py: --gpus {args.gpus} without WORLD_SIZE; launching {' '.join(cmd[1:4])} ...", file=sys.stderr,
+          flush=True)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    recs = []
+    for line in proc.stdout:
+        if line.startswith("{") and '"metric"' in line:
+            recs.append(line.strip())
+        else:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+    rc = proc.wait()
+    if rc != 0:
+        print(f"bench.py: torchrun child exited with {rc}", file=sys.stderr)
+        return rc if rc > 0 else 1
+    if len(recs) != 1:
+        print(f"bench.py: expected one JSON record from rank 0, got {len(recs)}", file=sys.stderr)
+        return 1
+    rec = json.loads(recs[0])
+    if rec.get("n_gpus") != args.gpus:
+        print(f"bench.py: child reported n_gpus={rec.get('n_gpus')} != --gpus {args.gpus}", file=sys.stderr)
+        return 1
+    print(recs[0], flush=True)
+    return 0
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -129,6 +178,8 @@ def main(argv=None):
                     help="1: after the timed training steps of a 1-GPU run, also time the InLoc inference configs "
                          "(BASELINE configs 3-5: 1600 px bf16, 3200 px bf16, 3200 px fp8) into config.secondary")
     args = ap.parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _self_launch(args, argv)
 
     from ncnet_amd.config import RuntimeConfig
     from ncnet_amd.engine.trainer import Trainer, make_adam
@@ -137,8 +188,10 @@ def main(argv=None):
                                          init_distributed)
 
     ctx = init_distributed()
-    if ctx.world_size != args.gpus and ctx.is_main:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}", file=sys.stderr)
+    if ctx.world_size != args.gpus:
+        # the record must describe the job that ran: never time one rank of a
+        # job that was asked for N (or N ranks of a job asked for 1)
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}")
     torch.manual_seed(1)
     torch.backends.cudnn.benchmark = True
     dev = ctx.device
@@ -146,7 +199,9 @@ def main(argv=None):
     model.train()
     params = [p for p in model.parameters() if p.requires_grad]
     broadcast_module(model, ctx)
-    opt = make_adam(params, 5e-4)
+    # the reference baseline keeps the reference's optimizer (train.py:71:
+    # torch.optim.Adam); the HIP path uses FlatAdam (engine/optim.py)
+    opt = make_adam(params, 5e-4) if args.impl == "hip" else torch.optim.Adam(params, lr=5e-4)
 
     # a small pool of synthetic batches (random normalised images), generated on device
     gen = torch.Generator(device=dev).manual_seed(1234 + ctx.rank)   # (CPU: gloo smoke runs only)
@@ -246,7 +301,10 @@ def main(argv=None):
                        "per_gpu_batch": args.batch, "seq_len": None, "image_size": s,
                        "parallelism": f"dp{ctx.world_size}", "impl": args.impl,
                        "baseline_pairs_per_s_1gpu": base, "final_loss": float(loss.detach()),
-                       "comm": comm_info(ctx), "optimizer": type(opt).__name__,
+                       "comm": comm_info(ctx),
+                       "launcher": ("self-launched torchrun" if os.environ.get("NCNET_BENCH_SELF_LAUNCHED")
+                                    else "torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else "python"),
+                       "optimizer": type(opt).__name__,
                        "hbm_peak_gb": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
                                        if dev.type == "cuda" else None),
                        "runtime": RuntimeConfig.from_env().as_dict(),
@@ -255,7 +313,8 @@ def main(argv=None):
         print(json.dumps(rec), flush=True)
     from ncnet_amd.parallel.dist import destroy
     destroy(ctx)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

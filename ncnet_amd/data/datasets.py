@@ -109,10 +109,11 @@ def gpu_pair_batch(batch, device, out_h: int, out_w: int):
     res = {k: (v.to(device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()
            if k not in ("pixels", "pixel_meta")}
     dev = torch.device(device)
-    if dev.type == "cuda" and _ext.use_hip(pix.to(dev, non_blocking=True)[:1]):
+    pix_d = pix.to(dev, non_blocking=True) if dev.type == "cuda" else None   # the batch's ONE pixel copy
+    if pix_d is not None and _ext.use_hip(pix_d):
         out = torch.empty((n, 3, out_h, out_w), dtype=torch.float32, device=dev)
-        _ext.ext().resize_norm_u8(pix.to(dev, non_blocking=True), meta.to(dev, non_blocking=True), out,
-                                  list(IMAGENET_MEAN), list(IMAGENET_STD))
+        _ext.ext().resize_norm_u8(pix_d, meta.to(dev, non_blocking=True), out, list(IMAGENET_MEAN),
+                                  list(IMAGENET_STD))
     else:
         ims = []
         for o, h, w in meta.tolist():

@@ -54,6 +54,7 @@ class FlatAdam(torch.optim.Optimizer):
         self._count = torch.zeros(1, dtype=torch.int32, device=dev)
         self._skipped = torch.zeros(1, dtype=torch.int32, device=dev)
         self.grad_scale = 1.0          # set to 1/world by a GradBucket that all-reduces flat_grad in place
+        self.guard = True              # False (Trainer(nan_guard=False)): no non-finite skip
         self.spans = []
         off = 0
         with torch.no_grad():
@@ -87,11 +88,13 @@ class FlatAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self.check_bindings()
         g = self.param_groups[0]
         lr, (b1, b2), eps, wd = float(g["lr"]), g["betas"], float(g["eps"]), float(g["weight_decay"])
         if self._hip:
             ext = _ext.ext()
-            ext.nonfinite_count(self.flat_grad, self._count)
+            if self.guard:
+                ext.nonfinite_count(self.flat_grad, self._count)   # else _count stays 0 (finalize resets it)
             ext.adam_masked(self.flat_param, self.flat_grad, self.exp_avg, self.exp_avg_sq, self._count, self._step,
                             lr, float(b1), float(b2), eps, wd, float(self.grad_scale))
             ext.adam_finalize(self._step, self._count, self._skipped)
@@ -103,8 +106,22 @@ class FlatAdam(torch.optim.Optimizer):
             self._step_torch(lr, float(b1), float(b2), eps, wd)
         return loss
 
+    def check_bindings(self) -> None:
+        """Every parameter must still be a view of ``flat_param``: a later
+        ``module._apply`` (``.to()``, ``.cuda()``, ``.half()``) or an assignment
+        to ``p.data`` rebinds it to new storage, after which this optimizer would
+        update buffers the model no longer reads.  make_adam must be the LAST
+        placement step (train.py / bench.py build the model on its device first)."""
+        base = self.flat_param.data_ptr()
+        esz = self.flat_param.element_size()
+        for i, (p, (off, _)) in enumerate(zip(self.params, self.spans)):
+            if p.data_ptr() != base + off * esz:
+                raise RuntimeError(f"FlatAdam: parameter {i} {tuple(p.shape)} is no longer a view of the flat "
+                                   "buffer (the module was moved or p.data reassigned after make_adam); "
+                                   "create the optimizer after the last .to()/.cuda()/load")
+
     def _step_torch(self, lr, b1, b2, eps, wd):
-        bad = int((~torch.isfinite(self.flat_grad)).sum())
+        bad = int((~torch.isfinite(self.flat_grad)).sum()) if self.guard else 0
         grad = self.flat_grad[: self.n]
         if bad:
             grad.zero_()

@@ -136,8 +136,14 @@ class Trainer:
         self.normalization = normalization
         self.nan_guard = nan_guard
         params = [p for p in model.parameters() if p.requires_grad]
-        self.bucket = GradBucket(params, ctx, optimizer)
+        # with a trainable backbone (--fe_finetune_params) the NC gradients are
+        # all-reduced while autograd is still in the backbone (GradBucket early segment)
+        nc = getattr(model, "NeighConsensus", None)
+        early = [p for p in nc.parameters() if p.requires_grad] if nc is not None else None
+        self.bucket = GradBucket(params, ctx, optimizer, early=early)
         self.flat = getattr(optimizer, "flat_grad", None) is not None
+        if self.flat:
+            optimizer.guard = nan_guard   # nan_guard=False: FlatAdam applies every step unguarded
         self.metrics_path = metrics_path if ctx.is_main else None
         self.global_step = 0
         self.fault_step = fault_step if fault_step is not None else int(os.environ.get("NCNET_FAULT_STEP", "-1"))
@@ -167,13 +173,14 @@ class Trainer:
         if self.fault_step >= 0 and self.global_step == self.fault_step:
             raise RuntimeError(f"injected fault at step {self.global_step} (NCNET_FAULT_STEP)")
         self.opt.zero_grad(set_to_none=True)
+        self.bucket.reset()
         with segment("forward"):
             feats = self.prefetch.take(batch)
             self.prefetch.submit(next_batch)
             loss = weak_loss_from_features(self.model, feats, self.normalization)
         with segment("backward"):
             loss.backward()
-        if self.flat:
+        if self.flat and self.nan_guard:
             # loss-finite indicator rides in the gradient bucket: every rank's
             # FlatAdam then skips the same (globally non-finite) step, with no host sync
             self.opt.mark_loss(loss)
@@ -202,7 +209,16 @@ class Trainer:
     @torch.inference_mode()
     def eval_step(self, batch) -> torch.Tensor:
         if self.prefetch.enabled:               # the batch was moved on the prefetch stream
-            torch.cuda.current_stream(self.prefetch.stream.device).wait_stream(self.prefetch.stream)
+            main = torch.cuda.current_stream(self.prefetch.stream.device)
+            main.wait_stream(self.prefetch.stream)
+            # the batch was allocated on the prefetch stream but is read here on
+            # main: without this, once the caller drops it, the allocator could
+            # hand its blocks to the next to_device on the prefetch stream while
+            # this step's kernels are still queued (train() does the same in
+            # TrunkPrefetcher.take)
+            for v in batch.values():
+                if torch.is_tensor(v) and v.is_cuda:
+                    v.record_stream(main)
         return weak_loss(self.model, batch, self.normalization).detach()
 
     def _log(self, rec: dict):

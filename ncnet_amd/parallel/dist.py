@@ -133,22 +133,73 @@ class GradBucket:
     pack -> all-reduce -> average -> unpack.
     """
 
-    def __init__(self, params, ctx: DistContext, optimizer=None):
+    def __init__(self, params, ctx: DistContext, optimizer=None, early=None):
         self.params = [p for p in params if p.requires_grad]
         self.ctx = ctx
         self.inplace = getattr(optimizer, "flat_grad", None) is not None
         self._work = None
+        self._early = []            # in-flight early segment all-reduces
+        self._early_seg = None      # (lo, hi) flat range reduced early, or None
         if self.inplace:
             self.flat = optimizer.flat_grad
             optimizer.grad_scale = 1.0 / ctx.world_size if ctx.enabled else 1.0
+            if early and ctx.enabled:
+                self._arm_early(optimizer, [p for p in early if p.requires_grad])
             return
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
 
+    def _arm_early(self, optimizer, early):
+        """Overlap: ``early`` parameters (the NeighConsensus weights, whose
+        gradients are final as soon as the NC backward ends) are all-reduced
+        from a post-accumulate hook while autograd continues into the backbone
+        (``--fe_finetune_params``); ``finish`` then reduces the rest.  Their
+        span of the flat buffer must be contiguous and must not hold the
+        loss-indicator slot (FlatAdam lays parameters out in order, the slot last)."""
+        spans = {id(p): sp for p, sp in zip(optimizer.params, optimizer.spans)}
+        if not early or len(early) == len(self.params) or any(id(p) not in spans for p in early):
+            return
+        lo = min(spans[id(p)][0] for p in early)
+        hi = max(spans[id(p)][0] + spans[id(p)][1] for p in early)
+        if hi - lo != sum(p.numel() for p in early):
+            return                                    # not contiguous: plain single bucket
+        self._early_seg = (lo, hi)
+        self._pending = set()
+        ids = {id(p) for p in early}
+
+        def hook(p):
+            if id(p) not in ids or self._early_seg is None:
+                return
+            self._pending.discard(id(p))
+            if not self._pending and not self._early:
+                self._early.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+                self.early_launches += 1
+
+        self._ids = ids
+        self.early_launches = 0
+        for p in early:
+            p.register_post_accumulate_grad_hook(hook)
+        self.reset()
+
+    def reset(self):
+        """Arm the early segment for the next backward (Trainer: before backward)."""
+        if self._early_seg is not None:
+            self._pending = set(self._ids)
+            self._early = []
+
     def start(self):
         """Launch the (async) all-reduce (packing the grads first unless in place)."""
         if not self.ctx.enabled:
+            return
+        if self._early_seg is not None:
+            lo, hi = self._early_seg
+            if not self._early:                       # hooks did not fire (no grads flowed): reduce it now
+                self._early.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+            # the rest: [0, lo) and [hi, end) (the latter holds the loss slot)
+            rest = [self.flat[:lo]] if lo > 0 else []
+            rest.append(self.flat[hi:])
+            self._work = [dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True) for t in rest]
             return
         if not self.inplace:
             off = 0
@@ -165,8 +216,10 @@ class GradBucket:
         """Wait (and, for a private bucket, scatter the averaged gradients back)."""
         if not self.ctx.enabled or self._work is None:
             return
-        self._work.wait()
+        for w in (self._work if isinstance(self._work, list) else [self._work]) + self._early:
+            w.wait()
         self._work = None
+        self._early = []
         if self.inplace:
             return
         self.flat.div_(self.ctx.world_size)

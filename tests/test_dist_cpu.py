@@ -95,6 +95,42 @@ def test_bench_torchrun_two_ranks_cpu(tmp_path):
     assert rec["value"] > 0 and rec["steps"] == 1 and rec["warmup"] == 1
 
 
+def test_bench_self_launch_two_ranks_cpu(tmp_path):
+    """Plain ``python bench.py --gpus 2`` (no launcher env): bench.py starts
+    torch.distributed.run itself as a child process and relays rank 0's record;
+    the record must say 2 ranks with a real process group."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID")}
+    env.update(OMP_NUM_THREADS="2", NCNET_FORCE_TORCH="1")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1", "--batch",
+           "2", "--image-size", "64"]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["comm"]["process_group"] is True and rec["config"]["comm"]["world_size"] == 2
+    assert rec["config"]["launcher"] == "self-launched torchrun"
+
+
+def test_bench_world_mismatch_fails(tmp_path):
+    """--gpus 1 inside a 2-rank launch must fail instead of timing a wrong job."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2", NCNET_FORCE_TORCH="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29735", os.path.join(root, "bench.py"), "--gpus", "1", "--steps", "1",
+           "--warmup", "0", "--batch", "1", "--image-size", "64"]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode != 0
+    assert "WORLD_SIZE=2" in out.stderr
+
+
 def test_train_torchrun_two_ranks_cpu(tmp_path):
     """train.py under torchrun with two gloo ranks: the Trainer's one-batch
     lookahead loop (TrunkPrefetcher hand-off), sharded sampler, gradient
@@ -198,3 +234,43 @@ def test_rank_failure_detected_by_pg_timeout(tmp_path):
     elapsed, err = (tmp_path / "hang.txt").read_text().split("\n", 1)
     assert err, "the all-reduce with a silent peer did not raise"
     assert float(elapsed) < 60
+
+
+def _overlap_worker(rank, world, port, out_dir, early):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from ncnet_amd.engine.trainer import Trainer, make_adam
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.parallel.dist import broadcast_module, destroy, init_distributed
+    ctx = init_distributed(device="cpu")
+    torch.manual_seed(7)
+    m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], use_cuda=False)
+    for p in m.FeatureExtraction.model[-1][-1].parameters():      # --fe_finetune_params 1
+        p.requires_grad = True
+    params = [p for p in m.parameters() if p.requires_grad]
+    broadcast_module(m, ctx)
+    tr = Trainer(m, make_adam(params, 5e-4), ctx)
+    if not early:
+        tr.bucket._early_seg = None                                 # the serial single-bucket path
+    for step in range(2):
+        tr.train_step(_batch(10 * step + rank))
+    launches = getattr(tr.bucket, "early_launches", 0) if early else 0
+    torch.save({"params": [p.detach().clone() for p in params], "early_launches": launches},
+               os.path.join(out_dir, f"{'e' if early else 's'}{rank}.pt"))
+    destroy(ctx)
+
+
+def test_early_nc_allreduce_matches_serial(tmp_path):
+    """GradBucket early segment (NC gradients all-reduced from a post-accumulate
+    hook while autograd continues into the trainable backbone) gives the same
+    parameters, bit for bit, as one bucket all-reduced after backward."""
+    world = 2
+    for early in (True, False):
+        mp.spawn(_overlap_worker, args=(world, _free_port(), str(tmp_path), early), nprocs=world, join=True)
+    for r in range(world):
+        e = torch.load(str(tmp_path / f"e{r}.pt"), weights_only=True)
+        s = torch.load(str(tmp_path / f"s{r}.pt"), weights_only=True)
+        assert e["early_launches"] == 2                            # one per step, from the hook
+        for a, b in zip(e["params"], s["params"]):
+            assert torch.equal(a, b)

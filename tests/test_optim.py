@@ -184,3 +184,30 @@ def test_bucket_inplace_world1_without_pg_is_noop():
     b = GradBucket(ps, DistContext(), opt)
     assert b.inplace and opt.grad_scale == 1.0
     b.allreduce()
+
+
+def test_rebound_parameter_raises():
+    """A module moved after make_adam detaches its parameters from the flat
+    buffers; step() must say so instead of updating storage nobody reads."""
+    m = torch.nn.Linear(4, 3)
+    opt = FlatAdam(list(m.parameters()), lr=1e-3)
+    opt.zero_grad()
+    m(torch.randn(2, 4)).sum().backward()
+    opt.step()                                   # bound: fine
+    m.double()                                   # module._apply: new storage
+    with pytest.raises(RuntimeError, match="no longer a view"):
+        opt.step()
+
+
+def test_guard_off_applies_nonfinite_step():
+    """Trainer(nan_guard=False) -> FlatAdam.guard False: no skip."""
+    p = _params()
+    opt = FlatAdam(p, lr=1e-3)
+    opt.guard = False
+    opt.zero_grad()
+    for q in p:
+        q.grad.fill_(1.0)
+    p[0].grad.view(-1)[0] = float("nan")
+    opt.step()
+    assert opt.skipped_steps == 0 and opt.steps_taken == 1
+    assert torch.isnan(p[0].detach().view(-1)[0])

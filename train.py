@@ -26,8 +26,12 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
+# RCCL under torchrun: the ROCm driver only supports dmabuf IPC; must be set
+# before any HIP initialisation (bench.py does the same).
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 from torch.utils.data import DataLoader, Subset
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
