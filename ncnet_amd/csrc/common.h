@@ -63,6 +63,24 @@ __device__ __forceinline__ f32x4 mfma16u(const u32x4& a, const u32x4& b, const f
                                                  0);
 }
 
+// LDS-DMA of 16 B per lane (global_load_lds_dwordx4) issued from inline asm.
+// The compiler's waitcnt pass cannot prove that an LDS-DMA misses a later
+// ds_read_b64_tr_b16 (intrinsic reads carry no alias info), so with the builtin
+// it drains EVERY in-flight DMA (s_waitcnt vmcnt(0)) before the first
+// transposed read -- the next step's prefetch is serialised with the compute.
+// Issued from asm the DMA is invisible to that pass; the kernel then owns the
+// wait: `s_waitcnt vmcnt(..)` + s_barrier (asm_barrier_vm below) before reading
+// what landed.  (Extra in-flight asm ops only make the compiler's own vmcnt
+// waits stricter, never weaker: completion is in issue order.)  M0 is set here;
+// kernels using this issue no other M0-based instruction.
+__device__ __forceinline__ void dma16_lds(const void* gsrc, const void* lds_dst) {
+  const uint32_t l = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst;
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(l) : "memory", "m0");
+}
+// Workgroup barrier that first waits for ALL of this wave's vector-memory ops
+// (incl. asm LDS-DMAs) and LDS ops.
+__device__ __forceinline__ void asm_barrier_vm0() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ bf16x8 lds_read16(const char* lds_base, uint32_t byte_off) {
   return *(const bf16x8*)(lds_base + byte_off);
 }

@@ -491,6 +491,239 @@ __global__ __launch_bounds__(512, 1) void conv16v3_fwd_kernel(const bf16* __rest
 }
 
 // ===========================================================================
+// conv16v4_fwd: conv16v3 at a compile-time (TK, TL) tile (the 25 x 25 (k, l)
+// planes of the training volume), rebuilt for latency hiding.  conv16v3's
+// compiled body issued each fragment's ds_read right before its 3-5 MFMAs and
+// waited lgkmcnt(0) in between (no read in flight while the matrix pipe ran),
+// and drained every in-flight plane DMA at each step's barrier, so the short
+// ramp steps of each di (1-2 dj slices) exposed a full plane load.  Here:
+//  * fragments are software-pipelined in registers: the weight / X fragments of
+//    K-step q + 1 are read while the MFMAs of q run (explicit double buffer);
+//  * X fragment addresses are per-lane bases plus compile-time offsets (RS is
+//    a constant): no address VALU in the loop; the two lane halves (taps 2q,
+//    2q + 1) differ by one voxel or by one row wrap, two base sets cover both;
+//  * three plane buffers, DMA two planes ahead, and a counted
+//    `s_waitcnt vmcnt(N)` before each step's barrier waits for the plane (and
+//    weights) that step reads but leaves the next plane's DMA in flight.  Every
+//    wave issues a FIXED number of DMA instructions per plane and per weight
+//    slot (rows / slots it does not own go to a trash KiB of LDS) so N is a
+//    compile-time count; buffer-resource DMAs return zeros out of range, so the
+//    halo is written by the DMA (no zero fill, no exec masks).
+// LDS (KS = 5, 25 x 25): 65 KB weights + 3 x 30.6 KB planes + 1 KB = 156 KB.
+// ===========================================================================
+// does step s of a di issue a weight slot (slot s - R of di + 1, or slot KS - 1 of di at s = 0)?
+__host__ __device__ constexpr bool v4_wstep(int s, int R) { return s == 0 || s >= R; }
+
+template <int KS, int R, int EPI, int TK, int TL>
+__global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
+                                                              const float* __restrict__ bias,
+                                                              const bf16* __restrict__ M, bf16* __restrict__ Y,
+                                                              ConvGeom g) {
+#if defined(__HIP_DEVICE_COMPILE__)   // device-only body (buffer-resource builtins): the host pass keeps the stub
+  constexpr int P = KS / 2;
+  constexpr int NT = KS * KS;
+  constexpr int NQ = (NT + 1) / 2;
+  constexpr int NW = 8;
+  constexpr int NVOX = TK * TL;
+  constexpr int NTILE = (NVOX + 15) / 16;
+  constexpr int MAXT = (NTILE + NW - 1) / NW;
+  constexpr int S = R + KS - 1;              // input j-planes per di
+  constexpr int RS = TL + 8;                 // row stride (voxels): a wrapping tile jumps one 256-B bank period
+  constexpr int PR = TK + KS - 1;            // staged rows
+  constexpr int PLANE = PR * RS * 32;
+  // LDS: weights first (so every fragment read is a base VGPR + a 16-bit
+  // immediate: bases at 0 and 32 KiB), then the three plane buffers, then trash
+  constexpr int WBYTES = KS * NQ * 1024;
+  constexpr int XOFF = WBYTES;
+  constexpr int TRASH = XOFF + 3 * PLANE;
+  constexpr int RPW = (PR + NW - 1) / NW;    // row DMAs per wave per plane (fixed)
+  constexpr int WPW = (NQ + NW - 1) / NW;    // weight DMAs per wave per slot (fixed)
+  static_assert(TL + KS - 1 <= 32, "one LDS-DMA wave-instruction per staged row");
+  static_assert(TRASH + 1024 <= 160 * 1024, "LDS");
+  static_assert(S >= 2, "prologue emulates two steps");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int lt = bid % g.nlt; bid /= g.nlt;
+  const int kt = bid % g.nkt; bid /= g.nkt;
+  const int jb = bid % g.njb; bid /= g.njb;
+  const int ti = bid % g.I, tv = bid / g.I;
+  const int k0 = kt * TK, l0 = lt * TL, j0 = jb * R;
+  const int di_lo = max(0, P - ti), di_hi = min(KS, g.I + P - ti);
+  const int ntot = (di_hi - di_lo) * S;
+
+  // per-lane X addresses of the current plane buffer (advanced by one buffer per
+  // step): c1 = half 1 on the next voxel (taps 2q, 2q + 1 in one row; also the
+  // padded last pair, whose half-1 weights are zero: it reads voxel ll + 5 of
+  // the same DMA-written row), c2 = half 1 one row down with dl wrapped
+  // (2q + 1 a multiple of KS)
+  uint32_t c1[MAXT], c2[MAXT];
+  {
+    const uint32_t hh = (uint32_t)(lane >> 5);
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      int vi = (wave + NW * tt) * 16 + (lane & 15);
+      if (vi >= NVOX) vi = 0;
+      const int kk = vi / TL, ll = vi - kk * TL;
+      const uint32_t b0 = (uint32_t)(XOFF + (kk * RS + ll) * 32 + ((lane >> 4) & 1) * 16);
+      c1[tt] = b0 + hh * 32u;
+      c2[tt] = b0 + hh * (uint32_t)((RS - KS + 1) * 32);
+    }
+  }
+  f32x4 acc[R][MAXT];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Plane DMA through a buffer resource over ONE (i, j) plane: every lane of a
+  // row instruction writes its 16-B chunk (row voxel lane / 2 = l0 - P + lane / 2),
+  // and a chunk outside the volume (halo column, halo row, or an invalid plane:
+  // num_records 0) reads out of range and lands as ZERO -- the halo is rewritten
+  // with zeros by the DMA itself, no zero fill, no per-lane exec masks.  Rows
+  // r >= PR of the fixed RPW per wave go to a trash KiB.
+  constexpr uint32_t OOB = 0x7ffffff0u;
+  uint32_t xvo[RPW];
+  uint32_t xld[RPW];
+#pragma unroll
+  for (int m = 0; m < RPW; ++m) {
+    const int r = wave + NW * m;
+    const int kg = k0 - P + r, lg = l0 - P + (lane >> 1);
+    const bool ok = r < PR && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L && (lane >> 1) < TL + KS - 1;
+    xvo[m] = ok ? (uint32_t)(((kg * g.L + lg) * 16 + (lane & 1) * 8) * 2) : OOB;
+    xld[m] = r < PR ? (uint32_t)(XOFF + r * RS * 32) : (uint32_t)TRASH;
+  }
+  const size_t plane_elems = (size_t)g.K * g.L * 16;
+  auto issue_x = [&](int n) {
+    const int dq = n / S, s = n - dq * S;
+    const int jp = j0 - P + s;
+    const bool pv = n < ntot && jp >= 0 && jp < g.J;
+    const bf16* xp = pv ? X + plane_offset(g, tv, ti + di_lo + dq - P, jp, 16) : X;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)xp, (short)0, pv ? (int)(plane_elems * 2) : 0, 0x00020000);
+    const uint32_t boff = (uint32_t)((n % 3) * PLANE);
+#pragma unroll
+    for (int m = 0; m < RPW; ++m) {
+      const uint32_t d = xld[m] == (uint32_t)TRASH ? (uint32_t)TRASH : xld[m] + boff;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + d), 16, xvo[m], 0, 0, 0);
+    }
+  };
+  // weight slot dj <- (di, dj) fragments; WPW DMAs per wave, always (invalid -> trash)
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, KS * KS * NQ * 1024, 0x00020000);
+  auto issue_w = [&](int di, int dj, bool valid) {
+#pragma unroll
+    for (int m = 0; m < WPW; ++m) {
+      const int q = wave + NW * m;
+      const bool v = valid && q < NQ;
+      const uint32_t d = v ? (uint32_t)((dj * NQ + q) * 1024) : (uint32_t)TRASH;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(void, smem + d), 16, (uint32_t)((q * 64 + lane) * 16),
+                                               (uint32_t)((di * KS + dj) * NQ * 1024), 0, 0);
+    }
+  };
+
+  for (int dj = 0; dj < KS; ++dj) issue_w(di_lo, dj, true);
+  issue_x(0);
+  issue_w(0, 0, false);   // step "-1" emulation: its weight slot (if any), then plane 1
+  issue_x(1);
+  static_assert(S - 1 >= R, "the emulated step issues a weight slot");
+
+  const uint32_t wb = (uint32_t)lane * 16u;
+  int n = 0;
+  for (int di = di_lo; di < di_hi; ++di) {
+    static_for<0, S>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      // DMAs younger than plane n: the previous step's weight slot (if any) and plane n + 1
+      constexpr int YOUNGER = RPW + (v4_wstep(s == 0 ? S - 1 : s - 1, R) ? WPW : 0);
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(YOUNGER) : "memory");
+      if constexpr (v4_wstep(s, R)) {
+        if constexpr (s >= R) issue_w(di + 1 < di_hi ? di + 1 : di, s - R, di + 1 < di_hi);
+        else issue_w(di, KS - 1, di > di_lo);
+      }
+      issue_x(n + 2);
+      const int jp = j0 - P + s;
+      if (jp >= 0 && jp < g.J) {
+        constexpr int dlo = (s - R + 1) > 0 ? (s - R + 1) : 0;
+        constexpr int dhi = s < KS - 1 ? s : KS - 1;  // inclusive
+        // (q, tt) MFMA groups in order k = q * MAXT + tt; the weight fragments
+        // of K-step q + 1 are read at group (q, 0) (double buffer), the X
+        // fragment of group k + 2 at group k (three registers in rotation);
+        // sched_group_barrier pins that order (the default scheduler sinks each
+        // read to just before its MFMAs and waits lgkmcnt(0) there)
+        constexpr int NDJ = dhi - dlo + 1;
+        constexpr int NK = NQ * MAXT;
+        bf16x8 A[2][KS], Xr[3];
+        auto load_a = [&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          static_for<dlo, dhi + 1>([&](auto dc) {
+            constexpr int dj = decltype(dc)::value;
+            constexpr int o = (dj * NQ + q) * 1024;
+            if constexpr (o < 32768) A[q & 1][dj] = *(const bf16x8*)(smem + wb + o);
+            else A[q & 1][dj] = *(const bf16x8*)(smem + (wb + 32768u) + (o - 32768));
+          });
+        };
+        auto load_x = [&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          constexpr int q = k / MAXT, tt = k % MAXT;
+          constexpr int t0 = 2 * q;
+          constexpr uint32_t T0 = (uint32_t)(((t0 / KS) * RS + t0 % KS) * 32);
+          const uint32_t base = ((2 * q + 1) % KS == 0 && 2 * q + 1 < NT) ? c2[tt] : c1[tt];
+          Xr[k % 3] = *(const bf16x8*)(smem + base + T0);
+        };
+        load_a(std::integral_constant<int, 0>{});
+        load_x(std::integral_constant<int, 0>{});
+        load_x(std::integral_constant<int, 1>{});
+        __builtin_amdgcn_sched_group_barrier(0x100, NDJ + 2, 0);
+        static_for<0, NK>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          constexpr int q = k / MAXT, tt = k % MAXT;
+          constexpr bool LA = tt == 0 && q + 1 < NQ;
+          constexpr bool LX = k + 2 < NK;
+          if constexpr (LA) load_a(std::integral_constant<int, q + 1>{});
+          if constexpr (LX) load_x(std::integral_constant<int, k + 2>{});
+          static_for<dlo, dhi + 1>([&](auto dc) {
+            constexpr int dj = decltype(dc)::value;
+            acc[s - dj][tt] = mfma16(A[q & 1][dj], Xr[k % 3], acc[s - dj][tt]);
+          });
+          if constexpr (LA || LX) __builtin_amdgcn_sched_group_barrier(0x100, (LA ? NDJ : 0) + (LX ? 1 : 0), 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NDJ, 0);
+        });
+      }
+      // advance the X addresses to the next step's buffer ((n + 1) % 3)
+      {
+        const uint32_t adv = (n % 3 == 2) ? (uint32_t)(-2 * PLANE) : (uint32_t)PLANE;
+#pragma unroll
+        for (int tt = 0; tt < MAXT; ++tt) { c1[tt] += adv; c2[tt] += adv; }
+      }
+      ++n;
+    });
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
+
+  const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = j0 + r;
+    if (j >= g.J) break;
+    const size_t vbase_out = plane_offset(g, tv, ti, j, 1);
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      const int tile = wave + NW * tt;
+      if (tile < NTILE) {
+        const int vi = tile * 16 + (lane & 15);
+        const int kk = vi / TL, ll = vi - kk * TL;
+        const int kg = k0 + kk, lg = l0 + ll;
+        if (vi < NVOX && kg < g.K && lg < g.L)
+          store16<EPI>(acc[r][tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco,
+                       g.nt);
+      }
+    }
+  }
+#endif
+}
+
+// ===========================================================================
 // conv16f8_fwd: inference Conv4d 16 -> 16 on OCP fp8 e4m3 operands
 // (v_mfma_f32_16x16x32_fp8_fp8, BASELINE config 5).  Same structure as
 // conv16v2 (8 waves, LDS-DMA, double-buffered planes, single weight buffer with
@@ -665,6 +898,11 @@ static void pick_tile(int K, int L, int& tk, int& tl) {
   while (tk * tl > 640) { if (tl > tk) --tl; else --tk; }
 }
 
+static bool getenv_flag(const char* k) {
+  const char* e = getenv(k);
+  return e && atoi(e) != 0;
+}
+
 // output j-tiles per workgroup of the group-plane conv (read per launch: tests / kbench switch it)
 static int gp_tpw() {
   const char* e = getenv("NCNET_GP_TPW");
@@ -702,8 +940,16 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
     // full (di, dj) sum: R = 5 output j-planes per workgroup, X reused across dj
     constexpr int R = 5;
     g.njb = cdiv(J, R);
-    size_t lds3 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)KS * nq * 1024;
     dim3 grid3((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block3(512);
+    if (tk == 25 && tl == 25 && KS == 5 && !getenv_flag("NCNET_CONV_V3")) {
+      // compile-time 25 x 25 tile: pipelined fragments, triple-buffered planes
+      size_t lds4 = 3 * (size_t)(25 + 4) * 33 * 32 + (size_t)5 * nq * 1024 + 1024;
+#define L16V4(EPIV) hipLaunchKernelGGL((conv16v4_fwd_kernel<5, R, EPIV, 25, 25>), grid3, block3, lds4, stream, x, w, bias, m, y, g)
+      if (epi == EPI_BIAS_RELU) L16V4(EPI_BIAS_RELU); else L16V4(EPI_MASK);
+#undef L16V4
+      return (int)hipGetLastError();
+    }
+    size_t lds3 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)KS * nq * 1024;
 #define L16V3(KSV, EPIV) hipLaunchKernelGGL((conv16v3_fwd_kernel<KSV, R, EPIV>), grid3, block3, lds3, stream, x, w, bias, m, y, g)
     if (KS == 5) { if (epi == EPI_BIAS_RELU) L16V3(5, EPI_BIAS_RELU); else L16V3(5, EPI_MASK); }
     else { if (epi == EPI_BIAS_RELU) L16V3(3, EPI_BIAS_RELU); else L16V3(3, EPI_MASK); }

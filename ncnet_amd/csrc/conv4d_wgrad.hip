@@ -334,8 +334,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
       const bool in_k = kg >= 0 && kg < g.K;
       if (in_k && lane < 2 * g.L && NCNET_OK((size_t)(xp - X) + (size_t)kg * g.L * 16 + lane * 8 + 8 <= ext) &&
           NCNET_OK(row * g.RS * 32 + P * 32 + lane * 16 + 16 <= g.PR * g.RS * 32))
-        __builtin_amdgcn_global_load_lds((const void*)(xp + (size_t)kg * g.L * 16 + lane * 8),
-                                         LDS_PTR(void, buf + row * g.RS * 32 + P * 32), 16, 0, 0);
+        dma16_lds(xp + (size_t)kg * g.L * 16 + lane * 8, buf + row * g.RS * 32 + P * 32);
       if (lane < 2 * g.RW && (!in_k || lane < 2 * P || lane >= 2 * P + 2 * g.L))
         *(u32x4*)(buf + row * g.RS * 32 + lane * 16) = u32x4{0u, 0u, 0u, 0u};
     }
@@ -347,7 +346,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
     for (int q = wave; q * 64 < 2 * g.VT; q += NW) {
       const int ci = q * 64 + lane;
       if (ci < 2 * r.nv && NCNET_OK((size_t)(gp - G) + ci * 8 + 8 <= ext))
-        __builtin_amdgcn_global_load_lds((const void*)(gp + ci * 8), LDS_PTR(void, buf + q * 1024), 16, 0, 0);
+        dma16_lds(gp + ci * 8, buf + q * 1024);
       else
         *(u32x4*)(buf + ci * 16) = u32x4{0u, 0u, 0u, 0u};
     }
@@ -394,7 +393,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
   for (; col < c_hi; col = next_col(col), base += g.I) {
     set_tile(decode_col(g, col));
     for (int ii = 0; ii < g.I; ++ii, ++step) {
-      __syncthreads();   // X[step] and the G tiles of this step landed; previous step's reads done
+      asm_barrier_vm0();   // X[step] and the G tiles of this step landed; previous step's reads done
       load_x_next();
       load_g_upto(base + max(0, ii - P) + NS - 1);
       const char* xc = xbuf + (step & 1) * xbytes;
@@ -554,8 +553,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16p_kernel(const bf16* __restrict
     const size_t po = (size_t)it * g.K * g.L * 16;
     for (int row = wave; row < g.K; row += NW) {
       if (lane < 2 * g.L && NCNET_OK(po + ((size_t)row * g.L) * 16 + lane * 8 + 8 <= ext))
-        __builtin_amdgcn_global_load_lds((const void*)(Xs + po + (size_t)row * g.L * 16 + lane * 8),
-                                         LDS_PTR(void, buf + ((row + P) * g.RS + P) * 32), 16, 0, 0);
+        dma16_lds(Xs + po + (size_t)row * g.L * 16 + lane * 8, buf + ((row + P) * g.RS + P) * 32);
     }
 #pragma unroll
     for (int n = 0; n < NGG; ++n) {
@@ -564,7 +562,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16p_kernel(const bf16* __restrict
       for (int q = wave; q * 64 < 2 * nvox; q += NW) {
         const int ci = q * 64 + lane;
         if (ci < 2 * nvox && NCNET_OK(po + ci * 8 + 8 <= ext))
-          __builtin_amdgcn_global_load_lds((const void*)(gp + ci * 8), LDS_PTR(void, gb + q * 1024), 16, 0, 0);
+          dma16_lds(gp + ci * 8, gb + q * 1024);
       }
     }
   };
@@ -573,7 +571,7 @@ __global__ __launch_bounds__(512, 1) void wgrad16p_kernel(const bf16* __restrict
   if (it_lo < it_hi) stage(it_lo, smem);
   for (int it = it_lo; it < it_hi; ++it) {
     const int n0 = it - it_lo;
-    __syncthreads();  // vmcnt(0) + barrier: item it landed; item it-1's reads of the other buffer done
+    asm_barrier_vm0();  // item it landed; item it-1's reads of the other buffer done
     if (it + 1 < it_hi) stage(it + 1, smem + ((n0 + 1) & 1) * bufbytes);
     const char* plane = smem + (n0 & 1) * bufbytes;
     const char* gt = plane + xbytes;

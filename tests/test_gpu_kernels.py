@@ -55,6 +55,31 @@ def test_conv16_fwd(ks, shape):
     assert relerr(y.permute(0, 5, 1, 2, 3, 4), yr) < 1e-2
 
 
+@pytest.mark.parametrize("epi", [1, 2])
+@pytest.mark.parametrize("shape", [(2, 25, 25, 25, 25), (1, 6, 7, 26, 29), (1, 4, 6, 50, 37), (1, 3, 11, 25, 25)])
+def test_conv16v4_matches_v3_bitwise(epi, shape, monkeypatch):
+    """conv16v4 (compile-time 25 x 25 tile: pipelined fragments, triple-buffered
+    planes with counted vmcnt, buffer-resource DMA that writes the halo zeros)
+    accumulates every output in conv16v3's order: bit-identical outputs for the
+    forward (bias + ReLU) and data-gradient (ReLU-mask) epilogues, including
+    partial (k, l) tiles and j-blocks, and against the fp64 oracle."""
+    from ncnet_amd.ops.packing import pack_w16
+    torch.manual_seed(1)
+    V, I, J, K, L = shape
+    x = torch.rand(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
+    m = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
+    w = pack_w16(torch.randn(16, 16, 5, 5, 5, 5, device=DEV) * 0.05)
+    b = torch.randn(16, device=DEV) * 0.1
+    outs = []
+    for v3 in ("0", "1"):
+        monkeypatch.setenv("NCNET_CONV_V3", v3)
+        y = torch.full_like(x, float("nan"))
+        _ext.ext().conv16_fwd(x, w, b if epi == 1 else None, m if epi == 2 else None, y, 5, epi)
+        outs.append(y)
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("ks,shape,cin,relu", [(5, (4, 25, 25, 25, 25), 16, 1), (5, (1, 6, 5, 26, 29), 16, 0),
                                                (3, (2, 7, 9, 11, 13), 10, 1), (3, (1, 3, 2, 30, 27), 16, 1),
                                                (7, (1, 9, 8, 25, 25), 16, 1), (1, (2, 5, 6, 25, 25), 16, 0),
