@@ -482,6 +482,305 @@ __global__ __launch_bounds__(512, 1) void wgrad16v3_kernel(const bf16* __restric
 
 
 // ===========================================================================
+// wgrad16v4: wgrad16v3's decomposition (workgroup = one dj, all di, columns
+// walked along ii, G tiles in a ring) at a compile-time (K, L) plane, rebuilt
+// like conv16v4 for latency hiding:
+//  * one X plane and one G tile per step, both DMA'd TWO steps ahead (3 X
+//    buffers, G ring of 2P + 3 slots + a zero slot), every wave issuing a fixed
+//    number of asm buffer-load->LDS DMAs per step (unowned rows / KiBs go to a
+//    trash KiB) so each step's barrier waits with a compile-time vmcnt for
+//    exactly the data it reads;
+//  * buffer resources return zeros out of range: the X halo rows / columns and
+//    the G voxels past the tile are written as zeros by the DMA itself (no
+//    per-step ds_write zero fill);
+//  * the tap group (wave & 3) is a template parameter of the whole loop, so
+//    every X-fragment tap offset is a compile-time immediate of the transposed
+//    read (no address VALU), and the X / G fragments of the next MFMA group are
+//    in flight while the current one runs (sched_group_barrier).
+// Same part / partb layout and grid as wgrad16v3.
+// ===========================================================================
+template <int KS, int K, int L>
+struct W4C {
+  static constexpr int P = KS / 2, NT = KS * KS, NW = 8;
+  static constexpr int TPG = (NT - 1) / 4, EXP = (KS + 2) / 3;
+  static constexpr int KL = K * L;
+  static constexpr int NTL = (KL + 319) / 320;
+  static constexpr int VT = (((KL + NTL - 1) / NTL) + 63) / 64 * 64;
+  static constexpr int NCH = VT / 64;                    // 32-voxel chunks per half
+  static constexpr int RS = L + 8, RW = L + KS - 1;
+  static constexpr int PR = (VT - 1) / L + 2 + KS - 1;   // staged X rows
+  static constexpr int XB = PR * RS * 32, GB = VT * 32;
+  static constexpr int NS = 2 * P + 3;                   // G ring slots (2 steps ahead)
+  static constexpr int GOFF = 0, ZOFF = NS * GB, XOFF = ZOFF + GB, TRASH = XOFF + 3 * XB;
+  static constexpr int LDS = TRASH + 1024;
+  static constexpr int RPW = (PR + NW - 1) / NW;         // X row DMAs per wave per step
+  static constexpr int GQ = GB / 1024;                   // 1-KiB G chunks per tile
+  static constexpr int GPW = (GQ + NW - 1) / NW;         // G DMAs per wave per step
+  static_assert((NT - 1) % 4 == 0, "NT must be 1 mod 4");
+  static_assert(RW <= 32, "one DMA wave-instruction per staged row");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+// 16-B-per-lane buffer load into LDS from asm (see dma16_lds in common.h):
+// out-of-range offsets land as zeros.
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4v make_rsrc(const void* base, uint32_t nbytes) {
+  const uint64_t b = (uint64_t)base;
+  i32x4v r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(b >> 32) & 0xffffu));
+  r[2] = __builtin_amdgcn_readfirstlane((int)nbytes);
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void bdma16_lds(const i32x4v& rs, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds)
+               : "memory", "m0");
+}
+
+template <int KS, int K, int L, int TG>
+__device__ __forceinline__ void wgrad16v4_body(const bf16* __restrict__ X, const bf16* __restrict__ G,
+                                               float* __restrict__ part, float* __restrict__ partb, const W3Geom& g,
+                                               int wave, int half, int dj, int grp) {
+  using C = W4C<KS, K, L>;
+  constexpr int P = C::P, NT = C::NT, TPG = C::TPG, EXP = C::EXP, NCH = C::NCH, NS = C::NS, NW = C::NW;
+  constexpr int RS = C::RS, PR = C::PR, XB = C::XB, GB = C::GB;
+  constexpr int RPW = C::RPW, GPW = C::GPW, GQ = C::GQ;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+  const int lane = threadIdx.x & 63;
+  const bool center_blk = dj == P;
+  constexpr int XLO = TG == 0 ? KS : (TG - 1) * EXP;              // di range of the last tap (NT - 1)
+  constexpr int XHI = TG == 0 ? KS : (TG * EXP < KS ? TG * EXP : KS);
+
+  f32x4 acc[TPG][KS];
+  f32x4 accx[EXP];
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < TPG; ++m)
+#pragma unroll
+    for (int d = 0; d < KS; ++d) acc[m][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < EXP; ++e) accx[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const u32x4 ones = {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};   // bf16 1.0 x 8
+
+  const int c_lo = grp * g.cpg, c_hi = min(g.ncols, c_lo + g.cpg);
+  auto col_ok = [&](int c) { const int gj = (c / C::NTL) % g.J - dj + P; return gj >= 0 && gj < g.J; };
+  auto next_col = [&](int c) { ++c; while (c < c_hi && !col_ok(c)) ++c; return c; };
+  int c0 = c_lo;
+  while (c0 < c_hi && !col_ok(c0)) ++c0;
+  int nsteps = 0;                                     // valid columns x I
+  for (int c = c0; c < c_hi; c = next_col(c)) nsteps += g.I;
+
+  // ---- loaders ------------------------------------------------------------
+  const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  // X: rows kf - P .. kf - P + PR - 1 of plane (v, ii, jj), col 0 <-> l = -P
+  uint32_t xvo[RPW];
+  auto set_xvo = [&](int kf) {
+#pragma unroll
+    for (int m = 0; m < RPW; ++m) {
+      const int r = wave + NW * m, kg = kf - P + r, l = (lane >> 1) - P;
+      const bool ok = r < PR && kg >= 0 && kg < K && l >= 0 && l < L && (lane >> 1) < C::RW;
+      xvo[m] = ok ? (uint32_t)(((kg * L + l) * 16 + (lane & 1) * 8) * 2) : 0x7ffffff0u;
+    }
+  };
+  // loader cursors keep their column decoded (a plane pointer at ii = 0 and the
+  // plane stride): the runtime divisions run once per column, not per step
+  const size_t pstride = (size_t)g.J * K * L * 16;       // elements between planes ii and ii + 1
+  auto col_base = [&](int c, int jshift, int a) {
+    const int v = (c / C::NTL) / g.J, jj = (c / C::NTL) % g.J;
+    return (((size_t)v * g.I) * g.J + (jj + jshift)) * (size_t)K * L * 16 + (size_t)a * 16;
+  };
+  int xl_c = c0, xl_ii = 0, xl_n = 0;
+  size_t xl_base = c0 < c_hi ? col_base(c0, 0, 0) : 0;
+  set_xvo(((c0 % C::NTL) * C::VT) / L);
+  auto issue_x = [&]() {
+    const bool live = xl_n < nsteps;
+    const bf16* xp = live ? X + xl_base + (size_t)xl_ii * pstride : X;
+    const i32x4v rs = make_rsrc(xp, live ? (uint32_t)(K * L * 32) : 0u);
+    const uint32_t xb = lds0 + C::XOFF + (uint32_t)((xl_n % 3) * XB);
+#pragma unroll
+    for (int m = 0; m < RPW; ++m) {
+      const int r = wave + NW * m;
+      bdma16_lds(rs, xvo[m], r < PR ? xb + (uint32_t)(r * RS * 32) : lds0 + C::TRASH);
+    }
+    ++xl_n;
+    if (++xl_ii == g.I) {
+      xl_ii = 0;
+      xl_c = next_col(xl_c);
+      if (xl_c < c_hi) {
+        set_xvo(((xl_c % C::NTL) * C::VT) / L);
+        xl_base = col_base(xl_c, 0, 0);
+      }
+    }
+  };
+  // G: the tile's voxels a .. a + nv - 1 of plane (v, gi, jj - dj + P); ring slot = seq % NS
+  int gl_c = c0, gl_gi = 0, gl_m = 0;
+  int gl_nvb = 0;                                        // the tile's bytes (nv * 32)
+  size_t gl_base = 0;
+  auto set_gcol = [&](int c) {
+    const int a = (c % C::NTL) * C::VT;
+    gl_nvb = min(C::VT, K * L - a) * 32;
+    gl_base = col_base(c, P - dj, a);
+  };
+  if (c0 < c_hi) set_gcol(c0);
+  auto issue_g = [&]() {
+    const bool live = gl_m < nsteps;
+    const bf16* gp = live ? G + gl_base + (size_t)gl_gi * pstride : G;
+    const i32x4v rs = make_rsrc(gp, live ? (uint32_t)gl_nvb : 0u);
+    const uint32_t gb = lds0 + C::GOFF + (uint32_t)((gl_m % NS) * GB);
+#pragma unroll
+    for (int m = 0; m < GPW; ++m) {
+      const int q = wave + NW * m;
+      bdma16_lds(rs, (uint32_t)((q * 64 + lane) * 16), q < GQ ? gb + (uint32_t)(q * 1024) : lds0 + C::TRASH);
+    }
+    ++gl_m;
+    if (++gl_gi == g.I) {
+      gl_gi = 0;
+      gl_c = next_col(gl_c);
+      if (gl_c < c_hi) set_gcol(gl_c);
+    }
+  };
+
+  // zero slot (G planes outside the volume), then the pipeline prologue:
+  // G tiles 0 .. P-1, then steps "-2" and "-1" (X 0 / G P, X 1 / G P+1)
+  for (int o = threadIdx.x * 16; o < GB; o += NW * 64 * 16) *(u32x4*)(smem + C::ZOFF + o) = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  for (int i = 0; i < P; ++i) issue_g();
+  issue_x(); issue_g();
+  issue_x(); issue_g();
+
+  // ---- compute ------------------------------------------------------------
+  const int ch_lo = half * NCH;
+  const uint32_t ga_base = (uint32_t)((ch_lo * 32 + gq * 4 + qq) * 32 + pp * 8);
+  uint32_t pav0[NCH], pav1[NCH];
+  auto set_tile = [&](int c) {
+    const int t = c % C::NTL, a = t * C::VT, nv = min(C::VT, K * L - a), kf = a / L;
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int e0 = (ch_lo + u) * 32 + gq * 4 + qq, e1 = e0 + 16;
+      const int f0 = a + e0, f1 = a + e1;
+      const int k0 = f0 / L, k1 = f1 / L;
+      pav0[u] = (uint32_t)((e0 < nv ? ((k0 - kf) * RS + f0 - k0 * L) * 32 : 0) + pp * 8);
+      pav1[u] = (uint32_t)((e1 < nv ? ((k1 - kf) * RS + f1 - k1 * L) * 32 : 0) + pp * 8);
+    }
+  };
+  int cc = c0, ii = 0;
+  if (cc < c_hi) set_tile(cc);
+  for (int n = 0; n < nsteps; ++n) {
+    // plane n and G tile n + P landed (issued two steps ago); only the previous
+    // step's RPW + GPW DMAs may still be in flight; previous step's reads done
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(RPW + GPW) : "memory");
+    issue_x();
+    issue_g();
+    const uint32_t xb = (uint32_t)(C::XOFF + (n % 3) * XB);
+    uint32_t xa0[NCH], xa1[NCH];
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) { xa0[u] = pav0[u] + xb; xa1[u] = pav1[u] + xb; }
+    uint32_t ga[KS];
+#pragma unroll
+    for (int d = 0; d < KS; ++d) {
+      const int gi = ii - d + P;
+      const int slot = (n - d + P) % NS;   // G sequence index n + P - d (same column when gi is valid)
+      ga[d] = ((gi >= 0 && gi < g.I) ? (uint32_t)(C::GOFF + slot * GB) : (uint32_t)C::ZOFF) + ga_base;
+    }
+    // MFMA groups k = (u, m): m < TPG regular taps (x KS di), m == TPG the last
+    // tap (this group's di range); fragments of group k + 1 read during k
+    constexpr int NM = TPG + 1;
+    constexpr int NKG = NCH * NM;
+    u32x4 bfr[2][KS], afr[2];
+    auto load_b = [&](auto uc, int d) {
+      constexpr int u = decltype(uc)::value;
+      bfr[u & 1][d] = cat4u(lds_read_tr16u(smem, ga[d] + u * 1024), lds_read_tr16u(smem, ga[d] + u * 1024 + 512));
+    };
+    auto load_a = [&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int u = k / NM, m = k % NM;
+      constexpr int tap = m < TPG ? TG + 4 * m : NT - 1;
+      constexpr uint32_t to = (uint32_t)(((tap / KS) * RS + tap % KS) * 32);
+      afr[k & 1] = cat4u(lds_read_tr16u(smem, xa0[u] + to), lds_read_tr16u(smem, xa1[u] + to));
+    };
+#pragma unroll
+    for (int d = 0; d < KS; ++d) load_b(std::integral_constant<int, 0>{}, d);
+    load_a(std::integral_constant<int, 0>{});
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * KS + 2, 0);
+    wstatic_for<0, NKG>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int u = k / NM, m = k % NM;
+      // reads issued in this group: the next group's X fragment, and (m < KS)
+      // the G fragment d = m of the next chunk
+      constexpr bool LA = k + 1 < NKG;
+      constexpr bool LB = u + 1 < NCH && m < KS;
+      if constexpr (LA) load_a(std::integral_constant<int, k + 1>{});
+      if constexpr (LB) load_b(std::integral_constant<int, u + 1>{}, m);
+      if constexpr (m < TPG) {
+#pragma unroll
+        for (int d = 0; d < KS; ++d) acc[m][d] = mfma16u(afr[k & 1], bfr[u & 1][d], acc[m][d]);
+      } else {
+        wstatic_for<XLO, XHI>([&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          accx[d - XLO] = mfma16u(afr[k & 1], bfr[u & 1][d], accx[d - XLO]);
+        });
+        if constexpr (TG == 0) {
+          if (center_blk) accb = mfma16u(ones, bfr[u & 1][P], accb);
+        }
+      }
+      constexpr int NR = (LA ? 2 : 0) + (LB ? 2 : 0);
+      if constexpr (NR > 0) __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+      constexpr int NMF = m < TPG ? KS : (XHI - XLO);
+      if constexpr (NMF > 0) __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);
+    });
+    if (++ii == g.I) {
+      ii = 0;
+      cc = next_col(cc);
+      if (cc < c_hi) set_tile(cc);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
+
+  // D[row = ci = 4(l>>4)+r][col = co = l&15]
+  const int row = grp * 2 + half;
+#pragma unroll
+  for (int m = 0; m < TPG; ++m) {
+    const int tap = TG + 4 * m;
+#pragma unroll
+    for (int d = 0; d < KS; ++d) {
+      float* pout = part + (((size_t)row * NT + (d * KS + dj)) * NT + tap) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pout[(4 * (lane >> 4) + r) * 16 + (lane & 15)] = acc[m][d][r];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EXP; ++e) {
+    const int d = XLO + e;
+    if (d < XHI) {
+      float* pout = part + (((size_t)row * NT + (d * KS + dj)) * NT + (NT - 1)) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pout[(4 * (lane >> 4) + r) * 16 + (lane & 15)] = accx[e][r];
+    }
+  }
+  if (TG == 0 && center_blk && lane < 16) partb[row * 16 + lane] = accb[0];
+}
+
+template <int KS, int K, int L>
+__global__ __launch_bounds__(512, 1) void wgrad16v4_kernel(const bf16* __restrict__ X, const bf16* __restrict__ G,
+                                                           float* __restrict__ part, float* __restrict__ partb,
+                                                           W3Geom g) {
+#if defined(__HIP_DEVICE_COMPILE__)   // device-only body (asm DMA); the host pass keeps the stub
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tg = wave & 3, half = wave >> 2;
+  const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int dj = lb % KS, grp = lb / KS;
+  switch (tg) {
+    case 0: wgrad16v4_body<KS, K, L, 0>(X, G, part, partb, g, wave, half, dj, grp); break;
+    case 1: wgrad16v4_body<KS, K, L, 1>(X, G, part, partb, g, wave, half, dj, grp); break;
+    case 2: wgrad16v4_body<KS, K, L, 2>(X, G, part, partb, g, wave, half, dj, grp); break;
+    default: wgrad16v4_body<KS, K, L, 3>(X, G, part, partb, g, wave, half, dj, grp); break;
+  }
+#endif
+}
+
+// ===========================================================================
 // wgrad16p: plane-only weight gradient of the ij-encoded 1-channel layers
 // (same math as wgrad16v2 with dj_center = 2) for whole-plane tiles
 // (K, L <= 25), with the next item's X plane and G tiles streaming into the
@@ -707,6 +1006,16 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
   }
   if (g.RW > 32) return -1;                 // one wave-instruction per staged row
   if (g.VT > 384) return -1;                // <= 6 chunks per half
+  {
+    const char* e = getenv("NCNET_WGRAD_V3");   // A/B switch (read per launch)
+    if (KS == 5 && K == 25 && L == 25 && !(e && atoi(e))) {
+      using C = W4C<5, 25, 25>;
+      dim3 grid((unsigned)(KS * ngroups)), block(512);
+      hipLaunchKernelGGL((wgrad16v4_kernel<5, 25, 25>), grid, block, (size_t)C::LDS, stream, (const bf16*)X,
+                         (const bf16*)G, part, partb, g);
+      return (int)hipGetLastError();
+    }
+  }
   size_t lds = 2 * (size_t)g.PR * g.RS * 32 + (size_t)(KS + 2) * g.VT * 32;
   if (lds > 160 * 1024) return -1;
   dim3 grid((unsigned)(KS * ngroups)), block(512);

@@ -107,6 +107,7 @@ def main():
         "conv16_dgrad_v3": (with_env("NCNET_CONV_V3", "1", lambda: C.conv16_fwd(g16, w16, None, x16, y16, ks, 2)), fl16),
         "conv16_f32": (lambda: C.conv16_fwd(x16, w16, None, None, torch.empty((16,) + shp, device=dev), ks, 4), fl16),
         "wgrad16v3": (lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3), fl16),
+        "wgrad16v3_old": (with_env("NCNET_WGRAD_V3", "1", lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3)), fl16),
         "wgrad16v2": (lambda: C.wgrad16(x16, g16, p2, p2b, ks, 0, 2), fl16),
         **{f"wgrad16v3_g{n}": ((lambda n=n: C.wgrad16(x16, g16, p3g[n][0], p3g[n][1], ks, 0, 3)), fl16)
            for n in (51, 204, 306)},

@@ -319,6 +319,30 @@ def test_correlation_v2_large_grids():
         assert (a.long() == b.long()).float().mean() > 0.999
 
 
+@pytest.mark.parametrize("shape,ng", [((2, 6, 5, 25, 25), 7), ((3, 25, 25, 25, 25), 102), ((1, 4, 7, 25, 25), 1),
+                                      ((2, 9, 3, 25, 25), 40)])
+def test_wgrad16v4_matches_v3(shape, ng, monkeypatch):
+    """wgrad16v4 (compile-time 25 x 25 plane: X and G DMA'd two steps ahead with
+    counted vmcnt, buffer-resource zero halo, per-tap-group specialised body)
+    walks the same columns, steps and chunks as wgrad16v3, so every partial
+    accumulates in the same order: identical partials (and the fp64 oracle
+    bound), incl. group counts that leave some workgroups without columns and
+    dj offsets whose columns are skipped."""
+    C = _ext.ext()
+    torch.manual_seed(12)
+    x = torch.rand(shape + (16,), device=DEV).to(torch.bfloat16)
+    g = torch.randn(shape + (16,), device=DEV).to(torch.bfloat16)
+    outs = []
+    for v3 in ("0", "1"):
+        monkeypatch.setenv("NCNET_WGRAD_V3", v3)
+        part = torch.full((2 * ng, 25, 25, 16, 16), float("nan"), device=DEV)
+        partb = torch.full((2 * ng, 16), float("nan"), device=DEV)
+        C.wgrad16(x, g, part, partb, 5, 0, 3)
+        outs.append((part, partb))
+    assert torch.isfinite(outs[0][0]).all() and torch.isfinite(outs[0][1]).all()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("variant", [2, 3])
 @pytest.mark.parametrize("ks,shape", [(5, (2, 6, 5, 25, 25)), (5, (1, 5, 4, 30, 27)), (3, (1, 4, 5, 9, 33)),
                                       (5, (1, 2, 3, 7, 6)), (7, (1, 3, 4, 25, 25)), (1, (1, 3, 4, 25, 26))])
