@@ -43,6 +43,10 @@ int ncnet_adam_masked(float*, float*, float*, float*, long long, const int*, con
 int ncnet_adam_finalize(float*, int*, int*, hipStream_t);
 int ncnet_resize_norm_u8(const void*, const long long*, float*, int, int, int, const float*, const float*, hipStream_t);
 int ncnet_debug_selftest(int*, hipStream_t);
+int ncnet_pad_geom(int, int, int, int*, int*);
+int ncnet_pad_planes(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv1x16(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int,
+                   hipStream_t);
 int ncnet_nc_fused_k3(const void*, const void*, const float*, const void*, const float*, float*, int, int, int, int,
                       int, int, int, int, int, hipStream_t);
 }
@@ -76,6 +80,57 @@ void check_ks(int64_t ks) { TORCH_CHECK(ks == 1 || ks == 3 || ks == 5 || ks == 7
 // (group planes: G input groups at the (i, j) plane, Wp [G, ...], in-plane taps only).
 // epi: 0 none -> bf16, 1 bias+ReLU -> bf16, 2 ReLU-mask M -> bf16,
 //      4 fp32 channel-planar [nco,V,I,J,K,L] (first nco <= 16 output channels).
+// padded 1-channel planes (csrc/conv1x.hip): {LP, PPL} of a (K, L) plane
+std::vector<int64_t> pad_geom(int64_t K, int64_t L, int64_t ks) {
+  int lp, ppl;
+  ncnet_pad_geom((int)K, (int)L, (int)ks, &lp, &ppl);
+  return {lp, ppl};
+}
+
+// x [V, R, C] (fp32 / bf16) -> y [N, PPL] bf16 padded planes (trans 0: N = V*R
+// planes [I2, J2] = rows of x; trans 1: N = V*C planes of the A<->B swap).  y's halo
+// must already be zero.
+void pad_planes(Tensor x, Tensor y, int64_t I2, int64_t J2, int64_t ks, int64_t trans) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 3, "x must be a contiguous [V, R, C] GPU tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be fp32 or bf16");
+  check(y, "y", at::kBFloat16);
+  check_ks(ks);
+  const int64_t V = x.size(0), R = x.size(1), C = x.size(2);
+  const int64_t planes = trans ? V * C : V * R;
+  TORCH_CHECK(I2 * J2 == (trans ? R : C), "plane dims do not match x");
+  const auto g = pad_geom(I2, J2, ks);
+  check_shape(y, "y", {planes, g[1]});
+  ok(ncnet_pad_planes(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(), (int)V, (int)R, (int)C, (int)I2,
+                      (int)J2, (int)ks, (int)trans, cur_stream(x)),
+     "pad_planes");
+}
+
+// 1 -> 16 Conv4d on padded 1-channel planes Xp [V*I*J, PPL] with A fragments Wa
+// [ks^2, 64, 8]; Y bf16 [V,I,J,K,L,16]; epi 1 (bias + ReLU) or 2 (ReLU mask M).
+// Returns false (nothing launched) for shapes without an instantiation.
+bool conv1x16(Tensor Xp, Tensor Wa, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks,
+              int64_t epi) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(Xp.device());
+  check(Xp, "Xp", at::kBFloat16); check(Wa, "Wa", at::kBFloat16); check(Y, "Y", at::kBFloat16);
+  check_ks(ks);
+  TORCH_CHECK(Y.dim() == 6 && Y.size(5) == 16, "Y must be [V,I,J,K,L,16]");
+  const int64_t V = Y.size(0), I = Y.size(1), J = Y.size(2), K = Y.size(3), L = Y.size(4);
+  const auto g = pad_geom(K, L, ks);
+  check_shape(Xp, "Xp", {V * I * J, g[1]});
+  check_shape(Wa, "Wa", {ks * ks, 64, 8});
+  TORCH_CHECK(epi == 1 || epi == 2, "conv1x16: epi must be 1 or 2");
+  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
+  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", {V, I, J, K, L, 16}); }
+  const char* e = getenv("NCNET_NT_STORE");
+  const int nt = e ? atoi(e) : 1;
+  const int r = ncnet_conv1x16(Xp.data_ptr(), Wa.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(),
+                               (int)V, (int)I, (int)J, (int)K, (int)L, (int)ks, (int)epi, nt, cur_stream(Xp));
+  if (r == -1) return false;
+  ok(r, "conv1x16");
+  return true;
+}
+
 void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks, int64_t epi) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   check(X, "X", at::kBFloat16); check(Wp, "Wp", at::kBFloat16);
@@ -549,6 +604,9 @@ void resize_norm_u8(Tensor src, Tensor meta, Tensor out, std::vector<double> mea
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for ncnet_amd";
   m.def("conv16_fwd", &conv16_fwd);
+  m.def("pad_geom", &pad_geom);
+  m.def("pad_planes", &pad_planes);
+  m.def("conv1x16", &conv1x16);
   m.def("conv16_blk_fwd", &conv16_blk_fwd);
   m.def("wgrad16p", &wgrad16p);
   m.def("wgrad16", &wgrad16);

@@ -1,0 +1,353 @@
+// Conv4d with a ONE-channel operand on gfx950 MFMA, without the ij packing.
+//
+// The 1 -> 16 convolutions of the NC-Net stack -- the first layer's forward
+// (input = MutualMatching output) and the last (16 -> 1) layer's data gradient
+// (input = the 1-channel output gradient, transposed flipped weights) -- were
+// run as 16 -> 16 group-plane convs on an ij-packed copy of the 1-channel
+// volume (csrc/jshift.hip): 16x the bytes of the volume written (1.6 GB at the
+// training shape) and re-read.  Here the 1-channel planes are staged as they
+// are, and the MFMA B operand (32 taps x 16 voxels) is gathered by the
+// hardware-transposing LDS read ds_read_b64_tr_b16: each lane addresses four
+// consecutive voxels of one tap row, so a fragment is any 32 (plane, tap) rows.
+//
+//  * input: zero-padded planes [N, PPL] bf16 (row stride LP = L + 2P, K + 2P
+//    rows, PPL a multiple of 8); a voxel (k, l) of plane n sits at flattened
+//    f = (k + P) LP + l + P and its tap (dk, dl) at f + (dk - P) LP + dl - P, so
+//    every tap is a 1-D shift and the halo reads zeros;
+//  * output voxels are 16-wide tiles of consecutive f (the 2P pad columns of
+//    each row are computed and dropped: LP / L = 1.16x work);
+//  * tr_b16 needs 8-byte-aligned rows: each staged plane is held as 4 copies
+//    shifted by 0..3 elements (4 LDS-DMAs from the same global plane at
+//    element offsets 0, -1, -2, -3, plus a bank-spreading shift; out-of-range
+//    reads land as zeros) and a tap row reads the copy that re-aligns its shift;
+//  * K = 32 per MFMA = the 25 (dk, dl) taps of one (di, dj) plane offset + 7
+//    zero-weight rows; the B fragment of an input plane is shared by every
+//    output plane it feeds (dj = 0..KS-1: up to KS MFMAs per 2 transposed reads);
+//  * work item = (v, i, R consecutive output j-planes), 8 waves x MAXT tiles;
+//    a step = one di: its R + KS - 1 input planes (j') land together in one
+//    of two LDS slots, DMA'd one step ahead (the 25 taps of a single plane are
+//    too little MFMA work to amortise a barrier);
+//  * persistent workgroups (one per CU) walk items bid, bid + G, ...: the plane
+//    DMA stream runs on across items, so the per-item prologue (weights, first
+//    planes) and epilogue (stores) no longer idle the CU -- with ~0.4 ms of MFMA
+//    work spread over 8000 items, one item per workgroup spent half its time
+//    there.
+// Reference semantics: lib/conv4d.py:11-51 (same-padded 4D cross-correlation),
+// the first / last NeighConsensus layers of lib/model.py:130-139.
+#include "common.h"
+#include <algorithm>
+#include <type_traits>
+
+namespace ncnet {
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void xstatic_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    xstatic_for<B + 1, E>(f);
+  }
+}
+
+enum Epi1x { EPI1X_BIAS_RELU = 1, EPI1X_MASK = 2 };
+
+template <int KS, int K, int L>
+struct C1X {
+  static constexpr int P = KS / 2, NT = KS * KS, NW = 8;
+  static constexpr int LP = L + 2 * P, KPR = K + 2 * P;
+  static constexpr int PPL = (KPR * LP + 7) / 8 * 8;          // padded plane (elements)
+  static constexpr int F0 = P * LP + P;                        // f of voxel (0, 0)
+  static constexpr int FN = (K - 1 + P) * LP + (L - 1 + P) + 1;
+  static constexpr int NTILE = (FN - F0 + 15) / 16;
+  static constexpr int MAXT = (NTILE + NW - 1) / NW;
+  // bytes per shifted copy: the plane + the largest shift (3 + 44), 16-B multiple
+  static constexpr int COPYB = ((PPL + 3 + 44) * 2 + 15) / 16 * 16;
+  // copy c holds element e at position e + c + DELTA(c): c re-aligns a tap row to
+  // 8 bytes, DELTA (a multiple of 4) spreads the rows of one transposed read over
+  // the LDS banks (exhaustive search over the KS = 5 tap rows: worst 2-way, mean
+  // 1.75 dwords per bank, vs 4-way / 3.75 without)
+  static constexpr int delta(int c) { return c == 0 ? 0 : c == 1 ? 12 : c == 2 ? 28 : 44; }
+  static constexpr int SLOTB = 4 * COPYB;                      // one staged plane (4 copies)
+  static constexpr int WOFF = 0, XOFF = NT * 1024;
+  static constexpr int lds(int np, int d) { return XOFF + (d + 1) * np * SLOTB + 256; }   // + tail pad
+  static_assert(NT <= 32, "one K fragment per plane offset");
+  // reads for real voxels stay inside their copy; junk columns / tiles may read
+  // past it into the next copy (finite data) or into the LDS tail pad
+  static_assert(FN - 1 + P * LP + P + 3 + 44 < COPYB / 2, "real-voxel tap reads stay inside one copy");
+  static_assert(COPYB > 1024 && COPYB <= 2048, "two DMA wave-instructions per copy");
+};
+
+// zero-padded planes (see the file comment): Y[n][(k+P)*LP + l + P] = X[n][k][l]
+// for n in [0, N); the halo must be zero beforehand (hipMemsetAsync).
+// TRANS: the planes of the A<->B-swapped volume of x [V, R = I*J, C = K*L]:
+// output plane v*C + c holds x[v, :, c] as an [I, J] plane (I = K, J = L here).
+template <typename T, bool TRANS>
+__global__ __launch_bounds__(256) void pad_planes_kernel(const T* __restrict__ x, bf16* __restrict__ y, int V, int R,
+                                                         int C, int I2, int J2, int LP, int PPL, int P) {
+  if constexpr (!TRANS) {
+    // one block per plane row-group: planes are rows of x ([V*R, C]), in-plane (k, l) = c
+    const long long row = blockIdx.x;
+    const T* xr = x + row * C;
+    bf16* yr = y + row * PPL;
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const int k = c / J2, l = c - k * J2;
+      yr[(k + P) * LP + l + P] = (bf16)(float)xr[c];
+    }
+  } else {
+    // 64 x 64 tile of x[v] ([R, C]) through LDS; output plane c, position r
+    __shared__ float tile[64][65];
+    const int ntc = (C + 63) / 64, ntr = (R + 63) / 64;
+    int b = blockIdx.x;
+    const int tc = b % ntc; b /= ntc;
+    const int tr = b % ntr;
+    const int v = b / ntr;
+    const int c0 = tc * 64, r0 = tr * 64;
+    const T* xv = x + (size_t)v * R * C;
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+      const int rr = e >> 6, cc = e & 63;
+      const int r = r0 + rr, c = c0 + cc;
+      tile[rr][cc] = (r < R && c < C) ? (float)xv[(size_t)r * C + c] : 0.f;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+      const int cc = e >> 6, rr = e & 63;
+      const int r = r0 + rr, c = c0 + cc;
+      if (r < R && c < C) {
+        const int i = r / J2, j = r - i * J2;
+        y[((size_t)v * C + c) * PPL + (i + P) * LP + j + P] = (bf16)tile[rr][cc];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// conv1x16: Y[v,i,j,k,l,co] = epi(sum_{di,dj,dk,dl} W[co][di,dj,dk,dl] X[v,i+di-P,j+dj-P,k+dk-P,l+dl-P])
+// Xp: padded 1-channel planes [V*I*J][PPL]; Wa: A fragments [NT plane offsets][64 lanes][8] bf16
+// (lane l: co = l & 15, K rows 8 (l >> 4) .. +7 = taps dk*KS+dl, >= NT zero);
+// Y: bf16 [V,I,J,K,L,16]; EPI1X_BIAS_RELU (bias [16]) or EPI1X_MASK (M bf16 [V,I,J,K,L,16]: y *= M > 0).
+// ---------------------------------------------------------------------------
+template <int KS, int R, int EPI, int K, int L>
+__global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict__ Xp, const u32x4* __restrict__ Wa,
+                                                          const float* __restrict__ bias, const bf16* __restrict__ M,
+                                                          bf16* __restrict__ Y, int V, int I, int J, int nt_store) {
+#if defined(__HIP_DEVICE_COMPILE__)   // device-only body (asm DMA); the host pass keeps the stub
+  using C = C1X<KS, K, L>;
+  constexpr int P = C::P, NT = C::NT, NW = C::NW, LP = C::LP, PPL = C::PPL, MAXT = C::MAXT;
+  constexpr int S = R + KS - 1;          // input j-planes per di = one step
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int njb = (J + R - 1) / R;
+  // persistent: items (v, i, j-block) bid, bid + G, ...; KS steps (di) per item,
+  // the plane DMA stream runs on across items (the next item's first di lands
+  // while the current item's last di computes and stores)
+  const int nitems = V * I * njb;
+  const int G = gridDim.x;
+  const int bid = blockIdx.x;
+  const int my_items = bid < nitems ? (nitems - 1 - bid) / G + 1 : 0;
+  const int nsteps = my_items * KS;
+
+  // weights (one KiB per plane offset) by LDS-DMA, before the first plane
+  for (int q = wave; q < NT; q += NW) dma16_lds(Wa + q * 64 + lane, smem + C::WOFF + q * 1024);
+
+  // step n: item bid + G (n / KS), di = n % KS; its S planes -> ring slot n % 2;
+  // wave w DMAs copy w >> 1, half w & 1 of each plane
+  const int cpy = wave >> 1, hlf = wave & 1;
+  const uint32_t dvo = (uint32_t)((hlf * 64 + lane) * 16 - 2 * (cpy + C::delta(cpy)));   // element e -> e + c + delta
+  auto issue = [&](int n) {
+    const int it = bid + G * (n / KS), di = n % KS;
+    int b = it;
+    const int jb = b % njb; b /= njb;
+    const int ti = b % I, tv = b / I;
+    const int ii = ti + di - P;
+    const bool iv = n < nsteps && ii >= 0 && ii < I;
+    const bf16* xrow = Xp + ((size_t)(tv * I + (iv ? ii : 0)) * J) * PPL;
+    const uint32_t slot = lds0 + C::XOFF + (uint32_t)((n & 1) * S * C::SLOTB + cpy * C::COPYB + hlf * 1024);
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      const int jp = jb * R - P + u;
+      const bool pv = iv && jp >= 0 && jp < J;
+      const uint64_t pb = (uint64_t)(pv ? xrow + (size_t)jp * PPL : Xp);
+      typedef int i32x4v __attribute__((ext_vector_type(4)));
+      i32x4v rs;
+      rs[0] = (int)(uint32_t)pb;
+      rs[1] = (int)((uint32_t)(pb >> 32) & 0xffffu);
+      rs[2] = pv ? PPL * 2 : 0;
+      rs[3] = 0x00020000;
+      const uint32_t d = slot + (uint32_t)(u * C::SLOTB);
+      // the second KiB of a copy is partial: its lanes past the copy stay off
+      // (exec never empty, so the instruction -- and the vmcnt count -- is fixed)
+      if (hlf == 0 || lane < C::COPYB / 16 - 64)
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(dvo), "s"(rs),
+                     "s"(d)
+                     : "memory", "m0");
+    }
+  };
+  issue(0);
+
+  // per-lane transposed-read row offsets (h = 0, 1): K row kk = 8 g + 4 h + q of
+  // lane (g = l >> 4, q = (l >> 2) & 3, p = l & 3): tap kk, 4 voxels from 4 p,
+  // in the copy that re-aligns the tap's shift; + this wave's first tile
+  uint32_t rowoff[2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kk = 8 * g + 4 * h + q;
+      int t = 0, c = 0;
+      if (kk < NT) {
+        const int dk = kk / KS, dl = kk - dk * KS;
+        t = (dk - P) * LP + (dl - P);
+        c = (4 - (((t % 4) + 4) % 4)) & 3;
+      }
+      rowoff[h] = (uint32_t)(C::XOFF + c * C::COPYB + (C::F0 + 16 * wave + t + c + C::delta(c) + 4 * p) * 2);
+    }
+  }
+  f32x4 acc[R][MAXT];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const size_t KLs = (size_t)K * L;
+  const int co0 = 4 * (lane >> 4);
+  for (int n = 0; n < nsteps; ++n) {
+    const int it = bid + G * (n / KS), di = n % KS;
+    int b = it;
+    const int jb = b % njb; b /= njb;
+    const int ti = b % I, tv = b / I;
+    const int j0 = jb * R;
+    // this step's planes landed (issued one step ago); the previous step's reads are done
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    issue(n + 1);
+    const int ii = ti + di - P;
+    if (ii >= 0 && ii < I) {
+      bf16x8 A[KS];
+#pragma unroll
+      for (int dj = 0; dj < KS; ++dj) A[dj] = lds_read16(smem, C::WOFF + (di * KS + dj) * 1024 + lane * 16);
+      const uint32_t sb = (uint32_t)((n & 1) * S * C::SLOTB);
+      xstatic_for<0, S>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;   // plane j' = j0 - P + s
+        const int jp = j0 - P + s;
+        if (jp >= 0 && jp < J) {
+          constexpr int dlo = (s - R + 1) > 0 ? (s - R + 1) : 0;
+          constexpr int dhi = s < KS - 1 ? s : KS - 1;   // inclusive
+          constexpr int NDJ = dhi - dlo + 1;
+          const uint32_t a0 = rowoff[0] + sb + s * C::SLOTB, a1 = rowoff[1] + sb + s * C::SLOTB;
+          u32x4 B[2];
+          auto load_b = [&](auto tc) {
+            constexpr int tt = decltype(tc)::value;
+            B[tt & 1] = cat4u(lds_read_tr16u(smem, a0 + tt * NW * 32), lds_read_tr16u(smem, a1 + tt * NW * 32));
+          };
+          load_b(std::integral_constant<int, 0>{});
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          xstatic_for<0, MAXT>([&](auto tc) {
+            constexpr int tt = decltype(tc)::value;
+            if constexpr (tt + 1 < MAXT) load_b(std::integral_constant<int, tt + 1>{});
+            xstatic_for<dlo, dhi + 1>([&](auto dc) {
+              constexpr int dj = decltype(dc)::value;
+              acc[s - dj][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[dj], __builtin_bit_cast(bf16x8, B[tt & 1]),
+                                                                        acc[s - dj][tt], 0, 0, 0);
+            });
+            if constexpr (tt + 1 < MAXT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NDJ, 0);
+          });
+        }
+      });
+    }
+    if (di == KS - 1) {
+      // item done: epilogue (stores are not waited for; the next item's planes are in flight)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int j = j0 + r;
+        const size_t pbase = (((size_t)tv * I + ti) * J + j) * KLs;
+#pragma unroll
+        for (int tt = 0; tt < MAXT; ++tt) {
+          const int f = C::F0 + 16 * (wave + NW * tt) + (lane & 15);
+          const int kp = f / LP, lp = f - kp * LP;
+          const int k = kp - P, l = lp - P;
+          if (j < J && f < C::FN && k >= 0 && k < K && l >= 0 && l < L) {
+            const size_t vox = pbase + (size_t)k * L + l;
+            float o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              float x = acc[r][tt][q];
+              if constexpr (EPI == EPI1X_BIAS_RELU) x = fmaxf(x + bias[co0 + q], 0.f);
+              o[q] = x;
+            }
+            if constexpr (EPI == EPI1X_MASK) {
+              const bf16x4 m = *(const bf16x4*)(M + vox * 16 + co0);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) o[q] = ((float)m[q] > 0.f) ? o[q] : 0.f;
+            }
+            bf16x4 out;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) out[q] = f2bf(o[q]);
+            if (nt_store) __builtin_nontemporal_store(__builtin_bit_cast(u32x2, out), (u32x2*)(Y + vox * 16 + co0));
+            else *(bf16x4*)(Y + vox * 16 + co0) = out;
+          }
+          acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
+#endif
+}
+
+}  // namespace ncnet
+
+using namespace ncnet;
+
+// padded-plane geometry of a (K, L) plane for kernel size KS: {LP, PPL}
+extern "C" int ncnet_pad_geom(int K, int L, int KS, int* lp, int* ppl) {
+  const int P = KS / 2;
+  *lp = L + 2 * P;
+  *ppl = ((K + 2 * P) * (L + 2 * P) + 7) / 8 * 8;
+  return 0;
+}
+
+// x: [V, R, C] fp32 or bf16 (x_is_bf16); planes of x (trans 0: N = V*R planes of
+// [I2=K, J2=L]) or of its A<->B swap (trans 1: N = V*C planes of [I2=I, J2=J]) into y
+// [N, PPL] bf16, whose halo the caller zeroed.
+extern "C" int ncnet_pad_planes(const void* x, int x_is_bf16, void* y, int V, int R, int C, int I2, int J2, int KS,
+                                int trans, hipStream_t s) {
+  int LP, PPL;
+  ncnet_pad_geom(I2, J2, KS, &LP, &PPL);
+  const int P = KS / 2;
+  bf16* yy = (bf16*)y;
+  if (!trans) {
+    dim3 grid((unsigned)((long long)V * R));
+    if (x_is_bf16) hipLaunchKernelGGL((pad_planes_kernel<bf16, false>), grid, dim3(256), 0, s, (const bf16*)x, yy, V, R, C, I2, J2, LP, PPL, P);
+    else hipLaunchKernelGGL((pad_planes_kernel<float, false>), grid, dim3(256), 0, s, (const float*)x, yy, V, R, C, I2, J2, LP, PPL, P);
+  } else {
+    dim3 grid((unsigned)((long long)V * cdiv(R, 64) * cdiv(C, 64)));
+    if (x_is_bf16) hipLaunchKernelGGL((pad_planes_kernel<bf16, true>), grid, dim3(256), 0, s, (const bf16*)x, yy, V, R, C, I2, J2, LP, PPL, P);
+    else hipLaunchKernelGGL((pad_planes_kernel<float, true>), grid, dim3(256), 0, s, (const float*)x, yy, V, R, C, I2, J2, LP, PPL, P);
+  }
+  return (int)hipGetLastError();
+}
+
+// conv1x16 at the training plane (K = L = 25, KS = 5): returns -1 when the
+// shape has no instantiation (the caller keeps the ij-packed path).
+extern "C" int ncnet_conv1x16(const void* Xp, const void* Wa, const float* bias, const void* M, void* Y, int V, int I,
+                              int J, int K, int L, int KS, int epi, int nt_store, hipStream_t s) {
+  if (!(KS == 5 && K == 25 && L == 25)) return -1;
+  if (epi != EPI1X_BIAS_RELU && epi != EPI1X_MASK) return -3;
+  constexpr int R = 5;
+  using C = C1X<5, 25, 25>;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  const int nitems = V * I * cdiv(J, R);
+  dim3 grid((unsigned)std::min(nitems, ncu)), block(512);   // persistent: one workgroup per CU
+  const bf16* x = (const bf16*)Xp; const u32x4* w = (const u32x4*)Wa; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
+  if (epi == EPI1X_BIAS_RELU)
+    hipLaunchKernelGGL((conv1x16_kernel<5, R, EPI1X_BIAS_RELU, 25, 25>), grid, block, (size_t)C::lds(R + 4, 1), s, x, w, bias, m, y, V, I, J, nt_store);
+  else
+    hipLaunchKernelGGL((conv1x16_kernel<5, R, EPI1X_MASK, 25, 25>), grid, block, (size_t)C::lds(R + 4, 1), s, x, w, bias, m, y, V, I, J, nt_store);
+  return (int)hipGetLastError();
+}

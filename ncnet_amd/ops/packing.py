@@ -150,3 +150,29 @@ def ij_out_grad(s: torch.Tensor, cin: int) -> torch.Tensor:
     ks = int(round(nt ** 0.5))
     d = s.permute(2, 0, 3, 1).reshape(16, G * 16, nt)[:cin, :nt]      # [ci, q, tap]
     return d.reshape(1, cin, ks, ks, ks, ks).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# 1-channel operand kernels (csrc/conv1x.hip): a 1 -> 16 conv's A fragments,
+# one K fragment of 32 rows per plane offset (di, dj): rows = the k*k in-plane
+# taps dk*k + dl (rows >= k*k zero).
+
+@functools.lru_cache(maxsize=None)
+def _idx1x(ks: int, device: str):
+    lane = torch.arange(64).view(64, 1)
+    j = torch.arange(8).view(1, 8)
+    kk = 8 * (lane >> 4) + j                      # K row
+    co = (lane & 15).expand(64, 8)
+    valid = kk < ks * ks
+    return co.contiguous().to(device), torch.clamp(kk, max=ks * ks - 1).contiguous().to(device), valid.to(device)
+
+
+def pack_w1x(w_std: torch.Tensor) -> torch.Tensor:
+    """[co<=16, 1, k, k, k, k] -> [k*k plane offsets, 64 lanes, 8] bf16:
+    lane l of plane offset p = di*k + dj holds W[co = l&15, 0, di, dj, tap kk]
+    for kk = 8 (l>>4) + j (taps dk*k + dl; zero for kk >= k*k or co >= Cout)."""
+    ks = w_std.shape[-1]
+    w = _as_std(w_std, 16, 1).reshape(16, ks * ks, ks * ks)      # [co, plane, tap]
+    co, kk, valid = _idx1x(ks, str(w.device))
+    vals = w[co, :, kk] * valid.unsqueeze(-1).to(w.dtype)          # [64, 8, plane]
+    return vals.permute(2, 0, 1).contiguous().to(torch.bfloat16)

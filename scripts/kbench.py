@@ -93,6 +93,12 @@ def main():
     nq = ks * ks
     zq = torch.empty((nq,) + shp, device=dev)
 
+    from ncnet_amd.ops.packing import pack_w1x
+    lp, ppl = C.pad_geom(S, S, ks)
+    xpad = torch.zeros((V * S * S, ppl), dtype=torch.bfloat16, device=dev)
+    C.pad_planes(x1.reshape(V, S * S, S * S), xpad, S, S, ks, 0)
+    w1x = pack_w1x(torch.randn(16, 1, ks, ks, ks, ks, device=dev) * 0.05)
+
     def ij_out_fwd():
         for gi in range(G):
             C.conv16_fwd(x16.unsqueeze(0), wz[gi:gi + 1], None, None, zq[16 * gi:min(nq, 16 * gi + 16)], ks, 4)
@@ -113,6 +119,10 @@ def main():
            for n in (51, 204, 306)},
         "wgrad16v3_prio": (with_env("NCNET_WGRAD_FLAGS", "1", lambda: C.wgrad16(x16, g16, p3, p3b, ks, 0, 3)), fl16),
         "ijpack": (lambda: C.ijpack(x1, xs, ks, 1), None),
+        "pad_planes": (lambda: C.pad_planes(x1.reshape(V, S * S, S * S), xpad, S, S, ks, 0), None),
+        "pad_planes_t": (lambda: C.pad_planes(x1.reshape(V, S * S, S * S), xpad, S, S, ks, 1), None),
+        "conv1x16_fwd": (lambda: C.conv1x16(xpad, w1x, b16, None, y16, ks, 1), fl1),
+        "conv1x16_dgrad": (lambda: C.conv1x16(xpad, w1x, None, x16, y16, ks, 2), fl1),
         "ij_1in_conv": (lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1), fl1),
         "ij_1in_conv_tpw1": (with_env("NCNET_GP_TPW", "1", lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1)), fl1),
         "ij_out_dgrad": (lambda: C.conv16_fwd(xs, wij, None, x16, y16, ks, 2), fl1),

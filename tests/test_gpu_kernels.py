@@ -805,3 +805,49 @@ def test_neigh_consensus_fused_symmetric_wrapper():
                                      [b1, b2], symmetric=True)
     yr = qo.neigh_consensus(x.double(), [w1.double(), w2.double()], [b1.double(), b2.double()], symmetric=True)
     assert relerr(y, yr) < 2e-3
+
+
+def _pad_1ch(x5, ks, trans=False):
+    """x5 [V, I, J, K, L] (any float dtype) -> padded bf16 planes via pad_planes."""
+    V, I, J, K, L = x5.shape
+    C = _ext.ext()
+    lp, ppl = C.pad_geom(K, L, ks) if not trans else C.pad_geom(I, J, ks)
+    n = V * (K * L if trans else I * J)
+    y = torch.zeros((n, ppl), dtype=torch.bfloat16, device=DEV)
+    C.pad_planes(x5.reshape(V, I * J, K * L).contiguous(), y, *((I, J) if trans else (K, L)), ks, 1 if trans else 0)
+    return y
+
+
+@pytest.mark.parametrize("shape", [(2, 25, 25, 25, 25), (1, 6, 7, 25, 25), (1, 3, 11, 25, 25)])
+@pytest.mark.parametrize("epi", [1, 2])
+def test_conv1x16_vs_oracle(shape, epi):
+    """1 -> 16 Conv4d on zero-padded 1-channel planes (csrc/conv1x.hip: taps
+    gathered by ds_read_b64_tr_b16 from 4 element-shifted LDS copies of each
+    plane) vs the fp64 oracle: bias + ReLU forward, and the ReLU-mask epilogue
+    of the last layer's data gradient."""
+    from ncnet_amd.ops.packing import pack_w1x
+    torch.manual_seed(3)
+    V, I, J, K, L = shape
+    x = torch.rand(V, I, J, K, L, device=DEV).to(torch.bfloat16)
+    w = torch.randn(16, 1, 5, 5, 5, 5, device=DEV) * 0.05
+    b = torch.randn(16, device=DEV) * 0.1
+    m = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
+    y = torch.full((V, I, J, K, L, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ran = _ext.ext().conv1x16(_pad_1ch(x, 5), pack_w1x(w), b if epi == 1 else None, m if epi == 2 else None, y, 5, epi)
+    assert ran
+    z = ref.conv4d(x.double().unsqueeze(1), ref.conv4d_weight_from_std(bf(w)), None)   # [V, 16, I, J, K, L]
+    if epi == 1:
+        want = torch.relu(z + b.double().view(1, 16, 1, 1, 1, 1))
+    else:
+        want = z * (m.double().permute(0, 5, 1, 2, 3, 4) > 0)
+    assert relerr(y.permute(0, 5, 1, 2, 3, 4), want) < 1e-2
+
+
+def test_pad_planes_transposed():
+    """pad_planes trans=1 writes the planes of the A<->B-swapped volume."""
+    torch.manual_seed(4)
+    V, I, J, K, L = 2, 9, 11, 9, 11
+    x = torch.randn(V, I, J, K, L, device=DEV)
+    a = _pad_1ch(x, 5, trans=True)
+    b = _pad_1ch(x.permute(0, 3, 4, 1, 2).contiguous(), 5)
+    assert torch.equal(a, b)
