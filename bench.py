@@ -88,6 +88,40 @@ def _inloc_secondary():
     return out
 
 
+def _nc_precision_secondary(batch: int, size: int, nc_precision: str, steps: int = 5, warmup: int = 2):
+    """The headline step with ``ImMatchNet(nc_precision=...)``: 'fp32' runs every
+    NeighConsensus conv, data gradient and weight gradient as a bf16x3 split
+    (the reference trains the NC in fp32: /root/reference/lib/conv4d.py:21-24,
+    /root/reference/train.py:110-156) -- the mode to use when the weak-loss
+    signal is below bf16 resolution (profiles/r2_quality)."""
+    from ncnet_amd.engine.trainer import Trainer, make_adam
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.parallel.dist import DistContext
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    model = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1], dtype="bf16",
+                       nc_precision=nc_precision).to(dev)
+    model.train()
+    params = [p for p in model.parameters() if p.requires_grad]
+    trainer = Trainer(model, make_adam(params, 5e-4), DistContext(device=dev))
+    g = torch.Generator(device=dev).manual_seed(98)
+    pool = [{"source_image": torch.randn(batch, 3, size, size, device=dev, generator=g),
+             "target_image": torch.randn(batch, 3, size, size, device=dev, generator=g)} for _ in range(2)]
+    for w in range(warmup):
+        trainer.train_step(pool[w % 2], pool[(w + 1) % 2])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = trainer.train_step(pool[i % 2], pool[(i + 1) % 2])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"pairs_per_s": round(batch * steps / dt, 3), "ms_per_step": round(1e3 * dt / steps, 3),
+           "nc_precision": nc_precision, "final_loss": float(loss.detach())}
+    del trainer, model
+    torch.cuda.empty_cache()
+    return out
+
+
 def _fe_finetune_secondary(batch: int, size: int, steps: int = 5, warmup: int = 2):
     """train.py --fe_finetune_params 1 (last layer3 bottleneck trainable,
     train.py:60-63): the trunk runs under autograd and the L2-norm,
@@ -174,12 +208,19 @@ def main(argv=None):
     ap.add_argument("--impl", choices=["hip", "reference"], default="hip")
     ap.add_argument("--ref-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--profile", type=str, default="", help="write a torch.profiler trace to this dir")
+    ap.add_argument("--only-secondary", type=str, default="",
+                    help="debug: skip the headline and print one secondary record (nc_fp32 | fe_finetune)")
     ap.add_argument("--inloc", type=int, default=1,
                     help="1: after the timed training steps of a 1-GPU run, also time the InLoc inference configs "
                          "(BASELINE configs 3-5: 1600 px bf16, 3200 px bf16, 3200 px fp8) into config.secondary")
     args = ap.parse_args(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return _self_launch(args, argv)
+    if args.only_secondary:
+        fn = {"nc_fp32": lambda: _nc_precision_secondary(args.batch, args.image_size, "fp32", args.steps, args.warmup),
+              "fe_finetune": lambda: _fe_finetune_secondary(args.batch, args.image_size, args.steps, args.warmup)}
+        print(json.dumps({"secondary": args.only_secondary, **fn[args.only_secondary]()}), flush=True)
+        return 0
 
     from ncnet_amd.config import RuntimeConfig
     from ncnet_amd.engine.trainer import Trainer, make_adam
@@ -283,6 +324,10 @@ def main(argv=None):
             secondary["fe_finetune_1"] = _fe_finetune_secondary(args.batch, s)
         except Exception as e:  # the headline record must still print
             secondary["fe_finetune_1"] = {"error": repr(e)}
+        try:
+            secondary["train_nc_fp32"] = _nc_precision_secondary(args.batch, s, "fp32")
+        except Exception as e:  # the headline record must still print
+            secondary["train_nc_fp32"] = {"error": repr(e)}
     if ctx.is_main:
         rec = {
             "metric": "image-pairs/sec fwd+bwd, ResNet-101+NC-Net(5,5,5) 400x400 bf16",
