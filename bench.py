@@ -70,15 +70,20 @@ def _inloc_secondary():
             # eval_inloc.py's schedule: 10 panos per query, query features extracted once
             r = bench_inloc.run_single(size, fp8, pairs=10, warmup=2, model=model, panos_per_query=10)
             r1 = bench_inloc.run_single(size, fp8, pairs=3, warmup=1, model=model, panos_per_query=1)
-            out[name] = {"ms_per_pair": r["value"], "stages_ms": r["stages_ms"], "panos_per_query": 10,
+            out[name] = {"ms_per_pair": r["value"], "stages_ms": r["stages_ms"],
+                         "stages_ms_eager": r.get("stages_ms_eager"), "panos_per_query": 10,
                          "ms_per_pair_both_backbones": r1["value"], "volume": r["config"]["volume"],
-                         "dtype": r["dtype"]}
+                         "dtype": r["dtype"], "pair_graph": r["pair_graph"]}
+            if "pair_graph_error" in r:
+                out[name]["pair_graph_error"] = r["pair_graph_error"]
         # the all-fp8 pipeline (fp8 Conv4d NC kernels instead of the fused bf16 stack)
         os.environ["NCNET_NC_FP8"] = "1"
         try:
             r = bench_inloc.run_single(3200, True, pairs=10, warmup=2, model=model, panos_per_query=10)
             out["inloc_3200_fp8_nc_fp8"] = {"ms_per_pair": r["value"], "stages_ms": r["stages_ms"],
-                                            "panos_per_query": 10, "dtype": r["dtype"]}
+                                            "stages_ms_eager": r.get("stages_ms_eager"),
+                                            "panos_per_query": 10, "dtype": r["dtype"],
+                                            "pair_graph": r["pair_graph"]}
         finally:
             os.environ.pop("NCNET_NC_FP8", None)
         del model

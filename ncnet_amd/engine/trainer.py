@@ -116,7 +116,8 @@ class TrunkPrefetcher:
             _, f, hw, b, done = pend
             main = torch.cuda.current_stream(self.stream.device)
             main.wait_event(done)
-            f.record_stream(main)
+            for t in (f if isinstance(f, tuple) else (f,)):    # split (hi, lo) operands in fp32 mode
+                t.record_stream(main)
             return f, hw, b
         if self.enabled:                        # batch may have been moved on the prefetch stream
             main = torch.cuda.current_stream(self.stream.device)

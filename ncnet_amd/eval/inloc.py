@@ -135,6 +135,12 @@ class PairMatcher:
         self.kw = dict(do_softmax=do_softmax, both_dirs=both_dirs, flip=flip)
         self.use_graph = (os.environ.get("NCNET_PAIR_GRAPH", "1") != "0") if use_graph is None else use_graph
         self._graphs = {}
+        self.capture_error = None
+
+    @property
+    def graphed(self) -> bool:
+        """True when at least one pair graph was captured and no capture failed."""
+        return bool(self._graphs) and self.capture_error is None
 
     def _eager(self, fa, hwa, fb, hwb):
         out = self.model.match_features(fa, hwa, fb, hwb, packed_offsets=True)
@@ -159,8 +165,10 @@ class PairMatcher:
                 with torch.cuda.graph(g):
                     res = self._eager(sa, hwa, sb, hwb)
                 ent = self._graphs[key] = (g, sa, sb, res)
-            except RuntimeError as err:      # capture unsupported -> eager from now on
+            except RuntimeError as err:      # capture unsupported -> eager from now on (loudly)
+                import traceback
                 import warnings
+                self.capture_error = "".join(traceback.format_exception(type(err), err, err.__traceback__))
                 warnings.warn(f"PairMatcher: HIP graph capture disabled ({err})")
                 self.use_graph = False
                 return self._eager(fa, hwa, fb, hwb)

@@ -800,6 +800,26 @@ def _fp8_weights(packed_bf16: torch.Tensor):
     return (packed_bf16.float() * 2.0 ** e).to(FP8), 2.0 ** -e
 
 
+_FP8_W_CACHE: dict = {}
+
+
+def _fp8_weights_of(w_ref: torch.Tensor, kind: str):
+    """Quantised fp8 fragments of one layer's weights, cached per weight tensor
+    version: the amax -> scale step reads the max on the host, which must not
+    happen per pair (it serialises the stream and is illegal inside the
+    InLoc PairMatcher HIP-graph capture)."""
+    key = (w_ref.data_ptr(), w_ref._version, tuple(w_ref.shape), kind)
+    hit = _FP8_W_CACHE.get(key)
+    if hit is None:
+        w = _std(w_ref)
+        packed = {"1in": lambda: pack_w16_planes(ij_in_weights(w)), "16": lambda: pack_w16(w),
+                  "1out": lambda: pack_w16_planes(ij_out_weights(w))}[kind]()
+        if len(_FP8_W_CACHE) > 64:
+            _FP8_W_CACHE.clear()
+        hit = _FP8_W_CACHE[key] = _fp8_weights(packed)
+    return hit
+
+
 def _stack_fwd_fp8(x0: torch.Tensor, ws, bs, kinds) -> torch.Tensor:
     """x0 [V,I,J,K,L] bf16 -> last layer output fp32 [V,I,J,K,L] (ReLU'd), fp8 inside."""
     C = _ext.ext()
@@ -807,21 +827,18 @@ def _stack_fwd_fp8(x0: torch.Tensor, ws, bs, kinds) -> torch.Tensor:
     h = x0
     for li, (w_ref, b, kind) in enumerate(zip(ws, bs, kinds)):
         ks = w_ref.shape[0]
-        w = _std(w_ref)
+        wq, osc = _fp8_weights_of(w_ref, kind)
         if kind == "1in":
             G = ij_groups(ks)
             xs = torch.empty((G, V, I, J, K, L, 16), dtype=FP8, device=x0.device)
             C.ijpack(h, xs, ks, 1)
-            wq, osc = _fp8_weights(pack_w16_planes(ij_in_weights(w)))
             y = torch.empty((V, I, J, K, L, 16), dtype=FP8, device=x0.device)
             C.conv16f8_fwd(xs, wq, _pad_bias(b, 16), y, ks, 1, osc)
         elif kind == "16":
-            wq, osc = _fp8_weights(pack_w16(w))
             y = torch.empty((V, I, J, K, L, 16), dtype=FP8, device=x0.device)
             C.conv16f8_fwd(h, wq, _pad_bias(b, 16), y, ks, 1, osc)
         else:  # "1out"
             G, nq = ij_groups(ks), ks * ks
-            wq, osc = _fp8_weights(pack_w16_planes(ij_out_weights(w)))
             z = torch.empty((nq, V, I, J, K, L), dtype=torch.float32, device=x0.device)
             hx = h.unsqueeze(0)
             for gi in range(G):

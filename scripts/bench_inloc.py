@@ -46,8 +46,9 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
     matches are identical), so ``pairs`` should be a multiple of it.  1: both
     backbones per pair.  pair_graph (default: with panos_per_query > 1, as
     eval_inloc.py does): everything after the backbones replayed as one HIP
-    graph (eval/inloc.py PairMatcher); its time is reported under "corr_pool"
-    with the later stages 0."""
+    graph (eval/inloc.py PairMatcher); its time is reported as "pair_graph",
+    and an untimed eager pass afterwards gives the per-stage breakdown
+    ("stages_ms_eager": corr_pool, mm_nc_mm, matches)."""
     dev = torch.device("cuda")
     torch.manual_seed(0)
     if model is None:
@@ -62,7 +63,10 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
     tgt = torch.randn(1, 3, h, w, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
     stages = {"backbone": 0.0, "corr_pool": 0.0, "mm_nc_mm": 0.0, "matches": 0.0}
+    if pair_graph:
+        stages = {"backbone": 0.0, "pair_graph": 0.0}
     nmatch = 0
+    eager_stages = False
 
     if impl == "reference":
         from ncnet_amd.engine.reference_impl import ReferenceAlgorithm, reference_inloc_forward
@@ -110,18 +114,15 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
                 fb = fpano["f"][fpano["i"]:fpano["i"] + 1]
                 fpano["i"] += 1
             ev[1].record()
-            if matcher is not None:
+            if matcher is not None and not eager_stages:
                 # correlation .. match extraction replayed as one HIP graph (eval_inloc.py)
                 res, cnt = matcher(fa, (fh, fw), fb, (fh, fw))
                 ev[2].record()
-                ev[3].record()
-                ev[4].record()
                 if timed:
                     nmatch = int(cnt)
-                if timed:
                     torch.cuda.synchronize()
-                    for i, kk in enumerate(stages):
-                        stages[kk] += ev[i].elapsed_time(ev[i + 1])
+                    stages["backbone"] += ev[0].elapsed_time(ev[1])
+                    stages["pair_graph"] += ev[1].elapsed_time(ev[2])
                 return
             if k == 2:
                 corr4d, delta = correlation_pool2(fa, fb, fh, fw, fh, fw)
@@ -147,6 +148,18 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
         one(True, i % max(1, panos_per_query) == 0)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / pairs
+    timed_stages = {kk: round(v / pairs, 3) for kk, v in stages.items()}
+    eager = None
+    if matcher is not None and impl != "reference":
+        # the graph replays correlation .. matches as one unit: break it down
+        # with an untimed eager pass over the same pairs (same kernels, with
+        # the launch gaps the graph removes)
+        eager_stages = True
+        stages = {"backbone": 0.0, "corr_pool": 0.0, "mm_nc_mm": 0.0, "matches": 0.0}
+        n_eager = min(pairs, 3)
+        for i in range(n_eager):
+            one(True, i == 0)
+        eager = {kk: round(v / n_eager, 3) for kk, v in stages.items() if kk != "backbone"}
     fs = (h // 16 // k, w // 16 // k)
     return {
         "metric": "InLoc dense matching latency per pair (fwd, k=%d relocalization)" % k,
@@ -160,8 +173,13 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
         "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,
                    "ncons": [list(ncons_kernel_sizes), list(ncons_channels)], "k": k,
                    "panos_per_query": panos_per_query},
-        "stages_ms": {kk: round(v / pairs, 3) for kk, v in stages.items()},
+        "stages_ms": timed_stages,
+        **({"stages_ms_eager": eager} if eager is not None else {}),
         "matches": nmatch, "matches_contract": n_matches(image_size, k, True),
+        # loud: the record says whether the pair graph actually replayed
+        "pair_graph": bool(matcher is not None and matcher.graphed),
+        **({"pair_graph_error": matcher.capture_error.strip().splitlines()[-1][:300]}
+           if matcher is not None and matcher.capture_error else {}),
     }
 
 

@@ -65,25 +65,57 @@ def test_point_transfer_demo_gpu(workdir):
     assert os.path.exists(out) and 0.0 <= acc <= 1.0
 
 
-def test_pair_matcher_graph_equals_eager():
+def _train_one_step_like_bench():
+    """The state bench.py leaves before its InLoc secondaries: cudnn.benchmark
+    on, a headline-config training step through the Trainer (side streams,
+    trunk prefetch, flat Adam)."""
+    import torch
+    from ncnet_amd.engine.trainer import Trainer, make_adam
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.parallel.dist import DistContext
+    torch.backends.cudnn.benchmark = True
+    dev = torch.device("cuda")
+    m = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1], dtype="bf16").to(dev).train()
+    params = [p for p in m.parameters() if p.requires_grad]
+    tr = Trainer(m, make_adam(params, 5e-4), DistContext(device=dev))
+    pool = [{"source_image": torch.randn(2, 3, 400, 400, device=dev),
+             "target_image": torch.randn(2, 3, 400, 400, device=dev)} for _ in range(2)]
+    for i in range(2):
+        tr.train_step(pool[i % 2], pool[(i + 1) % 2])
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("nc_fp8", [False, True])
+def test_pair_matcher_graph_equals_eager(nc_fp8, monkeypatch):
     """eval/inloc.py PairMatcher: the HIP-graph replay of correlation .. match
     extraction returns exactly the eager matches, for a fixed query and
-    changing panos (static inputs re-filled per replay)."""
+    changing panos (static inputs re-filled per replay) -- captured in the
+    bench process state (after training steps, cudnn.benchmark=True), and for
+    the all-fp8 pipeline (fp8 correlation + fp8 Conv4d NC) too."""
     import torch
     from ncnet_amd.eval.inloc import PairMatcher, pair_matches
     from ncnet_amd.models import ImMatchNet
-    torch.manual_seed(3)
-    m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], relocalization_k_size=2).cuda().eval()
-    src = torch.randn(1, 3, 320, 416, device="cuda")
-    panos = [torch.randn(1, 3, 320, 416, device="cuda") for _ in range(3)]
-    pm = PairMatcher(m, 2)
-    with torch.inference_mode():
-        fq = m.extract(src)
-        for t in panos:
-            fp = m.extract(t)
-            res, cnt = pm(fq[0], fq[1], fp[0], fp[1])
-            got = res[:int(cnt)].clone()
-            corr, delta = m.match_features(fq[0], fq[1], fp[0], fp[1])
-            want = pair_matches(corr, delta, 2)
-            assert torch.equal(got, want)
-    assert pm._graphs, "the pair graph was not captured"
+    old = torch.backends.cudnn.benchmark
+    try:
+        _train_one_step_like_bench()
+        if nc_fp8:
+            monkeypatch.setenv("NCNET_NC_FP8", "1")
+        torch.manual_seed(3)
+        m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], relocalization_k_size=2,
+                       half_precision=True, corr_dtype="fp8" if nc_fp8 else "bf16").cuda().eval()
+        src = torch.randn(1, 3, 320, 416, device="cuda")
+        panos = [torch.randn(1, 3, 320, 416, device="cuda") for _ in range(3)]
+        pm = PairMatcher(m, 2)
+        with torch.inference_mode():
+            fq = m.extract(src)
+            for t in panos:
+                fp = m.extract(t)
+                res, cnt = pm(fq[0], fq[1], fp[0], fp[1])
+                got = res[:int(cnt)].clone()
+                corr, delta = m.match_features(fq[0], fq[1], fp[0], fp[1])
+                want = pair_matches(corr, delta, 2)
+                assert torch.equal(got, want)
+        assert pm.capture_error is None, pm.capture_error
+        assert pm.graphed, "the pair graph was not captured"
+    finally:
+        torch.backends.cudnn.benchmark = old
