@@ -9,8 +9,10 @@
 #include <hip/hip_runtime.h>
 
 extern "C" {
-int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_conv16_blk_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int,
+                     long long, long long, hipStream_t);
+int ncnet_conv16_blk_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, int, long long,
+                         hipStream_t);
 int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_wgrad16p(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, int, long long,
                    long long, hipStream_t);
@@ -32,7 +34,7 @@ int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void
 int ncnet_mm_bwd(const float*, const float*, const float*, const int*, const float*, const int*, float*, float*, float*,
                  int, int, int, float, hipStream_t);
 int ncnet_combine_fwd(const float*, float*, int, int, int, hipStream_t);
-int ncnet_combine_bwd(const float*, const float*, void*, int, int, int, hipStream_t);
+int ncnet_combine_bwd(const float*, const float*, void*, void*, int, int, int, hipStream_t);
 int ncnet_softmax_max_bwd(const float*, const float*, const int*, const float*, const float*, const int*, const float*,
                           const float*, const float*, float*, int, int, int, int, float, hipStream_t);
 int ncnet_maxpool4d(const void*, int, float*, uint8_t*, int, int, int, int, int, int, hipStream_t);
@@ -154,8 +156,44 @@ void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<T
   if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
   if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", vs); }
   ok(ncnet_conv16_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), vs[0],
-                      vs[1], vs[2], vs[3], vs[4], ks, epi, (int)npg, (int)nco, cur_stream(X)),
+                      vs[1], vs[2], vs[3], vs[4], ks, epi, (int)npg, (int)nco, 0, 0, cur_stream(X)),
      "conv16_fwd");
+}
+
+// element offset of b from a (same dtype, same device): the kernels address the
+// lo operand of a bf16x3 layer relative to the hi one
+static long long elem_offset(const Tensor& a, const Tensor& b) {
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && a.device() == b.device(), "hi / lo operands must match");
+  const long long d = (long long)((const char*)b.data_ptr() - (const char*)a.data_ptr());
+  TORCH_CHECK(d % (long long)a.element_size() == 0, "misaligned lo operand");
+  return d / (long long)a.element_size();
+}
+
+// fp32-accurate ("bf16x3") Conv4d layer, KS 3 / 5:
+//   y = conv(Xh, Wh) + conv(Xh, Wl) + conv(Xl, Wh)   (one kernel, fp32 accumulators)
+// X / Xl: [V,I,J,K,L,16] or group planes [G,V,I,J,K,L,16]; Wp2 [2, planes, nq, 64, 8]
+// (hi set, lo set); epi 1: y = relu(y + bias), epi 2: y = y * (M > 0) (M: the hi part of
+// the previous layer's ReLU output).  Output split: Y = bf16(y), Yl = bf16(y - Y).
+void conv16_fwd_x3(Tensor X, Tensor Xl, Tensor Wp2, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y,
+                   Tensor Yl, int64_t ks, int64_t epi) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(Xl, "Xl", at::kBFloat16); check(Wp2, "Wp2", at::kBFloat16);
+  check(Y, "Y", at::kBFloat16); check(Yl, "Yl", at::kBFloat16);
+  TORCH_CHECK(ks == 3 || ks == 5, "conv16_fwd_x3: kernel size 3 or 5");
+  const bool grp = X.dim() == 7;
+  TORCH_CHECK((X.dim() == 6 || grp) && X.size(-1) == 16, "X must be [V,I,J,K,L,16] or [G,V,I,J,K,L,16]");
+  TORCH_CHECK(Xl.sizes() == X.sizes(), "Xl must match X");
+  const int64_t npg = grp ? X.size(0) : 0;
+  std::vector<int64_t> vs(X.sizes().begin() + (grp ? 1 : 0), X.sizes().end());
+  check_shape(Y, "Y", vs); check_shape(Yl, "Yl", vs);
+  check_shape(Wp2, "Wp2", {2, grp ? npg : ks * ks, conv_pairs16(ks), 64, 8});
+  TORCH_CHECK(epi == 1 || epi == 2, "conv16_fwd_x3: epi must be 1 or 2");
+  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
+  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", vs); }
+  ok(ncnet_conv16_fwd(X.data_ptr(), Wp2.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), vs[0],
+                      vs[1], vs[2], vs[3], vs[4], ks, (int)epi | 64, (int)npg, 16, elem_offset(X, Xl),
+                      elem_offset(Y, Yl), cur_stream(X)),
+     "conv16_fwd_x3");
 }
 
 // Cout = 1 layer (<= 16 input channels) in output-plane-block mode:
@@ -170,8 +208,27 @@ void conv16_blk_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, i
   check_shape(Wp, "Wp", {(ks + 3) * (ks + 3), conv_pairs16(ks), 64, 8});
   if (bias.has_value()) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == 1, "bias must have 1 element"); }
   ok(ncnet_conv16_blk_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), Y.data_ptr<float>(), vs[0], vs[1], vs[2],
-                          vs[3], vs[4], ks, (int)relu, cur_stream(X)),
+                          vs[3], vs[4], ks, (int)relu, 0, 0, cur_stream(X)),
      "conv16_blk_fwd");
+}
+
+// bf16x3 Cout = 1 layer in output-plane-block mode: X / Xl hi / lo input blocks,
+// Wp2 [2, (ks+3)^2, nq, 64, 8]; Y fp32 = act(bias + conv) accumulated over the three phases.
+void conv16_blk_fwd_x3(Tensor X, Tensor Xl, Tensor Wp2, c10::optional<Tensor> bias, Tensor Y, int64_t ks,
+                       int64_t relu) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(Xl, "Xl", at::kBFloat16); check(Wp2, "Wp2", at::kBFloat16);
+  check(Y, "Y", at::kFloat);
+  TORCH_CHECK(ks == 3 || ks == 5, "conv16_blk_fwd_x3: kernel size 3 or 5");
+  TORCH_CHECK(X.dim() == 6 && X.size(-1) == 16, "X must be [V,I,J,K,L,16]");
+  TORCH_CHECK(Xl.sizes() == X.sizes(), "Xl must match X");
+  std::vector<int64_t> vs(X.sizes().begin(), X.sizes().end() - 1);
+  check_shape(Y, "Y", vs);
+  check_shape(Wp2, "Wp2", {2, (ks + 3) * (ks + 3), conv_pairs16(ks), 64, 8});
+  if (bias.has_value()) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == 1, "bias must have 1 element"); }
+  ok(ncnet_conv16_blk_fwd(X.data_ptr(), Wp2.data_ptr(), opt_ptr<float>(bias), Y.data_ptr<float>(), vs[0], vs[1],
+                          vs[2], vs[3], vs[4], ks, (int)relu, 1, elem_offset(X, Xl), cur_stream(X)),
+     "conv16_blk_fwd_x3");
 }
 
 // Weight gradient partials.  mode 0: all KS*KS plane offsets (di, dj); mode 2:
@@ -399,13 +456,16 @@ void combine_fwd(Tensor z, Tensor y, int64_t R, int64_t C) {
   ok(ncnet_combine_fwd((float*)z.data_ptr(), (float*)y.data_ptr(), Vh, R, C, cur_stream(z)), "combine_fwd");
 }
 
-void combine_bwd(Tensor g, Tensor z, Tensor gz, int64_t R, int64_t C) {
+void combine_bwd(Tensor g, Tensor z, Tensor gz, int64_t R, int64_t C, c10::optional<Tensor> gzl) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(z.device());
   check(g, "g", at::kFloat); check(z, "z", at::kFloat); check(gz, "gz", at::kBFloat16);
   TORCH_CHECK(z.numel() % (2 * R * C) == 0);
-  const int64_t Vh = z.numel() / (2 * R * C);
-  TORCH_CHECK(g.numel() == Vh * R * C && gz.numel() == z.numel());
-  ok(ncnet_combine_bwd((float*)g.data_ptr(), (float*)z.data_ptr(), gz.data_ptr(), Vh, R, C, cur_stream(z)), "combine_bwd");
+  TORCH_CHECK(gz.numel() == z.numel() && g.numel() * 2 == z.numel(), "combine_bwd: size mismatch");
+  if (gzl.has_value()) { check(*gzl, "gzl", at::kBFloat16); TORCH_CHECK(gzl->numel() == z.numel()); }
+  const int Vh = (int)(z.numel() / (2 * R * C));
+  ok(ncnet_combine_bwd((float*)g.data_ptr(), (float*)z.data_ptr(), gz.data_ptr(), const_cast<void*>(opt_ptr<void>(gzl)), Vh, R, C,
+                       cur_stream(z)),
+     "combine_bwd");
 }
 
 // norm: 1 'softmax', 2 'l1' (eps), 0 None -- rse / cse from stats with the matching sum_kind
@@ -608,6 +668,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pad_planes", &pad_planes);
   m.def("conv1x16", &conv1x16);
   m.def("conv16_blk_fwd", &conv16_blk_fwd);
+  m.def("conv16_fwd_x3", &conv16_fwd_x3);
+  m.def("conv16_blk_fwd_x3", &conv16_blk_fwd_x3);
   m.def("wgrad16p", &wgrad16p);
   m.def("wgrad16", &wgrad16);
   m.def("ijpack", &ijpack);
@@ -624,7 +686,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mm_apply", &mm_apply);
   m.def("mm_bwd", &mm_bwd);
   m.def("combine_fwd", &combine_fwd);
-  m.def("combine_bwd", &combine_bwd);
+  m.def("combine_bwd", &combine_bwd, py::arg("g"), py::arg("z"), py::arg("gz"), py::arg("R"), py::arg("C"),
+        py::arg("gzl") = py::none());
   m.def("softmax_max_bwd", &softmax_max_bwd);
   m.def("maxpool4d", &maxpool4d);
   m.def("transpose", &transpose);

@@ -29,7 +29,12 @@ namespace ncnet {
 // EPI_BLK1: Cout = 1 layer in output-plane-block mode (conv16v2 only, below):
 // the 16 MFMA rows are a 4 x 4 block of output (i, j) planes; fp32 single-channel
 // output with bias (+ ReLU).
-enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32X16 = 4, EPI_BLK1 = 8 };
+// EPI_X3 (flag, with EPI_BIAS_RELU / EPI_MASK / EPI_BLK1): fp32-accurate "bf16x3"
+// layer -- the kernel runs three phases into the same accumulators,
+// (X_hi, W_hi), (X_hi, W_lo), (X_lo, W_hi), with X_lo = X + g.xlo and the lo
+// weight planes stored right after the hi ones; the bf16-block epilogues write
+// the result split as hi = bf16(y) at Y and lo = bf16(y - hi) at Y + g.ylo.
+enum Epi { EPI_NONE = 0, EPI_BIAS_RELU = 1, EPI_MASK = 2, EPI_F32X16 = 4, EPI_BLK1 = 8, EPI_X3 = 64 };
 
 struct ConvGeom {
   int V, I, J, K, L;  // volume dims
@@ -46,6 +51,8 @@ struct ConvGeom {
   int nt;             // v2 / v3 epilogues: non-temporal output stores (NCNET_NT_STORE)
   int nib;            // EPI_BLK1: 4-plane output blocks along i (njb: along j)
   int relu;           // EPI_BLK1: ReLU after the bias
+  long long xlo;      // EPI_X3: element offset of X_lo from X
+  long long ylo;      // EPI_X3: element offset of the lo output from Y
 };
 
 // Decode the workgroup's output tile.
@@ -73,9 +80,11 @@ __device__ __forceinline__ size_t plane_offset(const ConvGeom& g, int v, int i, 
 template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
                                         const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0,
-                                        int nco = 16, bool nt = false) {
+                                        int nco = 16, bool nt = false, long long ylo = 0) {
   if (!NCNET_OK(vox_index < nvox_all && co0 >= 0 && co0 + 4 <= 16)) return;
-  if (EPI == EPI_F32X16) {
+  constexpr bool X3 = (EPI & EPI_X3) != 0;
+  constexpr int E = EPI & ~EPI_X3;
+  if (E == EPI_F32X16) {
     // channel-planar fp32 [nco][nvox_all] (only the channels a consumer reads):
     // 16 lanes write 16 consecutive voxels of one channel
 #pragma unroll
@@ -91,10 +100,11 @@ __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, 
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float x = acc[r];
-    if (EPI == EPI_BIAS_RELU) x = fmaxf(x + bias[co0 + r], 0.f);
+    if (E == EPI_BIAS_RELU) x = fmaxf(x + bias[co0 + r], 0.f);
     o[r] = x;
   }
-  if (EPI == EPI_MASK) {
+  if (E == EPI_MASK) {
+    // (X3: the mask is the hi part of the ReLU output -- bf16(y) > 0 iff y > 0)
     bf16x4 m = *(const bf16x4*)(M + vox_index * 16 + co0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) o[r] = ((float)m[r] > 0.f) ? o[r] : 0.f;
@@ -104,6 +114,14 @@ __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, 
   for (int r = 0; r < 4; ++r) out[r] = f2bf(o[r]);
   if (nt) __builtin_nontemporal_store(__builtin_bit_cast(u32x2, out), (u32x2*)(Y + vox_index * 16 + co0));
   else *(bf16x4*)(Y + vox_index * 16 + co0) = out;
+  if constexpr (X3) {
+    bf16x4 lo;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lo[r] = f2bf(o[r] - bf2f(out[r]));
+    bf16* yl = Y + ylo + vox_index * 16 + co0;
+    if (nt) __builtin_nontemporal_store(__builtin_bit_cast(u32x2, lo), (u32x2*)yl);
+    else *(bf16x4*)yl = lo;
+  }
 }
 
 // ===========================================================================
@@ -140,7 +158,9 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
   char* wbuf = smem + 2 * plane_bytes;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr bool BLK = EPI == EPI_BLK1;
+  constexpr bool BLK = (EPI & ~EPI_X3) == EPI_BLK1;
+  constexpr bool X3 = (EPI & EPI_X3) != 0;
+  constexpr int PH = X3 ? 3 : 1;   // EPI_X3: phases (X_hi, W_hi), (X_hi, W_lo), (X_lo, W_hi)
   constexpr int SP = KS + 3;   // EPI_BLK1: input planes per block side (4 + KS - 1)
   TileId t;
   if (BLK) {
@@ -160,7 +180,8 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
   const int dj_lo = BLK ? max(0, t.j - P) : max(0, P - t.j);
   const int dj_hi = BLK ? min(g.J, t.j + 4 + P) : min(KS, g.J + P - t.j);
   const int ndj = dj_hi - dj_lo;
-  const int nplanes = g.npg > 0 ? g.npg : (di_hi - di_lo) * ndj;
+  const int nplanes1 = g.npg > 0 ? g.npg : (di_hi - di_lo) * ndj;   // planes of one phase
+  const int nplanes = PH * nplanes1;
   const int nvox = g.TK * g.TL;
   const int ntile = (nvox + 15) >> 4;
 
@@ -195,30 +216,43 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
   (void)xext;
   // plane s of output j-tile t.j + jt (jt > 0 only in multi-tile group-plane mode)
   auto issue_x = [&](int jt, int s, char* buf) {
+    const bf16* xb = X;
+    if constexpr (X3) {
+      const int ph = s / nplanes1;
+      s -= ph * nplanes1;
+      if (ph == 2) xb = X + g.xlo;
+    }
     const bf16* xp;
     if (BLK) {
-      xp = X + plane_offset(g, t.v, di_lo + s / ndj, dj_lo + s % ndj, 16);
+      xp = xb + plane_offset(g, t.v, di_lo + s / ndj, dj_lo + s % ndj, 16);
     } else if (g.npg > 0) {
-      xp = X + s * g.gstride + plane_offset(g, t.v, t.i, t.j + jt, 16);
+      xp = xb + s * g.gstride + plane_offset(g, t.v, t.i, t.j + jt, 16);
     } else {
       const int di = di_lo + s / ndj, dj = dj_lo + s % ndj;
-      xp = X + plane_offset(g, t.v, t.i + di - P, t.j + jt + dj - P, 16);
+      xp = xb + plane_offset(g, t.v, t.i + di - P, t.j + jt + dj - P, 16);
     }
     for (int r = wave; r < g.PR; r += NW) {
       const int kg = t.k0 - P + r;
       if (kg >= 0 && kg < g.K && lane < nchunk) {
         const bf16* src = xp + ((size_t)kg * g.L + lstart) * 16 + lane * 8;
-        if (NCNET_OK((size_t)(src - X) + 8 <= xext) &&
+        if (NCNET_OK((size_t)(src - xb) + 8 <= xext) &&
             NCNET_OK((r * g.RS + col0) * 32 + lane * 16 + 16 <= plane_bytes))
           __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(void, buf + (r * g.RS + col0) * 32), 16, 0, 0);
       }
     }
   };
+  const int nwp = BLK ? SP * SP : g.npg > 0 ? g.npg : NT;   // weight planes of one set
   auto issue_w = [&](int s) {
+    int wset = 0;
+    if constexpr (X3) {
+      const int ph = s / nplanes1;
+      s -= ph * nplanes1;
+      wset = ph == 1 ? nwp : 0;   // phase 1 reads the lo weight planes
+    }
     const int wplane = BLK ? (di_lo + s / ndj - (t.i - P)) * SP + dj_lo + s % ndj - (t.j - P)
                            : g.npg > 0 ? s : (di_lo + s / ndj) * KS + dj_lo + s % ndj;
-    const u32x4* wp = Wp + (size_t)wplane * (NQ * 64);
-    if (NCNET_OK(wplane >= 0 && wplane < (BLK ? SP * SP : g.npg > 0 ? g.npg : NT)))
+    const u32x4* wp = Wp + (size_t)(wset + wplane) * (NQ * 64);
+    if (NCNET_OK(wplane >= 0 && wplane < nwp))
       for (int q = wave; q < NQ; q += NW)
         __builtin_amdgcn_global_load_lds((const void*)(wp + q * 64 + lane), LDS_PTR(void, wbuf + q * 1024), 16, 0, 0);
   };
@@ -263,7 +297,8 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
         int kk = vi / g.TL, ll = vi - kk * g.TL;
         int kg = t.k0 + kk, lg = t.l0 + ll;
         if (vi < nvox && kg < g.K && lg < g.L)
-          store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco, g.nt);
+          store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco, g.nt,
+                       g.ylo);
       }
     }
   };
@@ -551,7 +586,13 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
   const int ti = bid % g.I, tv = bid / g.I;
   const int k0 = kt * TK, l0 = lt * TL, j0 = jb * R;
   const int di_lo = max(0, P - ti), di_hi = min(KS, g.I + P - ti);
-  const int ntot = (di_hi - di_lo) * S;
+  // EPI_X3: the di sweep runs once per phase, (X_hi, W_hi), (X_hi, W_lo),
+  // (X_lo, W_hi), into the same accumulators; dv = phase * ndi + (di - di_lo)
+  constexpr bool X3 = (EPI & EPI_X3) != 0;
+  constexpr int PH = X3 ? 3 : 1;
+  const int ndi = di_hi - di_lo;   // >= 1 (di = P is always valid)
+  const int nd = PH * ndi;
+  const int ntot = nd * S;
 
   // per-lane X addresses of the current plane buffer (advanced by one buffer per
   // step): c1 = half 1 on the next voxel (taps 2q, 2q + 1 in one row; also the
@@ -596,10 +637,17 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
   }
   const size_t plane_elems = (size_t)g.K * g.L * 16;
   auto issue_x = [&](int n) {
-    const int dq = n / S, s = n - dq * S;
+    int dq = n / S;
+    const int s = n - dq * S;
     const int jp = j0 - P + s;
     const bool pv = n < ntot && jp >= 0 && jp < g.J;
-    const bf16* xp = pv ? X + plane_offset(g, tv, ti + di_lo + dq - P, jp, 16) : X;
+    const bf16* xb = X;
+    if constexpr (X3) {
+      const int ph = dq / ndi;
+      dq -= ph * ndi;
+      if (ph == 2) xb = X + g.xlo;
+    }
+    const bf16* xp = pv ? xb + plane_offset(g, tv, ti + di_lo + dq - P, jp, 16) : X;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)xp, (short)0, pv ? (int)(plane_elems * 2) : 0, 0x00020000);
     const uint32_t boff = (uint32_t)((n % 3) * PLANE);
@@ -609,21 +657,30 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + d), 16, xvo[m], 0, 0, 0);
     }
   };
-  // weight slot dj <- (di, dj) fragments; WPW DMAs per wave, always (invalid -> trash)
+  // weight slot dj <- (di, dj) fragments of step dv; WPW DMAs per wave, always
+  // (invalid -> trash).  X3: the lo weight set follows the hi one in Wp.
   const __amdgpu_buffer_rsrc_t wrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, KS * KS * NQ * 1024, 0x00020000);
-  auto issue_w = [&](int di, int dj, bool valid) {
+      __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, PH == 3 ? 2 * KS * KS * NQ * 1024 : KS * KS * NQ * 1024,
+                                        0x00020000);
+  auto issue_w = [&](int dv, int dj, bool valid) {
+    int wplane;
+    if constexpr (X3) {
+      const int ph = dv / ndi;
+      wplane = (ph == 1 ? KS * KS : 0) + (di_lo + dv - ph * ndi) * KS + dj;
+    } else {
+      wplane = (di_lo + dv) * KS + dj;
+    }
 #pragma unroll
     for (int m = 0; m < WPW; ++m) {
       const int q = wave + NW * m;
       const bool v = valid && q < NQ;
       const uint32_t d = v ? (uint32_t)((dj * NQ + q) * 1024) : (uint32_t)TRASH;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, LDS_PTR(void, smem + d), 16, (uint32_t)((q * 64 + lane) * 16),
-                                               (uint32_t)((di * KS + dj) * NQ * 1024), 0, 0);
+                                               (uint32_t)(wplane * NQ * 1024), 0, 0);
     }
   };
 
-  for (int dj = 0; dj < KS; ++dj) issue_w(di_lo, dj, true);
+  for (int dj = 0; dj < KS; ++dj) issue_w(0, dj, true);
   issue_x(0);
   issue_w(0, 0, false);   // step "-1" emulation: its weight slot (if any), then plane 1
   issue_x(1);
@@ -631,15 +688,15 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
 
   const uint32_t wb = (uint32_t)lane * 16u;
   int n = 0;
-  for (int di = di_lo; di < di_hi; ++di) {
+  for (int dv = 0; dv < nd; ++dv) {
     static_for<0, S>([&](auto sc) {
       constexpr int s = decltype(sc)::value;
       // DMAs younger than plane n: the previous step's weight slot (if any) and plane n + 1
       constexpr int YOUNGER = RPW + (v4_wstep(s == 0 ? S - 1 : s - 1, R) ? WPW : 0);
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(YOUNGER) : "memory");
       if constexpr (v4_wstep(s, R)) {
-        if constexpr (s >= R) issue_w(di + 1 < di_hi ? di + 1 : di, s - R, di + 1 < di_hi);
-        else issue_w(di, KS - 1, di > di_lo);
+        if constexpr (s >= R) issue_w(dv + 1 < nd ? dv + 1 : dv, s - R, dv + 1 < nd);
+        else issue_w(dv, KS - 1, dv > 0);
       }
       issue_x(n + 2);
       const int jp = j0 - P + s;
@@ -716,7 +773,7 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
         const int kg = k0 + kk, lg = l0 + ll;
         if (vi < NVOX && kg < g.K && lg < g.L)
           store16<EPI>(acc[r][tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco,
-                       g.nt);
+                       g.nt, g.ylo);
       }
     }
   }
@@ -875,6 +932,7 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.RW = tl + KS - 1;
   g.RS = g.RW;
   g.npg = 0; g.gstride = 0; g.nco = 16; g.oscale = 1.f;
+  g.xlo = 0; g.ylo = 0;
   g.njb = J; g.tpw = 1;
   g.nib = I; g.relu = 0;
   {
@@ -920,35 +978,48 @@ static int gp_tpw() {
 // Y = sum_s conv_(dk,dl)(X[s] plane (i,j), Wp plane s): the (di, dj) offsets
 // live in the channels (ij encoding, csrc/jshift.hip) or s indexes 16-channel
 // input blocks of a wider layer.
+//
+// epi | EPI_X3 (KS 3 / 5, epi 1 or 2): the bf16x3 layer, X_lo = X + xlo,
+// Wp = [hi planes; lo planes], split output Y / Y + ylo (elements).
 extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias, const void* M, void* Y,
                                 int V, int I, int J, int K, int L, int KS, int epi, int npg, int nco,
-                                hipStream_t stream) {
+                                long long xlo, long long ylo, hipStream_t stream) {
   int tk, tl;
   pick_tile(K, L, tk, tl);
   ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl);
   g.npg = npg;
   g.gstride = (long long)V * I * J * K * L * 16;
   g.nco = nco;
+  g.xlo = xlo; g.ylo = ylo;
   if (g.RW > 32) return -1;   // one LDS-DMA wave-instruction per staged row
+  const bool x3 = (epi & EPI_X3) != 0;
+  if (x3 && !((KS == 5 || KS == 3) && ((epi & ~EPI_X3) == EPI_BIAS_RELU || (epi & ~EPI_X3) == EPI_MASK))) return -2;
   // Row stride RS = TL + 8: a 16-voxel tile that wraps to the next row then
   // jumps 256 B (the full 64-bank period), so every ds_read_b128 lane group
   // stays conflict-free (a TL + KS - 1 stride cost ~1/3 extra LDS cycles).
   g.RS = tl + ((KS - 1 + 7) / 8) * 8;
   const int nq = (KS * KS + 1) / 2;
   const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
-  if (npg == 0 && (epi == EPI_BIAS_RELU || epi == EPI_MASK) && (KS == 5 || KS == 3)) {
+  if (npg == 0 && (epi & ~EPI_X3) != EPI_NONE && (epi & ~EPI_X3) != EPI_F32X16 && (KS == 5 || KS == 3)) {
     // full (di, dj) sum: R = 5 output j-planes per workgroup, X reused across dj
     constexpr int R = 5;
+    const int njb1 = g.njb;
     g.njb = cdiv(J, R);
     dim3 grid3((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block3(512);
     if (tk == 25 && tl == 25 && KS == 5 && !getenv_flag("NCNET_CONV_V3")) {
       // compile-time 25 x 25 tile: pipelined fragments, triple-buffered planes
       size_t lds4 = 3 * (size_t)(25 + 4) * 33 * 32 + (size_t)5 * nq * 1024 + 1024;
 #define L16V4(EPIV) hipLaunchKernelGGL((conv16v4_fwd_kernel<5, R, EPIV, 25, 25>), grid3, block3, lds4, stream, x, w, bias, m, y, g)
-      if (epi == EPI_BIAS_RELU) L16V4(EPI_BIAS_RELU); else L16V4(EPI_MASK);
+      if (epi == EPI_BIAS_RELU) L16V4(EPI_BIAS_RELU);
+      else if (epi == EPI_MASK) L16V4(EPI_MASK);
+      else if (epi == (EPI_BIAS_RELU | EPI_X3)) L16V4(EPI_BIAS_RELU | EPI_X3);
+      else L16V4(EPI_MASK | EPI_X3);
 #undef L16V4
       return (int)hipGetLastError();
     }
+    g.njb = njb1;
+    if (x3) goto v2_x3;   // other shapes: the v2 kernel's phases
+    g.njb = cdiv(J, R);
     size_t lds3 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)KS * nq * 1024;
 #define L16V3(KSV, EPIV) hipLaunchKernelGGL((conv16v3_fwd_kernel<KSV, R, EPIV>), grid3, block3, lds3, stream, x, w, bias, m, y, g)
     if (KS == 5) { if (epi == EPI_BIAS_RELU) L16V3(5, EPI_BIAS_RELU); else L16V3(5, EPI_MASK); }
@@ -956,12 +1027,21 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
 #undef L16V3
     return (int)hipGetLastError();
   }
+v2_x3: {
   size_t lds2 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
   // group planes: tpw consecutive output j-tiles per workgroup (NCNET_GP_TPW,
   // default 5): the next tile's first plane DMA overlaps the current epilogue
   const bool mt = npg > 0 && gp_tpw() > 1;
   if (mt) { g.tpw = gp_tpw(); g.njb = cdiv(J, g.tpw); }
   dim3 grid2((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block2(512);
+  if (x3) {
+#define L16V2X(KSV, EPIV) do { if (mt) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, true>), grid2, block2, lds2, stream, x, w, bias, m, y, g); \
+                               else hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, false>), grid2, block2, lds2, stream, x, w, bias, m, y, g); } while (0)
+    if (KS == 5) { if (epi == (EPI_BIAS_RELU | EPI_X3)) L16V2X(5, EPI_BIAS_RELU | EPI_X3); else L16V2X(5, EPI_MASK | EPI_X3); }
+    else { if (epi == (EPI_BIAS_RELU | EPI_X3)) L16V2X(3, EPI_BIAS_RELU | EPI_X3); else L16V2X(3, EPI_MASK | EPI_X3); }
+#undef L16V2X
+    return (int)hipGetLastError();
+  }
 #define L16V2E(KSV, EPIV) do { if (mt) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, true>), grid2, block2, lds2, stream, x, w, bias, m, y, g); \
                                else hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPIV, false>), grid2, block2, lds2, stream, x, w, bias, m, y, g); } while (0)
 #define L16V2(KSV, _) do { if (epi == EPI_BIAS_RELU) L16V2E(KSV, EPI_BIAS_RELU); else if (epi == EPI_MASK) L16V2E(KSV, EPI_MASK); \
@@ -971,17 +1051,21 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
 #undef L16V2E
   return (int)hipGetLastError();
 }
+}
 
 // Cout = 1 layer (16 input channels) in output-plane-block mode: Y fp32
 // [V,I,J,K,L] = act(bias + conv(X, W)); Wp [(KS+3)^2 relative planes][nq][64][8]
 // (ops/packing.py blk_out_weights): the 16 MFMA rows are a 4 x 4 block of output
 // planes, so every input plane staged in LDS feeds up to 16 output planes and
 // no combo-planar partials (ij encoding + ijsum) round-trip HBM.
+// xlo >= 0 ... any value with x3 != 0: the bf16x3 layer (X_lo = X + xlo, Wp = [hi; lo] planes).
 extern "C" int ncnet_conv16_blk_fwd(const void* X, const void* Wp, const float* bias, float* Y, int V, int I, int J,
-                                    int K, int L, int KS, int relu, hipStream_t stream) {
+                                    int K, int L, int KS, int relu, int x3, long long xlo, hipStream_t stream) {
   int tk, tl;
   pick_tile(K, L, tk, tl);
   ConvGeom g = make_geom(V, I, J, K, L, KS, tk, tl);
+  g.xlo = xlo;
+  if (x3 && KS != 5 && KS != 3) return -2;
   if (g.RW > 32) return -1;
   g.RS = tl + ((KS - 1 + 7) / 8) * 8;
   g.nib = cdiv(I, 4); g.njb = cdiv(J, 4);
@@ -991,6 +1075,12 @@ extern "C" int ncnet_conv16_blk_fwd(const void* X, const void* Wp, const float* 
   dim3 grid((unsigned)(V * g.nib * g.njb * g.nkt * g.nlt)), block(512);
   const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp;
 #define LBLK(KSV, _) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPI_BLK1, false>), grid, block, lds2, stream, x, w, bias, nullptr, (bf16*)Y, g)
+#define LBLKX(KSV) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPI_BLK1 | EPI_X3, false>), grid, block, lds2, stream, x, w, bias, nullptr, (bf16*)Y, g)
+  if (x3) {
+    if (KS == 5) LBLKX(5); else LBLKX(3);
+    return (int)hipGetLastError();
+  }
+#undef LBLKX
   KS_DISPATCH(LBLK, 0);
 #undef LBLK
   return (int)hipGetLastError();

@@ -259,9 +259,17 @@ __global__ __launch_bounds__(256) void combine_fwd_kernel(const float* __restric
   }
 }
 
-// gz[v] = g[v] * (z[v] > 0), gz[v+Vh] = g[v]^T * (z[v+Vh] > 0) as bf16.
+// gz[v] = g[v] * (z[v] > 0), gz[v+Vh] = g[v]^T * (z[v+Vh] > 0) as bf16; with
+// gzl (bf16x3 training): also the residual gzl = bf16(value - gz).
+__device__ __forceinline__ void put_split(bf16* __restrict__ gz, bf16* __restrict__ gzl, size_t o, float x) {
+  const bf16 h = f2bf(x);
+  gz[o] = h;
+  if (gzl) gzl[o] = f2bf(x - bf2f(h));
+}
+
 __global__ __launch_bounds__(256) void combine_bwd_kernel(const float* __restrict__ g, const float* __restrict__ z,
-                                                          bf16* __restrict__ gz, int Vh, int R, int C) {
+                                                          bf16* __restrict__ gz, bf16* __restrict__ gzl, int Vh, int R,
+                                                          int C) {
   __shared__ float tile[64][65];
   const int ntr = (R + 63) / 64, ntc = (C + 63) / 64;
   int b = blockIdx.x;
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(256) void combine_bwd_kernel(const float* __restric
     float gv = 0.f;
     if (rr < R && cc < C) {
       gv = g[vb1 + (size_t)rr * C + cc];
-      gz[vb1 + (size_t)rr * C + cc] = f2bf(z[vb1 + (size_t)rr * C + cc] > 0.f ? gv : 0.f);
+      put_split(gz, gzl, vb1 + (size_t)rr * C + cc, z[vb1 + (size_t)rr * C + cc] > 0.f ? gv : 0.f);
     }
     tile[rl][tx] = gv;
   }
@@ -284,7 +292,7 @@ __global__ __launch_bounds__(256) void combine_bwd_kernel(const float* __restric
     int cc = c0 + cl, rr = r0 + tx;
     if (cc < C && rr < R) {
       size_t o = vb2 + (size_t)cc * R + rr;
-      gz[o] = f2bf(z[o] > 0.f ? tile[tx][cl] : 0.f);
+      put_split(gz, gzl, o, z[o] > 0.f ? tile[tx][cl] : 0.f);
     }
   }
 }
@@ -433,8 +441,10 @@ extern "C" int ncnet_combine_fwd(const float* z, float* y, int Vh, int R, int C,
   hipLaunchKernelGGL(combine_fwd_kernel, dim3(tiles64(Vh, R, C)), dim3(256), 0, s, z, y, Vh, R, C);
   return (int)hipGetLastError();
 }
-extern "C" int ncnet_combine_bwd(const float* g, const float* z, void* gz, int Vh, int R, int C, hipStream_t s) {
-  hipLaunchKernelGGL(combine_bwd_kernel, dim3(tiles64(Vh, R, C)), dim3(256), 0, s, g, z, (bf16*)gz, Vh, R, C);
+extern "C" int ncnet_combine_bwd(const float* g, const float* z, void* gz, void* gzl, int Vh, int R, int C,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(combine_bwd_kernel, dim3(tiles64(Vh, R, C)), dim3(256), 0, s, g, z, (bf16*)gz, (bf16*)gzl, Vh, R,
+                     C);
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_softmax_max_bwd(const float* x, const float* rmax, const int* rarg, const float* rse,

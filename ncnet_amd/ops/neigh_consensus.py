@@ -786,6 +786,165 @@ class NeighConsensusX3Fn(torch.autograd.Function):
 
 
 # ---------------------------------------------------------------------------
+# fp32-accurate training on the fused bf16x3 kernels (csrc/conv4d_fwd.hip
+# EPI_X3).  Every activation and gradient between layers is kept as a hi / lo
+# bf16 pair (x = hi + lo to ~16 mantissa bits); each Conv4d is ONE launch that
+# runs the three phases (X_hi, W_hi), (X_hi, W_lo), (X_lo, W_hi) into its fp32
+# accumulators and writes the split result from its epilogue (bias + ReLU, or
+# the previous layer's ReLU mask for data gradients).  Weight gradients are the
+# three (X, G) products on the bf16 wgrad kernels, summed.  Covers the
+# 1 -> (16 ->)* 1 stacks with KS 3 / 5 (every NC-Net config); others use
+# NeighConsensusX3Fn's per-conv path.
+
+def _wsplit(w: torch.Tensor):
+    hi = w.to(torch.bfloat16).float()
+    return hi, w - hi
+
+
+def _pack2(fn, w: torch.Tensor) -> torch.Tensor:
+    """[2, ...] packed weights: the hi set, then the lo set (the kernels' layout)."""
+    hi, lo = _wsplit(w)
+    return torch.stack((fn(hi), fn(lo))).contiguous()
+
+
+def x3_fused_ok(kinds, channels, kernel_sizes, x: torch.Tensor, symmetric: bool) -> bool:
+    I, J, K, L = x.shape[2:6]
+    return (kinds is not None and len(kinds) >= 2 and kinds[0] == "1in" and kinds[-1] == "1out"
+            and all(k == "16" for k in kinds[1:-1]) and max(channels) <= 16
+            and all(k in (3, 5) for k in kernel_sizes) and symmetric and (I, J) == (K, L))
+
+
+def _split_bf16(t: torch.Tensor, out: torch.Tensor):
+    """fp32 t -> out[0] = bf16(t), out[1] = bf16(t - out[0])."""
+    out[0].copy_(t)
+    out[1].copy_(t - out[0].float())
+    return out
+
+
+class NeighConsensusX3FusedFn(torch.autograd.Function):
+    """fp32-accurate TRAINING NeighConsensus (symmetric, square volumes) on the
+    fused bf16x3 kernels; same math as NeighConsensusX3Fn."""
+
+    @staticmethod
+    def forward(ctx, x, kinds, channels, *params):
+        C = _ext.ext()
+        ws = [_std(w) for w in params[0::2]]
+        bs = params[1::2]
+        V, _, I, J, K, L = x.shape
+        R, Cc = I * J, K * L
+        x0 = x.reshape(V, I, J, K, L).float()
+        x0 = torch.cat((x0, x0.permute(0, 3, 4, 1, 2)), 0)      # both symmetric branches
+        shp = tuple(x0.shape)
+        dev = x.device
+        xsp = torch.empty((2,) + shp, dtype=torch.bfloat16, device=dev)
+        _split_bf16(x0, xsp)
+        del x0
+        ks0 = ws[0].shape[-1]
+        xs = torch.empty((2, ij_groups(ks0)) + shp + (16,), dtype=torch.bfloat16, device=dev)
+        C.ijpack(xsp[0], xs[0], ks0, 1)
+        C.ijpack(xsp[1], xs[1], ks0, 1)
+        del xsp
+        saved = [xs]
+        h = None
+        for li, kind in enumerate(kinds):
+            w, b = ws[li], bs[li]
+            ks = w.shape[-1]
+            if kind == "1out":
+                y = torch.empty(shp, dtype=torch.float32, device=dev)
+                C.conv16_blk_fwd_x3(h[0], h[1], _pack2(lambda t: pack_w16_planes(blk_out_weights(t)), w),
+                                    b.float().reshape(1).contiguous(), y, ks, 1)
+                h = y
+                break
+            a = torch.empty((2,) + shp + (16,), dtype=torch.bfloat16, device=dev)
+            if kind == "1in":
+                C.conv16_fwd_x3(xs[0], xs[1], _pack2(lambda t: pack_w16_planes(ij_in_weights(t)), w),
+                                _pad_bias(b, 16), None, a[0], a[1], ks, 1)
+            else:
+                C.conv16_fwd_x3(h[0], h[1], _pack2(pack_w16, w), _pad_bias(b, 16), None, a[0], a[1], ks, 1)
+            saved.append(a)
+            h = a
+        z = h                                                      # [2V, I, J, K, L] fp32 (ReLU'd)
+        y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=dev)
+        C.combine_fwd(z.reshape(-1), y, R, Cc)
+        ctx.kinds, ctx.channels, ctx.dims = kinds, channels, (V, I, J, K, L)
+        ctx.save_for_backward(z, *params, *saved)
+        return y.reshape(V, 1, I, J, K, L)
+
+    @staticmethod
+    def backward(ctx, gy):
+        C = _ext.ext()
+        kinds, channels = ctx.kinds, ctx.channels
+        nl = len(kinds)
+        z, *rest = ctx.saved_tensors
+        params, saved = rest[:2 * nl], rest[2 * nl:]
+        ws = [_std(w) for w in params[0::2]]
+        V, I, J, K, L = ctx.dims
+        R, Cc = I * J, K * L
+        shp = tuple(z.shape)
+        dev = z.device
+        g = torch.empty((2,) + shp, dtype=torch.bfloat16, device=dev)   # d/d(last pre-activation), hi / lo
+        C.combine_bwd(gy.reshape(V, R, Cc).float().contiguous(), z, g[0], R, Cc, g[1])
+        xs = saved[0]
+        acts = saved[1:]                                              # per hidden layer: [2, 2V, ..., 16]
+        dws, dbs = [None] * nl, [None] * nl
+        gx = None
+        main = side = None
+        if BWD_OVERLAP and z.is_cuda:
+            main = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+        for li in range(nl - 1, -1, -1):
+            kind, w = kinds[li], ws[li]
+            ks = w.shape[-1]
+            cout = channels[li]
+            cin = 1 if li == 0 else channels[li - 1]
+            xin = xs if li == 0 else acts[li - 1]                     # [2, (G,) 2V, ..., 16]
+            gs = None
+            if kind == "1out":
+                gs = torch.empty((2, ij_groups(ks)) + shp + (16,), dtype=torch.bfloat16, device=dev)
+                C.ijpack(g[0], gs[0], ks, -1)
+                C.ijpack(g[1], gs[1], ks, -1)
+            # the three (X, G) products; the bias gradient is sum(G_hi) + sum(G_lo)
+            if kind == "1out":
+                combos = [(xin[0:1], g[0], gs[0]), (xin[0:1], g[1], gs[1]), (xin[1:2], g[0], gs[0])]
+            elif kind == "1in":
+                combos = [(xin[0], g[0:1], None), (xin[0], g[1:2], None), (xin[1], g[0:1], None)]
+            else:
+                combos = [(xin[0:1], g[0:1], None), (xin[0:1], g[1:2], None), (xin[1:2], g[0:1], None)]
+            on_side = li > 0
+            with _OnSide(main if on_side else None, side if on_side else None,
+                         tuple(t for t in (xin, g, gs) if t is not None)):
+                res = [_layer_wgrad(C, kind, xi, gi, gsi, ks, cin, cout) for xi, gi, gsi in combos]
+                dws[li] = ref.conv4d_weight_from_std(res[0][0] + res[1][0] + res[2][0])
+                dbs[li] = res[0][1] + res[1][1]
+            if li == 0:
+                if ctx.needs_input_grad[0]:
+                    wt = transpose_for_dgrad(w)
+                    gx = (conv_layer(g[0:1], _wsplit(wt)[0], cout, 1, relu=False)
+                          + conv_layer(g[0:1], _wsplit(wt)[1], cout, 1, relu=False)
+                          + conv_layer(g[1:2], _wsplit(wt)[0], cout, 1, relu=False))
+                break
+            gn = torch.empty((2,) + shp + (16,), dtype=torch.bfloat16, device=dev)
+            if kind == "1out":
+                wp2 = _pack2(lambda t: pack_w16_planes(plane_dgrad_weights(ij_out_weights(t))), w)
+                C.conv16_fwd_x3(gs[0], gs[1], wp2, None, xin[0], gn[0], gn[1], ks, 2)
+            else:
+                C.conv16_fwd_x3(g[0], g[1], _pack2(pack_w16, transpose_for_dgrad(w)), None, xin[0], gn[0], gn[1],
+                                ks, 2)
+            g = gn
+        if side is not None:
+            main.wait_stream(side)
+            for t in dws + dbs:
+                t.record_stream(main)
+        if gx is not None:
+            gx = gx[:V] + gx[V:].permute(0, 3, 4, 1, 2)
+            gx = gx.reshape(V, 1, I, J, K, L)
+        grads = []
+        for dw, db in zip(dws, dbs):
+            grads += [dw, db]
+        return (gx, None, None, *grads)
+
+
+# ---------------------------------------------------------------------------
 # fp8 inference path (BASELINE config 5): OCP e4m3 activations and weights on
 # the fp8 MFMA conv kernel, ij encoding for the 1-channel layers.
 
@@ -1018,6 +1177,10 @@ def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool 
                     params = []
                     for w, b in zip(weights, biases):
                         params += [w, b]
+                    if x3_fused_ok(kinds, channels, kernel_sizes, x, symmetric):
+                        _ext.count("nc_x3_fused")
+                        return NeighConsensusX3FusedFn.apply(x.float().contiguous(), tuple(kinds), tuple(channels),
+                                                             *params)
                     return NeighConsensusX3Fn.apply(x.float().contiguous(), symmetric, tuple(kinds),
                                                     tuple(channels), *params)
                 return neigh_consensus_x3(x, weights, biases, channels, symmetric)

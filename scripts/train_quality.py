@@ -83,10 +83,13 @@ def run(args):
         if p.dim() == 1:
             p.data.uniform_(0.0, 0.05)
     m_r = copy.deepcopy(m_h)
-    if args.nc_precision == "fp32":      # fp32-accurate HIP training: fp32 trunk, bf16x3 correlation + NC
+    if args.nc_precision == "fp32":      # fp32-accurate HIP training: bf16x3 correlation + NC
         m_h.nc_precision = "fp32"
-        m_h.compute_dtype = torch.float32
-    alg = ReferenceAlgorithm(m_r, torch.float32, conv=ref.conv4d)   # same fp32 sums, k conv3d per layer
+        m_h.compute_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[args.hip_trunk]
+    rdt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[args.ref_dtype]
+    alg = ReferenceAlgorithm(m_r, rdt, conv=ref.conv4d)   # same sums as the reference, k conv3d per layer
+    # fp16 autocast needs loss scaling (the weak loss is ~1e-8 in this regime)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 24) if args.ref_dtype == "fp16" else None
     p_h = [p for p in m_h.parameters() if p.requires_grad]
     p_r = [p for p in m_r.parameters() if p.requires_grad]
     opt_h = make_adam(p_h, args.lr)
@@ -111,8 +114,13 @@ def run(args):
         opt_h.step()
         opt_r.zero_grad(set_to_none=True)
         loss_r = reference_weak_loss(alg, batch)
-        loss_r.backward()
-        opt_r.step()
+        if scaler is None:
+            loss_r.backward()
+            opt_r.step()
+        else:
+            scaler.scale(loss_r).backward()
+            scaler.step(opt_r)
+            scaler.update()
         lh.append(float(loss.detach()))
         lr_.append(float(loss_r.detach()))
         if step % 5 == 0 or step == args.steps - 1:
@@ -154,6 +162,10 @@ def main(argv=None):
     ap.add_argument("--last-layer", type=str, default="", help="trunk cut (default layer3, the reference's)")
     ap.add_argument("--nc-precision", choices=["bf16", "fp32"], default="bf16",
                     help="HIP run's NeighConsensus precision (fp32: bf16x3 forward+backward)")
+    ap.add_argument("--hip-trunk", choices=["bf16", "fp32"], default="fp32",
+                    help="trunk dtype of the --nc-precision fp32 HIP run (the trunk is frozen)")
+    ap.add_argument("--ref-dtype", choices=["fp32", "bf16", "fp16"], default="fp32",
+                    help="the reference run's compute dtype (bf16 / fp16: autocast; fp16 with loss scaling)")
     ap.add_argument("--out", type=str, default="")
     a = ap.parse_args(argv)
     res = run(a)

@@ -161,13 +161,48 @@ def combine_fwd(z, y, R, C):
     y.view(Vh, R, C).copy_(z1 + z2.transpose(1, 2))
 
 
-def combine_bwd(g, z, gz, R, C):
+def combine_bwd(g, z, gz, R, C, gzl=None):
     z = z.reshape(-1)
     Vh = g.numel() // (R * C)
     z1, z2 = z[:Vh * R * C].view(Vh, R, C), z[Vh * R * C:].view(Vh, C, R)
     g3 = g.view(Vh, R, C)
-    gz[:Vh * R * C].view(Vh, R, C).copy_(g3 * (z1 > 0))
-    gz[Vh * R * C:].view(Vh, C, R).copy_(g3.transpose(1, 2) * (z2 > 0))
+    full = torch.cat(((g3 * (z1 > 0)).reshape(-1), (g3.transpose(1, 2) * (z2 > 0)).reshape(-1)))
+    gz.reshape(-1).copy_(full)
+    if gzl is not None:
+        gzl.reshape(-1).copy_(full - gz.reshape(-1).float())
+
+
+def _split_into(out_hi, out_lo, y):
+    out_hi.copy_(y)
+    out_lo.copy_(y - out_hi.double())
+
+
+def conv16_fwd_x3(X, Xl, Wp2, bias, M, Y, Yl, ks, epi):
+    """bf16x3 layer: conv(Xh, Wh) + conv(Xh, Wl) + conv(Xl, Wh) in fp64, then the
+    epilogue, written split (hi, lo)."""
+    shp = tuple(Y.shape)
+    outs = []
+    for xx, ww in ((X, Wp2[0]), (X, Wp2[1]), (Xl, Wp2[0])):
+        z = torch.empty((16,) + shp[:5], dtype=torch.float32)
+        conv16_fwd(xx, ww, None, None, z, ks, 4)
+        outs.append(z.double())
+    y = (outs[0] + outs[1] + outs[2]).permute(1, 2, 3, 4, 5, 0)
+    if epi == 1:
+        y = torch.relu(y + bias.double())
+    else:
+        y = y * (M.double() > 0)
+    _split_into(Y, Yl, y)
+
+
+def conv16_blk_fwd_x3(X, Xl, Wp2, bias, Y, ks, relu):
+    acc = 0
+    for xx, ww in ((X, Wp2[0]), (X, Wp2[1]), (Xl, Wp2[0])):
+        z = torch.empty(Y.shape, dtype=torch.float64)
+        conv16_blk_fwd(xx, ww, None, z, ks, 0)
+        acc = acc + z
+    if bias is not None:
+        acc = acc + float(bias.reshape(-1)[0])
+    Y.copy_(torch.relu(acc) if relu else acc)
 
 
 def transpose(x, y):
@@ -178,6 +213,8 @@ class EmuExt:
     """Namespace with the binding names used by ops/neigh_consensus.py and ops/conv4d.py."""
     conv16_fwd = staticmethod(conv16_fwd)
     conv16_blk_fwd = staticmethod(conv16_blk_fwd)
+    conv16_fwd_x3 = staticmethod(conv16_fwd_x3)
+    conv16_blk_fwd_x3 = staticmethod(conv16_blk_fwd_x3)
     wgrad16 = staticmethod(wgrad16)
     wgrad16p = staticmethod(wgrad16p)
     ijpack = staticmethod(ijpack)

@@ -168,3 +168,39 @@ def test_nc_x3_training_gradients(emu, ks, ch):
     errs = {"y": rl2(y, yr)}
     errs.update({f"g{i}": rl2(a, b) for i, (a, b) in enumerate(zip(got, want))})
     assert max(errs.values()) < 1e-3, errs
+
+
+@pytest.mark.parametrize("ks,ch", [((5, 5, 5), (16, 16, 1)), ((3, 3), (16, 1)), ((3, 3, 3), (10, 10, 1))])
+def test_nc_x3_fused_training_gradients(emu, ks, ch):
+    """The fused bf16x3 training NC (one kernel per conv with the three phases,
+    split hi / lo activations and gradients) against autograd of the fp64
+    oracle, through the dispatcher (precision='fp32', parameters requiring grad)."""
+    from ncnet_amd.ops.neigh_consensus import neigh_consensus
+    torch.manual_seed(5)
+    ws, bs = _params(ks, ch, "mixed")
+    x = torch.rand(2, 1, 5, 4, 5, 4)
+    xa = x.clone().requires_grad_(True)
+    n0 = _ext.DISPATCH["nc_x3_fused"]
+    old = _ext.use_hip
+    _ext.use_hip = lambda t: True
+    try:
+        y = neigh_consensus(xa, ws, bs, list(ch), symmetric=True, precision="fp32")
+    finally:
+        _ext.use_hip = old
+    assert _ext.DISPATCH["nc_x3_fused"] == n0 + 1
+    gy = torch.randn_like(y)
+    (y * gy).sum().backward()
+    got = [xa.grad]
+    for w, b in zip(ws, bs):
+        got += [w.grad.clone(), b.grad.clone()]
+    xr = x.double().requires_grad_(True)
+    wd = [w.detach().double().requires_grad_(True) for w in ws]
+    bd = [b.detach().double().requires_grad_(True) for b in bs]
+    yr = ref.neigh_consensus(xr, wd, bd, True)
+    (yr * gy.double()).sum().backward()
+    want = [xr.grad]
+    for w, b in zip(wd, bd):
+        want += [w.grad, b.grad]
+    errs = {"y": rl2(y, yr)}
+    errs.update({f"g{i}": rl2(a, b) for i, (a, b) in enumerate(zip(got, want))})
+    assert max(errs.values()) < 1e-3, errs
