@@ -1,9 +1,13 @@
 """Typed view of the framework's runtime configuration.
 
-The CLIs keep the reference's argparse flags (Appendix A); the kernel and
-execution toggles are environment variables read at import time by the op
-modules.  ``RuntimeConfig.from_env()`` collects them in one dataclass so a
-run can log exactly which code paths it used (bench.py puts it in its JSON).
+The CLIs keep the reference's argparse flags (Appendix A); the execution
+toggles are environment variables read HERE, once, when the op modules are
+imported (``RUNTIME``) -- the op modules read no environment themselves --
+and the dataclass is logged so a run records exactly which code paths it used
+(bench.py puts it in its JSON).  The kernel launchers' tuning switches
+(non-temporal stores, group-plane tiles per workgroup, A/B kernel variants)
+live in csrc/common.h NcnetTuning, seeded from NCNET_* once and changed
+in-process with ``_ext.ext().set_tuning``.
 """
 from __future__ import annotations
 
@@ -23,6 +27,7 @@ class RuntimeConfig:
     nt_store: bool = True            # NCNET_NT_STORE: non-temporal Conv4d epilogue stores
     bwd_overlap: bool = True         # NCNET_BWD_OVERLAP: NC weight gradients on a side stream
     trunk_prefetch: bool = True      # NCNET_TRUNK_PREFETCH: next batch's frozen backbone on a side stream
+    nc_fused: bool = True            # NCNET_NC_FUSED: fused (3,3)/(<=16,1) inference NeighConsensus kernel
 
     @classmethod
     def from_env(cls, env=None) -> "RuntimeConfig":
@@ -35,7 +40,11 @@ class RuntimeConfig:
                    gp_tpw=int(e.get("NCNET_GP_TPW", "5")),
                    nt_store=e.get("NCNET_NT_STORE", "1") != "0",
                    bwd_overlap=e.get("NCNET_BWD_OVERLAP", "1") == "1",
-                   trunk_prefetch=e.get("NCNET_TRUNK_PREFETCH", "1") == "1")
+                   trunk_prefetch=e.get("NCNET_TRUNK_PREFETCH", "1") == "1",
+                   nc_fused=e.get("NCNET_NC_FUSED", "1") != "0")
 
     def as_dict(self) -> dict:
         return dataclasses.asdict(self)
+
+
+RUNTIME = RuntimeConfig.from_env()

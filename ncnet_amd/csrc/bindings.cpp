@@ -11,6 +11,7 @@
 extern "C" {
 int ncnet_conv16_fwd(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int,
                      long long, long long, hipStream_t);
+int ncnet_set_tuning(const char*, int, int);
 int ncnet_conv16_blk_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, int, long long,
                          hipStream_t);
 int ncnet_wgrad16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
@@ -124,8 +125,7 @@ bool conv1x16(Tensor Xp, Tensor Wa, c10::optional<Tensor> bias, c10::optional<Te
   TORCH_CHECK(epi == 1 || epi == 2, "conv1x16: epi must be 1 or 2");
   if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
   if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", {V, I, J, K, L, 16}); }
-  const char* e = getenv("NCNET_NT_STORE");
-  const int nt = e ? atoi(e) : 1;
+  const int nt = ncnet_set_tuning("nt_store", 0, 0);
   const int r = ncnet_conv1x16(Xp.data_ptr(), Wa.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(),
                                (int)V, (int)I, (int)J, (int)K, (int)L, (int)ks, (int)epi, nt, cur_stream(Xp));
   if (r == -1) return false;
@@ -158,6 +158,14 @@ void conv16_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, c10::optional<T
   ok(ncnet_conv16_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(), vs[0],
                       vs[1], vs[2], vs[3], vs[4], ks, epi, (int)npg, (int)nco, 0, 0, cur_stream(X)),
      "conv16_fwd");
+}
+
+// Launcher tuning switch ``name`` (common.h NcnetTuning): returns its value
+// before the call and sets it when ``value`` is given.  A/B tests and kbench.
+int64_t set_tuning(const std::string& name, c10::optional<int64_t> value) {
+  const int old = ncnet_set_tuning(name.c_str(), value.has_value() ? (int)*value : 0, value.has_value() ? 1 : 0);
+  TORCH_CHECK(old != INT32_MIN, "set_tuning: unknown switch ", name);
+  return old;
 }
 
 // element offset of b from a (same dtype, same device): the kernels address the
@@ -669,6 +677,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x16", &conv1x16);
   m.def("conv16_blk_fwd", &conv16_blk_fwd);
   m.def("conv16_fwd_x3", &conv16_fwd_x3);
+  m.def("set_tuning", &set_tuning, py::arg("name"), py::arg("value") = py::none());
   m.def("conv16_blk_fwd_x3", &conv16_blk_fwd_x3);
   m.def("wgrad16p", &wgrad16p);
   m.def("wgrad16", &wgrad16);

@@ -364,10 +364,9 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
   // smaller grids and the 64-channel layers stay on the v1 kernel.
   // NCNET_CONV2D_VARIANT=1 / 2 forces v1 / the DMA ring (with 128-row tiles
   // unless NCNET_CONV2D_BIG is set or the grid is large).
-  const char* ev = getenv("NCNET_CONV2D_VARIANT");
-  const int variant = ev ? atoi(ev) : 0;
+  const int variant = tuning().conv2d_variant;
   const int t256 = cdiv(p.M, 256) * p.tiles_n;
-  const bool big = BN == 128 && (variant == 0 ? t256 >= 384 : (t256 >= 512 || (t256 >= 256 && getenv("NCNET_CONV2D_BIG"))));
+  const bool big = BN == 128 && (variant == 0 ? t256 >= 384 : (t256 >= 512 || (t256 >= 256 && tuning().conv2d_big)));
   if (big && variant != 1) {
     p.tiles_m = cdiv(p.M, 256);
     dim3 g2((unsigned)(p.tiles_m * p.tiles_n)), b2(512);

@@ -935,11 +935,8 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
   g.xlo = 0; g.ylo = 0;
   g.njb = J; g.tpw = 1;
   g.nib = I; g.relu = 0;
-  {
-    // default on: conv16v3 5.51 -> 5.31 ms at 64 x 25^4 (profiles/r1s3_kbench_nt.json)
-    const char* e = getenv("NCNET_NT_STORE");   // read per launch: tests / kbench switch it in-process
-    g.nt = e ? atoi(e) : 1;
-  }
+  // default on: conv16v3 5.51 -> 5.31 ms at 64 x 25^4 (profiles/r1s3_kbench_nt.json)
+  g.nt = tuning().nt_store;
   return g;
 }
 
@@ -956,16 +953,8 @@ static void pick_tile(int K, int L, int& tk, int& tl) {
   while (tk * tl > 640) { if (tl > tk) --tl; else --tk; }
 }
 
-static bool getenv_flag(const char* k) {
-  const char* e = getenv(k);
-  return e && atoi(e) != 0;
-}
-
-// output j-tiles per workgroup of the group-plane conv (read per launch: tests / kbench switch it)
-static int gp_tpw() {
-  const char* e = getenv("NCNET_GP_TPW");
-  return e ? atoi(e) : 5;
-}
+// output j-tiles per workgroup of the group-plane conv
+static int gp_tpw() { return tuning().gp_tpw; }
 
 // KS = 5 and 3 are NC-Net's kernel sizes (lib/model.py:125-139 defaults, the
 // InLoc and PF-Pascal checkpoints); 1 and 7 complete the general Conv4d.
@@ -1006,7 +995,7 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
     const int njb1 = g.njb;
     g.njb = cdiv(J, R);
     dim3 grid3((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block3(512);
-    if (tk == 25 && tl == 25 && KS == 5 && !getenv_flag("NCNET_CONV_V3")) {
+    if (tk == 25 && tl == 25 && KS == 5 && !tuning().conv_v3) {
       // compile-time 25 x 25 tile: pipelined fragments, triple-buffered planes
       size_t lds4 = 3 * (size_t)(25 + 4) * 33 * 32 + (size_t)5 * nq * 1024 + 1024;
 #define L16V4(EPIV) hipLaunchKernelGGL((conv16v4_fwd_kernel<5, R, EPIV, 25, 25>), grid3, block3, lds4, stream, x, w, bias, m, y, g)
@@ -1108,4 +1097,13 @@ extern "C" int ncnet_conv16f8_fwd(const void* X, const void* Wp, const float* bi
   KS_DISPATCH(LF8, 0);
 #undef LF8
   return (int)hipGetLastError();
+}
+
+// set_tuning binding: name -> previous value (INT32_MIN for an unknown name)
+extern "C" int ncnet_set_tuning(const char* name, int value, int set) {
+  int* p = tuning_slot(name);
+  if (!p) return INT32_MIN;
+  const int old = *p;
+  if (set) *p = value;
+  return old;
 }

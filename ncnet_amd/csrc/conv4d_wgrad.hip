@@ -1000,15 +1000,11 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
   g.PR = (g.VT - 1) / L + 2 + KS - 1;
   g.ncols = V * J * g.ntl;
   g.cpg = cdiv(g.ncols, ngroups);
-  {
-    const char* e = getenv("NCNET_WGRAD_FLAGS");   // read per launch: tests / kbench switch it in-process
-    g.flags = e ? atoi(e) : 0;
-  }
+  g.flags = tuning().wgrad_flags;
   if (g.RW > 32) return -1;                 // one wave-instruction per staged row
   if (g.VT > 384) return -1;                // <= 6 chunks per half
   {
-    const char* e = getenv("NCNET_WGRAD_V3");   // A/B switch (read per launch)
-    if (KS == 5 && K == 25 && L == 25 && !(e && atoi(e))) {
+    if (KS == 5 && K == 25 && L == 25 && !tuning().wgrad_v3) {
       using C = W4C<5, 25, 25>;
       dim3 grid((unsigned)(KS * ngroups)), block(512);
       hipLaunchKernelGGL((wgrad16v4_kernel<5, 25, 25>), grid, block, (size_t)C::LDS, stream, (const bf16*)X,

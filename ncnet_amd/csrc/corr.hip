@@ -613,15 +613,14 @@ extern "C" int ncnet_l2norm_rows_bwd(const float* x, const float* g, const float
 // 0 for bf16, K % 128 == 0 for fp8).
 static bool use_v2(bool f8, int batch, int M, int N, int K) {
   if (K % (f8 ? 128 : cg2::BK) != 0) return false;
-  static const int force = [] { const char* e = getenv("NCNET_CORR_V2"); return e ? atoi(e) : -1; }();
+  const int force = tuning().corr_v2;
   if (force >= 0) return force == 1;
   return (long long)batch * cdiv(M, cg2::BM) * cdiv(N, cg2::BN) >= 512;
 }
 
 // ring depth: 4 stages (96 KB, one workgroup per CU) or 3 (72 KB, two per CU); NCNET_CORR_NS
 static int cg2_stages() {
-  static const int ns = [] { const char* e = getenv("NCNET_CORR_NS"); return e && atoi(e) == 4 ? 4 : 3; }();
-  return ns;
+  return tuning().corr_ns == 4 ? 4 : 3;
 }
 
 // C[b] = A[amap[b]] . B[bmap[b]]^T ; out_bf16 selects the output dtype.

@@ -38,6 +38,7 @@ import os as _os
 import numpy as np
 import torch
 
+from .. import config as _config
 from . import _ext
 from . import reference as ref
 from .packing import (blk_out_weights, ij_groups, ij_in_grad, ij_in_weights, ij_out_grad, ij_out_weights, pack_w16,
@@ -45,8 +46,9 @@ from .packing import (blk_out_weights, ij_groups, ij_in_grad, ij_in_weights, ij_
 
 HIP_KS = (1, 3, 5, 7)
 # Cout=1 layers with <= 16 input channels run in output-plane-block mode
-# (conv16_blk_fwd); NCNET_BLK1OUT=0 selects the ij encoding + ijsum instead.
-BLK_1OUT = _os.environ.get("NCNET_BLK1OUT", "1") != "0"
+# (conv16_blk_fwd); False selects the ij encoding + ijsum instead (A/B tests
+# and scripts/kbench.py set the module attribute; no environment knob).
+BLK_1OUT = True
 
 
 def nblocks(c: int) -> int:
@@ -78,24 +80,19 @@ def wgrad_v3_groups(shape, ks: int) -> int:
     ntl = -(-(K * L) // 320)
     ncols = V * J * ntl
     target = max(1, 512 // ks)
-    env = _os.environ.get("NCNET_WGRAD_GROUPS")
-    if env:
-        target = int(env)
     return max(1, min(target, ncols))
 
 
 def wgrad_groups(ks: int, nitems: int) -> int:
     """K-split groups of wgrad16v2 in full mode (~3000 workgroups over the
     KS*KS plane offsets; 120 groups at KS=5 beat 20 by 1.4x on MI355X)."""
-    env = _os.environ.get("NCNET_WGRAD_GROUPS")
-    target = int(env) if env else max(1, 3072 // (ks * ks))
+    target = max(1, 3072 // (ks * ks))
     return max(1, min(target, nitems))
 
 
 def wgrad_plane_groups(nitems: int) -> int:
     """Groups of the plane-only wgrad (grid = groups): ~3 workgroups per CU."""
-    env = _os.environ.get("NCNET_WGRAD_PLANE_GROUPS")
-    return max(1, min(int(env) if env else 768, nitems))
+    return max(1, min(768, nitems))
 
 
 def _nitems(shape) -> int:
@@ -127,10 +124,10 @@ def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, plane_onl
 # Plane-only weight gradient of the Cout=1 layer on wgrad16p (double-buffered
 # items, both ij groups of ijpack(g, -1) against one staged X plane: 0.81 ms vs
 # 2 x 0.44 ms at the training shape) when the (k, l) plane is one tile;
-# NCNET_WGRAD_P=0 selects the per-group wgrad16v2 calls.  The Cin=1 layer stays
+# WGRAD_P = False (module attribute, A/B only) selects the per-group wgrad16v2 calls.  The Cin=1 layer stays
 # on wgrad16v2: with one G operand every X fragment feeds a single MFMA, the
 # kernel is LDS-bound and v2's 2-3 workgroups per CU hide more (1.18 vs 0.89 ms).
-WGRAD_P = _os.environ.get("NCNET_WGRAD_P", "1") != "0"
+WGRAD_P = True
 
 
 def wgrad_p_ok(shape) -> bool:
@@ -332,20 +329,18 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
 
 
 # Weight gradients of the layers after the first on a second HIP stream
-# (NCNET_BWD_OVERLAP=0 disables): they depend only on the layer input and the
+# (NCNET_BWD_OVERLAP=0 disables, read by config.RUNTIME): they depend only on the layer input and the
 # incoming gradient, so wgrad(l) runs while the data-gradient chain continues
 # on the main stream (dgrad(l) -> dgrad(l-1) -> ...).  The first layer's
 # weight gradient stays on the main stream, which is idle by then.
-BWD_OVERLAP = _os.environ.get("NCNET_BWD_OVERLAP", "1") == "1"
+BWD_OVERLAP = _config.RUNTIME.bwd_overlap
 _SIDE_STREAMS: dict = {}
 
 
 def _side_stream(dev: torch.device):
     st = _SIDE_STREAMS.get(dev.index)
     if st is None:
-        # NCNET_BWD_SIDE_PRIO=-1: high-priority side stream (tuning knob)
-        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(
-            device=dev, priority=int(_os.environ.get("NCNET_BWD_SIDE_PRIO", "0")))
+        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
     return st
 
 
@@ -1033,7 +1028,7 @@ def neigh_consensus_fp8(x: torch.Tensor, weights, biases, kinds, symmetric: bool
 # Fused InLoc NC (csrc/nc_fused.hip): kernel sizes (3, 3), channels (<=16, 1),
 # inference.  The hidden activation stays in LDS; HBM sees the input and the
 # output volume once.  NCNET_NC_FUSED=0 falls back to the layer-by-layer path.
-FUSED = _os.environ.get("NCNET_NC_FUSED", "1") != "0"
+FUSED = _config.RUNTIME.nc_fused
 _FUSED_LDS = 78 * 1024          # two workgroups per CU (160 KB LDS)
 
 

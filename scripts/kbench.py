@@ -21,18 +21,20 @@ from ncnet_amd.ops.neigh_consensus import wgrad_groups, wgrad_plane_groups, wgra
 from ncnet_amd.ops.packing import ij_groups, ij_in_weights, ij_out_weights, pack_w16, pack_w16_planes  # noqa: E402
 
 
+_TUNING = {"NCNET_CONV_V3": "conv_v3", "NCNET_WGRAD_V3": "wgrad_v3", "NCNET_GP_TPW": "gp_tpw",
+           "NCNET_NT_STORE": "nt_store", "NCNET_WGRAD_FLAGS": "wgrad_flags"}
+
+
 def with_env(key, val, fn):
-    """Run fn with os.environ[key] = val (the launchers read their tuning switches per call)."""
+    """Run fn with launcher tuning switch ``key`` (its NCNET_* name) set to val
+    (the set_tuning binding; the launchers never read the environment)."""
     def run():
-        old = os.environ.get(key)
-        os.environ[key] = val
+        C = _ext.ext()
+        old = C.set_tuning(_TUNING[key], int(val))
         try:
             fn()
         finally:
-            if old is None:
-                os.environ.pop(key, None)
-            else:
-                os.environ[key] = old
+            C.set_tuning(_TUNING[key], old)
     return run
 
 

@@ -39,3 +39,19 @@ def _ncnet_debug_kernel_checks(request):
     if "NCNET_CHECK failed" in out + err and "selftest" not in request.node.name:
         pytest.fail("device bounds check failed:\n" + "\n".join(
             ln for ln in (out + err).splitlines() if "NCNET_CHECK" in ln)[:4000])
+
+
+@pytest.fixture
+def tune():
+    """tune(name, value): set a launcher tuning switch (csrc/common.h
+    NcnetTuning, the set_tuning binding) for this test; restored afterwards."""
+    from ncnet_amd.ops import _ext
+    saved = {}
+
+    def set_(name, value):
+        old = _ext.ext().set_tuning(name, int(value))
+        saved.setdefault(name, old)
+
+    yield set_
+    for k, v in saved.items():
+        _ext.ext().set_tuning(k, v)

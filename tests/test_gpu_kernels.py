@@ -57,7 +57,7 @@ def test_conv16_fwd(ks, shape):
 
 @pytest.mark.parametrize("epi", [1, 2])
 @pytest.mark.parametrize("shape", [(2, 25, 25, 25, 25), (1, 6, 7, 26, 29), (1, 4, 6, 50, 37), (1, 3, 11, 25, 25)])
-def test_conv16v4_matches_v3_bitwise(epi, shape, monkeypatch):
+def test_conv16v4_matches_v3_bitwise(epi, shape, monkeypatch, tune):
     """conv16v4 (compile-time 25 x 25 tile: pipelined fragments, triple-buffered
     planes with counted vmcnt, buffer-resource DMA that writes the halo zeros)
     accumulates every output in conv16v3's order: bit-identical outputs for the
@@ -72,7 +72,7 @@ def test_conv16v4_matches_v3_bitwise(epi, shape, monkeypatch):
     b = torch.randn(16, device=DEV) * 0.1
     outs = []
     for v3 in ("0", "1"):
-        monkeypatch.setenv("NCNET_CONV_V3", v3)
+        tune("conv_v3", v3)
         y = torch.full_like(x, float("nan"))
         _ext.ext().conv16_fwd(x, w, b if epi == 1 else None, m if epi == 2 else None, y, 5, epi)
         outs.append(y)
@@ -321,7 +321,7 @@ def test_correlation_v2_large_grids():
 
 @pytest.mark.parametrize("shape,ng", [((2, 6, 5, 25, 25), 7), ((3, 25, 25, 25, 25), 102), ((1, 4, 7, 25, 25), 1),
                                       ((2, 9, 3, 25, 25), 40)])
-def test_wgrad16v4_matches_v3(shape, ng, monkeypatch):
+def test_wgrad16v4_matches_v3(shape, ng, monkeypatch, tune):
     """wgrad16v4 (compile-time 25 x 25 plane: X and G DMA'd two steps ahead with
     counted vmcnt, buffer-resource zero halo, per-tap-group specialised body)
     walks the same columns, steps and chunks as wgrad16v3, so every partial
@@ -334,7 +334,7 @@ def test_wgrad16v4_matches_v3(shape, ng, monkeypatch):
     g = torch.randn(shape + (16,), device=DEV).to(torch.bfloat16)
     outs = []
     for v3 in ("0", "1"):
-        monkeypatch.setenv("NCNET_WGRAD_V3", v3)
+        tune("wgrad_v3", v3)
         part = torch.full((2 * ng, 25, 25, 16, 16), float("nan"), device=DEV)
         partb = torch.full((2 * ng, 16), float("nan"), device=DEV)
         C.wgrad16(x, g, part, partb, 5, 0, 3)
@@ -382,11 +382,11 @@ def test_wgrad16_kernel(variant, ks, shape):
 
 
 @pytest.mark.parametrize("flags", ["0", "1"])
-def test_wgrad16v3_priority_flag(flags, monkeypatch):
+def test_wgrad16v3_priority_flag(flags, monkeypatch, tune):
     """wgrad16v3 with the waves-4..7 s_setprio tuning bit: same sums as the oracle."""
     import importlib
     nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
-    monkeypatch.setenv("NCNET_WGRAD_FLAGS", flags)
+    tune("wgrad_flags", flags)
     torch.manual_seed(12)
     V, I, J, K, L, ks = 2, 6, 5, 25, 25, 5
     x = torch.rand(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
@@ -619,7 +619,7 @@ def test_conv2d_nhwc_kernel(cin, cout, k, stride, pad, res, relu, shape):
 
 
 @pytest.mark.parametrize("ks,shape", [(5, (2, 6, 7, 25, 25)), (3, (1, 4, 9, 30, 27)), (5, (1, 3, 12, 9, 7))])
-def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch):
+def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch, tune):
     """The multi-tile group-plane conv16v2 (NCNET_GP_TPW consecutive j-tiles per
     workgroup, one plane stream) does the same MFMAs in the same order as one
     tile per workgroup: outputs are bitwise equal for the bias+ReLU, ReLU-mask
@@ -639,7 +639,7 @@ def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch):
     m = (torch.rand(shape + (16,), device=DEV) > 0.5).to(torch.bfloat16)
     outs = {}
     for tpw in ("1", "5", "3"):
-        monkeypatch.setenv("NCNET_GP_TPW", tpw)
+        tune("gp_tpw", tpw)
         y1 = torch.full(shape + (16,), float("nan"), device=DEV, dtype=torch.bfloat16)
         C.conv16_fwd(xs, wp, b, None, y1, ks, 1)
         y2 = torch.full(shape + (16,), float("nan"), device=DEV, dtype=torch.bfloat16)
@@ -655,7 +655,7 @@ def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch):
 
 
 
-def test_nontemporal_epilogue_stores_bitwise(monkeypatch):
+def test_nontemporal_epilogue_stores_bitwise(monkeypatch, tune):
     """NCNET_NT_STORE=1 (streaming epilogue stores) writes the same bytes as the
     default stores for the v3 16->16 conv, the ReLU-mask data gradient and the
     planar fp32 epilogue (ij-encoded Cout=1 partials)."""
@@ -669,7 +669,7 @@ def test_nontemporal_epilogue_stores_bitwise(monkeypatch):
     b = torch.randn(16, device=DEV) * 0.1
     outs = {}
     for nt in ("0", "1"):
-        monkeypatch.setenv("NCNET_NT_STORE", nt)
+        tune("nt_store", nt)
         y = torch.full_like(x, float("nan"))
         C.conv16_fwd(x, w, b, None, y, 5, 1)
         yd = torch.full_like(x, float("nan"))

@@ -59,9 +59,11 @@ def test_bindings_reject_cpu_tensors():
     names = [n for n in dir(C) if not n.startswith("_") and callable(getattr(C, n))]
     assert len(names) >= 20
     for n in names:
+        if n in ("set_tuning", "pad_geom"):   # no tensor operands (switches, geometry helper)
+            continue
         sig = getattr(C, n).__doc__.strip().splitlines()[0]
         args = re.match(r"\w+\((.*)\) ->", sig).group(1)
-        kinds = [a.split(":", 1)[1].strip() for a in re.split(r", (?=arg\d+:)", args)] if args else []
+        kinds = [a.split(":", 1)[1].split(" = ")[0].strip() for a in re.split(r", (?=\w+:)", args)] if args else []
         with pytest.raises(RuntimeError):
             getattr(C, n)(*[_dummy(k) for k in kinds])
 
