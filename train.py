@@ -8,7 +8,26 @@ Same flags and defaults as the reference, plus:
   --resume PATH        real resume: weights + optimizer + epoch + RNG state
   --max_steps S        stop after S training steps (smoke / profiling)
   --metrics PATH       JSONL metrics (rank 0)
-  --dtype bf16|fp32    backbone compute dtype (NC path is always bf16 MFMA on GPU)
+  --dtype bf16|fp32    backbone compute dtype of the default (bf16) NC mode
+  --nc_precision bf16|fp32
+                       bf16 (default, the headline benchmark): bf16 MFMA operands,
+                       fp32 accumulation.  fp32: fp32-accurate training -- fp32
+                       trunk, bf16x3 correlation and a bf16x3 NeighConsensus
+                       forward AND backward on the fused kernels (~16 mantissa
+                       bits per operand; 204 pairs/s vs 682 on one MI355X,
+                       profiles/r3/x3/).
+
+Which precision to train with: use --nc_precision fp32 whenever the weak
+loss's signal is below bf16 resolution -- the first steps from a random or
+weakly trained NC, or a trunk whose features are nearly collinear (random-init
+trunks: per-step loss ~1e-8).  There the bf16 mode loses the gradient
+direction and its ReLUs die within ~10 steps (PCK stays ~0), while fp32 mode
+learns like the fp32 reference (PCK 0.64 vs 0.68 after 80 steps,
+profiles/r3/x3/README.md).  Measured NOT to be enough in that regime, so not
+offered: a bf16 trunk under an fp32-accurate NC (PCK 0.003), and fp16 autocast
+with loss scaling (the reference algorithm in fp16: PCK 0.003).  Once the loss
+signal is well above bf16 resolution (a pretrained trunk, |loss| >> 1e-3),
+the default bf16 mode trains 3.3x faster.
   --segment_timing     HIP-event timers per step segment (backbone, correlation,
                        mutual_matching, neigh_consensus, forward, backward,
                        allreduce, optimizer), written to the --metrics records
@@ -72,7 +91,9 @@ def build_parser():
     p.add_argument("--metrics", type=str, default="")
     p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--nc_precision", type=str, default="bf16", choices=["bf16", "fp32"],
-                   help="fp32: fp32-accurate NeighConsensus training (bf16x3 splits, 3x NC cost)")
+                   help="fp32: fp32-accurate training (fp32 trunk, bf16x3 correlation + NeighConsensus fwd/bwd on "
+                        "the fused kernels); use it when the weak-loss signal is below bf16 resolution (see --help text "
+                        "at the top of train.py)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--segment_timing", action="store_true")
     p.add_argument("--profile", type=str, default="")
