@@ -55,8 +55,10 @@ def _baseline():
 def _inloc_secondary():
     """BASELINE configs 3-5 (InLoc dense matching, NC 3,3/16,1, k=2), measured
     after the headline window on rank 0 so the driver's run records them:
-    ms/pair at 1600 px and 3200 px (bf16) and 3200 px (fp8 correlation; fused bf16 NC or, in
-    inloc_3200_fp8_nc_fp8, the fp8 Conv4d NC kernels)."""
+    ms/pair at 1600 px and 3200 px in bf16 and in fp16 (IEEE half end to end,
+    the reference's half_precision numerics), and 3200 px fp8 (e4m3
+    correlation; fused bf16 NC or, in inloc_3200_fp8_nc_fp8, the fp8 Conv4d NC
+    kernels)."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import bench_inloc
     from ncnet_amd.models import ImMatchNet
@@ -65,11 +67,12 @@ def _inloc_secondary():
         torch.manual_seed(0)
         model = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], half_precision=True,
                            relocalization_k_size=2).cuda().eval()
-        for name, size, fp8 in (("inloc_1600_bf16", 1600, False), ("inloc_3200_bf16", 3200, False),
-                                ("inloc_3200_fp8", 3200, True)):
+        for name, size, prec in (("inloc_1600_bf16", 1600, "bf16"), ("inloc_3200_bf16", 3200, "bf16"),
+                                 ("inloc_1600_fp16", 1600, "fp16"), ("inloc_3200_fp16", 3200, "fp16"),
+                                 ("inloc_3200_fp8", 3200, "fp8")):
             # eval_inloc.py's schedule: 10 panos per query, query features extracted once
-            r = bench_inloc.run_single(size, fp8, pairs=10, warmup=2, model=model, panos_per_query=10)
-            r1 = bench_inloc.run_single(size, fp8, pairs=3, warmup=1, model=model, panos_per_query=1)
+            r = bench_inloc.run_single(size, pairs=10, warmup=2, model=model, panos_per_query=10, precision=prec)
+            r1 = bench_inloc.run_single(size, pairs=3, warmup=1, model=model, panos_per_query=1, precision=prec)
             out[name] = {"ms_per_pair": r["value"], "stages_ms": r["stages_ms"],
                          "stages_ms_eager": r.get("stages_ms_eager"), "panos_per_query": 10,
                          "ms_per_pair_both_backbones": r1["value"], "volume": r["config"]["volume"],
@@ -79,7 +82,7 @@ def _inloc_secondary():
         # the all-fp8 pipeline (fp8 Conv4d NC kernels instead of the fused bf16 stack)
         os.environ["NCNET_NC_FP8"] = "1"
         try:
-            r = bench_inloc.run_single(3200, True, pairs=10, warmup=2, model=model, panos_per_query=10)
+            r = bench_inloc.run_single(3200, pairs=10, warmup=2, model=model, panos_per_query=10, precision="fp8")
             out["inloc_3200_fp8_nc_fp8"] = {"ms_per_pair": r["value"], "stages_ms": r["stages_ms"],
                                             "stages_ms_eager": r.get("stages_ms_eager"),
                                             "panos_per_query": 10, "dtype": r["dtype"],

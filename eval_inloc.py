@@ -9,9 +9,13 @@ sharded over ranks (torchrun) and existing outputs are skipped (resume).
 
 Extras: --synthetic_queries N builds a fake shortlist and random images in a
 temp dir (smoke / benchmark without the dataset); --ncons_* for
-checkpoint-less runs; --output_dir (default matches/); --fp8 (e4m3
-correlation + NC on the fp8 MFMA); --volume_parallel (under torchrun, every
-pair's volume is sharded over all ranks instead of sharding the queries).
+checkpoint-less runs; --output_dir (default matches/); --precision
+fp16|bf16|fp8|fp32 (default fp16, the reference's half_precision numerics:
+bf16 trunk, IEEE-half features, correlation and NeighConsensus on the f16 MFMA;
+bf16: bf16 operands; fp8: e4m3 correlation operands on the MX-fp8 MFMA with
+the fused bf16 NeighConsensus; fp32: fp32 trunk + bf16x3 correlation and NC);
+--fp8 = --precision fp8; --volume_parallel (under torchrun, every pair's
+volume is sharded over all ranks instead of sharding the queries).
 """
 from __future__ import annotations
 
@@ -62,6 +66,12 @@ def make_synthetic_inloc(root: str, n_queries: int, n_panos: int, h: int = 768, 
     return path, qdir + "/", pdir + "/"
 
 
+def _precision_kwargs(precision: str) -> dict:
+    """--precision -> ImMatchNet (trunk dtype, correlation / NC operand dtype)."""
+    return {"fp16": dict(dtype="bf16", corr_dtype="fp16"), "bf16": dict(dtype="bf16", corr_dtype="bf16"),
+            "fp8": dict(dtype="bf16", corr_dtype="fp8"), "fp32": dict(dtype="fp32", corr_dtype="fp32")}[precision]
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="Compute InLoc matches")
     ap.add_argument("--checkpoint", type=str, default="")
@@ -79,8 +89,13 @@ def main(argv=None):
     ap.add_argument("--synthetic_queries", type=int, default=0)
     ap.add_argument("--ncons_kernel_sizes", nargs="+", type=int, default=[3, 3])
     ap.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 1])
+    ap.add_argument("--precision", choices=["fp16", "bf16", "fp8", "fp32"], default="fp16",
+                    help="fp16 (default; the reference's half precision on the f16 MFMA), bf16, fp8 (e4m3 "
+                         "correlation operands, fused bf16 NeighConsensus), fp32 (fp32 trunk, bf16x3 correlation + NC)")
     ap.add_argument("--fp8", action="store_true",
-                    help="OCP fp8 e4m3 correlation operands + fp8 NeighConsensus (MI355X fp8 MFMA)")
+                    help="= --precision fp8: OCP e4m3 correlation operands on the MX-fp8 MFMA; the NeighConsensus "
+                         "stays on the fused bf16 kernel (measured faster; NCNET_NC_FP8=1 selects the fp8 Conv4d "
+                         "kernels)")
     ap.add_argument("--volume_parallel", action="store_true",
                     help="all ranks cooperate on every pair, sharding its 4D volume along the A rows "
                          "(ncnet_amd/parallel/volume_parallel.py); default: queries sharded over ranks")
@@ -97,7 +112,7 @@ def main(argv=None):
     model = ImMatchNet(use_cuda=ctx.device.type == "cuda", checkpoint=args.checkpoint or None,
                        ncons_kernel_sizes=args.ncons_kernel_sizes, ncons_channels=args.ncons_channels,
                        half_precision=True, relocalization_k_size=args.k_size,
-                       corr_dtype="fp8" if args.fp8 else "bf16").to(ctx.device)
+                       **_precision_kwargs("fp8" if args.fp8 else args.precision)).to(ctx.device)
     model.eval()
     vp = None
     if args.volume_parallel and ctx.world_size > 1:

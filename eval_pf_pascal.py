@@ -4,8 +4,12 @@
 Flags as in the reference (--checkpoint, --image_size, --eval_dataset_path),
 plus --batch_size (the reference only supports 1), --synthetic N (random
 pairs with random keypoints, for smoke tests without the dataset) and
---ncons_* for checkpoint-less runs.  Multi-GPU: pairs are sharded over ranks
-and the per-pair PCK values are gathered on rank 0.
+--ncons_* for checkpoint-less runs, and --precision bf16|fp16|fp32 (the
+reference evaluates in fp32: eval_pf_pascal.py never halves; default bf16
+here, fp32 = fp32 trunk + bf16x3 correlation and NeighConsensus, fp16 = bf16
+trunk, IEEE-half features / correlation on the f16 MFMA, the NeighConsensus on
+the bf16 Conv4d kernels).  Multi-GPU: pairs are sharded over ranks and the
+per-pair PCK values are gathered on rank 0.
 """
 from __future__ import annotations
 
@@ -54,12 +58,16 @@ def main(argv=None):
     ap.add_argument("--synthetic", type=int, default=0)
     ap.add_argument("--ncons_kernel_sizes", nargs="+", type=int, default=[5, 5, 5])
     ap.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 16, 1])
+    ap.add_argument("--precision", choices=["bf16", "fp16", "fp32"], default="bf16",
+                    help="bf16 (default), fp16 (IEEE-half features + correlation), fp32 (fp32-accurate: fp32 trunk, "
+                         "bf16x3 correlation and NeighConsensus, the reference's numerics)")
     args = ap.parse_args(argv)
     ctx = init_distributed()
     if ctx.is_main:
         print("NC-Net evaluation script - PF Pascal dataset (ncnet_amd)")
     model = ImMatchNet(use_cuda=ctx.device.type == "cuda", checkpoint=args.checkpoint or None,
-                       ncons_kernel_sizes=args.ncons_kernel_sizes, ncons_channels=args.ncons_channels).to(ctx.device)
+                       ncons_kernel_sizes=args.ncons_kernel_sizes, ncons_channels=args.ncons_channels,
+                       dtype="fp32" if args.precision == "fp32" else "bf16", corr_dtype=args.precision).to(ctx.device)
     model.eval()
     size = (args.image_size, args.image_size)
     if args.synthetic:

@@ -21,17 +21,17 @@ int ncnet_wgrad16v3(const void*, const void*, float*, float*, int, int, int, int
 int ncnet_ijpack(const void*, int, void*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv16f8_fwd(const void*, const void*, const float*, void*, int, int, int, int, int, int, int, int, int, float, hipStream_t);
 int ncnet_ijsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_bias_act(void*, const float*, long long, int, int, hipStream_t);
-int ncnet_conv2d_nhwc(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, void*, hipStream_t);
+int ncnet_bias_act(void*, const float*, long long, int, int, int, hipStream_t);
+int ncnet_conv2d_nhwc(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, void*, int, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
 int ncnet_corr_gemm(const void*, const void*, void*, const int*, const int*, int, int, int, int, long long, long long,
-                    long long, int, float, hipStream_t);
+                    long long, int, float, int, hipStream_t);
 int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, int, int, int, int, long long, long long,
-                          float, hipStream_t);
+                          float, int, hipStream_t);
 int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, int, hipStream_t);
 int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, float*, int, int, hipStream_t);
-int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, hipStream_t);
+int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, int, hipStream_t);
 int ncnet_mm_bwd(const float*, const float*, const float*, const int*, const float*, const int*, float*, float*, float*,
                  int, int, int, float, hipStream_t);
 int ncnet_combine_fwd(const float*, float*, int, int, int, hipStream_t);
@@ -51,7 +51,7 @@ int ncnet_pad_planes(const void*, int, void*, int, int, int, int, int, int, int,
 int ncnet_conv1x16(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int,
                    hipStream_t);
 int ncnet_nc_fused_k3(const void*, const void*, const float*, const void*, const float*, float*, int, int, int, int,
-                      int, int, int, int, int, hipStream_t);
+                      int, int, int, int, int, int, hipStream_t);
 }
 
 namespace {
@@ -313,24 +313,25 @@ void ijsum(Tensor Z, c10::optional<Tensor> bias, Tensor y, int64_t ks, int64_t r
                  Z.size(4), Z.size(5), ks, relu ? 1 : 0, (int)sgn, cur_stream(Z)), "ijsum");
 }
 
-// y: bf16, or OCP fp8 e4m3 holding fp8_scale * x / ||x|| (fp8_scale > 0);
+// y: bf16, IEEE half, or OCP fp8 e4m3 holding fp8_scale * x / ||x|| (fp8_scale > 0);
 // y_lo (bf16 y only): the rounding residual bf16(x / ||x|| - y) (bf16x3 mode)
 void l2norm_rows(Tensor x, Tensor y, c10::optional<Tensor> inv, double fp8_scale, c10::optional<Tensor> y_lo) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   TORCH_CHECK(x.is_cuda() && x.is_contiguous());
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat);
-  const bool f8 = y.scalar_type() == at::kFloat8_e4m3fn;
-  check(y, "y", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
+  const bool f8 = y.scalar_type() == at::kFloat8_e4m3fn, h = y.scalar_type() == at::kHalf;
+  check(y, "y", f8 ? at::kFloat8_e4m3fn : h ? at::kHalf : at::kBFloat16);
   TORCH_CHECK(!f8 || fp8_scale > 0, "fp8 output needs fp8_scale > 0");
   TORCH_CHECK(x.dim() == 2 && y.sizes() == x.sizes(), "x,y must be [rows, C]");
   if (inv.has_value()) { check(*inv, "inv", at::kFloat); check_shape(*inv, "inv", {x.size(0)}); }
   if (y_lo.has_value()) {
-    TORCH_CHECK(!f8, "l2norm_rows: y_lo needs bf16 y");
+    TORCH_CHECK(!f8 && !h, "l2norm_rows: y_lo needs bf16 y");
     check(*y_lo, "y_lo", at::kBFloat16); check_shape(*y_lo, "y_lo", y.sizes().vec());
   }
   ok(ncnet_l2norm_rows(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(),
                        inv.has_value() ? (float*)inv->data_ptr() : nullptr, x.size(0), x.size(1),
-                       f8 ? (float)fp8_scale : 0.f, y_lo.has_value() ? y_lo->data_ptr() : nullptr, cur_stream(x)),
+                       f8 ? (float)fp8_scale : 0.f, y_lo.has_value() ? y_lo->data_ptr() : nullptr, h ? 1 : 0,
+                       cur_stream(x)),
      "l2norm");
 }
 
@@ -343,14 +344,18 @@ void l2norm_rows_bwd(Tensor x, Tensor g, Tensor inv, Tensor gx) {
                            x.size(0), x.size(1), cur_stream(x)), "l2norm_bwd");
 }
 
-// A [Ba, M, K], B [Bb, N, K] bf16 (or both OCP fp8 e4m3: C = out_scale * A.B^T); C [batch, M, N] fp32/bf16
+// A [Ba, M, K], B [Bb, N, K] bf16 or IEEE half (or both OCP fp8 e4m3: C = out_scale * A.B^T);
+// C [batch, M, N] fp32, or 16-bit of the operands' type (bf16 for fp8 operands)
 void corr_gemm(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> amap, c10::optional<Tensor> bmap,
                double out_scale) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
-  const bool f8 = A.scalar_type() == at::kFloat8_e4m3fn;
-  check(A, "A", f8 ? at::kFloat8_e4m3fn : at::kBFloat16); check(B, "B", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
+  const bool f8 = A.scalar_type() == at::kFloat8_e4m3fn, h = A.scalar_type() == at::kHalf;
+  const auto dt = f8 ? at::kFloat8_e4m3fn : h ? at::kHalf : at::kBFloat16;
+  check(A, "A", dt); check(B, "B", dt);
   TORCH_CHECK(!f8 || A.size(2) % 16 == 0, "fp8 K must be a multiple of 16");
-  TORCH_CHECK(C.is_cuda() && C.is_contiguous() && (C.scalar_type() == at::kFloat || C.scalar_type() == at::kBFloat16));
+  const auto c16 = h ? at::kHalf : at::kBFloat16;
+  TORCH_CHECK(C.is_cuda() && C.is_contiguous() && (C.scalar_type() == at::kFloat || C.scalar_type() == c16),
+              "corr_gemm: C must be fp32 or the operands' 16-bit type");
   TORCH_CHECK(A.dim() == 3 && B.dim() == 3 && C.dim() == 3);
   TORCH_CHECK(A.size(2) == B.size(2), "K mismatch");
   TORCH_CHECK(A.size(2) % 8 == 0, "K must be a multiple of 8");
@@ -366,14 +371,16 @@ void corr_gemm(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> amap, c10::op
   } else TORCH_CHECK(B.size(0) == batch);
   ok(ncnet_corr_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), opt_ptr<int>(amap), opt_ptr<int>(bmap), batch, A.size(1),
                      B.size(1), A.size(2), A.size(1) * A.size(2), B.size(1) * B.size(2), C.size(1) * C.size(2),
-                     C.scalar_type() == at::kBFloat16, f8 ? (float)out_scale : 0.f, cur_stream(A)), "corr_gemm");
+                     C.scalar_type() != at::kFloat, f8 ? (float)out_scale : 0.f, h ? 1 : 0, cur_stream(A)),
+     "corr_gemm");
 }
 
 void corr_gemm_pool2(Tensor A, Tensor B, Tensor val, Tensor idx, int64_t hA, int64_t wA, int64_t hB, int64_t wB,
                      double out_scale) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
-  const bool f8 = A.scalar_type() == at::kFloat8_e4m3fn;
-  check(A, "A", f8 ? at::kFloat8_e4m3fn : at::kBFloat16); check(B, "B", f8 ? at::kFloat8_e4m3fn : at::kBFloat16);
+  const bool f8 = A.scalar_type() == at::kFloat8_e4m3fn, h = A.scalar_type() == at::kHalf;
+  const auto dt = f8 ? at::kFloat8_e4m3fn : h ? at::kHalf : at::kBFloat16;
+  check(A, "A", dt); check(B, "B", dt);
   check(val, "val", at::kFloat); check(idx, "idx", at::kByte);
   TORCH_CHECK(!f8 || A.size(2) % 16 == 0, "fp8 K must be a multiple of 16");
   TORCH_CHECK(A.dim() == 3 && B.dim() == 3 && A.size(0) == B.size(0));
@@ -384,7 +391,7 @@ void corr_gemm_pool2(Tensor A, Tensor B, Tensor val, Tensor idx, int64_t hA, int
   check_shape(idx, "idx", {A.size(0), hA / 2, wA / 2, hB / 2, wB / 2});
   ok(ncnet_corr_gemm_pool2(A.data_ptr(), B.data_ptr(), (float*)val.data_ptr(), (uint8_t*)idx.data_ptr(), A.size(0), hA,
                            wA, hB, wB, A.size(2), A.size(1) * A.size(2), B.size(1) * B.size(2),
-                           f8 ? (float)out_scale : 0.f, cur_stream(A)),
+                           f8 ? (float)out_scale : 0.f, h ? 1 : 0, cur_stream(A)),
      "corr_gemm_pool2");
 }
 
@@ -432,11 +439,16 @@ void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10
   const int64_t V = c.size(0), R = c.size(1), C = c.size(2);
   check_shape(rmax, "rmax", {V, R}); check_shape(cmax, "cmax", {V, C});
   if (out.has_value()) { check(*out, "out", at::kFloat); check_shape(*out, "out", {V, R, C}); }
-  if (out_x.has_value()) { check(*out_x, "out_x", at::kBFloat16); check_shape(*out_x, "out_x", {V, R, C}); }
-  if (out_xt.has_value()) { check(*out_xt, "out_xt", at::kBFloat16); check_shape(*out_xt, "out_xt", {V, C, R}); }
+  // out_x / out_xt: bf16 or IEEE half (both the same)
+  const bool h = (out_x.has_value() && out_x->scalar_type() == at::kHalf) ||
+                 (out_xt.has_value() && out_xt->scalar_type() == at::kHalf);
+  const auto xt = h ? at::kHalf : at::kBFloat16;
+  if (out_x.has_value()) { check(*out_x, "out_x", xt); check_shape(*out_x, "out_x", {V, R, C}); }
+  if (out_xt.has_value()) { check(*out_xt, "out_xt", xt); check_shape(*out_xt, "out_xt", {V, C, R}); }
   ok(ncnet_mm_apply((float*)c.data_ptr(), (float*)rmax.data_ptr(), (float*)cmax.data_ptr(),
                     out.has_value() ? (float*)out->data_ptr() : nullptr, out_x.has_value() ? out_x->data_ptr() : nullptr,
-                    out_xt.has_value() ? out_xt->data_ptr() : nullptr, V, R, C, (float)eps, cur_stream(c)), "mm_apply");
+                    out_xt.has_value() ? out_xt->data_ptr() : nullptr, V, R, C, (float)eps, h ? 1 : 0, cur_stream(c)),
+     "mm_apply");
 }
 
 void mm_bwd(Tensor c, Tensor g, Tensor rmax, Tensor rarg, Tensor cmax, Tensor carg, Tensor gc, double eps) {
@@ -523,7 +535,8 @@ void transpose(Tensor x, Tensor y) {
 // [rows, C] matrix or a channels-last [N, C, H, W] tensor; b fp32 [C].
 void bias_act_(Tensor Y, Tensor b, int64_t relu) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(Y.device());
-  TORCH_CHECK(Y.is_cuda() && Y.scalar_type() == at::kBFloat16, "bias_act_: Y must be a bf16 GPU tensor");
+  TORCH_CHECK(Y.is_cuda() && (Y.scalar_type() == at::kBFloat16 || Y.scalar_type() == at::kHalf),
+              "bias_act_: Y must be a bf16 / fp16 GPU tensor");
   int64_t C;
   if (Y.dim() == 4) {
     TORCH_CHECK(Y.is_contiguous(at::MemoryFormat::ChannelsLast), "bias_act_: 4-D Y must be channels-last");
@@ -535,7 +548,8 @@ void bias_act_(Tensor Y, Tensor b, int64_t relu) {
   check(b, "b", at::kFloat);
   check_shape(b, "b", {C});
   TORCH_CHECK(C % 8 == 0, "bias_act_: C must be a multiple of 8");
-  ok(ncnet_bias_act(Y.data_ptr(), (const float*)b.data_ptr(), Y.numel() / C, (int)C, relu ? 1 : 0, cur_stream(Y)),
+  ok(ncnet_bias_act(Y.data_ptr(), (const float*)b.data_ptr(), Y.numel() / C, (int)C, relu ? 1 : 0,
+                    Y.scalar_type() == at::kHalf ? 1 : 0, cur_stream(Y)),
      "bias_act_");
 }
 
@@ -568,12 +582,14 @@ void conv16f8_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, int
      "conv16f8_fwd");
 }
 
-// Fused NC (1 -> 16 -> 1, k = 3): X bf16 [V,I,J,K,L] -> Y fp32 [V,I,J,K,L];
-// W1p / W2p bf16 [5, 64, 8]; b1 [16], b2 [1] fp32; tile (TK, TL), R planes and IR rows per workgroup.
+// Fused NC (1 -> 16 -> 1, k = 3): X bf16 or IEEE half [V,I,J,K,L] -> Y fp32 [V,I,J,K,L];
+// W1p / W2p [5, 64, 8] of X's type; b1 [16], b2 [1] fp32; tile (TK, TL), R planes and IR rows per workgroup.
 void nc_fused_k3(Tensor X, Tensor W1p, Tensor b1, Tensor W2p, Tensor b2, Tensor Y, int64_t R, int64_t IR, int64_t TK,
                  int64_t TL) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
-  check(X, "X", at::kBFloat16); check(W1p, "W1p", at::kBFloat16); check(W2p, "W2p", at::kBFloat16);
+  const bool h = X.scalar_type() == at::kHalf;
+  const auto dt = h ? at::kHalf : at::kBFloat16;
+  check(X, "X", dt); check(W1p, "W1p", dt); check(W2p, "W2p", dt);
   check(b1, "b1", at::kFloat); check(b2, "b2", at::kFloat); check(Y, "Y", at::kFloat);
   TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
   check_shape(Y, "Y", X.sizes().vec());
@@ -582,7 +598,7 @@ void nc_fused_k3(Tensor X, Tensor W1p, Tensor b1, Tensor W2p, Tensor b2, Tensor 
   TORCH_CHECK(R >= 1 && IR >= 1 && TK >= 1 && TL >= 1, "nc_fused_k3: bad tiling");
   ok(ncnet_nc_fused_k3(X.data_ptr(), W1p.data_ptr(), (const float*)b1.data_ptr(), W2p.data_ptr(),
                        (const float*)b2.data_ptr(), (float*)Y.data_ptr(), X.size(0), X.size(1), X.size(2), X.size(3),
-                       X.size(4), (int)R, (int)IR, (int)TK, (int)TL, cur_stream(X)),
+                       X.size(4), (int)R, (int)IR, (int)TK, (int)TL, h ? 1 : 0, cur_stream(X)),
      "nc_fused_k3");
 }
 
@@ -592,25 +608,27 @@ void conv2d_nhwc(Tensor X, Tensor W, Tensor bias, c10::optional<Tensor> R, Tenso
                  int64_t relu) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   auto cl = at::MemoryFormat::ChannelsLast;
-  TORCH_CHECK(X.is_cuda() && X.scalar_type() == at::kBFloat16 && X.dim() == 4 && X.is_contiguous(cl),
-              "conv2d_nhwc: X must be bf16 channels-last [N,C,H,W]");
-  TORCH_CHECK(W.is_cuda() && W.scalar_type() == at::kBFloat16 && W.dim() == 4 && W.is_contiguous(cl),
-              "conv2d_nhwc: W must be bf16 channels-last [Cout,Cin,KH,KW]");
+  const bool h = X.scalar_type() == at::kHalf;
+  const auto dt = h ? at::kHalf : at::kBFloat16;   // all operands bf16, or all IEEE half
+  TORCH_CHECK(X.is_cuda() && (X.scalar_type() == at::kBFloat16 || h) && X.dim() == 4 && X.is_contiguous(cl),
+              "conv2d_nhwc: X must be bf16 / fp16 channels-last [N,C,H,W]");
+  TORCH_CHECK(W.is_cuda() && W.scalar_type() == dt && W.dim() == 4 && W.is_contiguous(cl),
+              "conv2d_nhwc: W must be channels-last [Cout,Cin,KH,KW] of X's dtype");
   const int64_t N = X.size(0), Cin = X.size(1), H = X.size(2), Wd = X.size(3);
   const int64_t Cout = W.size(0), KH = W.size(2), KW = W.size(3);
   TORCH_CHECK(W.size(1) == Cin, "conv2d_nhwc: Cin mismatch");
   TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "conv2d_nhwc: channels must be multiples of 64");
   const int64_t Ho = (H + 2 * pad - KH) / stride + 1, Wo = (Wd + 2 * pad - KW) / stride + 1;
   check(bias, "bias", at::kFloat); check_shape(bias, "bias", {Cout});
-  TORCH_CHECK(Y.is_cuda() && Y.scalar_type() == at::kBFloat16 && Y.is_contiguous(cl), "conv2d_nhwc: Y must be bf16 channels-last");
+  TORCH_CHECK(Y.is_cuda() && Y.scalar_type() == dt && Y.is_contiguous(cl), "conv2d_nhwc: Y must be channels-last of X's dtype");
   check_shape(Y, "Y", {N, Cout, Ho, Wo});
   if (R.has_value()) {
-    TORCH_CHECK(R->is_cuda() && R->scalar_type() == at::kBFloat16 && R->is_contiguous(cl), "conv2d_nhwc: R must be bf16 channels-last");
+    TORCH_CHECK(R->is_cuda() && R->scalar_type() == dt && R->is_contiguous(cl), "conv2d_nhwc: R must be channels-last of X's dtype");
     check_shape(*R, "R", {N, Cout, Ho, Wo});
   }
   TORCH_CHECK(N * Ho * Wo < (1LL << 31) && Cout * KH * KW * Cin < (1LL << 31), "conv2d_nhwc: sizes exceed int32");
   ok(ncnet_conv2d_nhwc(X.data_ptr(), W.data_ptr(), (const float*)bias.data_ptr(), R.has_value() ? R->data_ptr() : nullptr,
-                       Y.data_ptr(), N, H, Wd, Cin, Cout, KH, KW, stride, pad, relu ? 1 : 0, cur_stream(X)),
+                       Y.data_ptr(), N, H, Wd, Cin, Cout, KH, KW, stride, pad, relu ? 1 : 0, h ? 1 : 0, cur_stream(X)),
      "conv2d_nhwc");
 }
 

@@ -65,6 +65,32 @@ __device__ __forceinline__ f32x4 mfma16u(const u32x4& a, const u32x4& b, const f
                                                  0);
 }
 
+// IEEE half (f16) operands: v_mfma_f32_16x16x32_f16 has the bf16 form's
+// fragment layout and rate with 3 more mantissa bits (the reference's
+// half-precision InLoc path, eval_inloc.py:50).  Kernels templated on F16 move
+// 16-bit operands as raw bits and pick the MFMA / the output rounding here.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma16h(const u32x4& a, const u32x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16t(const u32x4& a, const u32x4& b, const f32x4& c) {
+  if constexpr (F16) return mfma16h(a, b, c);
+  else return mfma16u(a, b, c);
+}
+// 16-bit storage bits of x (round to nearest even): bf16, or IEEE half
+template <bool F16>
+__device__ __forceinline__ uint16_t f2s16(float x) {
+  if constexpr (F16) return __builtin_bit_cast(uint16_t, (_Float16)x);
+  else return __builtin_bit_cast(uint16_t, (__bf16)x);
+}
+template <bool F16>
+__device__ __forceinline__ float s162f(uint16_t x) {
+  if constexpr (F16) return (float)__builtin_bit_cast(_Float16, x);
+  else return (float)__builtin_bit_cast(__bf16, x);
+}
+
 // LDS-DMA of 16 B per lane (global_load_lds_dwordx4) issued from inline asm.
 // The compiler's waitcnt pass cannot prove that an LDS-DMA misses a later
 // ds_read_b64_tr_b16 (intrinsic reads carry no alias info), so with the builtin

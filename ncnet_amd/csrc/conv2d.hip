@@ -32,9 +32,59 @@ struct Conv2dArgs {
   int M, tiles_m, tiles_n, relu;
 };
 
+// Epilogue shared by both kernels, staged through LDS so the global writes
+// (and the residual reads) are full 16-B-per-lane row segments: (acc + bias)
+// -> 16-bit tile [BM][BN] in LDS (row = pixel), then + residual, ReLU, store.
+// The staging rounds to the output type first, as the residual add did in
+// bf16 (bit-for-bit the pre-F16 kernels for F16 = false).
+template <int BM, int BN, int TM, int TN, int NT, bool F16>
+__device__ __forceinline__ void conv2d_epilogue(const f32x4 (&acc)[TM][TN], const Conv2dArgs& p, char* smem, int m0,
+                                                int n0, int wm, int wn, int fr, int fq) {
+  uint16_t* Ts = (uint16_t*)smem;                 // BM * BN * 2 bytes (fits the operand buffers)
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wn * TN * 16 + j * 16 + fr;
+    const float b = p.bias[n0 + col];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ts[(wm * TM * 16 + i * 16 + 4 * fq + r) * BN + col] = f2s16<F16>(acc[i][j][r] + b);
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;                     // 16-B chunks per tile row
+  const uint16_t* R = (const uint16_t*)p.R;
+  uint16_t* Y = (uint16_t*)p.Y;
+#pragma unroll
+  for (int c = threadIdx.x; c < BM * CPR; c += NT) {
+    const int row = c / CPR, cc = c - row * CPR;
+    const int pix = m0 + row;
+    if (pix < p.M) {
+      const u32x4 tv = *(const u32x4*)(Ts + row * BN + cc * 8);
+      const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
+      u32x4 rv = {0u, 0u, 0u, 0u};
+      if (R) rv = *(const u32x4*)(R + o);
+      u32x4 out;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v = s162f<F16>((uint16_t)(tv[e] >> (16 * h)));
+          if (R) v = s162f<F16>(f2s16<F16>(v + s162f<F16>((uint16_t)(rv[e] >> (16 * h)))));
+          if (p.relu) v = fmaxf(v, 0.f);
+          w |= (uint32_t)f2s16<F16>(v) << (16 * h);
+        }
+        out[e] = w;
+      }
+      *(u32x4*)(Y + o) = out;
+    }
+  }
+}
+
 // BM x BN output tile: BM = 128, or 64 when the grid would not fill the chip
 // (layer3 at the training size: 157 x 2 tiles of 128 on 256 CUs).
-template <int BM, int BN>
+// F16: IEEE-half X / W / R / Y (f16 MFMA; the fp16 inference precision)
+template <int BM, int BN, bool F16 = false>
 __global__ __launch_bounds__(256, 2) void conv2d_nhwc_kernel(Conv2dArgs p) {
   using namespace cv;
   constexpr int WN = BN == 128 ? 2 : 1;          // waves along N
@@ -125,7 +175,8 @@ __global__ __launch_bounds__(256, 2) void conv2d_nhwc_kernel(Conv2dArgs p) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfv[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = mfma16t<F16>(__builtin_bit_cast(u32x4, af[i]), __builtin_bit_cast(u32x4, bfv[j]), acc[i][j]);
     }
     __syncthreads();
     if (more) store();
@@ -135,37 +186,7 @@ __global__ __launch_bounds__(256, 2) void conv2d_nhwc_kernel(Conv2dArgs p) {
   // epilogue, staged through LDS so the global writes (and the residual
   // reads) are full 16-B-per-lane row segments: (acc + bias) -> bf16 tile
   // [BM][BN] in LDS (row = pixel), then + residual, ReLU, store.
-  bf16* Ts = (bf16*)smem;                         // BM * BN * 2 <= (BM + BN) * 128 bytes
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = wn * TN * 16 + j * 16 + fr;
-    const float b = p.bias[n0 + col];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Ts[(wm * TM * 16 + i * 16 + 4 * fq + r) * BN + col] = f2bf(acc[i][j][r] + b);
-  }
-  __syncthreads();
-  constexpr int CPR = BN / 8;                     // 16-B chunks per tile row
-#pragma unroll
-  for (int c = threadIdx.x; c < BM * CPR; c += 256) {
-    const int row = c / CPR, cc = c - row * CPR;
-    const int pix = m0 + row;
-    if (pix < p.M) {
-      bf16x8 v = *(const bf16x8*)(Ts + row * BN + cc * 8);
-      const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
-      if (p.R) {
-        const bf16x8 rr = *(const bf16x8*)(p.R + o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[e]));
-      }
-      if (p.relu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf(bf2f(v[e]), 0.f));
-      }
-      *(bf16x8*)(p.Y + o) = v;
-    }
-  }
+  conv2d_epilogue<BM, BN, TM, TN, 256, F16>(acc, p, smem, m0, n0, wm, wn, fr, fq);
 }
 
 
@@ -200,7 +221,7 @@ __device__ __forceinline__ void c2_wait_barrier() {
 
 // NW waves (4: 2x2 / 4x1 of 64x64 / 32x64; 8: 4x2 of 64x64 for the 256x128
 // tile, 85 FLOP per L2 byte instead of 64), NSTG ring stages.
-template <int BM, int BN, int NW, int NSTG>
+template <int BM, int BN, int NW, int NSTG, bool F16 = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void conv2d_nhwc_v2_kernel(Conv2dArgs p) {
   using namespace cv2;
   constexpr int NS = NSTG;
@@ -299,50 +320,22 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void conv2d_nhwc_v2_kernel(Conv2dA
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfv[j], acc[i][j]);
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = mfma16t<F16>(__builtin_bit_cast(u32x4, af[i]), __builtin_bit_cast(u32x4, bfv[j]), acc[i][j]);
     buf = (buf + 1 == NS) ? 0 : buf + 1;
   }
   __syncthreads();   // all fragment reads done before the epilogue reuses the LDS
 
-  bf16* Ts = (bf16*)smem;                         // BM * BN * 2 <= NS * STAGE bytes
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = wn * TN * 16 + j * 16 + fr;
-    const float b = p.bias[n0 + col];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Ts[(wm * TM * 16 + i * 16 + 4 * fq + r) * BN + col] = f2bf(acc[i][j][r] + b);
-  }
-  __syncthreads();
-  constexpr int CPR = BN / 8;
-#pragma unroll
-  for (int c = threadIdx.x; c < BM * CPR; c += NT) {
-    const int row = c / CPR, cc = c - row * CPR;
-    const int pix = m0 + row;
-    if (pix < p.M) {
-      bf16x8 v = *(const bf16x8*)(Ts + row * BN + cc * 8);
-      const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
-      if (p.R) {
-        const bf16x8 rr = *(const bf16x8*)(p.R + o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(rr[e]));
-      }
-      if (p.relu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf(bf2f(v[e]), 0.f));
-      }
-      *(bf16x8*)(p.Y + o) = v;
-    }
-  }
+  conv2d_epilogue<BM, BN, TM, TN, NT, F16>(acc, p, smem, m0, n0, wm, wn, fr, fq);
 }
 
 }  // namespace ncnet
 
 using namespace ncnet;
 
+// f16: X / W / R / Y are IEEE half (else bf16).
 extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias, const void* R, void* Y, int N, int H,
-                                 int Wd, int Cin, int Cout, int KH, int KW, int stride, int pad, int relu,
+                                 int Wd, int Cin, int Cout, int KH, int KW, int stride, int pad, int relu, int f16,
                                  hipStream_t stream) {
   if (Cin % 64 || Cout % 64 || stride < 1) return -1;   // (v2 needs Cin % 32; both kernels share the check)
   Conv2dArgs p;
@@ -371,10 +364,11 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
     p.tiles_m = cdiv(p.M, 256);
     dim3 g2((unsigned)(p.tiles_m * p.tiles_n)), b2(512);
     const size_t lds = (size_t)3 * (256 + BN) * 64;
-    hipLaunchKernelGGL((conv2d_nhwc_v2_kernel<256, 128, 8, 3>), g2, b2, lds, stream, p);
+    if (f16) hipLaunchKernelGGL((conv2d_nhwc_v2_kernel<256, 128, 8, 3, true>), g2, b2, lds, stream, p);
+    else hipLaunchKernelGGL((conv2d_nhwc_v2_kernel<256, 128, 8, 3>), g2, b2, lds, stream, p);
     return (int)hipGetLastError();
   }
-  if (variant == 2) {
+  if (variant == 2 && !f16) {
     const size_t lds = (size_t)4 * (BM + BN) * 64;
 #define LC3(BMV, BNV) hipLaunchKernelGGL((conv2d_nhwc_v2_kernel<BMV, BNV, 4, 4>), grid, block, lds, stream, p)
     if (BM == 128) { if (BN == 128) LC3(128, 128); else LC3(128, 64); }
@@ -383,7 +377,8 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
     return (int)hipGetLastError();
   }
   const size_t lds = (size_t)(BM + BN) * 128;
-#define LC2(BMV, BNV) hipLaunchKernelGGL((conv2d_nhwc_kernel<BMV, BNV>), grid, block, lds, stream, p)
+#define LC2(BMV, BNV) do { if (f16) hipLaunchKernelGGL((conv2d_nhwc_kernel<BMV, BNV, true>), grid, block, lds, stream, p); \
+                           else hipLaunchKernelGGL((conv2d_nhwc_kernel<BMV, BNV>), grid, block, lds, stream, p); } while (0)
   if (BM == 128) { if (BN == 128) LC2(128, 128); else LC2(128, 64); }
   else { if (BN == 128) LC2(64, 128); else LC2(64, 64); }
 #undef LC2

@@ -21,10 +21,12 @@
 namespace ncnet {
 
 // ---------------------------------------------------------------------------
-template <typename TIN, bool FP8>
+// OUT: 0 bf16 (+ optional lo half), 1 OCP fp8 e4m3 (scaled), 2 IEEE half
+template <typename TIN, int OUT>
 __global__ __launch_bounds__(256) void l2norm_rows_kernel(const TIN* __restrict__ x, void* __restrict__ yv,
                                                           float* __restrict__ inv_norm, int rows, int C,
                                                           float out_scale, bf16* __restrict__ ylo) {
+  constexpr bool FP8 = OUT == 1;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -60,6 +62,22 @@ __global__ __launch_bounds__(256) void l2norm_rows_kernel(const TIN* __restrict_
       } else {
         for (int e = 0; c + e < C; ++e)
           yr[c + e] = (uint8_t)__hip_cvt_float_to_fp8((float)xr[c + e] * s, __HIP_SATFINITE, __HIP_E4M3);
+      }
+    }
+    return;
+  }
+  if (OUT == 2) {
+    uint16_t* hr = (uint16_t*)yv + (size_t)row * C;
+    for (int c = lane * 8; c < C; c += 512) {
+      if (c + 8 <= C) {
+        u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[e] = (uint32_t)f2s16<true>((float)xr[c + 2 * e] * inv) |
+                 ((uint32_t)f2s16<true>((float)xr[c + 2 * e + 1] * inv) << 16);
+        *(u32x4*)(hr + c) = o;
+      } else {
+        for (int e = 0; c + e < C; ++e) hr[c + e] = f2s16<true>((float)xr[c + e] * inv);
       }
     }
     return;
@@ -124,7 +142,8 @@ struct GemmArgs {
   int hA, wA, hB, wB;    // full-res feature grid (pooling only)
 };
 
-template <bool OUT_BF16, bool POOL, bool FP8>
+// F16 (with !FP8): IEEE-half operands (f16 MFMA) and, with OUT_BF16, an IEEE-half output.
+template <bool OUT_BF16, bool POOL, bool FP8, bool F16 = false>
 __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
   constexpr int EB = FP8 ? 1 : 2;            // bytes per element
   constexpr int KT = 128 / EB;               // k per 128-B LDS row
@@ -216,7 +235,8 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfv[j], acc[i][j]);
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = mfma16t<F16>(__builtin_bit_cast(u32x4, af[i]), __builtin_bit_cast(u32x4, bfv[j]), acc[i][j]);
       }
     }
     __syncthreads();
@@ -236,7 +256,7 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
           int gm = m0 + wm * 64 + i * 16 + 4 * fq + r, gn = n0 + wn * 64 + j * 16 + fr;
           if (gm < p.M && gn < p.N) {
             size_t o = (size_t)b * p.sC + (size_t)gm * p.N + gn;
-            if (OUT_BF16) ((bf16*)p.C)[o] = f2bf(acc[i][j][r]);
+            if (OUT_BF16) ((uint16_t*)p.C)[o] = f2s16<F16>(acc[i][j][r]);
             else ((float*)p.C)[o] = acc[i][j][r];
           }
         }
@@ -313,7 +333,7 @@ __device__ __forceinline__ void cg2_wait_barrier() {
 
 // Epilogue of the v2 kernels for one wave's TM x TN 16 x 16 sub-tiles at
 // (row0, col0): plain fp32 / bf16 store, or the fused 2x2x2x2 max-pool.
-template <int TM, int TN, bool OUT_BF16, bool POOL>
+template <int TM, int TN, bool OUT_BF16, bool POOL, bool F16 = false>
 __device__ __forceinline__ void corr_v2_epilogue(const f32x4 (&acc)[TM][TN], const GemmArgs& p, int b, int row0,
                                                  int col0, int lane) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -327,7 +347,7 @@ __device__ __forceinline__ void corr_v2_epilogue(const f32x4 (&acc)[TM][TN], con
           const int gm = row0 + i * 16 + 4 * fq + r, gn = col0 + j * 16 + fr;
           if (gm < p.M && gn < p.N) {
             const size_t o = (size_t)b * p.sC + (size_t)gm * p.N + gn;
-            if (OUT_BF16) ((bf16*)p.C)[o] = f2bf(acc[i][j][r]);
+            if (OUT_BF16) ((uint16_t*)p.C)[o] = f2s16<F16>(acc[i][j][r]);
             else ((float*)p.C)[o] = acc[i][j][r];
           }
         }
@@ -370,7 +390,7 @@ __device__ __forceinline__ void corr_v2_epilogue(const f32x4 (&acc)[TM][TN], con
   }
 }
 
-template <bool OUT_BF16, bool POOL, int NS>
+template <bool OUT_BF16, bool POOL, int NS, bool F16 = false>
 __global__ __launch_bounds__(512, NS <= 3 ? 2 : 1) void corr_gemm_v2_kernel(GemmArgs p) {
   constexpr int BM = cg2::BM, BN = cg2::BN, BK = cg2::BK, GM = cg2::GM;
   constexpr int APW = cg2::APW, BPW = cg2::BPW, PER = cg2::PER, STAGE = cg2::STAGE;
@@ -453,14 +473,15 @@ __global__ __launch_bounds__(512, NS <= 3 ? 2 : 1) void corr_gemm_v2_kernel(Gemm
       if (j + 1 < TN) bnext = lds_read16(Bs, roff(wn * 64 + (j + 1) * 16 + fr, fq));
       __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of these MFMAs (counted lgkmcnt)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) acc[i][j] = mfma16(af[i], bcur, acc[i][j]);
+      for (int i = 0; i < TM; ++i)
+        acc[i][j] = mfma16t<F16>(__builtin_bit_cast(u32x4, af[i]), __builtin_bit_cast(u32x4, bcur), acc[i][j]);
       __builtin_amdgcn_sched_barrier(0);
       bcur = bnext;
     }
     buf = (buf + 1 == NS) ? 0 : buf + 1;
   }
 
-  corr_v2_epilogue<TM, TN, OUT_BF16, POOL>(acc, p, b, m0 + wm * 64, n0 + wn * 64, lane);
+  corr_v2_epilogue<TM, TN, OUT_BF16, POOL, F16>(acc, p, b, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
 
@@ -585,18 +606,20 @@ __global__ __launch_bounds__(512, 1) void corr_gemm_f8v2_kernel(GemmArgs p) {
 using namespace ncnet;
 
 // y dtype: bf16 (fp8_scale == 0; ylo: optional low half) or OCP fp8 e4m3 scaled by fp8_scale.
+// y_f16: y is IEEE half (no lo half, no fp8).
 extern "C" int ncnet_l2norm_rows(const void* x, int x_is_bf16, void* y, float* inv_norm, int rows, int C,
-                                 float fp8_scale, void* ylo, hipStream_t stream) {
+                                 float fp8_scale, void* ylo, int y_f16, hipStream_t stream) {
   bf16* lo = (bf16*)ylo;
   dim3 grid((unsigned)cdiv(rows, 4)), block(256);
   const bool f8 = fp8_scale != 0.f;
-  if (x_is_bf16) {
-    if (f8) hipLaunchKernelGGL((l2norm_rows_kernel<bf16, true>), grid, block, 0, stream, (const bf16*)x, y, inv_norm, rows, C, fp8_scale, nullptr);
-    else hipLaunchKernelGGL((l2norm_rows_kernel<bf16, false>), grid, block, 0, stream, (const bf16*)x, y, inv_norm, rows, C, 1.f, lo);
-  } else {
-    if (f8) hipLaunchKernelGGL((l2norm_rows_kernel<float, true>), grid, block, 0, stream, (const float*)x, y, inv_norm, rows, C, fp8_scale, nullptr);
-    else hipLaunchKernelGGL((l2norm_rows_kernel<float, false>), grid, block, 0, stream, (const float*)x, y, inv_norm, rows, C, 1.f, lo);
-  }
+  if (y_f16 && (f8 || lo)) return -1;
+#define L2N(TIN) do { \
+    if (f8) hipLaunchKernelGGL((l2norm_rows_kernel<TIN, 1>), grid, block, 0, stream, (const TIN*)x, y, inv_norm, rows, C, fp8_scale, nullptr); \
+    else if (y_f16) hipLaunchKernelGGL((l2norm_rows_kernel<TIN, 2>), grid, block, 0, stream, (const TIN*)x, y, inv_norm, rows, C, 1.f, nullptr); \
+    else hipLaunchKernelGGL((l2norm_rows_kernel<TIN, 0>), grid, block, 0, stream, (const TIN*)x, y, inv_norm, rows, C, 1.f, lo); \
+  } while (0)
+  if (x_is_bf16) L2N(bf16); else L2N(float);
+#undef L2N
   return (int)hipGetLastError();
 }
 
@@ -625,10 +648,12 @@ static int cg2_stages() {
 
 // C[b] = A[amap[b]] . B[bmap[b]]^T ; out_bf16 selects the output dtype.
 // fp8_out_scale != 0: A, B are OCP fp8 e4m3 and C = fp8_out_scale * (A . B^T).
+// f16: A, B (and a 16-bit C) are IEEE half.
 extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int* amap, const int* bmap, int batch,
                                int M, int N, int K, long long sA, long long sB, long long sC, int out_bf16,
-                               float fp8_out_scale, hipStream_t stream) {
+                               float fp8_out_scale, int f16, hipStream_t stream) {
   const bool f8 = fp8_out_scale != 0.f;
+  if (f8 && f16) return -1;
   if (K % (f8 ? 16 : 8) != 0) return -1;
   GemmArgs p{};
   p.A = A; p.B = B; p.C = C; p.amap = amap; p.bmap = bmap;
@@ -645,13 +670,15 @@ extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int*
   if (use_v2(f8, batch, M, N, K)) {
     p.tiles_m = cdiv(M, cg2::BM); p.tiles_n = cdiv(N, cg2::BN);
     dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);
+#define CG2(OB, NSV, H) hipLaunchKernelGGL((corr_gemm_v2_kernel<OB, false, NSV, H>), grid, block, NSV * cg2::STAGE, stream, p)
     if (cg2_stages() == 3) {
-      if (out_bf16) hipLaunchKernelGGL((corr_gemm_v2_kernel<true, false, 3>), grid, block, 3 * cg2::STAGE, stream, p);
-      else hipLaunchKernelGGL((corr_gemm_v2_kernel<false, false, 3>), grid, block, 3 * cg2::STAGE, stream, p);
+      if (f16) { if (out_bf16) CG2(true, 3, true); else CG2(false, 3, true); }
+      else { if (out_bf16) CG2(true, 3, false); else CG2(false, 3, false); }
     } else {
-      if (out_bf16) hipLaunchKernelGGL((corr_gemm_v2_kernel<true, false, 4>), grid, block, 4 * cg2::STAGE, stream, p);
-      else hipLaunchKernelGGL((corr_gemm_v2_kernel<false, false, 4>), grid, block, 4 * cg2::STAGE, stream, p);
+      if (f16) { if (out_bf16) CG2(true, 4, true); else CG2(false, 4, true); }
+      else { if (out_bf16) CG2(true, 4, false); else CG2(false, 4, false); }
     }
+#undef CG2
     return (int)hipGetLastError();
   }
   p.tiles_m = cdiv(M, BM); p.tiles_n = cdiv(N, BN);
@@ -660,6 +687,9 @@ extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int*
   if (f8) {
     if (out_bf16) hipLaunchKernelGGL((corr_gemm_kernel<true, false, true>), grid, block, lds, stream, p);
     else hipLaunchKernelGGL((corr_gemm_kernel<false, false, true>), grid, block, lds, stream, p);
+  } else if (f16) {
+    if (out_bf16) hipLaunchKernelGGL((corr_gemm_kernel<true, false, false, true>), grid, block, lds, stream, p);
+    else hipLaunchKernelGGL((corr_gemm_kernel<false, false, false, true>), grid, block, lds, stream, p);
   } else {
     if (out_bf16) hipLaunchKernelGGL((corr_gemm_kernel<true, false, false>), grid, block, lds, stream, p);
     else hipLaunchKernelGGL((corr_gemm_kernel<false, false, false>), grid, block, lds, stream, p);
@@ -671,8 +701,9 @@ extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int*
 // 2x2-block order (see ncnet_block_order_rows); hA, wA, hB, wB even.
 extern "C" int ncnet_corr_gemm_pool2(const void* A, const void* B, float* pool_val, uint8_t* pool_idx, int batch,
                                      int hA, int wA, int hB, int wB, int K, long long sA, long long sB,
-                                     float fp8_out_scale, hipStream_t stream) {
+                                     float fp8_out_scale, int f16, hipStream_t stream) {
   const bool f8 = fp8_out_scale != 0.f;
+  if (f8 && f16) return -1;
   if (K % (f8 ? 16 : 8) != 0 || (hA & 1) || (wA & 1) || (hB & 1) || (wB & 1)) return -1;
   GemmArgs p{};
   p.A = A; p.B = B; p.C = nullptr;
@@ -689,14 +720,20 @@ extern "C" int ncnet_corr_gemm_pool2(const void* A, const void* B, float* pool_v
   if (use_v2(f8, batch, p.M, p.N, K)) {
     p.tiles_m = cdiv(p.M, cg2::BM); p.tiles_n = cdiv(p.N, cg2::BN);
     dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);
-    if (cg2_stages() == 3) hipLaunchKernelGGL((corr_gemm_v2_kernel<false, true, 3>), grid, block, 3 * cg2::STAGE, stream, p);
-    else hipLaunchKernelGGL((corr_gemm_v2_kernel<false, true, 4>), grid, block, 4 * cg2::STAGE, stream, p);
+    if (f16) {
+      if (cg2_stages() == 3) hipLaunchKernelGGL((corr_gemm_v2_kernel<false, true, 3, true>), grid, block, 3 * cg2::STAGE, stream, p);
+      else hipLaunchKernelGGL((corr_gemm_v2_kernel<false, true, 4, true>), grid, block, 4 * cg2::STAGE, stream, p);
+    } else {
+      if (cg2_stages() == 3) hipLaunchKernelGGL((corr_gemm_v2_kernel<false, true, 3>), grid, block, 3 * cg2::STAGE, stream, p);
+      else hipLaunchKernelGGL((corr_gemm_v2_kernel<false, true, 4>), grid, block, 4 * cg2::STAGE, stream, p);
+    }
     return (int)hipGetLastError();
   }
   p.tiles_m = cdiv(p.M, BM); p.tiles_n = cdiv(p.N, BN);
   dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(256);
   size_t lds = (size_t)(BM + BN) * 128;
   if (f8) hipLaunchKernelGGL((corr_gemm_kernel<false, true, true>), grid, block, lds, stream, p);
+  else if (f16) hipLaunchKernelGGL((corr_gemm_kernel<false, true, false, true>), grid, block, lds, stream, p);
   else hipLaunchKernelGGL((corr_gemm_kernel<false, true, false>), grid, block, lds, stream, p);
   return (int)hipGetLastError();
 }

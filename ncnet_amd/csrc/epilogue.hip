@@ -10,22 +10,28 @@
 
 namespace ncnet {
 
-// 8 channels (16 B) per thread; C % 8 == 0.
-template <bool RELU>
-__global__ __launch_bounds__(256) void bias_act_kernel(bf16* __restrict__ Y, const float* __restrict__ b,
+// 8 channels (16 B) per thread; C % 8 == 0.  F16: Y is IEEE half.
+template <bool RELU, bool F16>
+__global__ __launch_bounds__(256) void bias_act_kernel(uint16_t* __restrict__ Y, const float* __restrict__ b,
                                                        long long n8, int C8) {
   const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
   if (e >= n8) return;
   const int c0 = (int)(e % C8) * 8;
-  bf16x8 v = *(const bf16x8*)(Y + e * 8);
+  u32x4 v = *(const u32x4*)(Y + e * 8);
   const f32x4 b0 = *(const f32x4*)(b + c0), b1 = *(const f32x4*)(b + c0 + 4);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    float x = bf2f(v[q]) + (q < 4 ? b0[q] : b1[q - 4]);
-    if (RELU) x = fmaxf(x, 0.f);
-    v[q] = f2bf(x);
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 2 * q + h;
+      float x = s162f<F16>((uint16_t)(v[q] >> (16 * h))) + (k < 4 ? b0[k] : b1[k - 4]);
+      if (RELU) x = fmaxf(x, 0.f);
+      w |= (uint32_t)f2s16<F16>(x) << (16 * h);
+    }
+    v[q] = w;
   }
-  *(bf16x8*)(Y + e * 8) = v;
+  *(u32x4*)(Y + e * 8) = v;
 }
 
 // Sanitizer-tier self test: out[0] = 1 in release; in the debug build the
@@ -43,12 +49,18 @@ extern "C" int ncnet_debug_selftest(int* out, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-extern "C" int ncnet_bias_act(void* Y, const float* b, long long rows, int C, int relu, hipStream_t stream) {
+extern "C" int ncnet_bias_act(void* Y, const float* b, long long rows, int C, int relu, int f16, hipStream_t stream) {
   if (C % 8) return -1;
   const long long n8 = rows * (C / 8);
   if (n8 == 0) return 0;
   dim3 grid((unsigned)((n8 + 255) / 256)), block(256);
-  if (relu) hipLaunchKernelGGL((bias_act_kernel<true>), grid, block, 0, stream, (bf16*)Y, b, n8, C / 8);
-  else hipLaunchKernelGGL((bias_act_kernel<false>), grid, block, 0, stream, (bf16*)Y, b, n8, C / 8);
+  uint16_t* y = (uint16_t*)Y;
+  if (f16) {
+    if (relu) hipLaunchKernelGGL((bias_act_kernel<true, true>), grid, block, 0, stream, y, b, n8, C / 8);
+    else hipLaunchKernelGGL((bias_act_kernel<false, true>), grid, block, 0, stream, y, b, n8, C / 8);
+  } else {
+    if (relu) hipLaunchKernelGGL((bias_act_kernel<true, false>), grid, block, 0, stream, y, b, n8, C / 8);
+    else hipLaunchKernelGGL((bias_act_kernel<false, false>), grid, block, 0, stream, y, b, n8, C / 8);
+  }
   return (int)hipGetLastError();
 }

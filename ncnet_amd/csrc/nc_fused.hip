@@ -48,6 +48,9 @@ constexpr int NCF_NW = 8;          // waves per workgroup
 constexpr int NCF_MAXT1 = 4;       // layer-1 tiles per wave: (TK+2)(TL+2) <= 512 voxels
 constexpr int NCF_MAXT2 = 3;       // layer-2 tiles per wave: TK*TL <= 384 voxels
 
+// F16: IEEE-half x0, weights and hidden activation (half_precision=True, as
+// eval_inloc.py runs the reference: lib/model.py:265-267), f16 MFMA.
+template <bool F16>
 __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ W1p,
                                                              const float* __restrict__ b1,
                                                              const u32x4* __restrict__ W2p,
@@ -211,11 +214,14 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
       if (wave + NCF_NW * u >= nt1) continue;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc = mfma16u(wl[q * 64 + lane], *(const u32x4*)(S + b1off[u] + toff1[q]), acc);
-      bf16x4 o;
+      for (int q = 0; q < NQ; ++q)
+        acc = mfma16t<F16>(wl[q * 64 + lane], *(const u32x4*)(S + b1off[u] + toff1[q]), acc);
+      u32x2 o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = f2bf(h_in[u] ? fmaxf(acc[r] + bias1[r], 0.f) : 0.f);
-      if (h_ok[u]) *(bf16x4*)(H + h_wr[u]) = o;
+      for (int r = 0; r < 2; ++r)
+        o[r] = (uint32_t)f2s16<F16>(h_in[u] ? fmaxf(acc[2 * r] + bias1[2 * r], 0.f) : 0.f) |
+               ((uint32_t)f2s16<F16>(h_in[u] ? fmaxf(acc[2 * r + 1] + bias1[2 * r + 1], 0.f) : 0.f) << 16);
+      if (h_ok[u]) *(u32x2*)(H + h_wr[u]) = o;
     }
     __syncthreads();                   // h complete
     // ---- C: layer 2 combos -> ring ----
@@ -227,7 +233,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
-        acc = mfma16u(wl[(NQ + q) * 64 + lane], *(const u32x4*)(H + b2off[u] + toff2[q]), acc);
+        acc = mfma16t<F16>(wl[(NQ + q) * 64 + lane], *(const u32x4*)(H + b2off[u] + toff2[q]), acc);
       if (vo[u] < 0 || !p_ok) continue;
       // MFMA row 4 * dj2 + di2 <-> combo (di2, dj2): this lane's rows r share
       // one output plane p2 and differ in the output row ih - r + 1 (uniform)
@@ -263,8 +269,9 @@ using namespace ncnet;
 
 // x0 bf16 [V,I,J,K,L]; W1p / W2p bf16 [5][64][8] (pack_w16_planes of the ij layer weights);
 // b1 fp32 [16], b2 fp32 [1]; y fp32 [V,I,J,K,L].
+// f16: x0 / W1p / W2p are IEEE half (f16 MFMA, f16 hidden activation).
 extern "C" int ncnet_nc_fused_k3(const void* X, const void* W1p, const float* b1, const void* W2p, const float* b2,
-                                 float* Y, int V, int I, int J, int K, int L, int R, int IR, int TK, int TL,
+                                 float* Y, int V, int I, int J, int K, int L, int R, int IR, int TK, int TL, int f16,
                                  hipStream_t stream) {
   NCFGeom g{};
   g.V = V; g.I = I; g.J = J; g.K = K; g.L = L;
@@ -280,7 +287,11 @@ extern "C" int ncnet_nc_fused_k3(const void* X, const void* W1p, const float* b1
                2 * 5 * 64 * 16;
   if (lds > 160 * 1024) return -3;
   dim3 grid((unsigned)((size_t)V * g.nib * g.njb * g.nkt * g.nlt)), block(512);
-  hipLaunchKernelGGL(nc_fused_k3_kernel, grid, block, lds, stream, (const bf16*)X, (const u32x4*)W1p, b1,
-                     (const u32x4*)W2p, b2, Y, g);
+  if (f16)
+    hipLaunchKernelGGL(nc_fused_k3_kernel<true>, grid, block, lds, stream, (const bf16*)X, (const u32x4*)W1p, b1,
+                       (const u32x4*)W2p, b2, Y, g);
+  else
+    hipLaunchKernelGGL(nc_fused_k3_kernel<false>, grid, block, lds, stream, (const bf16*)X, (const u32x4*)W1p, b1,
+                       (const u32x4*)W2p, b2, Y, g);
   return (int)hipGetLastError();
 }

@@ -131,9 +131,11 @@ __global__ __launch_bounds__(256) void stats_cols_merge_kernel(const float* __re
 // cmax: [V,C] (max over A for each B column).
 //   out_f32 [V,R,C] (optional), out_x bf16 [V,R,C] at volume slot v (optional),
 //   out_xt bf16 [V,C,R] at volume slot v (optional; A<->B swapped copy).
+// F16: out_x / out_xt are IEEE half (the half_precision NC input).
+template <bool F16>
 __global__ __launch_bounds__(256) void mm_apply_kernel(const float* __restrict__ c, const float* __restrict__ rmax,
                                                        const float* __restrict__ cmax, float* __restrict__ out_f32,
-                                                       bf16* __restrict__ out_x, bf16* __restrict__ out_xt,
+                                                       uint16_t* __restrict__ out_x, uint16_t* __restrict__ out_xt,
                                                        int R, int C, float eps) {
   __shared__ float tile[64][65];
   const int ntr = (R + 63) / 64, ntc = (C + 63) / 64;
@@ -153,7 +155,7 @@ __global__ __launch_bounds__(256) void mm_apply_kernel(const float* __restrict__
       float ra = rmax[(size_t)v * R + r] + eps;
       o = x * ((x / ra) * (x / cm));
       if (out_f32) out_f32[vb + (size_t)r * C + cc] = o;
-      if (out_x) out_x[vb + (size_t)r * C + cc] = f2bf(o);
+      if (out_x) out_x[vb + (size_t)r * C + cc] = f2s16<F16>(o);
     }
     tile[rr][tx] = o;
   }
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(256) void mm_apply_kernel(const float* __restrict__
     const int rw = r0 + tx;
     for (int cl = ty; cl < 64; cl += 4) {
       int ccol = c0 + cl;
-      if (ccol < C && rw < R) out_xt[vb + (size_t)ccol * R + rw] = f2bf(tile[tx][cl]);
+      if (ccol < C && rw < R) out_xt[vb + (size_t)ccol * R + rw] = f2s16<F16>(tile[tx][cl]);
     }
   }
 }
@@ -419,9 +421,13 @@ extern "C" int ncnet_stats_cols(const float* x, float* mx, int* arg, float* se, 
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_mm_apply(const float* c, const float* rmax, const float* cmax, float* out_f32, void* out_x,
-                              void* out_xt, int V, int R, int C, float eps, hipStream_t s) {
-  hipLaunchKernelGGL(mm_apply_kernel, dim3(tiles64(V, R, C)), dim3(256), 0, s, c, rmax, cmax, out_f32, (bf16*)out_x,
-                     (bf16*)out_xt, R, C, eps);
+                              void* out_xt, int V, int R, int C, float eps, int x_f16, hipStream_t s) {
+  if (x_f16)
+    hipLaunchKernelGGL(mm_apply_kernel<true>, dim3(tiles64(V, R, C)), dim3(256), 0, s, c, rmax, cmax, out_f32,
+                       (uint16_t*)out_x, (uint16_t*)out_xt, R, C, eps);
+  else
+    hipLaunchKernelGGL(mm_apply_kernel<false>, dim3(tiles64(V, R, C)), dim3(256), 0, s, c, rmax, cmax, out_f32,
+                       (uint16_t*)out_x, (uint16_t*)out_xt, R, C, eps);
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_mm_bwd(const float* c, const float* g, const float* rmax, const int* rarg, const float* cmax,

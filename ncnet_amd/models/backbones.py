@@ -325,7 +325,7 @@ class FrozenResNetPlan(nn.Module):
 
     @staticmethod
     def _bias_act(y: torch.Tensor, b: torch.Tensor, relu: bool) -> torch.Tensor:
-        if y.is_cuda and y.dtype == torch.bfloat16:
+        if y.is_cuda and y.dtype in (torch.bfloat16, torch.float16):
             from ..ops import _ext
             if _ext.use_hip(y):
                 _ext.ext().bias_act_(y, b, 1 if relu else 0)
@@ -434,7 +434,7 @@ class FrozenResNetPlan(nn.Module):
                                    b, relu)
             elif kind == "maxpool":
                 x = F.max_pool2d(x, *p).contiguous(memory_format=torch.channels_last)
-            elif self.conv_mode in ("native", "auto") and x.is_cuda and self.dtype == torch.bfloat16:
+            elif self.conv_mode in ("native", "auto") and x.is_cuda and self.dtype in (torch.bfloat16, torch.float16):
                 y1 = self._n1(x, p, bi) if self.conv_mode == "auto" else self._nconv(x, p["n1"], True)
                 y2 = self._nconv(y1, p["n2"], True)
                 idt = x if p["nd"] is None else self._nconv(x, p["nd"], False)

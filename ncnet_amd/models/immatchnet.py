@@ -24,8 +24,8 @@ import torch.nn.functional as F
 
 from ..ops import reference as ref
 from ..ops.conv4d import Conv4d
-from ..ops.correlation import (correlation, correlation_pool2, correlation_x3, l2norm_pack, l2norm_pack_fp8,
-                               l2norm_pack_split, maxpool4d as _maxpool4d)
+from ..ops.correlation import (correlation, correlation_pool2, correlation_x3, l2norm_pack, l2norm_pack_f16,
+                               l2norm_pack_fp8, l2norm_pack_split, maxpool4d as _maxpool4d)
 from ..ops import _ext as _ext_mod
 from ..ops.mutual import mutual_matching, mutual_matching_nc_input as _mm_nc_input
 from ..ops.neigh_consensus import neigh_consensus
@@ -191,8 +191,8 @@ class ImMatchNet(nn.Module):
                  feature_extraction_model_file: str | None = None, return_correlation: bool = False,
                  ncons_kernel_sizes=(3, 3, 3), ncons_channels=(10, 10, 1), normalize_features: bool = True,
                  train_fe: bool = False, use_cuda: bool = True, relocalization_k_size: int = 0,
-                 half_precision: bool = False, checkpoint: str | None = None, dtype: str = "bf16",
-                 fold_bn: bool = True, corr_dtype: str = "bf16", nc_precision: str = "bf16"):
+                 half_precision: bool = False, checkpoint: str | None = None, dtype: str | None = None,
+                 fold_bn: bool = True, corr_dtype: str | None = None, nc_precision: str = "bf16"):
         super().__init__()
         ck = None
         if checkpoint:
@@ -206,10 +206,20 @@ class ImMatchNet(nn.Module):
         self.return_correlation = return_correlation
         self.relocalization_k_size = relocalization_k_size
         self.half_precision = half_precision
+        # half_precision (the reference's eval_inloc.py setting, lib/model.py:253-267):
+        # the reference halves AFTER its fp32 trunk and L2 norm, so do we -- IEEE-half
+        # features, correlation, NeighConsensus input and hidden activation on the
+        # f16 MFMA (the bf16 rate, 3 more mantissa bits), fp32 accumulation; the
+        # trunk keeps bf16 (fp32's exponent range: unnormalised activations of a
+        # deep trunk overflow fp16 -- measured on the random-init ResNet-101)
+        if dtype is None:
+            dtype = "bf16"
+        if corr_dtype is None:
+            corr_dtype = "fp16" if half_precision else "bf16"
         self.compute_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype]
         self.fold_bn = fold_bn
-        if corr_dtype not in ("bf16", "fp8", "fp32"):
-            raise ValueError("corr_dtype must be 'bf16', 'fp8' or 'fp32'")
+        if corr_dtype not in ("bf16", "fp16", "fp8", "fp32"):
+            raise ValueError("corr_dtype must be 'bf16', 'fp16', 'fp8' or 'fp32'")
         # fp8: OCP e4m3 correlation operands on the MX-fp8 MFMA and fp8
         # NeighConsensus (fp8 MFMA Conv4d) -- inference only.
         # fp32: fp32-accurate correlation + NeighConsensus (bf16x3 split on the
@@ -262,6 +272,8 @@ class ImMatchNet(nn.Module):
             if torch.is_grad_enabled() and self.training:
                 raise RuntimeError("corr_dtype='fp8' is an inference path (no autograd)")
             return l2norm_pack_fp8(f), tuple(f.shape[-2:])
+        if self.corr_dtype == "fp16" and not (torch.is_grad_enabled() and self.training):
+            return l2norm_pack_f16(f), tuple(f.shape[-2:])
         if self.corr_dtype == "fp32" or self.nc_precision == "fp32":
             if f.requires_grad:
                 if self.corr_dtype == "fp32":
@@ -283,7 +295,7 @@ class ImMatchNet(nn.Module):
             # input of both symmetric branches directly
             layers = nc.conv_layers()
             with segment("mutual_matching"):
-                x2 = _mm_nc_input(corr4d)
+                x2 = _mm_nc_input(corr4d, torch.float16 if self.corr_dtype == "fp16" else torch.bfloat16)
             _ext_count("nc_fused_k3")
             with segment("neigh_consensus"):
                 corr4d = _nc_ops.neigh_consensus_fused_x2(

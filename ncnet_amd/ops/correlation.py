@@ -9,6 +9,8 @@
 * ``correlation_pool2``: the InLoc relocalization path; GEMM with a fused
   2x2x2x2 max-pool epilogue (lib/model.py:177-191) -- only the pooled volume
   and packed argmax offsets are written.
+* IEEE-half inference (``corr_dtype='fp16'``, half_precision models as the
+  reference's eval_inloc.py): ``l2norm_pack_f16`` operands on the f16 MFMA.
 * fp32-accurate inference ("bf16x3", ``corr_dtype='fp32'``): the L2-norm
   kernel also writes the bf16 rounding residual and the correlation is three
   bf16 GEMMs (hi.hi + hi.lo + lo.hi), matching the reference's fp32 bmm
@@ -83,6 +85,23 @@ def l2norm_pack_fp8(feat: torch.Tensor) -> torch.Tensor:
     return y.reshape(n, h * w, c)
 
 
+def l2norm_pack_f16(feat: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] -> L2-normalised [N, H*W, C] in IEEE half (the reference's
+    half_precision features, lib/model.py:263-265; inference).  The GEMMs then
+    run on the f16 MFMA: 3 more mantissa bits than bf16 at the same rate."""
+    n, c, h, w = feat.shape
+    if not _ext.use_hip(feat):
+        return ref.feature_l2norm(feat.float()).reshape(n, c, h * w).transpose(1, 2).to(torch.float16)
+    x = feat.permute(0, 2, 3, 1)
+    if not x.is_contiguous():
+        x = x.contiguous()
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        x = x.float()
+    y = torch.empty((n * h * w, c), dtype=torch.float16, device=feat.device)
+    _ext.ext().l2norm_rows(x.reshape(n * h * w, c), y, None, 0.0, None)
+    return y.reshape(n, h * w, c)
+
+
 def l2norm_pack_split(feat: torch.Tensor):
     """[N, C, H, W] -> (hi, lo) bf16 [N, H*W, C] with hi + lo = the L2-normalised
     rows to ~16 mantissa bits (fp32-accurate "bf16x3" inference mode)."""
@@ -145,8 +164,9 @@ class CorrelationFn(torch.autograd.Function):
     def forward(ctx, fa, fb, amap, bmap):
         V = amap.numel()
         out = torch.empty((V, fa.shape[1], fb.shape[1]), dtype=torch.float32, device=fa.device)
-        a = fa.to(torch.bfloat16).contiguous()
-        b = fb.to(torch.bfloat16).contiguous()
+        dt = torch.float16 if fa.dtype == torch.float16 else torch.bfloat16   # f16 MFMA for half operands
+        a = fa.to(dt).contiguous()
+        b = fb.to(dt).contiguous()
         _ext.ext().corr_gemm(a, b, out, amap, bmap, 1.0)
         ctx.save_for_backward(a, b, amap, bmap)
         ctx.dtypes = (fa.dtype, fb.dtype)
@@ -218,8 +238,9 @@ def correlation_pool2(fa: torch.Tensor, fb: torch.Tensor, hA: int, wA: int, hB: 
     if fp8:
         a, b = _fp8_rows(fa, pa), _fp8_rows(fb, pb)
     else:
-        a = fa.to(torch.bfloat16)[:, pa].contiguous()
-        b = fb.to(torch.bfloat16)[:, pb].contiguous()
+        dt = torch.float16 if fa.dtype == torch.float16 else torch.bfloat16
+        a = fa.to(dt)[:, pa].contiguous()
+        b = fb.to(dt)[:, pb].contiguous()
     shape = (V, hA // 2, wA // 2, hB // 2, wB // 2)
     val = torch.empty(shape, dtype=torch.float32, device=fa.device)
     code = torch.empty(shape, dtype=torch.uint8, device=fa.device)

@@ -53,17 +53,17 @@ class MutualMatchingFn(torch.autograd.Function):
         return gc.reshape(ctx.shape)
 
 
-def mutual_matching_nc_input(corr4d: torch.Tensor) -> torch.Tensor:
+def mutual_matching_nc_input(corr4d: torch.Tensor, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
     """Inference MutualMatching written straight as the bf16 input of both
     symmetric NeighConsensus branches: [2V, I, J, K, L] with x in the first V
     volumes and its A<->B swap in the last V (mm_apply's bf16 and transposed
     bf16 outputs; no fp32 volume, no cast, no separate transpose).  Square
-    volumes only (I, J) == (K, L)."""
+    volumes only (I, J) == (K, L).  ``dtype``: bf16, or float16 (half_precision models)."""
     V, ch, I, J, K, L = corr4d.shape
     assert ch == 1 and (I, J) == (K, L)
     c3 = corr4d.reshape(V, I * J, K * L).float().contiguous()
     rmax, _, cmax, _ = _stats(c3)
-    x2 = torch.empty((2 * V, I, J, K, L), dtype=torch.bfloat16, device=c3.device)
+    x2 = torch.empty((2 * V, I, J, K, L), dtype=dtype, device=c3.device)
     _ext.ext().mm_apply(c3, rmax, cmax, None, x2[:V].view(V, I * J, K * L), x2[V:].view(V, K * L, I * J), EPS)
     return x2
 

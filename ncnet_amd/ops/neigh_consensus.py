@@ -1072,9 +1072,11 @@ def fused_tiles(V: int, I: int, J: int, K: int, L: int):
     return tk, tl, R, IR
 
 
-def _fused_weights(weights, biases):
+def _fused_weights(weights, biases, dtype=torch.bfloat16):
+    """Packed fused-kernel weights in the operand dtype (bf16, or float16 for the
+    IEEE-half kernel of half_precision models)."""
     w1, w2 = _std(weights[0]), _std(weights[1])
-    W1p = pack_w16_planes(ij_in_weights(w1))[0].contiguous()
+    W1p = pack_w16_planes(ij_in_weights(w1), dtype)[0].contiguous()
     # layer-2 MFMA rows: row 4 * dj + di <- ij combo di * 3 + dj (nc_fused.hip: a
     # lane's four rows then share dj and one output plane); other rows zero
     wo = ij_out_weights(w2)
@@ -1082,7 +1084,7 @@ def _fused_weights(weights, biases):
     for di in range(3):
         for dj in range(3):
             wr[:, 4 * dj + di] = wo[:, 3 * di + dj]
-    W2p = pack_w16_planes(wr)[0].contiguous()
+    W2p = pack_w16_planes(wr, dtype)[0].contiguous()
     return W1p, _pad_bias(biases[0], 16), W2p, _pad_bias(biases[1], 1)
 
 
@@ -1095,11 +1097,11 @@ def _run_fused(xb: torch.Tensor, wts) -> torch.Tensor:
 
 
 def neigh_consensus_fused_x2(x2: torch.Tensor, weights, biases) -> torch.Tensor:
-    """Symmetric fused NC on a prepared [2V, I, J, K, L] bf16 input (x, then its
-    A<->B swap: ops/mutual.py mutual_matching_nc_input) -> [V, 1, I, J, K, L] fp32."""
+    """Symmetric fused NC on a prepared [2V, I, J, K, L] bf16 / float16 input (x,
+    then its A<->B swap: ops/mutual.py mutual_matching_nc_input) -> [V, 1, I, J, K, L] fp32."""
     V2, I, J, K, L = x2.shape
     V = V2 // 2
-    z = _run_fused(x2, _fused_weights(weights, biases))
+    z = _run_fused(x2, _fused_weights(weights, biases, x2.dtype))
     y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=x2.device)
     _ext.ext().combine_fwd(z, y, I * J, K * L)
     return y.reshape(V, 1, I, J, K, L)

@@ -75,13 +75,14 @@ def ij_groups(ks: int) -> int:
     return (ks * ks + 15) // 16
 
 
-def pack_w16_planes(wp: torch.Tensor) -> torch.Tensor:
-    """[NPL, 16 co, 16 ci, k, k] -> [NPL, ceil(k*k/2), 64, 8] (pack_w16 per plane)."""
+def pack_w16_planes(wp: torch.Tensor, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """[NPL, 16 co, 16 ci, k, k] -> [NPL, ceil(k*k/2), 64, 8] (pack_w16 per plane);
+    ``dtype`` bf16, or float16 for the IEEE-half kernels (rounded once, from fp32)."""
     npl, ks = wp.shape[0], wp.shape[-1]
     w = wp.reshape(npl, 16, 16, ks * ks)
     co, ci, tap, valid = _idx16(ks, w.device)
     vals = w[:, co, ci, tap] * valid.to(w.dtype)      # [npl, nq, 64, 8]
-    return vals.contiguous().to(torch.bfloat16)
+    return vals.contiguous().to(dtype)
 
 
 def ij_in_weights(w_std: torch.Tensor) -> torch.Tensor:

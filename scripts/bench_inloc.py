@@ -37,7 +37,8 @@ from ncnet_amd.ops.correlation import correlation, correlation_pool2  # noqa: E4
 
 def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup: int = 2, k: int = 2,
                ncons_kernel_sizes=(3, 3), ncons_channels=(16, 1), src_hw=(3024, 4032), no_matches: bool = False,
-               impl: str = "hip", model=None, panos_per_query: int = 1, pair_graph: bool | None = None) -> dict:
+               impl: str = "hip", model=None, panos_per_query: int = 1, pair_graph: bool | None = None,
+               precision: str | None = None) -> dict:
     """One InLoc query/pano pair per forward on one GPU; returns the JSON record.
 
     panos_per_query > 1: eval_inloc.py's schedule -- the query's features are
@@ -51,11 +52,17 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
     ("stages_ms_eager": corr_pool, mm_nc_mm, matches)."""
     dev = torch.device("cuda")
     torch.manual_seed(0)
+    # precision: bf16 (bf16 trunk + operands), fp16 (bf16 trunk, IEEE-half
+    # features / correlation / NC: the reference's half_precision numerics on the
+    # f16 MFMA), fp8 (bf16 trunk, e4m3 correlation operands)
+    precision = precision or ("fp8" if fp8 else "bf16")
     if model is None:
         model = ImMatchNet(use_cuda=True, ncons_kernel_sizes=list(ncons_kernel_sizes),
                            ncons_channels=list(ncons_channels), half_precision=True, relocalization_k_size=k,
-                           corr_dtype="fp8" if fp8 else "bf16").to(dev).eval()
-    model.corr_dtype = "fp8" if fp8 else "bf16"
+                           corr_dtype=precision).to(dev).eval()
+    model.corr_dtype = precision
+    model.compute_dtype = torch.bfloat16     # the trunk (fp16: halved after the L2 norm, as the reference)
+    fp8 = precision == "fp8"
     h, w = target_size(src_hw[0], src_hw[1], image_size, k)
     if pair_graph is None:
         pair_graph = panos_per_query > 1 and os.environ.get("NCNET_PAIR_GRAPH", "1") != "0"
@@ -168,7 +175,7 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
         "impl": impl,
         "dtype": ("fp32-backbone/fp16-volume" if impl == "reference" else
                   (("fp8-corr+fp8-nc" if os.environ.get("NCNET_NC_FP8") == "1" else "fp8-corr+bf16-fused-nc")
-                   if fp8 else "bf16")),
+                   if fp8 else precision)),
         "data": "synthetic (random 4:3 images, random-init weights)",
         "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,
                    "ncons": [list(ncons_kernel_sizes), list(ncons_channels)], "k": k,
@@ -195,7 +202,12 @@ def main():
     ap.add_argument("--no-matches", action="store_true")
     ap.add_argument("--panos-per-query", type=int, default=1,
                     help="eval_inloc.py schedule: query features extracted once per this many pairs (10 in InLoc)")
-    ap.add_argument("--fp8", action="store_true", help="OCP fp8 correlation operands (MX-fp8 MFMA) + fp8 NC")
+    ap.add_argument("--fp8", action="store_true",
+                    help="OCP e4m3 correlation operands (MX-fp8 MFMA); the NC runs the fused bf16 kernel "
+                         "(NCNET_NC_FP8=1: the fp8 Conv4d kernels instead)")
+    ap.add_argument("--precision", choices=["bf16", "fp16", "fp8"], default=None,
+                    help="operand precision (default bf16, or fp8 with --fp8); fp16 = the reference's half "
+                         "precision on the f16 MFMA")
     ap.add_argument("--impl", choices=["hip", "reference"], default="hip",
                     help="reference: the reference algorithm in plain PyTorch-ROCm (fp32 backbone, fp16 volume)")
     ap.add_argument("--volume-parallel", action="store_true")
@@ -203,7 +215,8 @@ def main():
     if a.volume_parallel:
         return bench_volume_parallel(a)
     print(json.dumps(run_single(a.image_size, a.fp8, a.pairs, a.warmup, a.k, a.ncons_kernel_sizes, a.ncons_channels,
-                                a.src_hw, a.no_matches, a.impl, panos_per_query=a.panos_per_query)))
+                                a.src_hw, a.no_matches, a.impl, panos_per_query=a.panos_per_query,
+                                precision=a.precision)))
 
 
 def bench_volume_parallel(a):

@@ -6,6 +6,9 @@ similarity warps) the same random-init model is evaluated by
 * ``ref``  -- engine.reference_impl, the reference's fp32 computation
   (fp32 trunk, torch.bmm, per-slice conv3d NeighConsensus);
 * ``bf16`` -- the default HIP path (bf16 operands, fp32 accumulation);
+* ``fp16`` -- ``corr_dtype='fp16'``: bf16 trunk, IEEE-half features,
+  correlation and NC on the f16 MFMA (the reference's half_precision; for
+  PF-Pascal the 5,5,5 NC stays on the bf16 Conv4d kernels);
 * ``fp32`` -- ``corr_dtype='fp32'``: fp32 trunk, bf16x3 correlation and NC;
 * ``fp8``  -- ``corr_dtype='fp8'`` (InLoc config only): e4m3 correlation + NC.
 Reported per precision: relative L2 of the output volume vs ``ref``, the
@@ -91,10 +94,13 @@ def main(argv=None):
     ap.add_argument("--out", type=str, default="")
     ap.add_argument("--pf-batches", type=int, default=4)
     ap.add_argument("--inloc-batches", type=int, default=2)
+    ap.add_argument("--inloc-sizes", type=int, nargs="+", default=[1600])
     a = ap.parse_args(argv)
     dev = torch.device("cuda")
-    res = [run_cfg("pf_pascal_400", 400, [5, 5, 5], [16, 16, 1], 0, a.pf_batches, 4, ["bf16", "fp32"], dev),
-           run_cfg("inloc_1600_k2", 1600, [3, 3], [16, 1], 2, a.inloc_batches, 1, ["bf16", "fp32", "fp8"], dev)]
+    res = [run_cfg("pf_pascal_400", 400, [5, 5, 5], [16, 16, 1], 0, a.pf_batches, 4, ["bf16", "fp16", "fp32"], dev)]
+    for size in a.inloc_sizes:
+        res.append(run_cfg(f"inloc_{size}_k2", size, [3, 3], [16, 1], 2, a.inloc_batches, 1,
+                           ["bf16", "fp16", "fp32", "fp8"], dev))
     for r in res:
         print(json.dumps(r), flush=True)
     if a.out:
