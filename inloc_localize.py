@@ -19,6 +19,13 @@ comparing dense RootSIFT with the query image (--query_dir); the candidates are
 re-ranked by that score ('InLoc + NCNet').  --plot writes the localization
 curves of both methods (generate_ncnet_plot.m).
 
+Every (query, cutout) pair is an independent task with its own seeded
+generator, run on --workers spawned processes (the reference's parfor over
+queries, ir_top100_NC4D_localization_pnponly.m:25, and over unique scans for
+PV, ht_top10_NC4D_PV_localization.m:44); results do not depend on the worker
+count.  --cache_dir keeps one file per pair (parfor_NC4D_PE_pnponly.m:4-6
+skips pairs whose .mat exists), so an interrupted run resumes.
+
 Inputs on disk (InLoc layout): --cutout_dir/<dbname>.mat with 'XYZcut'
 [H,W,3]; optional --trans_dir/<dbname>.txt holding the 4x4 (or 3x4)
 scan-to-global matrix.  --synthetic N builds a fake scene to smoke-test the
@@ -57,28 +64,101 @@ def load_refposes(path: str):
     return refs
 
 
-def localize_query(q_matches: np.ndarray, db_names, q_size, args, rng):
-    """q_matches [1, n_panos, N, 5] -> list of (dbname, P or None, n_inliers)."""
-    out = []
-    for jj, dbname in enumerate(db_names[: args.pnp_topN]):
-        xyz_path = os.path.join(args.cutout_dir, dbname + ".mat")
-        if not os.path.exists(xyz_path) or jj >= q_matches.shape[1]:
-            out.append((dbname, None, 0))
-            continue
+def _pair_rng(seed: int, q: int, jj: int):
+    """Per-(query, cutout) generator: results do not depend on the worker count
+    or the order the pairs run in."""
+    return np.random.default_rng([seed, q, jj])
+
+
+def _cache_path(cache_dir: str, qname: str, dbname: str, kind: str) -> str:
+    """parfor_NC4D_PE_pnponly.m:4 / parfor_nc4d_PV.m: one file per (query, db)."""
+    return os.path.join(cache_dir, kind, qname, os.path.basename(dbname) + ".npz")
+
+
+def _pnp_pair(task):
+    """One (query, cutout) pair: threshold, tentatives, P3P LO-RANSAC
+    (parfor_NC4D_PE_pnponly.m).  Cached on disk when cache_dir is set."""
+    q, jj, qname, dbname, m, q_size, cfg = task
+    cpath = _cache_path(cfg["cache_dir"], qname, dbname, "pnp") if cfg["cache_dir"] else None
+    if cpath and os.path.exists(cpath):
+        z = np.load(cpath)
+        P = z["P"]
+        return q, jj, dbname, (None if np.isnan(P).all() else P), int(z["n_inliers"])
+    P, n_inl = None, 0
+    xyz_path = os.path.join(cfg["cutout_dir"], dbname + ".mat")
+    if m is not None and os.path.exists(xyz_path):
         xyz = _loadmat(xyz_path)["XYZcut"].astype(np.float64)
         P_after = None
-        if args.trans_dir:
-            tp = os.path.join(args.trans_dir, dbname + ".txt")
+        if cfg["trans_dir"]:
+            tp = os.path.join(cfg["trans_dir"], dbname + ".txt")
             if os.path.exists(tp):
                 P_after = np.loadtxt(tp)
-        rays, X, _, _ = tentative_correspondences(q_matches[0, jj], args.thr, q_size, xyz, args.focal, P_after,
-                                                  args.n_subsample, rng)
-        if rays.shape[1] < 3:
-            out.append((dbname, None, 0))
-            continue
-        P, inl = p3p_ransac(rays, X, np.radians(args.pnp_thr), args.ransac_iters, rng=rng)
-        out.append((dbname, P, int(inl.sum())))
+        rng = _pair_rng(cfg["seed"], q, jj)
+        rays, X, _, _ = tentative_correspondences(m, cfg["thr"], q_size, xyz, cfg["focal"], P_after,
+                                                  cfg["n_subsample"], rng)
+        if rays.shape[1] >= 3:
+            P, inl = p3p_ransac(rays, X, np.radians(cfg["pnp_thr"]), cfg["ransac_iters"], rng=rng)
+            n_inl = int(inl.sum())
+    if cpath:
+        os.makedirs(os.path.dirname(cpath), exist_ok=True)
+        tmp = cpath + ".tmp.npz"
+        np.savez(tmp, P=np.full((3, 4), np.nan) if P is None else P, n_inliers=n_inl)
+        os.replace(tmp, cpath)
+    return q, jj, dbname, P, n_inl
+
+
+def _cfg(args) -> dict:
+    return {k: getattr(args, k) for k in ("cutout_dir", "trans_dir", "thr", "focal", "n_subsample", "pnp_thr",
+                                          "ransac_iters", "seed", "cache_dir", "query_dir", "pv_device")}
+
+
+def localize_query(q_matches: np.ndarray, db_names, q_size, args, q: int = 0, qname: str = "query"):
+    """q_matches [1, n_panos, N, 5] -> list of (dbname, P or None, n_inliers), serially."""
+    cfg = _cfg(args)
+    out = []
+    for jj, dbname in enumerate(db_names[: args.pnp_topN]):
+        m = q_matches[0, jj] if jj < q_matches.shape[1] else None
+        _, _, name, P, n = _pnp_pair((q, jj, qname, dbname, m, q_size, cfg))
+        out.append((name, P, n))
     return out
+
+
+def _executor(workers: int):
+    """Spawned worker processes (the parent may hold OpenMP / torch threads that
+    do not survive a fork); MATLAB's parpool in the reference."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    return ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn"),
+                               initializer=_worker_init)
+
+
+def _worker_init():
+    try:
+        import torch
+        torch.set_num_threads(1)
+    except Exception:  # pragma: no cover
+        pass
+
+
+def localize_all(jobs, args):
+    """jobs: [(q, qname, matches [1, n_panos, N, 5], db_names)] -> {q: [(dbname, P, n_inl)] * topN}.
+    Every (query, cutout) pair is one task (ir_top100_NC4D_localization_pnponly.m:25
+    parfors over queries; pairs balance better when queries have few panos)."""
+    cfg, q_size = _cfg(args), tuple(args.query_size)
+    tasks = []
+    for q, qname, mats, names in jobs:
+        for jj, dbname in enumerate(list(names)[: args.pnp_topN]):
+            m = mats[0, jj] if jj < mats.shape[1] else None
+            tasks.append((q, jj, qname, dbname, m, q_size, cfg))
+    res = {q: [None] * min(len(names), args.pnp_topN) for q, _, _, names in jobs}
+    if args.workers > 1 and len(tasks) > 1:
+        with _executor(args.workers) as ex:
+            outs = list(ex.map(_pnp_pair, tasks, chunksize=max(1, len(tasks) // (4 * args.workers))))
+    else:
+        outs = [_pnp_pair(t) for t in tasks]
+    for q, jj, dbname, P, n in outs:
+        res[q][jj] = (dbname, P, n)
+    return res
 
 
 def _texture(Xw: np.ndarray) -> np.ndarray:
@@ -164,41 +244,62 @@ def make_synthetic(root: str, n_queries: int, n_panos: int, rng):
     return refs, (hq, wq), focal
 
 
-class ScanCache:
-    """Loads each scan once (at_pv_wrapper.m groups candidates by scan)."""
-
-    def __init__(self, scan_dir: str, suffix: str):
-        self.scan_dir, self.suffix, self.cache = scan_dir, suffix, {}
-
-    def get(self, dbname: str):
-        scan_path, trans_path = pv.scan_paths(dbname, self.scan_dir, self.suffix)
-        if scan_path not in self.cache:
-            if not os.path.exists(scan_path):
-                self.cache[scan_path] = None
-            else:
-                P_after = pv.load_transformation(trans_path) if os.path.exists(trans_path) else None
-                self.cache[scan_path] = pv.load_scan(scan_path, P_after)
-        return self.cache[scan_path]
-
-
-def verify_query(qname: str, res, args, scans: ScanCache):
-    """Dense-PV scores of one query's candidates, re-ranked (descending)."""
+def _pv_scan(task):
+    """All candidates that render from one scan (at_pv_wrapper.m: load the scan
+    once, then parfor_nc4d_PV.m per (query, cutout, P)).  Returns
+    [(q, jj, score)]; scores are cached per pair when cache_dir is set."""
+    scan_path, trans_path, items, cfg = task
     from PIL import Image
+    out, todo = [], []
+    for q, jj, qname, dbname, P in items:
+        cpath = _cache_path(cfg["cache_dir"], qname, dbname, "pv") if cfg["cache_dir"] else None
+        if cpath and os.path.exists(cpath):
+            out.append((q, jj, float(np.load(cpath)["score"])))
+        else:
+            todo.append((q, jj, qname, dbname, P, cpath))
+    if not todo:
+        return out
+    scan = None
+    if os.path.exists(scan_path):
+        P_after = pv.load_transformation(trans_path) if os.path.exists(trans_path) else None
+        scan = pv.load_scan(scan_path, P_after)
+    qimgs = {}
+    for q, jj, qname, dbname, P, cpath in todo:
+        qpath = os.path.join(cfg["query_dir"], qname)
+        s = 0.0
+        if scan is not None and P is not None and os.path.exists(qpath):
+            if qname not in qimgs:
+                qimgs[qname] = np.asarray(Image.open(qpath).convert("RGB"))
+            s = float(pv.pv_score(qimgs[qname], scan[0], scan[1], P, cfg["focal"], device=cfg["pv_device"])[0])
+        if cpath:
+            os.makedirs(os.path.dirname(cpath), exist_ok=True)
+            tmp = cpath + ".tmp.npz"
+            np.savez(tmp, score=s)
+            os.replace(tmp, cpath)
+        out.append((q, jj, s))
+    return out
 
-    qpath = os.path.join(args.query_dir, qname)
-    if not os.path.exists(qpath):
-        return res, [0.0] * len(res)
-    qimg = np.asarray(Image.open(qpath).convert("RGB"))
-    scores = []
-    for dbname, P, _ in res[: args.pv_topN]:
-        scan = scans.get(dbname) if P is not None else None
-        if scan is None:
-            scores.append(0.0)
-            continue
-        s, _, _, _ = pv.pv_score(qimg, scan[0], scan[1], P, args.focal, device=args.pv_device)
-        scores.append(float(s))
-    ranked, sc = pv.rerank(res[: args.pv_topN], scores)
-    return ranked, sc
+
+def verify_all(results, qnames, args):
+    """Dense pose verification of every query's top-N candidates, grouped by
+    scan (ht_top10_NC4D_PV_localization.m:30-47), then the per-query re-rank.
+    results: {q: [(dbname, P, n)]} -> {q: (ranked candidates, scores)}."""
+    cfg = _cfg(args)
+    groups = {}
+    for q, res in results.items():
+        for jj, (dbname, P, _) in enumerate(res[: args.pv_topN]):
+            scan_path, trans_path = pv.scan_paths(dbname, args.scan_dir, args.scan_suffix)
+            groups.setdefault((scan_path, trans_path), []).append((q, jj, qnames[q], dbname, P))
+    tasks = [(sp, tp, items, cfg) for (sp, tp), items in sorted(groups.items())]
+    if args.workers > 1 and len(tasks) > 1 and args.pv_device == "cpu":
+        with _executor(args.workers) as ex:
+            outs = [o for part in ex.map(_pv_scan, tasks) for o in part]
+    else:
+        outs = [o for t in tasks for o in _pv_scan(t)]
+    scores = {q: [0.0] * min(len(res), args.pv_topN) for q, res in results.items()}
+    for q, jj, s in outs:
+        scores[q][jj] = s
+    return {q: pv.rerank(results[q][: args.pv_topN], scores[q]) for q in results}
 
 
 def main(argv=None):
@@ -227,6 +328,10 @@ def main(argv=None):
     ap.add_argument("--plot", type=str, default="", help="write the localization curves to this image")
     ap.add_argument("--synthetic", type=int, default=0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1),
+                    help="worker processes for the per-pair P3P RANSAC and the per-scan PV (1 = serial)")
+    ap.add_argument("--cache_dir", type=str, default="",
+                    help="per-(query, cutout) result cache (pnp/<query>/<db>.npz, pv/...); reruns skip cached pairs")
     args = ap.parse_args(argv)
     rng = np.random.default_rng(args.seed)
     refs = None
@@ -239,19 +344,23 @@ def main(argv=None):
         args.scan_dir, args.query_dir = os.path.join(tmp, "scans"), os.path.join(tmp, "queries")
     queries, panos, _ = load_shortlist(args.shortlist)
     estimates, estimates_pv, records = {}, {}, []
-    scans = ScanCache(args.scan_dir, args.scan_suffix) if args.pv else None
+    jobs = []
     for q, qname in enumerate(queries):
         mpath = os.path.join(args.matches_dir, f"{q + 1}.mat")
-        if not os.path.exists(mpath):
-            continue
-        res = localize_query(_loadmat(mpath)["matches"], list(panos[q]), tuple(args.query_size), args, rng)
+        if os.path.exists(mpath):
+            jobs.append((q, qname, _loadmat(mpath)["matches"], list(panos[q])))
+    results = localize_all(jobs, args)
+    qnames = {q: qname for q, qname, _, _ in jobs}
+    verified = verify_all(results, qnames, args) if args.pv else {}
+    for q, qname, _, _ in jobs:
+        res = results[q]
         pick = 0
         if args.rerank == "inliers":
             pick = int(np.argmax([r[2] for r in res]))
         estimates[qname] = (res[pick][0], res[pick][1])
         msg = f"{qname}: top-1 {res[pick][0]} inliers {res[pick][2]}"
         if args.pv:
-            ranked, sc = verify_query(qname, res, args, scans)
+            ranked, sc = verified[q]
             estimates_pv[qname] = (ranked[0][0], ranked[0][1])
             msg += f" | PV top-1 {ranked[0][0]} score {sc[0]:.3f}"
         records.append((qname, res))

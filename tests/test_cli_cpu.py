@@ -75,6 +75,28 @@ def test_inloc_localize_synthetic(workdir):
     assert os.path.exists("error_NCNet_PV.txt")
 
 
+def test_inloc_localize_parallel_cached(workdir):
+    """Pair tasks on 2 spawned workers match the serial run exactly; a rerun
+    with the per-pair cache recomputes nothing and returns the same poses."""
+    import numpy as np
+    import inloc_localize
+    cache = os.path.join(workdir, "cache")
+    base = ["--synthetic", "2", "--ransac_iters", "500", "--pv", "--out", os.path.join(workdir, "p.npz")]
+    est1, _ = inloc_localize.main(base + ["--workers", "1"])
+    est2, _ = inloc_localize.main(base + ["--workers", "2", "--cache_dir", cache])
+    n_pnp = sum(len(f) for _, _, f in os.walk(os.path.join(cache, "pnp")))
+    n_pv = sum(len(f) for _, _, f in os.walk(os.path.join(cache, "pv")))
+    assert n_pnp == 2 * 3 and n_pv == 2 * 3
+    stamp = {os.path.join(d, f): os.path.getmtime(os.path.join(d, f)) for d, _, fs in os.walk(cache) for f in fs}
+    est3, _ = inloc_localize.main(base + ["--workers", "2", "--cache_dir", cache])
+    assert stamp == {os.path.join(d, f): os.path.getmtime(os.path.join(d, f)) for d, _, fs in os.walk(cache) for f in fs}
+    for e in (est2, est3):
+        assert est1.keys() == e.keys()
+        for k in est1:
+            assert est1[k][0] == e[k][0]
+            np.testing.assert_array_equal(est1[k][1], e[k][1])
+
+
 def test_reference_refposes_parse():
     """The reference's own GT pose file (MATLAB v5, read with scipy.io.loadmat)."""
     import inloc_localize
