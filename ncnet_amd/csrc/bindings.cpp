@@ -50,6 +50,7 @@ int ncnet_pad_geom(int, int, int, int*, int*);
 int ncnet_pad_planes(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_conv1x16(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int,
                    hipStream_t);
+int ncnet_wgrad1x16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_nc_fused_k3(const void*, const void*, const float*, const void*, const float*, float*, int, int, int, int,
                       int, int, int, int, int, int, hipStream_t);
 }
@@ -130,6 +131,31 @@ bool conv1x16(Tensor Xp, Tensor Wa, c10::optional<Tensor> bias, c10::optional<Te
                                (int)V, (int)I, (int)J, (int)K, (int)L, (int)ks, (int)epi, nt, cur_stream(Xp));
   if (r == -1) return false;
   ok(r, "conv1x16");
+  return true;
+}
+
+// Weight-gradient partials of a Conv4d with a 1-channel operand (csrc/conv1x.hip
+// wgrad1x16): D bf16 [V,I,J,K,L,16], X1 padded planes [V*I*J, PPL];
+// part fp32 [G, ks^2, 32, 16] (G workgroups, one partial each), partb fp32 [G, 16]
+// (the sum of D) or None.  Returns false for shapes without an instantiation.
+bool wgrad1x16(Tensor D, Tensor X1, Tensor part, c10::optional<Tensor> partb, int64_t ks) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(D.device());
+  check(D, "D", at::kBFloat16); check(X1, "X1", at::kBFloat16); check(part, "part", at::kFloat);
+  check_ks(ks);
+  TORCH_CHECK(D.dim() == 6 && D.size(5) == 16, "D must be [V,I,J,K,L,16]");
+  const int64_t V = D.size(0), I = D.size(1), J = D.size(2), K = D.size(3), L = D.size(4);
+  const auto g = pad_geom(K, L, ks);
+  check_shape(X1, "X1", {V * I * J, g[1]});
+  TORCH_CHECK(part.dim() == 4 && part.size(0) >= 1, "part must be [G, ks^2, 32, 16]");
+  const int64_t G = part.size(0);
+  check_shape(part, "part", {G, ks * ks, 32, 16});
+  if (partb.has_value()) { check(*partb, "partb", at::kFloat); check_shape(*partb, "partb", {G, 16}); }
+  TORCH_CHECK(V * I * J < (1ll << 31), "too many planes");
+  const int r = ncnet_wgrad1x16(D.data_ptr(), X1.data_ptr(), (float*)part.data_ptr(),
+                                partb.has_value() ? (float*)partb->data_ptr() : nullptr, (int)G, (int)V, (int)I,
+                                (int)J, (int)K, (int)L, (int)ks, cur_stream(D));
+  if (r == -1) return false;
+  ok(r, "wgrad1x16");
   return true;
 }
 
@@ -693,6 +719,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pad_geom", &pad_geom);
   m.def("pad_planes", &pad_planes);
   m.def("conv1x16", &conv1x16);
+  m.def("wgrad1x16", &wgrad1x16);
   m.def("conv16_blk_fwd", &conv16_blk_fwd);
   m.def("conv16_fwd_x3", &conv16_fwd_x3);
   m.def("set_tuning", &set_tuning, py::arg("name"), py::arg("value") = py::none());

@@ -295,6 +295,209 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// wgrad1x16: weight gradient of a Conv4d whose one operand has ONE channel,
+// straight from the padded 1-channel planes (no ij packing):
+//
+//   R[tap = (dk, dl)][combo = (di, dj)][c] =
+//       sum_{o = (v, i, j)} sum_f D[o][f][c] * X1[(v, i+di-P, j+dj-P)][f + s(tap)]
+//
+// with D a 16-channel volume [V,I,J,K,L,16], X1 padded planes [V*I*J][PPL]
+// (pad_planes), f = k*LP + l the padded-stride voxel index and s(tap) =
+// dk*LP + dl.  Layer 1 (Cin = 1): D = gradient of its pre-activation, X1 = the
+// NC input -> dW1[c][di,dj,dk,dl] = R; the Cout = 1 last layer: D = its input,
+// X1 = the output gradient -> dW[0][c][t] = R[c][2P - t] (all four axes flipped).
+//
+// MFMA: rows = 16 combos (X1 planes of the 5 x 5 neighbourhood, two groups of
+// 16: 25 valid), cols = the 16 channels, K = padded positions q = f + s:
+//   A[combo][q] = X1[plane(combo)][q]     (ds_read_b64 x 2 at 16-B-aligned q:
+//                                          independent of the tap -> reused by 13 taps)
+//   B[q][c]     = D[q - s][c]             (ds_read_b64_tr_b16 from the staged D plane,
+//                                          any voxel offset is 8-B aligned)
+// so the in-plane tap shift moves into the D read and no shifted copies are
+// needed.  K index k of a lane group g (= lane >> 4) maps to q0 + 4g + 16h + e
+// (h = 0, 1; e = 0..3), which makes both the A reads and the transposed B reads
+// of one instruction cover 256 contiguous / bank-distinct bytes.
+//
+// Work: a step = one output plane o = (v, i, j) in (v, i, j) order; a
+// persistent workgroup (one per CU) owns a contiguous range of steps, D planes
+// stream through two LDS buffers (read from HBM exactly once), X1 planes
+// through a ring of KS rows x (KS + 1) column slots (each X1 plane is DMA'd by
+// the KS rows i that use it: L2 traffic on 50 MB).  Wave w accumulates taps
+// 13 (w & 1) .. +12 over the q chunks w >> 1, +4, ...; the 4 chunk-waves of a
+// tap half are reduced through LDS atomics at the end into one partial per
+// workgroup [G][NT][32 combos][16] (+ the bias sum of D on the ones-row MFMA).
+// Reference: the autograd of lib/conv4d.py:11-51 for the first / last
+// NeighConsensus layers (lib/model.py:130-139).
+// ---------------------------------------------------------------------------
+template <int KS, int K, int L>
+struct W1X {
+  static constexpr int P = KS / 2, NT = KS * KS, NW = 8;
+  static constexpr int LP = L + 2 * P, PPL = ((K + 2 * P) * LP + 7) / 8 * 8;
+  static constexpr int FV = (K - 1) * LP + L;                 // valid f in [0, FV)
+  static constexpr int SMAX = (KS - 1) * LP + KS - 1;         // largest tap shift
+  static constexpr int NQC = (FV + SMAX + 31) / 32;           // q chunks
+  static constexpr int QN = NQC * 32;
+  static constexpr int GM = (SMAX + 7) / 8 * 8;               // zero voxels before f = 0
+  static constexpr int GBYTES = (GM + QN) * 32;               // one staged D plane
+  static constexpr int XS = ((QN * 2 + 255) / 256) * 256 + 16;   // X1 slot stride: = 16 (mod 256) B
+  static constexpr int NCOL = KS + 1;
+  static constexpr int GOFF = 0, XOFF = 2 * GBYTES;
+  static constexpr int LDS = XOFF + KS * NCOL * XS;
+  static constexpr int NTW = (NT + 1) / 2;                    // taps per wave half
+  static constexpr int NU = (NQC + 3) / 4;                    // chunks per wave (upper bound)
+  static constexpr int XDMA2 = (QN * 2 - 1024) / 16;          // lanes of an X1 plane's second DMA
+  static_assert(QN * 2 > 1024 && QN * 2 <= 2048, "two DMA wave-instructions per X1 plane");
+  static_assert(L * 32 % 16 == 0 && L * 2 <= 64, "one DMA wave-instruction per D row");
+  static_assert(NT * 32 * 16 * 4 + 64 <= KS * NCOL * XS, "reduction scratch fits the X1 ring");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+template <int KS, int K, int L, bool BIAS>
+__global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restrict__ D, const bf16* __restrict__ X1,
+                                                           float* __restrict__ part, float* __restrict__ partb,
+                                                           int V, int I, int J) {
+#if defined(__HIP_DEVICE_COMPILE__)   // device-only body (asm DMA); the host pass keeps the stub
+  using C = W1X<KS, K, L>;
+  constexpr int P = C::P, NT = C::NT, NW = C::NW, LP = C::LP, PPL = C::PPL, NCOL = C::NCOL;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int th = wave & 1, cq = wave >> 1;
+  const int T = V * I * J;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int t0 = (int)((long long)bid * T / G), t1 = (int)((long long)(bid + 1) * T / G);
+
+  // ---- DMA helpers (asm LDS-DMA; waited for by the vmcnt(0) barriers) ----
+  auto dma_x = [&](int v, int i, int di, int jc, int half) {   // X1 plane (v, i+di-P, jc) -> its ring slot
+    const int ip = i + di - P;
+    const bool pv = ip >= 0 && ip < I && jc >= 0 && jc < J;
+    const uint64_t pb = (uint64_t)(pv ? X1 + ((size_t)(v * I + ip) * J + jc) * PPL : X1);
+    typedef int i32x4v __attribute__((ext_vector_type(4)));
+    i32x4v rs;
+    rs[0] = (int)(uint32_t)pb;
+    rs[1] = (int)((uint32_t)(pb >> 32) & 0xffffu);
+    rs[2] = pv ? PPL * 2 : 0;            // an absent plane reads as zeros
+    rs[3] = 0x00020000;
+    const uint32_t d = __builtin_amdgcn_readfirstlane(
+        lds0 + (uint32_t)(C::XOFF + (di * NCOL + (jc + P + NCOL) % NCOL) * C::XS + half * 1024));
+    const uint32_t vo = (uint32_t)(half * 1024 + lane * 16);
+    if (half == 0 || lane < C::XDMA2)
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(vo), "s"(rs), "s"(d)
+                   : "memory", "m0");
+  };
+  auto issue_g = [&](int t, int buf) {                          // D plane t (K rows of L voxels) -> buffer
+    const bf16* src = D + (size_t)t * K * L * 16;
+    for (int k = wave; k < K; k += NW) {
+      const uint32_t d = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(C::GOFF + buf * C::GBYTES + (C::GM + k * LP) * 32));
+      const bf16* a = src + (size_t)k * L * 16 + lane * 8;
+      if (lane < L * 2)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(a), "s"(d) : "memory", "m0");
+    }
+  };
+  auto issue_x_all = [&](int t) {                               // the KS x KS neighbourhood of step t
+    const int vi = t / J, j = t - vi * J, v = vi / I, i = vi - v * I;
+    for (int e = wave; e < 2 * NT; e += NW) {
+      const int pl = e >> 1;
+      dma_x(v, i, pl / KS, j - P + pl % KS, e & 1);
+    }
+  };
+  auto issue_x_col = [&](int t) {                               // the new column j + P of step t
+    const int vi = t / J, j = t - vi * J, v = vi / I, i = vi - v * I;
+    for (int e = wave; e < 2 * KS; e += NW) dma_x(v, i, e >> 1, j + P, e & 1);
+  };
+
+  // zero both D buffers once: margins, pad columns and the tail stay zero (the DMA writes rows only)
+  for (int o = threadIdx.x * 16; o < 2 * C::GBYTES; o += 512 * 16) *(u32x4*)(smem + C::GOFF + o) = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  if (t0 < t1) issue_g(t0, 0);
+
+  f32x4 acc[C::NTW][2];
+#pragma unroll
+  for (int a = 0; a < C::NTW; ++a) acc[a][0] = acc[a][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+  const u32x4 ones = {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
+
+  // lane constants: combo rows of the two groups, K group, transposed-read row/column
+  const int kg = lane >> 4, li = lane & 15;
+  const int c0 = li, c1 = (16 + li < NT) ? 16 + li : 16;      // rows >= NT repeat combo 16 (broadcast)
+  const int di0 = c0 / KS, dj0 = c0 - di0 * KS, di1 = c1 / KS, dj1 = c1 - di1 * KS;
+  const uint32_t gl = (uint32_t)((C::GM + 4 * kg + (li >> 2)) * 32 + 8 * (li & 3) + cq * 1024 - 32 * C::GM);
+
+  auto body = [&](auto thc, uint32_t xa0, uint32_t xa1, uint32_t ga) {
+    constexpr int TH = decltype(thc)::value;
+    xstatic_for<0, C::NU>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if (cq + 4 * u < C::NQC) {
+        const u32x4 A0 = cat4u(*(const u32x2*)(smem + xa0 + 256 * u), *(const u32x2*)(smem + xa0 + 256 * u + 32));
+        const u32x4 A1 = cat4u(*(const u32x2*)(smem + xa1 + 256 * u), *(const u32x2*)(smem + xa1 + 256 * u + 32));
+        xstatic_for<0, C::NTW>([&](auto tc) {
+          constexpr int tt = decltype(tc)::value;
+          constexpr int tap = C::NTW * TH + tt;
+          if constexpr (tap < NT) {
+            constexpr int s = (tap / KS) * LP + tap % KS;
+            constexpr uint32_t off = 4096u * u + 32u * (C::GM - s);
+            const u32x4 B = cat4u(lds_read_tr16u(smem, ga + off), lds_read_tr16u(smem, ga + off + 512));
+            acc[tt][0] = mfma16u(A0, B, acc[tt][0]);
+            acc[tt][1] = mfma16u(A1, B, acc[tt][1]);
+            if constexpr (BIAS && TH == 0 && tt == 0) accb = mfma16u(ones, B, accb);
+          }
+        });
+      }
+    });
+  };
+
+  for (int t = t0; t < t1; ++t) {
+    const int n = t - t0;
+    const int j = t % J;
+    if (t == t0 || j == 0) {
+      // a new (v, i) row: its whole X1 neighbourhood (the ring slots of the
+      // previous row are free once every wave finished the previous step)
+      asm_barrier_vm0();
+      issue_x_all(t);
+    }
+    asm_barrier_vm0();                 // this step's D plane and X1 planes landed; previous step's reads done
+    if (t + 1 < t1) {
+      issue_g(t + 1, (n + 1) & 1);
+      if ((t + 1) % J != 0) issue_x_col(t + 1);
+    }
+    const int s0 = di0 * NCOL + (j + dj0 + NCOL) % NCOL, s1 = di1 * NCOL + (j + dj1 + NCOL) % NCOL;
+    const uint32_t xa0 = (uint32_t)(C::XOFF + s0 * C::XS + 8 * kg + 64 * cq);
+    const uint32_t xa1 = (uint32_t)(C::XOFF + s1 * C::XS + 8 * kg + 64 * cq);
+    const uint32_t ga = (uint32_t)(C::GOFF + (n & 1) * C::GBYTES) + gl;
+    if (th == 0) body(std::integral_constant<int, 0>{}, xa0, xa1, ga);
+    else body(std::integral_constant<int, 1>{}, xa0, xa1, ga);
+  }
+  asm_barrier_vm0();
+
+  // ---- reduce the 4 chunk-waves of each tap half, one partial per workgroup ----
+  float* red = (float*)(smem + C::XOFF);                      // [NT][32][16] + bias [16]
+  for (int o = threadIdx.x; o < NT * 512 + 16; o += 512) red[o] = 0.f;
+  __syncthreads();
+  auto flush = [&](auto thc) {
+    constexpr int TH = decltype(thc)::value;
+    xstatic_for<0, C::NTW>([&](auto tc) {
+      constexpr int tt = decltype(tc)::value;
+      constexpr int tap = C::NTW * TH + tt;
+      if constexpr (tap < NT) {
+#pragma unroll
+        for (int grp = 0; grp < 2; ++grp)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            atomicAdd(&red[(tap * 32 + 16 * grp + 4 * kg + r) * 16 + li], acc[tt][grp][r]);
+      }
+    });
+  };
+  if (th == 0) flush(std::integral_constant<int, 0>{});
+  else flush(std::integral_constant<int, 1>{});
+  if (BIAS && th == 0 && lane < 16) atomicAdd(&red[NT * 512 + lane], accb[0]);
+  __syncthreads();
+  for (int o = threadIdx.x; o < NT * 512; o += 512) part[(size_t)bid * NT * 512 + o] = red[o];
+  if (BIAS && threadIdx.x < 16) partb[(size_t)bid * 16 + threadIdx.x] = red[NT * 512 + threadIdx.x];
+#endif
+}
+
 }  // namespace ncnet
 
 using namespace ncnet;
@@ -349,5 +552,23 @@ extern "C" int ncnet_conv1x16(const void* Xp, const void* Wa, const float* bias,
     hipLaunchKernelGGL((conv1x16_kernel<5, R, EPI1X_BIAS_RELU, 25, 25>), grid, block, (size_t)C::lds(R + 4, 1), s, x, w, bias, m, y, V, I, J, nt_store);
   else
     hipLaunchKernelGGL((conv1x16_kernel<5, R, EPI1X_MASK, 25, 25>), grid, block, (size_t)C::lds(R + 4, 1), s, x, w, bias, m, y, V, I, J, nt_store);
+  return (int)hipGetLastError();
+}
+
+// wgrad1x16 at the training plane (K = L = 25, KS = 5): D bf16 [V,I,J,K,L,16],
+// X1 padded planes [V*I*J][PPL]; part fp32 [G][KS*KS taps][32 combos][16] (one
+// partial per workgroup, G <= the CU count), partb fp32 [G][16] (sum of D; null: none).  Returns -1 for shapes without an instantiation.
+extern "C" int ncnet_wgrad1x16(const void* Dp, const void* X1p, float* part, float* partb, int G, int V, int I, int J,
+                               int K, int L, int KS, hipStream_t s) {
+  if (!(KS == 5 && K == 25 && L == 25)) return -1;
+  using C = W1X<5, 25, 25>;
+  if (G < 1) return -2;
+  const bf16* d = (const bf16*)Dp; const bf16* x = (const bf16*)X1p;
+  if (partb)
+    hipLaunchKernelGGL((wgrad1x16_kernel<5, 25, 25, true>), dim3((unsigned)G), dim3(512), (size_t)C::LDS, s, d, x, part,
+                       partb, V, I, J);
+  else
+    hipLaunchKernelGGL((wgrad1x16_kernel<5, 25, 25, false>), dim3((unsigned)G), dim3(512), (size_t)C::LDS, s, d, x,
+                       part, partb, V, I, J);
   return (int)hipGetLastError();
 }

@@ -42,7 +42,7 @@ from .. import config as _config
 from . import _ext
 from . import reference as ref
 from .packing import (blk_out_weights, ij_groups, ij_in_grad, ij_in_weights, ij_out_grad, ij_out_weights, pack_w16,
-                      pack_w16_planes, plane_dgrad_weights, transpose_for_dgrad)
+                      pack_w1x, pack_w16_planes, plane_dgrad_weights, transpose_for_dgrad)
 
 HIP_KS = (1, 3, 5, 7)
 # Cout=1 layers with <= 16 input channels run in output-plane-block mode
@@ -301,7 +301,57 @@ def _gather(outs, f32: bool, cout: int):
     return torch.stack(outs) if len(outs) > 1 else outs[0].unsqueeze(0)
 
 
-def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
+# ---------------------------------------------------------------------------
+# Padded-plane 1-channel layers (csrc/conv1x.hip) for the NC-Net training stack
+# [1 -> 16 (k=5), 16 -> 16 ..., 16 -> 1 (k=5)] at a 25 x 25 (k, l) plane: the
+# 1-channel operands (the NC input, the last layer's output gradient) are kept
+# as zero-padded planes (0.07 GB) instead of the 16x ij-packed copies (1.6 GB
+# each): the first layer's forward and the last layer's data gradient run on
+# conv1x16, both weight gradients on wgrad1x16.
+
+FAST1X = True    # module attribute (A/B tests, scripts/kbench.py); no environment knob
+
+
+def fast1x_ok(kinds, channels, kernel_sizes, x: torch.Tensor, symmetric: bool) -> bool:
+    if not (FAST1X and x.is_cuda and len(kinds) >= 2 and kinds[0] == "1in" and kinds[-1] == "1out"):
+        return False
+    if any(k != "16" for k in kinds[1:-1]) or any(c != 16 for c in channels[:-1]):
+        return False
+    if kernel_sizes[0] != 5 or kernel_sizes[-1] != 5:
+        return False
+    _, _, I, J, K, L = x.shape
+    if symmetric and (I, J) != (K, L):
+        return False
+    return (K, L) == (25, 25)
+
+
+@functools.lru_cache(maxsize=None)
+def _num_cus(index: int) -> int:
+    return torch.cuda.get_device_properties(index).multi_processor_count
+
+
+def _pad_1ch(x3: torch.Tensor, I2: int, J2: int, ks: int, trans: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """x3 [V, R, C] (fp32 / bf16) -> zero-padded bf16 planes [N, PPL] (csrc/conv1x.hip
+    pad_planes; trans 1: the planes of the A<->B-swapped volume)."""
+    C = _ext.ext()
+    _, ppl = C.pad_geom(I2, J2, ks)
+    n = x3.shape[0] * (x3.shape[2] if trans else x3.shape[1])
+    if out is None:
+        out = torch.zeros((n, ppl), dtype=torch.bfloat16, device=x3.device)
+    C.pad_planes(x3.contiguous(), out, I2, J2, ks, trans)
+    return out
+
+
+def _wgrad1x(C, d16: torch.Tensor, xp: torch.Tensor, ks: int, bias: bool):
+    """wgrad1x16 partials, reduced: R [ks^2 taps, ks^2 combos, 16] and the bias sum [16] (or None)."""
+    G = _num_cus(d16.device.index)
+    part = torch.empty((G, ks * ks, 32, 16), dtype=torch.float32, device=d16.device)
+    partb = torch.empty((G, 16), dtype=torch.float32, device=d16.device) if bias else None
+    C.wgrad1x16(d16, xp, part, partb, ks)
+    return part.sum(0)[:, : ks * ks], (partb.sum(0) if bias else None)
+
+
+def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list, xp=None, shp=None):
     """x0: [V,I,J,K,L] bf16 -> last layer's ReLU output, fp32: [V,I,J,K,L] if it
     has one channel, else planar [C, V,I,J,K,L].  Appends, per layer, what its
     backward reads: the ij-packed input (1-channel inputs) or the bf16 input blocks."""
@@ -314,6 +364,12 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list):
         ks, cout = w.shape[-1], w.shape[0]
         last = li == nl - 1
         xs = None
+        if li == 0 and xp is not None:      # padded-plane first layer (fast1x_ok)
+            y = torch.empty(tuple(shp) + (16,), dtype=torch.bfloat16, device=xp.device)
+            C.conv1x16(xp, pack_w1x(w), _pad_bias(b, 16), None, y, ks, 1)
+            save.append(xp)
+            h, cin = y.unsqueeze(0), cout
+            continue
         if cin == 1:
             xs = torch.empty((ij_groups(ks),) + tuple(h.shape) + (16,), dtype=torch.bfloat16, device=h.device)
             C.ijpack(h.contiguous(), xs, ks, 1)
@@ -419,7 +475,7 @@ def _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout):
     return ij_in_grad(torch.stack([p[0][0] for p in parts]), 1), parts[0][1][:1].clone()
 
 
-def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool):
+def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool, fast1x: bool = False):
     """g_last: grad w.r.t. the last conv's PRE-activation, bf16: [V,I,J,K,L] for
     a 1-channel output, else blocks [NB, V,I,J,K,L,16].
     Returns (dW list in checkpoint layout, db list, grad of x0 fp32 or None)."""
@@ -444,6 +500,27 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool)
         else:
             xin = hin = sv
         gs = None
+        if fast1x and kind in ("1in", "1out"):
+            if kind == "1out":                       # padded planes of the 1-channel output gradient
+                gp = _pad_1ch(g.reshape(g.shape[0], g.shape[1] * g.shape[2], g.shape[3] * g.shape[4]),
+                              g.shape[3], g.shape[4], ks, 0)
+                with _OnSide(main if li > 0 else None, side if li > 0 else None, (xin, g, gp)):
+                    R, _ = _wgrad1x(C, xin[0], gp, ks, False)
+                    dw = R.permute(2, 1, 0)[:cin].reshape((cin,) + (ks,) * 4).flip(1, 2, 3, 4).unsqueeze(0)
+                    db = g.float().sum().reshape(1)
+                if li > 0 or need_dx0:
+                    gn = torch.empty((1,) + tuple(hin.shape[1:]), dtype=torch.bfloat16, device=g.device)
+                    C.conv1x16(gp, pack_w1x(transpose_for_dgrad(w)), None, hin[0], gn[0], ks, 2)
+                    g = gn
+            else:                                    # first layer: xin = padded NC-input planes
+                R, sb = _wgrad1x(C, g[0], xin, ks, True)
+                dw = R.permute(2, 1, 0)[:cout].reshape((cout, 1) + (ks,) * 4).contiguous()
+                db = sb[:cout].contiguous()
+                if need_dx0:
+                    gx0 = conv_layer(g, transpose_for_dgrad(w), cout, 1, relu=False)
+            dws[li] = dw
+            dbs[li] = db
+            continue
         if cout == 1 and kind == "1out":
             gs = torch.empty((ij_groups(ks),) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=g.device)
             C.ijpack(g, gs, ks, -1)                  # adjoint of ijsum: shared by wgrad and dgrad
@@ -500,20 +577,39 @@ class NeighConsensusFn(torch.autograd.Function):
         V, _, I, J, K, L = x.shape
         R, Cc = I * J, K * L
         cl = channels[-1]
-        xb = x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous()
         saved_layers = []
         square = (I, J) == (K, L)
-        if symmetric:
+        fast = fast1x_ok(kinds, channels, [w.shape[0] for w in ws], x, symmetric)
+        if fast:
+            # the 1-channel input as padded planes, both branches in one batch
+            # (pad_planes trans=1 writes the swapped branch's planes directly)
+            x3 = x.reshape(V, R, Cc)
+            if symmetric:
+                _, ppl = _ext.ext().pad_geom(K, L, 5)
+                xp = torch.zeros((2 * V * R, ppl), dtype=torch.bfloat16, device=x.device)
+                _pad_1ch(x3, K, L, 5, 0, out=xp[:V * R])
+                _pad_1ch(x3, I, J, 5, 1, out=xp[V * R:])
+                z = _stack_fwd(None, ws, bs, kinds, saved_layers, xp=xp, shp=(2 * V, I, J, K, L))
+            else:
+                z = _stack_fwd(None, ws, bs, kinds, saved_layers, xp=_pad_1ch(x3, K, L, 5, 0), shp=(V, I, J, K, L))
+            branches = [saved_layers]
+        elif symmetric:
+            xb = x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous()
             xt = _swap_flat(xb.reshape(V, R, Cc), (I, J, K, L)).reshape(V, K, L, I, J)
             if square:
                 z = _stack_fwd(torch.cat((xb, xt), 0), ws, bs, kinds, saved_layers)
                 branches = [saved_layers]
-                z1, z2 = (z[:V], z[V:]) if cl == 1 else (z[:, :V], z[:, V:])
             else:
                 s1, s2 = [], []
                 z1 = _stack_fwd(xb, ws, bs, kinds, s1)
                 z2 = _stack_fwd(xt, ws, bs, kinds, s2)
                 branches = [s1, s2]
+        else:
+            z = _stack_fwd(x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous(), ws, bs, kinds, saved_layers)
+            branches = [saved_layers]
+        if symmetric:
+            if square:
+                z1, z2 = (z[:V], z[V:]) if cl == 1 else (z[:, :V], z[:, V:])
             if cl == 1:
                 if not square:
                     z = torch.cat((z1.reshape(-1), z2.reshape(-1)))
@@ -525,9 +621,8 @@ class NeighConsensusFn(torch.autograd.Function):
                     z = torch.cat((z1.reshape(cl, -1), z2.reshape(cl, -1)), 1)
                 y = _combine_multi(z1, z2, (V, I, J, K, L))
         else:
-            z = _stack_fwd(xb, ws, bs, kinds, saved_layers)
-            branches = [saved_layers]
             y = z.reshape(V, 1, I, J, K, L) if cl == 1 else z.transpose(0, 1).contiguous()
+        ctx.fast1x = fast
         ctx.symmetric = symmetric
         ctx.kinds = kinds
         ctx.channels = channels
@@ -594,7 +689,7 @@ class NeighConsensusFn(torch.autograd.Function):
                           planar_to_blocks(gz2.reshape(cl, V, K, L, I, J))]
             else:
                 gl = [planar_to_blocks(g1 * (z > 0))]
-        res = [_stack_bwd(g, br, ws, ctx.kinds, ctx.channels, need_dx0) for g, br in zip(gl, branches)]
+        res = [_stack_bwd(g, br, ws, ctx.kinds, ctx.channels, need_dx0, ctx.fast1x) for g, br in zip(gl, branches)]
         dws = [sum(r[0][i] for r in res) for i in range(len(ws))]
         dbs = [sum(r[1][i] for r in res) for i in range(len(ws))]
         gx = None

@@ -101,6 +101,10 @@ def main():
     C.pad_planes(x1.reshape(V, S * S, S * S), xpad, S, S, ks, 0)
     w1x = pack_w1x(torch.randn(16, 1, ks, ks, ks, ks, device=dev) * 0.05)
 
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    p1x = torch.empty((ncu, ks * ks, 32, 16), device=dev)
+    p1xb = torch.empty((ncu, 16), device=dev)
+
     def ij_out_fwd():
         for gi in range(G):
             C.conv16_fwd(x16.unsqueeze(0), wz[gi:gi + 1], None, None, zq[16 * gi:min(nq, 16 * gi + 16)], ks, 4)
@@ -125,6 +129,8 @@ def main():
         "pad_planes_t": (lambda: C.pad_planes(x1.reshape(V, S * S, S * S), xpad, S, S, ks, 1), None),
         "conv1x16_fwd": (lambda: C.conv1x16(xpad, w1x, b16, None, y16, ks, 1), fl1),
         "conv1x16_dgrad": (lambda: C.conv1x16(xpad, w1x, None, x16, y16, ks, 2), fl1),
+        "wgrad1x16": (lambda: C.wgrad1x16(g16, xpad, p1x, p1xb, ks), fl1),
+        "wgrad1x16_nobias": (lambda: C.wgrad1x16(x16, xpad, p1x, None, ks), fl1),
         "ij_1in_conv": (lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1), fl1),
         "ij_1in_conv_tpw1": (with_env("NCNET_GP_TPW", "1", lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1)), fl1),
         "ij_out_dgrad": (lambda: C.conv16_fwd(xs, wij, None, x16, y16, ks, 2), fl1),

@@ -851,3 +851,77 @@ def test_pad_planes_transposed():
     a = _pad_1ch(x, 5, trans=True)
     b = _pad_1ch(x.permute(0, 3, 4, 1, 2).contiguous(), 5)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("shape,G", [((2, 25, 25, 25, 25), 256), ((1, 6, 7, 25, 25), 7), ((1, 3, 11, 25, 25), 64),
+                                     ((1, 5, 5, 25, 25), 1)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_wgrad1x16_vs_oracle(shape, G, bias):
+    """Weight gradient with a 1-channel operand straight from padded planes
+    (csrc/conv1x.hip wgrad1x16: tap shift moved into the transposed D read, one
+    partial per persistent workgroup, item starts at arbitrary (v, i, j) steps)
+    vs autograd of the fp64 oracle, for both uses: the first layer (D = output
+    gradient, X1 = input: R = dW) and the Cout = 1 last layer (D = input,
+    X1 = output gradient: dW = R with all four kernel axes flipped)."""
+    torch.manual_seed(21)
+    V, I, J, K, L = shape
+    x1 = torch.rand(V, I, J, K, L, device=DEV).to(torch.bfloat16)
+    d = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
+    part = torch.full((G, 25, 32, 16), float("nan"), device=DEV)
+    partb = torch.full((G, 16), float("nan"), device=DEV) if bias else None
+    assert _ext.ext().wgrad1x16(d, _pad_1ch(x1, 5), part, partb, 5)
+    R = part.sum(0)[:, :25, :]                                   # [tap, combo, c]
+    # first layer: y[co] = conv(x1; W[co, 0]), dL/dy = d  ->  dW[co, 0, di, dj, dk, dl]
+    wr = torch.zeros(5, 16, 1, 5, 5, 5, device=DEV, dtype=torch.float64, requires_grad=True)
+    yr = ref.conv4d(x1.double().unsqueeze(1), wr, None)
+    (yr * d.double().permute(0, 5, 1, 2, 3, 4)).sum().backward()
+    want = ref.conv4d_weight_to_std(wr.grad)[:, 0].reshape(16, 25, 25)      # [co, combo, tap]
+    assert relerr(R.permute(2, 1, 0), want) < 1e-4
+    # last layer: y = conv(d; W[0, ci]), dL/dy = x1  ->  dW[0, ci, t] = R[2P - t][ci]
+    w3 = torch.zeros(5, 1, 16, 5, 5, 5, device=DEV, dtype=torch.float64, requires_grad=True)
+    y3 = ref.conv4d(d.double().permute(0, 5, 1, 2, 3, 4), w3, None)
+    (y3 * x1.double().unsqueeze(1)).sum().backward()
+    want3 = ref.conv4d_weight_to_std(w3.grad)[0]                               # [ci, di, dj, dk, dl]
+    got3 = R.permute(2, 1, 0).reshape(16, 5, 5, 5, 5).flip(1, 2, 3, 4)
+    assert relerr(got3, want3) < 1e-4
+    if bias:
+        assert relerr(partb.sum(0), d.double().sum(dim=(0, 1, 2, 3, 4))) < 1e-4
+
+
+@pytest.mark.parametrize("symmetric", [True, False])
+def test_neigh_consensus_fast1x_matches_ij_path(monkeypatch, symmetric):
+    """The training stack 5,5,5 / 16,16,1 at a 25^4 volume on the padded-plane
+    1-channel kernels (conv1x16 forward / data gradient, wgrad1x16 for both
+    1-channel layers) vs the ij-packed path and the fp64 oracle: output and every
+    gradient."""
+    import importlib
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    torch.manual_seed(31)
+    x = torch.rand(2, 1, 25, 25, 25, 25, device=DEV).to(torch.bfloat16).float()
+    ws, bs, cin = [], [], 1
+    for k, c in zip((5, 5, 5), (16, 16, 1)):
+        ws.append((torch.randn(k, c, cin, k, k, k, device=DEV) * 0.05).to(torch.bfloat16).float())
+        bs.append(0.2 + torch.rand(c, device=DEV) * 0.1)
+        cin = c
+    g = torch.randn(2, 1, 25, 25, 25, 25, device=DEV)
+    outs = {}
+    for fast in (True, False):
+        monkeypatch.setattr(nc, "FAST1X", fast)
+        xx = x.clone().requires_grad_(True)
+        pw = [w.clone().requires_grad_(True) for w in ws]
+        pb = [b.clone().requires_grad_(True) for b in bs]
+        assert nc.fast1x_ok(["1in", "16", "1out"], [16, 16, 1], [5, 5, 5], xx, symmetric) == fast
+        y = nc.neigh_consensus(xx, pw, pb, [16, 16, 1], symmetric=symmetric)
+        (y * g).sum().backward()
+        outs[fast] = [y.detach(), xx.grad] + [p.grad for p in pw + pb]
+    xr = x.double().requires_grad_(True)
+    wr = [w.double().requires_grad_(True) for w in ws]
+    br = [b.double().requires_grad_(True) for b in bs]
+    yr = ref.neigh_consensus(xr, wr, br, symmetric=symmetric)
+    (yr * g.double()).sum().backward()
+    want = [yr, xr.grad] + [p.grad for p in wr + br]
+    names = ["y", "gx", "gw0", "gw1", "gw2", "gb0", "gb1", "gb2"]
+    for n, a, b, r in zip(names, outs[True], outs[False], want):
+        ea, eb = rel_l2(a, r), rel_l2(b, r)
+        assert ea < max(2 * eb, 2e-2), (n, ea, eb)
+        assert rel_l2(a, b) < 5e-2, (n, rel_l2(a, b))

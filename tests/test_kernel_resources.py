@@ -24,6 +24,7 @@ HOT = [
     ("wgrad16v2_kernel", None),
     ("wgrad16p_kernel", None),
     ("conv1x16_kernel", None),                      # 1 -> 16 on padded 1-channel planes
+    ("wgrad1x16_kernel", None),                     # 1-channel-operand weight gradients
     ("corr_gemm", None),                            # correlation GEMMs (bf16 v1 / v2, MX-fp8)
     ("nc_fused_k3_kernel", None),                   # fused InLoc NC
     ("conv2d_nhwc", None),                          # native trunk convs
