@@ -211,6 +211,7 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
 
   const size_t KLs = (size_t)K * L;
   const int co0 = 4 * (lane >> 4);
+  u32x2 mreg[EPI == EPI1X_MASK ? R : 1][EPI == EPI1X_MASK ? MAXT : 1];
   for (int n = 0; n < nsteps; ++n) {
     const int it = bid + G * (n / KS), di = n % KS;
     int b = it;
@@ -220,6 +221,27 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
     // this step's planes landed (issued one step ago); the previous step's reads are done
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     issue(n + 1);
+    if constexpr (EPI == EPI1X_MASK) {
+      // the item's last step: fetch the ReLU mask of its outputs now, so the
+      // loads land under this step's MFMAs instead of stalling the epilogue
+      // (issued after the DMA: in-order completion keeps the DMA count exact)
+      if (di == KS - 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int j = j0 + r;
+          const size_t pbase = (((size_t)tv * I + ti) * J + j) * KLs;
+#pragma unroll
+          for (int tt = 0; tt < MAXT; ++tt) {
+            const int f = C::F0 + 16 * (wave + NW * tt) + (lane & 15);
+            const int kp = f / LP, lp = f - kp * LP;
+            const int k = kp - P, l = lp - P;
+            mreg[r][tt] = (j < J && f < C::FN && k >= 0 && k < K && l >= 0 && l < L)
+                              ? *(const u32x2*)(M + (pbase + (size_t)k * L + l) * 16 + co0)
+                              : u32x2{0u, 0u};
+          }
+        }
+      }
+    }
     const int ii = ti + di - P;
     if (ii >= 0 && ii < I) {
       bf16x8 A[KS];
@@ -276,7 +298,7 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
               o[q] = x;
             }
             if constexpr (EPI == EPI1X_MASK) {
-              const bf16x4 m = *(const bf16x4*)(M + vox * 16 + co0);
+              const bf16x4 m = __builtin_bit_cast(bf16x4, mreg[r][tt]);
 #pragma unroll
               for (int q = 0; q < 4; ++q) o[q] = ((float)m[q] > 0.f) ? o[q] : 0.f;
             }
@@ -425,18 +447,22 @@ __global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restric
   const int di0 = c0 / KS, dj0 = c0 - di0 * KS, di1 = c1 / KS, dj1 = c1 - di1 * KS;
   const uint32_t gl = (uint32_t)((C::GM + 4 * kg + (li >> 2)) * 32 + 8 * (li & 3) + cq * 1024 - 32 * C::GM);
 
-  auto body = [&](auto thc, uint32_t xa0, uint32_t xa1, uint32_t ga) {
-    constexpr int TH = decltype(thc)::value;
+  // one body per wave (tap half TH, chunk residue CQ, both compile-time): a
+  // (tap, chunk) pair whose positions q miss [s, s + FV) of that tap is never
+  // issued (12 % of the MFMAs and transposed reads of a full 27-chunk sweep)
+  auto body = [&](auto thc, auto cqc, uint32_t xa0, uint32_t xa1, uint32_t ga) {
+    constexpr int TH = decltype(thc)::value, CQ = decltype(cqc)::value;
     xstatic_for<0, C::NU>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
-      if (cq + 4 * u < C::NQC) {
+      constexpr int chunk = CQ + 4 * u;
+      if constexpr (chunk < C::NQC) {
         const u32x4 A0 = cat4u(*(const u32x2*)(smem + xa0 + 256 * u), *(const u32x2*)(smem + xa0 + 256 * u + 32));
         const u32x4 A1 = cat4u(*(const u32x2*)(smem + xa1 + 256 * u), *(const u32x2*)(smem + xa1 + 256 * u + 32));
         xstatic_for<0, C::NTW>([&](auto tc) {
           constexpr int tt = decltype(tc)::value;
           constexpr int tap = C::NTW * TH + tt;
-          if constexpr (tap < NT) {
-            constexpr int s = (tap / KS) * LP + tap % KS;
+          constexpr int s = (tap / KS) * LP + tap % KS;
+          if constexpr (tap < NT && chunk >= s / 32 && chunk <= (s + C::FV - 1) / 32) {
             constexpr uint32_t off = 4096u * u + 32u * (C::GM - s);
             const u32x4 B = cat4u(lds_read_tr16u(smem, ga + off), lds_read_tr16u(smem, ga + off + 512));
             acc[tt][0] = mfma16u(A0, B, acc[tt][0]);
@@ -448,35 +474,35 @@ __global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restric
     });
   };
 
-  for (int t = t0; t < t1; ++t) {
-    const int n = t - t0;
-    const int j = t % J;
-    if (t == t0 || j == 0) {
-      // a new (v, i) row: its whole X1 neighbourhood (the ring slots of the
-      // previous row are free once every wave finished the previous step)
-      asm_barrier_vm0();
-      issue_x_all(t);
-    }
-    asm_barrier_vm0();                 // this step's D plane and X1 planes landed; previous step's reads done
-    if (t + 1 < t1) {
-      issue_g(t + 1, (n + 1) & 1);
-      if ((t + 1) % J != 0) issue_x_col(t + 1);
-    }
-    const int s0 = di0 * NCOL + (j + dj0 + NCOL) % NCOL, s1 = di1 * NCOL + (j + dj1 + NCOL) % NCOL;
-    const uint32_t xa0 = (uint32_t)(C::XOFF + s0 * C::XS + 8 * kg + 64 * cq);
-    const uint32_t xa1 = (uint32_t)(C::XOFF + s1 * C::XS + 8 * kg + 64 * cq);
-    const uint32_t ga = (uint32_t)(C::GOFF + (n & 1) * C::GBYTES) + gl;
-    if (th == 0) body(std::integral_constant<int, 0>{}, xa0, xa1, ga);
-    else body(std::integral_constant<int, 1>{}, xa0, xa1, ga);
-  }
-  asm_barrier_vm0();
-
-  // ---- reduce the 4 chunk-waves of each tap half, one partial per workgroup ----
+  // the whole persistent loop per wave specialisation (one dispatch, so each
+  // body's register allocation is its own)
   float* red = (float*)(smem + C::XOFF);                      // [NT][32][16] + bias [16]
-  for (int o = threadIdx.x; o < NT * 512 + 16; o += 512) red[o] = 0.f;
-  __syncthreads();
-  auto flush = [&](auto thc) {
+  auto run = [&](auto thc, auto cqc) {
     constexpr int TH = decltype(thc)::value;
+    for (int t = t0; t < t1; ++t) {
+      const int n = t - t0;
+      const int j = t % J;
+      if (t == t0 || j == 0) {
+        // a new (v, i) row: its whole X1 neighbourhood (the ring slots of the
+        // previous row are free once every wave finished the previous step)
+        asm_barrier_vm0();
+        issue_x_all(t);
+      }
+      asm_barrier_vm0();               // this step's D plane and X1 planes landed; previous step's reads done
+      if (t + 1 < t1) {
+        issue_g(t + 1, (n + 1) & 1);
+        if ((t + 1) % J != 0) issue_x_col(t + 1);
+      }
+      const int s0 = di0 * NCOL + (j + dj0 + NCOL) % NCOL, s1 = di1 * NCOL + (j + dj1 + NCOL) % NCOL;
+      const uint32_t xa0 = (uint32_t)(C::XOFF + s0 * C::XS + 8 * kg + 64 * cq);
+      const uint32_t xa1 = (uint32_t)(C::XOFF + s1 * C::XS + 8 * kg + 64 * cq);
+      const uint32_t ga = (uint32_t)(C::GOFF + (n & 1) * C::GBYTES) + gl;
+      body(thc, cqc, xa0, xa1, ga);
+    }
+    asm_barrier_vm0();
+    // ---- reduce the 4 chunk-waves of each tap half, one partial per workgroup ----
+    for (int o = threadIdx.x; o < NT * 512 + 16; o += 512) red[o] = 0.f;
+    __syncthreads();
     xstatic_for<0, C::NTW>([&](auto tc) {
       constexpr int tt = decltype(tc)::value;
       constexpr int tap = C::NTW * TH + tt;
@@ -489,8 +515,20 @@ __global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restric
       }
     });
   };
-  if (th == 0) flush(std::integral_constant<int, 0>{});
-  else flush(std::integral_constant<int, 1>{});
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  switch (wave) {
+    case 0: run(I0{}, I0{}); break;
+    case 1: run(I1{}, I0{}); break;
+    case 2: run(I0{}, I1{}); break;
+    case 3: run(I1{}, I1{}); break;
+    case 4: run(I0{}, I2{}); break;
+    case 5: run(I1{}, I2{}); break;
+    case 6: run(I0{}, I3{}); break;
+    default: run(I1{}, I3{}); break;
+  }
   if (BIAS && th == 0 && lane < 16) atomicAdd(&red[NT * 512 + lane], accb[0]);
   __syncthreads();
   for (int o = threadIdx.x; o < NT * 512; o += 512) part[(size_t)bid * NT * 512 + o] = red[o];
