@@ -415,14 +415,20 @@ __global__ __launch_bounds__(512, 1) void conv16v3_fwd_kernel(const bf16* __rest
     int kk = vi / g.TL, ll = vi - kk * g.TL;
     vbase[tt] = (uint32_t)((kk * g.RS + ll) * 32 + ((lane >> 4) & 1) * 16);
   }
-  uint32_t toff[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    int tap = 2 * q + (lane >> 5);
-    if (tap >= NT) tap = NT - 1;
-    int dk = tap / KS, dl = tap - dk * KS;
-    toff[q] = (uint32_t)((dk * g.RS + dl) * 32);
-  }
+  // tap-pair offsets without a per-lane table (13 VGPRs at KS = 5, which
+  // pushed the <5, 5, *> bodies into scratch): tap 2q + h of lane half h sits
+  // at the wave-uniform offset of tap 2q plus h x (one column or one row wrap)
+  const uint32_t rs32 = (uint32_t)g.RS * 32u;
+  const uint32_t hcol = (lane >> 5) ? 32u : 0u, hwrap = (lane >> 5) ? rs32 - (uint32_t)(KS - 1) * 32u : 0u;
+  auto toff_q = [&](auto qc) -> uint32_t {
+    constexpr int q = decltype(qc)::value;
+    constexpr int ta = 2 * q, tb = (2 * q + 1 < NT) ? 2 * q + 1 : NT - 1;
+    constexpr int dka = ta / KS, dla = ta % KS, dkb = tb / KS, dlb = tb % KS;
+    const uint32_t base = (uint32_t)dka * rs32 + (uint32_t)dla * 32u;
+    if constexpr (tb == ta) return base;                                  // padding tap: both halves alike
+    else if constexpr (dkb == dka) { static_assert(dlb == dla + 1); return base + hcol; }
+    else { static_assert(dkb == dka + 1 && dlb == 0 && dla == KS - 1); return base + hwrap; }
+  };
   f32x4 acc[R][MAXT];
 #pragma unroll
   for (int r = 0; r < R; ++r)
@@ -480,8 +486,9 @@ __global__ __launch_bounds__(512, 1) void conv16v3_fwd_kernel(const bf16* __rest
       if (jp >= 0 && jp < g.J) {
         constexpr int dlo = (s - R + 1) > 0 ? (s - R + 1) : 0;
         constexpr int dhi = s < KS - 1 ? s : KS - 1;  // inclusive
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
+        static_for<0, NQ>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          const uint32_t tq = toff_q(qc);
           bf16x8 a[KS];
           static_for<dlo, dhi + 1>([&](auto dc) {
             constexpr int dj = decltype(dc)::value;
@@ -492,13 +499,13 @@ __global__ __launch_bounds__(512, 1) void conv16v3_fwd_kernel(const bf16* __rest
           // serialises every LDS read with its MFMAs)
 #pragma unroll
           for (int tt = 0; tt < MAXT; ++tt) {
-            const bf16x8 xf = lds_read16(cur, vbase[tt] + toff[q]);
+            const bf16x8 xf = lds_read16(cur, vbase[tt] + tq);
             static_for<dlo, dhi + 1>([&](auto dc) {
               constexpr int dj = decltype(dc)::value;
               acc[s - dj][tt] = mfma16(a[dj], xf, acc[s - dj][tt]);
             });
           }
-        }
+        });
       }
       ++n;
     });

@@ -18,8 +18,7 @@ HOT = [
     ("conv16v4_fwd_kernel", "5, 5, 1, 25, 25"),     # 16->16 forward (training)
     ("conv16v4_fwd_kernel", "5, 5, 2, 25, 25"),     # 16->16 data gradient (training)
     ("wgrad16v4_kernel", "5, 25, 25"),              # 16->16 weight gradient (training)
-    ("conv16v3_fwd_kernel", "3, 5, 1"),             # general-shape 16->16 (k = 3)
-    ("conv16v3_fwd_kernel", "3, 5, 2"),
+    ("conv16v3_fwd_kernel", None),                  # general-shape 16->16 (k = 3, 5; fwd / dgrad)
     ("conv16v2_fwd_kernel", None),                  # 1-channel layers (group-plane / block modes)
     ("wgrad16v2_kernel", None),
     ("wgrad16p_kernel", None),
