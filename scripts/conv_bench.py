@@ -59,13 +59,14 @@ def main():
         M, K = n * Ho * Wo, cin * k * k
         fl = 2.0 * M * cout * K
         run = lambda: C.conv2d_nhwc(x, w, b, None, y, s, k // 2, 1)   # noqa: E731
-        os.environ["NCNET_CONV2D_VARIANT"] = "1"
+        C.set_tuning("conv2d_variant", 1)
         t_1 = timeit(run)
-        os.environ["NCNET_CONV2D_VARIANT"] = "2"
+        C.set_tuning("conv2d_variant", 2)
         t_n = timeit(run)
-        os.environ["NCNET_CONV2D_BIG"] = "1"
+        C.set_tuning("conv2d_big", 1)
         t_b = timeit(run)
-        del os.environ["NCNET_CONV2D_BIG"]
+        C.set_tuning("conv2d_big", 0)
+        C.set_tuning("conv2d_variant", 0)
         if k == 1 and s == 1:
             x2 = x.permute(0, 2, 3, 1).reshape(M, cin)
             w2 = w.reshape(cout, cin)

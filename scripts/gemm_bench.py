@@ -46,6 +46,8 @@ def main():
     pv = torch.empty(1, h // 2, w // 2, h // 2, w // 2, device="cuda")
     pi = torch.empty(pv.shape, dtype=torch.uint8, device="cuda")
     res["hip bf16 pool2"] = timeit(lambda: C.corr_gemm_pool2(A, B, pv, pi, h, w, h, w, 0.0))
+    Ah, Bh = A.half(), B.half()
+    res["hip f16 pool2"] = timeit(lambda: C.corr_gemm_pool2(Ah, Bh, pv, pi, h, w, h, w, 0.0))
     A8, B8 = (A.float() * FP8_FEAT_SCALE).to(FP8), (B.float() * FP8_FEAT_SCALE).to(FP8)
     res["hip fp8 plain (fp32 out)"] = timeit(lambda: C.corr_gemm(A8, B8, out, None, None, 1.0 / FP8_FEAT_SCALE ** 2))
     res["hip fp8 pool2"] = timeit(lambda: C.corr_gemm_pool2(A8, B8, pv, pi, h, w, h, w, 1.0 / FP8_FEAT_SCALE ** 2))
