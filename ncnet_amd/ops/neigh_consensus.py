@@ -482,6 +482,7 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
     C = _ext.ext()
     nl = len(kinds)
     dws, dbs = [None] * nl, [None] * nl
+    ref_layout = [False] * nl          # True: dW already in the checkpoint layout
     g = g_last
     gx0 = None
     main = side = None
@@ -506,20 +507,24 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
                               g.shape[3], g.shape[4], ks, 0)
                 with _OnSide(main if li > 0 else None, side if li > 0 else None, (xin, g, gp)):
                     R, _ = _wgrad1x(C, xin[0], gp, ks, False)
-                    dw = R.permute(2, 1, 0)[:cin].reshape((cin,) + (ks,) * 4).flip(1, 2, 3, 4).unsqueeze(0)
-                    db = g.float().sum().reshape(1)
+                    # dW[0, ci, t] = R[2P - t][ci], straight into the checkpoint layout [k, 1, ci, k, k, k]
+                    Rf = R[:, :, :cin].reshape((ks,) * 4 + (cin,)).flip(0, 1, 2, 3)     # [dk, dl, di, dj, ci]
+                    dw = Rf.permute(2, 4, 3, 0, 1).unsqueeze(1).contiguous()
+                    db = g.sum(dtype=torch.float32).reshape(1)
                 if li > 0 or need_dx0:
                     gn = torch.empty((1,) + tuple(hin.shape[1:]), dtype=torch.bfloat16, device=g.device)
                     C.conv1x16(gp, pack_w1x(transpose_for_dgrad(w)), None, hin[0], gn[0], ks, 2)
                     g = gn
             else:                                    # first layer: xin = padded NC-input planes
                 R, sb = _wgrad1x(C, g[0], xin, ks, True)
-                dw = R.permute(2, 1, 0)[:cout].reshape((cout, 1) + (ks,) * 4).contiguous()
-                db = sb[:cout].contiguous()
+                # dW[co, 0, di, dj, dk, dl] = R[(dk, dl)][(di, dj)][co] -> checkpoint layout [k, co, 1, k, k, k]
+                dw = R[:, :, :cout].reshape((ks,) * 4 + (cout,)).permute(2, 4, 3, 0, 1).unsqueeze(2).contiguous()
+                db = sb[:cout]
                 if need_dx0:
                     gx0 = conv_layer(g, transpose_for_dgrad(w), cout, 1, relu=False)
             dws[li] = dw
             dbs[li] = db
+            ref_layout[li] = True
             continue
         if cout == 1 and kind == "1out":
             gs = torch.empty((ij_groups(ks),) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=g.device)
@@ -551,7 +556,7 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
         main.wait_stream(side)
         for t in dws + dbs:          # produced on the side stream, consumed (and freed) on main
             t.record_stream(main)
-    return [ref.conv4d_weight_from_std(d) for d in dws], dbs, gx0
+    return [d if ref_layout[i] else ref.conv4d_weight_from_std(d) for i, d in enumerate(dws)], dbs, gx0
 
 
 def _swap_flat(x: torch.Tensor, shape_ab):
@@ -690,8 +695,11 @@ class NeighConsensusFn(torch.autograd.Function):
             else:
                 gl = [planar_to_blocks(g1 * (z > 0))]
         res = [_stack_bwd(g, br, ws, ctx.kinds, ctx.channels, need_dx0, ctx.fast1x) for g, br in zip(gl, branches)]
-        dws = [sum(r[0][i] for r in res) for i in range(len(ws))]
-        dbs = [sum(r[1][i] for r in res) for i in range(len(ws))]
+        if len(res) == 1:            # one batched branch: no accumulation copies
+            dws, dbs = res[0][0], res[0][1]
+        else:
+            dws = [sum(r[0][i] for r in res) for i in range(len(ws))]
+            dbs = [sum(r[1][i] for r in res) for i in range(len(ws))]
         gx = None
         if need_dx0:
             if ctx.symmetric:
