@@ -50,7 +50,12 @@ constexpr int NCF_MAXT2 = 3;       // layer-2 tiles per wave: TK*TL <= 384 voxel
 
 // F16: IEEE-half x0, weights and hidden activation (half_precision=True, as
 // eval_inloc.py runs the reference: lib/model.py:265-267), f16 MFMA.
-template <bool F16>
+// CTK, CTL, CR: compile-time tile (k, l) and planes per workgroup for the
+// InLoc shapes (0 = the runtime value of g): the tile counts, LDS row strides,
+// tap offsets and ring indexing then fold into immediates -- the runtime
+// geometry kept ~50 SGPRs live (spilled to VGPR lanes) and cost ~10 SALU per
+// MFMA (profiles/r2_inloc/pmc_corr_ncfused_before.md).
+template <bool F16, int CTK = 0, int CTL = 0, int CR = 0>
 __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ W1p,
                                                              const float* __restrict__ b1,
                                                              const u32x4* __restrict__ W2p,
@@ -58,13 +63,15 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
                                                              NCFGeom g) {
   constexpr int NQ = 5;            // tap pairs of the 3x3 (dk, dl) taps
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int TK = g.TK, TL = g.TL;
+  const int TK = CTK ? CTK : g.TK, TL = CTL ? CTL : g.TL;
+  const int GR = CR ? CR : g.R;                       // planes per workgroup (ring depth)
+  const int SRS = CTL ? CTL + 10 : g.SRS, HRS = CTL ? CTL + 8 : g.HRS;
   const int SR = TK + 4, SW = TL + 4;        // S tile (layer-1 input): tile + 2 halo
   const int HR = TK + 2, HW = TL + 2;        // h tile (layer-2 input): tile + 1 halo
   char* S = smem;
-  char* H = S + SR * g.SRS * 32;
-  float* ring = (float*)(H + HR * g.HRS * 32);
-  u32x4* wl = (u32x4*)(ring + 3 * g.R * TK * TL);   // [2 layers][5 tap pairs][64 lanes] fragments
+  char* H = S + SR * SRS * 32;
+  float* ring = (float*)(H + HR * HRS * 32);
+  u32x4* wl = (u32x4*)(ring + 3 * GR * TK * TL);   // [2 layers][5 tap pairs][64 lanes] fragments
   const int nvox = TK * TL;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -74,9 +81,9 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   const int jb = bid % g.njb; bid /= g.njb;
   const int ib = bid % g.nib;
   const int v = bid / g.nib;
-  const int k0 = kt * TK, l0 = lt * TL, j0 = jb * g.R, i0 = ib * g.IR;
+  const int k0 = kt * TK, l0 = lt * TL, j0 = jb * GR, i0 = ib * g.IR;
   const int i1 = min(g.I, i0 + g.IR);
-  const int R = min(g.R, g.J - j0);
+  const int R = min(GR, g.J - j0);
   const size_t KL = (size_t)g.K * g.L;
   const int KLi = g.K * g.L;
   // this volume's x0 through a buffer resource: a lane whose S voxel lies
@@ -94,7 +101,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     const int e = threadIdx.x;
     const int r = e / SW, c = e - r * SW;
     const int kg = k0 - 2 + r, lg = l0 - 2 + c;
-    s_lds = (e < SR * SW) ? (r * g.SRS + c) * 32 : -1;
+    s_lds = (e < SR * SW) ? (r * SRS + c) * 32 : -1;
     s_in = e < SR * SW && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
     s_goff = s_in ? (kg * g.L + lg) * 2 : 0x7ffffff0;   // byte offset in the plane / out of range
   }
@@ -108,8 +115,8 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     const bool ok = e < HR * HW;
     if (!ok) e = 0;
     const int r = e / HW, c = e - r * HW;
-    b1off[t] = (uint32_t)((r * g.SRS + c) * 32 + ((lane >> 4) & 1) * 16);
-    h_wr[t] = (uint32_t)((r * g.HRS + c) * 32 + 8 * (lane >> 4));
+    b1off[t] = (uint32_t)((r * SRS + c) * 32 + ((lane >> 4) & 1) * 16);
+    h_wr[t] = (uint32_t)((r * HRS + c) * 32 + 8 * (lane >> 4));
     const int kg = k0 - 1 + r, lg = l0 - 1 + c;
     h_ok[t] = ok;    // lanes past the h region of the last tile must not write (their e was clamped to 0)
     h_in[t] = ok && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
@@ -124,7 +131,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     vo[t] = vi < nvox ? vi : -1;
     if (vi >= nvox) vi = 0;
     const int kk = vi / TL, ll = vi - kk * TL;
-    b2off[t] = (uint32_t)((kk * g.HRS + ll) * 32 + ((lane >> 4) & 1) * 16);
+    b2off[t] = (uint32_t)((kk * HRS + ll) * 32 + ((lane >> 4) & 1) * 16);
   }
   // tap offsets of the pair q: tap 2q + (lane >> 5) (the 10th tap is padding with zero weights)
   uint32_t toff1[NQ], toff2[NQ];
@@ -133,8 +140,8 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     int tap = 2 * q + (lane >> 5);
     if (tap > 8) tap = 8;
     const int dk = tap / 3, dl = tap - dk * 3;
-    toff1[q] = (uint32_t)((dk * g.SRS + dl) * 32);
-    toff2[q] = (uint32_t)((dk * g.HRS + dl) * 32);
+    toff1[q] = (uint32_t)((dk * SRS + dl) * 32);
+    toff2[q] = (uint32_t)((dk * HRS + dl) * 32);
   }
   for (int o = threadIdx.x; o < NQ * 64; o += 512) { wl[o] = W1p[o]; wl[NQ * 64 + o] = W2p[o]; }
   const int co0 = 4 * (lane >> 4);
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   const float bias2 = b2[0];
 
   // zero the output ring (3 row slots x R planes x TK*TL)
-  for (int o = threadIdx.x; o < 3 * g.R * nvox; o += 512) ring[o] = 0.f;
+  for (int o = threadIdx.x; o < 3 * GR * nvox; o += 512) ring[o] = 0.f;
 
   const int ih_lo = max(0, i0 - 1), ih_hi = min(g.I, i1 + 1);   // hidden rows [lo, hi)
   const int jh_lo = max(0, j0 - 1), jh_hi = min(g.J, j0 + R + 1); // hidden planes [lo, hi)
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
       const int kg = k0 + kk, lg = l0 + ll;
       const bool ok = kg < g.K && lg < g.L;
       for (int p = 0; p < R; ++p) {
-        float* rp = ring + (slot * g.R + p) * nvox + vo[t];
+        float* rp = ring + (slot * GR + p) * nvox + vo[t];
         if (ok) Y[(((size_t)v * g.I + io) * g.J + j0 + p) * KL + (size_t)kg * g.L + lg] = fmaxf(*rp + bias2, 0.f);
         *rp = 0.f;
       }
@@ -241,7 +248,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
       for (int r = 0; r < 3; ++r) {
         const int io = ih - r + 1;
         if (io < i0 || io >= i1) continue;
-        ring[((io % 3) * g.R + p2) * nvox + vo[u]] += acc[r];
+        ring[((io % 3) * GR + p2) * nvox + vo[u]] += acc[r];
       }
     }
     // hidden row ih done: output row ih - 1 has all three contributions
@@ -287,11 +294,16 @@ extern "C" int ncnet_nc_fused_k3(const void* X, const void* W1p, const float* b1
                2 * 5 * 64 * 16;
   if (lds > 160 * 1024) return -3;
   dim3 grid((unsigned)((size_t)V * g.nib * g.njb * g.nkt * g.nlt)), block(512);
-  if (f16)
-    hipLaunchKernelGGL(nc_fused_k3_kernel<true>, grid, block, lds, stream, (const bf16*)X, (const u32x4*)W1p, b1,
-                       (const u32x4*)W2p, b2, Y, g);
-  else
-    hipLaunchKernelGGL(nc_fused_k3_kernel<false>, grid, block, lds, stream, (const bf16*)X, (const u32x4*)W1p, b1,
-                       (const u32x4*)W2p, b2, Y, g);
+#define NCF(H, A, B, C) hipLaunchKernelGGL((nc_fused_k3_kernel<H, A, B, C>), grid, block, lds, stream, (const bf16*)X, \
+                                           (const u32x4*)W1p, b1, (const u32x4*)W2p, b2, Y, g)
+  // the tiles ops/neigh_consensus.py fused_tiles picks at 3200 px (75x100 planes)
+  // and 1600 px (37x50) get compile-time geometry; anything else the runtime one
+  const bool t3200 = TK == 15 && TL == 20 && R == 10, t1600 = TK == 19 && TL == 17 && R == 8;
+  if (f16) {
+    if (t3200) NCF(true, 15, 20, 10); else if (t1600) NCF(true, 19, 17, 8); else NCF(true, 0, 0, 0);
+  } else {
+    if (t3200) NCF(false, 15, 20, 10); else if (t1600) NCF(false, 19, 17, 8); else NCF(false, 0, 0, 0);
+  }
+#undef NCF
   return (int)hipGetLastError();
 }
