@@ -22,6 +22,8 @@ int ncnet_ijpack(const void*, int, void*, int, int, int, int, int, int, int, int
 int ncnet_conv16f8_fwd(const void*, const void*, const float*, void*, int, int, int, int, int, int, int, int, int, float, hipStream_t);
 int ncnet_ijsum(const float*, const float*, float*, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_bias_act(void*, const float*, long long, int, int, int, hipStream_t);
+int ncnet_maxpool_bias_act(const void*, void*, const float*, int, int, int, int, int, int, int, int, int, int, int,
+                           hipStream_t);
 int ncnet_conv2d_nhwc(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, void*, int, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
@@ -559,6 +561,28 @@ void transpose(Tensor x, Tensor y) {
 
 // In place Y = act(Y + b) over the channel axis: Y bf16, either a contiguous
 // [rows, C] matrix or a channels-last [N, C, H, W] tensor; b fp32 [C].
+// Y = act(maxpool_{k,stride,pad}(X) + b): X, Y channels-last [N, C, H, W] /
+// [N, C, Ho, Wo] bf16 or fp16 (same dtype), b fp32 [C], C % 8 == 0.
+void maxpool_bias_act(Tensor X, Tensor b, Tensor Y, int64_t k, int64_t stride, int64_t pad, int64_t relu) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  TORCH_CHECK(X.is_cuda() && X.dim() == 4 && X.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  (X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kHalf),
+              "maxpool_bias_act: X must be a channels-last bf16 / fp16 [N, C, H, W] GPU tensor");
+  TORCH_CHECK(Y.is_cuda() && Y.dim() == 4 && Y.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  Y.scalar_type() == X.scalar_type(), "maxpool_bias_act: Y must be channels-last like X");
+  check(b, "b", at::kFloat);
+  const int64_t N = X.size(0), C = X.size(1), H = X.size(2), W = X.size(3);
+  TORCH_CHECK(k >= 1 && stride >= 1 && pad >= 0 && 2 * pad <= k, "maxpool_bias_act: bad window");
+  const int64_t Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  check_shape(Y, "Y", {N, C, Ho, Wo});
+  check_shape(b, "b", {C});
+  TORCH_CHECK(C % 8 == 0, "maxpool_bias_act: C must be a multiple of 8");
+  ok(ncnet_maxpool_bias_act(X.data_ptr(), Y.data_ptr(), (const float*)b.data_ptr(), (int)N, (int)H, (int)W, (int)C,
+                            (int)Ho, (int)Wo, (int)k, (int)stride, (int)pad, relu ? 1 : 0,
+                            X.scalar_type() == at::kHalf ? 1 : 0, cur_stream(X)),
+     "maxpool_bias_act");
+}
+
 void bias_act_(Tensor Y, Tensor b, int64_t relu) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(Y.device());
   TORCH_CHECK(Y.is_cuda() && (Y.scalar_type() == at::kBFloat16 || Y.scalar_type() == at::kHalf),
@@ -730,6 +754,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv16f8_fwd", &conv16f8_fwd);
   m.def("ijsum", &ijsum);
   m.def("bias_act_", &bias_act_);
+  m.def("maxpool_bias_act", &maxpool_bias_act);
   m.def("conv2d_nhwc", &conv2d_nhwc);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("l2norm_rows_bwd", &l2norm_rows_bwd);

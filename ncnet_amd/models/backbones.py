@@ -335,6 +335,28 @@ class FrozenResNetPlan(nn.Module):
         return y.relu_() if relu else y
 
     @staticmethod
+    def _pool_args(p):
+        k, st, pad = p
+        one = lambda v: v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else None)   # noqa: E731
+        return one(k), one(st if st is not None else k), one(pad)
+
+    def _pool_fusable(self, y: torch.Tensor, p) -> bool:
+        if not (y.is_cuda and y.dtype in (torch.bfloat16, torch.float16) and y.shape[1] % 8 == 0):
+            return False
+        from ..ops import _ext
+        k, st, pad = self._pool_args(p)
+        return _ext.use_hip(y) and None not in (k, st, pad) and 2 * pad <= k
+
+    def _maxpool_bias_act(self, y: torch.Tensor, b: torch.Tensor, p, relu: bool) -> torch.Tensor:
+        from ..ops import _ext
+        k, st, pad = self._pool_args(p)
+        n, c, h, w = y.shape
+        ho, wo = (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1
+        out = torch.empty((n, c, ho, wo), dtype=y.dtype, device=y.device, memory_format=torch.channels_last)
+        _ext.ext().maxpool_bias_act(y, b.float().contiguous(), out, k, st, pad, 1 if relu else 0)
+        return out
+
+    @staticmethod
     def _nconv(x: torch.Tensor, p, relu: bool, res: torch.Tensor | None = None) -> torch.Tensor:
         from ..ops import _ext
         w, b, stride, pad = p
@@ -425,15 +447,25 @@ class FrozenResNetPlan(nn.Module):
     def _run(self, x: torch.Tensor) -> torch.Tensor:
         x = x.to(self.dtype).contiguous(memory_format=torch.channels_last)
         bi = -1
-        for kind, p in self.steps:
+        fused_pool = False
+        for si, (kind, p) in enumerate(self.steps):
             if kind == "bottleneck":
                 bi += 1
             if kind == "conv":
                 w, b, stride, pad, relu = p
-                x = self._bias_act(F.conv2d(x, w, None, stride, pad).contiguous(memory_format=torch.channels_last),
-                                   b, relu)
+                y = F.conv2d(x, w, None, stride, pad).contiguous(memory_format=torch.channels_last)
+                nxt = self.steps[si + 1] if si + 1 < len(self.steps) else None
+                if nxt is not None and nxt[0] == "maxpool" and self._pool_fusable(y, nxt[1]):
+                    # stem: bias + ReLU + max-pool in one pass (csrc/epilogue.hip maxpool_bias_act)
+                    x = self._maxpool_bias_act(y, b, nxt[1], relu)
+                    fused_pool = True
+                else:
+                    x = self._bias_act(y, b, relu)
             elif kind == "maxpool":
-                x = F.max_pool2d(x, *p).contiguous(memory_format=torch.channels_last)
+                if fused_pool:
+                    fused_pool = False
+                else:
+                    x = F.max_pool2d(x, *p).contiguous(memory_format=torch.channels_last)
             elif self.conv_mode in ("native", "auto") and x.is_cuda and self.dtype in (torch.bfloat16, torch.float16):
                 y1 = self._n1(x, p, bi) if self.conv_mode == "auto" else self._nconv(x, p["n1"], True)
                 y2 = self._nconv(y1, p["n2"], True)

@@ -925,3 +925,19 @@ def test_neigh_consensus_fast1x_matches_ij_path(monkeypatch, symmetric):
         ea, eb = rel_l2(a, r), rel_l2(b, r)
         assert ea < max(2 * eb, 2e-2), (n, ea, eb)
         assert rel_l2(a, b) < 5e-2, (n, rel_l2(a, b))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("hw", [(50, 50), (37, 61)])
+def test_maxpool_bias_act_matches_separate_passes(dtype, hw):
+    """The trunk stem's fused bias + ReLU + 3x3/2 max-pool (csrc/epilogue.hip)
+    equals bias_act followed by PyTorch's max_pool2d bit for bit (the rounded
+    activation is monotonic, so it commutes with max)."""
+    torch.manual_seed(41)
+    x = torch.randn(3, 64, *hw, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(64, device=DEV)
+    want = torch.nn.functional.max_pool2d(torch.relu(x.float() + b.view(1, -1, 1, 1)).to(dtype), 3, 2, 1)
+    ho, wo = want.shape[2:]
+    y = torch.empty((3, 64, ho, wo), dtype=dtype, device=DEV, memory_format=torch.channels_last)
+    _ext.ext().maxpool_bias_act(x, b, y, 3, 2, 1, 1)
+    assert torch.equal(y, want)
