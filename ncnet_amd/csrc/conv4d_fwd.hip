@@ -80,7 +80,8 @@ __device__ __forceinline__ size_t plane_offset(const ConvGeom& g, int v, int i, 
 template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
                                         const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0,
-                                        int nco = 16, bool nt = false, long long ylo = 0) {
+                                        int nco = 16, bool nt = false, long long ylo = 0,
+                                        const u32x2* mpre = nullptr) {
   if (!NCNET_OK(vox_index < nvox_all && co0 >= 0 && co0 + 4 <= 16)) return;
   constexpr bool X3 = (EPI & EPI_X3) != 0;
   constexpr int E = EPI & ~EPI_X3;
@@ -105,7 +106,8 @@ __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, 
   }
   if (E == EPI_MASK) {
     // (X3: the mask is the hi part of the ReLU output -- bf16(y) > 0 iff y > 0)
-    bf16x4 m = *(const bf16x4*)(M + vox_index * 16 + co0);
+    // mpre: the mask the caller fetched ahead (conv16v4), else loaded here
+    const bf16x4 m = mpre ? __builtin_bit_cast(bf16x4, *mpre) : *(const bf16x4*)(M + vox_index * 16 + co0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) o[r] = ((float)m[r] > 0.f) ? o[r] : 0.f;
   }
@@ -766,21 +768,40 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 
   const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
+  auto out_vox = [&](int r, int tt, size_t& vox) -> bool {
+    const int j = j0 + r;
+    const int tile = wave + NW * tt;
+    const int vi = tile * 16 + (lane & 15);
+    const int kk = vi / TL, ll = vi - kk * TL;
+    const int kg = k0 + kk, lg = l0 + ll;
+    const bool ok = j < g.J && tile < NTILE && vi < NVOX && kg < g.K && lg < g.L;
+    vox = ok ? plane_offset(g, tv, ti, j, 1) + (size_t)kg * g.L + lg : 0;
+    return ok;
+  };
+  // EPI_MASK: every ReLU-mask load of the item first (fixed count, out-of-range
+  // voxels read voxel 0), then the stores: a load -> wait -> store sequence per
+  // (r, tt) serialised 25 memory round trips (stores count in vmcnt here)
+  constexpr bool MPF = (EPI & ~EPI_X3) == EPI_MASK;
+  u32x2 mreg[MPF ? R : 1][MPF ? MAXT : 1];
+  if constexpr (MPF) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int tt = 0; tt < MAXT; ++tt) {
+        size_t vox;
+        out_vox(r, tt, vox);
+        mreg[r][tt] = *(const u32x2*)(M + vox * 16 + 4 * (lane >> 4));
+      }
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int j = j0 + r;
-    if (j >= g.J) break;
-    const size_t vbase_out = plane_offset(g, tv, ti, j, 1);
 #pragma unroll
     for (int tt = 0; tt < MAXT; ++tt) {
-      const int tile = wave + NW * tt;
-      if (tile < NTILE) {
-        const int vi = tile * 16 + (lane & 15);
-        const int kk = vi / TL, ll = vi - kk * TL;
-        const int kg = k0 + kk, lg = l0 + ll;
-        if (vi < NVOX && kg < g.K && lg < g.L)
-          store16<EPI>(acc[r][tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco,
-                       g.nt, g.ylo);
+      size_t vox;
+      if (out_vox(r, tt, vox)) {
+        const u32x2* mp = nullptr;
+        if constexpr (MPF) mp = &mreg[r][tt];
+        store16<EPI>(acc[r][tt], Y, M, bias, vox, 4 * (lane >> 4), nvox_all, g.nco, g.nt, g.ylo, mp);
       }
     }
   }
