@@ -212,6 +212,8 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
   const size_t KLs = (size_t)K * L;
   const int co0 = 4 * (lane >> 4);
   u32x2 mreg[EPI == EPI1X_MASK ? R : 1][EPI == EPI1X_MASK ? MAXT : 1];
+  f32x4 bv = {0.f, 0.f, 0.f, 0.f};   // this lane's 4 channels' bias, loaded once (not per store)
+  if constexpr (EPI == EPI1X_BIAS_RELU) bv = *(const f32x4*)(bias + co0);
   for (int n = 0; n < nsteps; ++n) {
     const int it = bid + G * (n / KS), di = n % KS;
     int b = it;
@@ -294,7 +296,7 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               float x = acc[r][tt][q];
-              if constexpr (EPI == EPI1X_BIAS_RELU) x = fmaxf(x + bias[co0 + q], 0.f);
+              if constexpr (EPI == EPI1X_BIAS_RELU) x = fmaxf(x + bv[q], 0.f);
               o[q] = x;
             }
             if constexpr (EPI == EPI1X_MASK) {

@@ -81,7 +81,7 @@ template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
                                         const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0,
                                         int nco = 16, bool nt = false, long long ylo = 0,
-                                        const u32x2* mpre = nullptr) {
+                                        const u32x2* mpre = nullptr, const f32x4* bpre = nullptr) {
   if (!NCNET_OK(vox_index < nvox_all && co0 >= 0 && co0 + 4 <= 16)) return;
   constexpr bool X3 = (EPI & EPI_X3) != 0;
   constexpr int E = EPI & ~EPI_X3;
@@ -101,7 +101,7 @@ __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, 
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float x = acc[r];
-    if (E == EPI_BIAS_RELU) x = fmaxf(x + bias[co0 + r], 0.f);
+    if (E == EPI_BIAS_RELU) x = fmaxf(x + (bpre ? (*bpre)[r] : bias[co0 + r]), 0.f);
     o[r] = x;
   }
   if (E == EPI_MASK) {
@@ -783,6 +783,20 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
   // (r, tt) serialised 25 memory round trips (stores count in vmcnt here)
   constexpr bool MPF = (EPI & ~EPI_X3) == EPI_MASK;
   u32x2 mreg[MPF ? R : 1][MPF ? MAXT : 1];
+  // bias + ReLU: this lane's 4 output channels' bias, loaded once (per store it
+  // was a load -> vmcnt(0) -> store chain like the mask's)
+  // (scalar loads of all 16 + a per-lane select: no vector load whose use the
+  // waitcnt pass would re-wait for -- with the stores in vmcnt -- in every
+  // conditional store block)
+  f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+  if constexpr ((EPI & ~EPI_X3) == EPI_BIAS_RELU) {
+    float bs[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) bs[c] = bias[c];   // uniform addresses: s_load
+    const int gq = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = gq == 0 ? bs[r] : gq == 1 ? bs[4 + r] : gq == 2 ? bs[8 + r] : bs[12 + r];
+  }
   if constexpr (MPF) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -801,7 +815,7 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
       if (out_vox(r, tt, vox)) {
         const u32x2* mp = nullptr;
         if constexpr (MPF) mp = &mreg[r][tt];
-        store16<EPI>(acc[r][tt], Y, M, bias, vox, 4 * (lane >> 4), nvox_all, g.nco, g.nt, g.ylo, mp);
+        store16<EPI>(acc[r][tt], Y, M, bias, vox, 4 * (lane >> 4), nvox_all, g.nco, g.nt, g.ylo, mp, &bv);
       }
     }
   }
