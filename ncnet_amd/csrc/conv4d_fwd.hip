@@ -77,6 +77,25 @@ __device__ __forceinline__ size_t plane_offset(const ConvGeom& g, int v, int i, 
 // nt: streaming (non-temporal) stores -- the volumes written here (0.1-1.6 GB)
 // never stay in the 4 MB L2s, so a write-allocating store only evicts the
 // operands the running kernel is still reading.
+// This lane's 4 output-channel biases (rows 4 (lane >> 4) + r) for the bias +
+// ReLU epilogues, read once before the store loop as 16 uniform scalar loads and
+// a per-lane select.  A vector load used inside each conditional store block
+// makes the waitcnt pass re-wait vmcnt(0) there -- stores count in vmcnt -- and
+// serialises the epilogue (26-34 waits per kernel before, 1 after).
+template <int EPI>
+__device__ __forceinline__ f32x4 lane_bias4(const float* __restrict__ bias, int lane) {
+  f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+  if constexpr ((EPI & ~EPI_X3) == EPI_BIAS_RELU) {
+    float bs[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) bs[c] = bias[c];
+    const int gq = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = gq == 0 ? bs[r] : gq == 1 ? bs[4 + r] : gq == 2 ? bs[8 + r] : bs[12 + r];
+  }
+  return bv;
+}
+
 template <int EPI>
 __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, const bf16* __restrict__ M,
                                         const float* __restrict__ bias, size_t vox_index, int co0, size_t nvox_all = 0,
@@ -260,6 +279,7 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
   };
 
   const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
+  const f32x4 bv = lane_bias4<EPI>(bias, lane);
   auto store_tile = [&](int jt) {
     if constexpr (BLK) {
       // row co = 4 (lane >> 4) + r is output plane (i0 + (lane >> 4), j0 + r)
@@ -291,16 +311,32 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
       return;
     }
     const size_t vbase_out = plane_offset(g, t.v, t.i, t.j + jt, 1);
+    auto out_vox = [&](int tt, size_t& vox) -> bool {
+      const int tile = wave + NW * tt;
+      const int vi = tile * 16 + (lane & 15);
+      const int kk = vi / g.TL, ll = vi - kk * g.TL;
+      const int kg = t.k0 + kk, lg = t.l0 + ll;
+      vox = vbase_out + (size_t)kg * g.L + lg;
+      return tile < ntile && vi < nvox && kg < g.K && lg < g.L;
+    };
+    // ReLU-mask epilogue: all of the tile's mask loads before the first store
+    constexpr bool MPF = (EPI & ~EPI_X3) == EPI_MASK;
+    u32x2 mreg[MPF ? MAXT : 1];
+    if constexpr (MPF) {
+#pragma unroll
+      for (int tt = 0; tt < MAXT; ++tt) {
+        size_t vox;
+        if (!out_vox(tt, vox)) vox = 0;   // select, not a branch: one unconditional load each
+        mreg[tt] = *(const u32x2*)(M + vox * 16 + 4 * (lane >> 4));
+      }
+    }
 #pragma unroll
     for (int tt = 0; tt < MAXT; ++tt) {
-      int tile = wave + NW * tt;
-      if (tile < ntile) {
-        int vi = tile * 16 + (lane & 15);
-        int kk = vi / g.TL, ll = vi - kk * g.TL;
-        int kg = t.k0 + kk, lg = t.l0 + ll;
-        if (vi < nvox && kg < g.K && lg < g.L)
-          store16<EPI>(acc[tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco, g.nt,
-                       g.ylo);
+      size_t vox;
+      if (out_vox(tt, vox)) {
+        const u32x2* mp = nullptr;
+        if constexpr (MPF) mp = &mreg[tt];
+        store16<EPI>(acc[tt], Y, M, bias, vox, 4 * (lane >> 4), nvox_all, g.nco, g.nt, g.ylo, mp, &bv);
       }
     }
   };
@@ -514,21 +550,38 @@ __global__ __launch_bounds__(512, 1) void conv16v3_fwd_kernel(const bf16* __rest
   }
 
   const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
+  const f32x4 bv = lane_bias4<EPI>(bias, lane);
+  // data-gradient epilogue: every ReLU-mask load of the item issued before the
+  // first store (as in conv16v4), not one load -> vmcnt(0) -> store per tile
+  constexpr bool MPF = (EPI & ~EPI_X3) == EPI_MASK;
+  u32x2 mreg[MPF ? R : 1][MPF ? MAXT : 1];
+  auto out_vox = [&](int r, int tt, size_t& vox) -> bool {
+    const int j = j0 + r;
+    const int tile = wave + NW * tt;
+    const int vi = tile * 16 + (lane & 15);
+    const int kk = vi / g.TL, ll = vi - kk * g.TL;
+    const int kg = k0 + kk, lg = l0 + ll;
+    vox = plane_offset(g, tv, ti, j, 1) + (size_t)kg * g.L + lg;
+    return j < g.J && tile < ntile && vi < nvox && kg < g.K && lg < g.L;
+  };
+  if constexpr (MPF) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int tt = 0; tt < MAXT; ++tt) {
+        size_t vox;
+        mreg[r][tt] = out_vox(r, tt, vox) ? *(const u32x2*)(M + vox * 16 + 4 * (lane >> 4)) : u32x2{0u, 0u};
+      }
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int j = j0 + r;
-    if (j >= g.J) break;
-    const size_t vbase_out = plane_offset(g, tv, ti, j, 1);
 #pragma unroll
     for (int tt = 0; tt < MAXT; ++tt) {
-      int tile = wave + NW * tt;
-      if (tile < ntile) {
-        int vi = tile * 16 + (lane & 15);
-        int kk = vi / g.TL, ll = vi - kk * g.TL;
-        int kg = k0 + kk, lg = l0 + ll;
-        if (vi < nvox && kg < g.K && lg < g.L)
-          store16<EPI>(acc[r][tt], Y, M, bias, vbase_out + (size_t)kg * g.L + lg, 4 * (lane >> 4), nvox_all, g.nco,
-                       g.nt);
+      size_t vox;
+      if (out_vox(r, tt, vox)) {
+        const u32x2* mp = nullptr;
+        if constexpr (MPF) mp = &mreg[r][tt];
+        store16<EPI>(acc[r][tt], Y, M, bias, vox, 4 * (lane >> 4), nvox_all, g.nco, g.nt, 0, mp, &bv);
       }
     }
   }
@@ -783,20 +836,7 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
   // (r, tt) serialised 25 memory round trips (stores count in vmcnt here)
   constexpr bool MPF = (EPI & ~EPI_X3) == EPI_MASK;
   u32x2 mreg[MPF ? R : 1][MPF ? MAXT : 1];
-  // bias + ReLU: this lane's 4 output channels' bias, loaded once (per store it
-  // was a load -> vmcnt(0) -> store chain like the mask's)
-  // (scalar loads of all 16 + a per-lane select: no vector load whose use the
-  // waitcnt pass would re-wait for -- with the stores in vmcnt -- in every
-  // conditional store block)
-  f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-  if constexpr ((EPI & ~EPI_X3) == EPI_BIAS_RELU) {
-    float bs[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) bs[c] = bias[c];   // uniform addresses: s_load
-    const int gq = lane >> 4;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bv[r] = gq == 0 ? bs[r] : gq == 1 ? bs[4 + r] : gq == 2 ? bs[8 + r] : bs[12 + r];
-  }
+  const f32x4 bv = lane_bias4<EPI>(bias, lane);
   if constexpr (MPF) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
