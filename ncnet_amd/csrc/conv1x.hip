@@ -237,9 +237,11 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
             const int f = C::F0 + 16 * (wave + NW * tt) + (lane & 15);
             const int kp = f / LP, lp = f - kp * LP;
             const int k = kp - P, l = lp - P;
-            mreg[r][tt] = (j < J && f < C::FN && k >= 0 && k < K && l >= 0 && l < L)
-                              ? *(const u32x2*)(M + (pbase + (size_t)k * L + l) * 16 + co0)
-                              : u32x2{0u, 0u};
+            // address select, not a branch: straight-line loads the waitcnt
+            // pass can count past the epilogue's conditional stores
+            const bool ok = j < J && f < C::FN && k >= 0 && k < K && l >= 0 && l < L;
+            const size_t vox = ok ? pbase + (size_t)k * L + l : 0;
+            mreg[r][tt] = *(const u32x2*)(M + vox * 16 + co0);
           }
         }
       }
