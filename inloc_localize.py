@@ -71,8 +71,43 @@ def _pair_rng(seed: int, q: int, jj: int):
 
 
 def _cache_path(cache_dir: str, qname: str, dbname: str, kind: str) -> str:
-    """parfor_NC4D_PE_pnponly.m:4 / parfor_nc4d_PV.m: one file per (query, db)."""
-    return os.path.join(cache_dir, kind, qname, os.path.basename(dbname) + ".npz")
+    """parfor_NC4D_PE_pnponly.m:4 / parfor_nc4d_PV.m: one file per (query, db).
+    The full relative cutout name keeps same-named cutouts of different scans
+    apart."""
+    rel = os.path.normpath(dbname).lstrip(os.sep)
+    if rel.startswith(".."):
+        raise ValueError(f"cutout name escapes the cache dir: {dbname!r}")
+    return os.path.join(cache_dir, kind, qname, rel + ".npz")
+
+
+_PNP_KEYS = ("thr", "pnp_thr", "ransac_iters", "n_subsample", "seed", "focal")
+
+
+def _cache_key(cfg: dict, keys, *arrays, extra=()) -> str:
+    """Hash of everything a cached result depends on: the run settings named in
+    ``keys``, the pair's inputs (its match rows, the scored pose P) and
+    ``extra``.  A cached file whose key differs is recomputed, never reused."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(repr([(k, cfg[k]) for k in keys] + list(extra)).encode())
+    for a in arrays:
+        if a is None:
+            h.update(b"<none>")
+        else:
+            a = np.ascontiguousarray(np.asarray(a, np.float64))
+            h.update(repr(a.shape).encode())
+            h.update(a.tobytes())
+    return h.hexdigest()
+
+
+def _cache_load(cpath, key):
+    """The cached npz when it exists and was written under ``key``, else None."""
+    if not cpath or not os.path.exists(cpath):
+        return None
+    z = np.load(cpath)   # plain arrays only (allow_pickle stays False)
+    if "key" not in z.files or str(z["key"]) != key:
+        return None
+    return z
 
 
 def _pnp_pair(task):
@@ -80,8 +115,9 @@ def _pnp_pair(task):
     (parfor_NC4D_PE_pnponly.m).  Cached on disk when cache_dir is set."""
     q, jj, qname, dbname, m, q_size, cfg = task
     cpath = _cache_path(cfg["cache_dir"], qname, dbname, "pnp") if cfg["cache_dir"] else None
-    if cpath and os.path.exists(cpath):
-        z = np.load(cpath)
+    key = _cache_key(cfg, _PNP_KEYS, m, extra=(tuple(q_size), q, jj)) if cpath else ""
+    z = _cache_load(cpath, key)
+    if z is not None:
         P = z["P"]
         return q, jj, dbname, (None if np.isnan(P).all() else P), int(z["n_inliers"])
     P, n_inl = None, 0
@@ -102,7 +138,7 @@ def _pnp_pair(task):
     if cpath:
         os.makedirs(os.path.dirname(cpath), exist_ok=True)
         tmp = cpath + ".tmp.npz"
-        np.savez(tmp, P=np.full((3, 4), np.nan) if P is None else P, n_inliers=n_inl)
+        np.savez(tmp, P=np.full((3, 4), np.nan) if P is None else P, n_inliers=n_inl, key=key)
         os.replace(tmp, cpath)
     return q, jj, dbname, P, n_inl
 
@@ -253,10 +289,12 @@ def _pv_scan(task):
     out, todo = [], []
     for q, jj, qname, dbname, P in items:
         cpath = _cache_path(cfg["cache_dir"], qname, dbname, "pv") if cfg["cache_dir"] else None
-        if cpath and os.path.exists(cpath):
-            out.append((q, jj, float(np.load(cpath)["score"])))
+        key = _cache_key(cfg, ("focal",), P, extra=(os.path.basename(scan_path),)) if cpath else ""
+        z = _cache_load(cpath, key)
+        if z is not None:
+            out.append((q, jj, float(z["score"])))
         else:
-            todo.append((q, jj, qname, dbname, P, cpath))
+            todo.append((q, jj, qname, dbname, P, cpath, key))
     if not todo:
         return out
     scan = None
@@ -264,7 +302,7 @@ def _pv_scan(task):
         P_after = pv.load_transformation(trans_path) if os.path.exists(trans_path) else None
         scan = pv.load_scan(scan_path, P_after)
     qimgs = {}
-    for q, jj, qname, dbname, P, cpath in todo:
+    for q, jj, qname, dbname, P, cpath, key in todo:
         qpath = os.path.join(cfg["query_dir"], qname)
         s = 0.0
         if scan is not None and P is not None and os.path.exists(qpath):
@@ -274,7 +312,7 @@ def _pv_scan(task):
         if cpath:
             os.makedirs(os.path.dirname(cpath), exist_ok=True)
             tmp = cpath + ".tmp.npz"
-            np.savez(tmp, score=s)
+            np.savez(tmp, score=s, key=key)
             os.replace(tmp, cpath)
         out.append((q, jj, s))
     return out

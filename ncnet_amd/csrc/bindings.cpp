@@ -114,7 +114,8 @@ void pad_planes(Tensor x, Tensor y, int64_t I2, int64_t J2, int64_t ks, int64_t 
 
 // 1 -> 16 Conv4d on padded 1-channel planes Xp [V*I*J, PPL] with A fragments Wa
 // [ks^2, 64, 8]; Y bf16 [V,I,J,K,L,16]; epi 1 (bias + ReLU) or 2 (ReLU mask M).
-// Returns false (nothing launched) for shapes without an instantiation.
+// Raises for shapes without an instantiation (ops/neigh_consensus.py fast1x_ok
+// must never route one here: the outputs are uninitialised buffers).
 bool conv1x16(Tensor Xp, Tensor Wa, c10::optional<Tensor> bias, c10::optional<Tensor> M, Tensor Y, int64_t ks,
               int64_t epi) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(Xp.device());
@@ -131,7 +132,7 @@ bool conv1x16(Tensor Xp, Tensor Wa, c10::optional<Tensor> bias, c10::optional<Te
   const int nt = ncnet_set_tuning("nt_store", 0, 0);
   const int r = ncnet_conv1x16(Xp.data_ptr(), Wa.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(),
                                (int)V, (int)I, (int)J, (int)K, (int)L, (int)ks, (int)epi, nt, cur_stream(Xp));
-  if (r == -1) return false;
+  TORCH_CHECK(r != -1, "conv1x16: no kernel instantiation for ks=", ks, " K=", K, " L=", L, " epi=", epi);
   ok(r, "conv1x16");
   return true;
 }
@@ -139,7 +140,7 @@ bool conv1x16(Tensor Xp, Tensor Wa, c10::optional<Tensor> bias, c10::optional<Te
 // Weight-gradient partials of a Conv4d with a 1-channel operand (csrc/conv1x.hip
 // wgrad1x16): D bf16 [V,I,J,K,L,16], X1 padded planes [V*I*J, PPL];
 // part fp32 [G, ks^2, 32, 16] (G workgroups, one partial each), partb fp32 [G, 16]
-// (the sum of D) or None.  Returns false for shapes without an instantiation.
+// (the sum of D) or None.  Raises for shapes without an instantiation.
 bool wgrad1x16(Tensor D, Tensor X1, Tensor part, c10::optional<Tensor> partb, int64_t ks) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(D.device());
   check(D, "D", at::kBFloat16); check(X1, "X1", at::kBFloat16); check(part, "part", at::kFloat);
@@ -156,7 +157,7 @@ bool wgrad1x16(Tensor D, Tensor X1, Tensor part, c10::optional<Tensor> partb, in
   const int r = ncnet_wgrad1x16(D.data_ptr(), X1.data_ptr(), (float*)part.data_ptr(),
                                 partb.has_value() ? (float*)partb->data_ptr() : nullptr, (int)G, (int)V, (int)I,
                                 (int)J, (int)K, (int)L, (int)ks, cur_stream(D));
-  if (r == -1) return false;
+  TORCH_CHECK(r != -1, "wgrad1x16: no kernel instantiation for ks=", ks, " K=", K, " L=", L);
   ok(r, "wgrad1x16");
   return true;
 }

@@ -329,6 +329,263 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void conv2d_nhwc_v2_kernel(Conv2dA
   conv2d_epilogue<BM, BN, TM, TN, NT, F16>(acc, p, smem, m0, n0, wm, wn, fr, fq);
 }
 
+
+// ===========================================================================
+// conv2d_nhwc_v3: the implicit GEMM as ONE round of workgroups sized to the
+// chip (layer 3 at the training size: M = 32 x 25 x 25 = 20,000 pixels, N =
+// 256).  v1's 64 x 128 tiles give 626 workgroups = 1.22 rounds of two per CU
+// and v2's 256 x 128 tiles 158, so either leaves up to half the chip idle for
+// the last round; here the host picks BM = 16 TM rows so that
+// ceil(tiles / CUs) x BM is smallest (BM = 80: 250 tiles of 80 x 256, one per
+// CU).  BN = 64 TN covers all of N = 256 (TN = 4): per k-step an 80 x 256 tile
+// reads 43 KB for 655 K MACs, 30 MAC per L2 byte.
+//  * 8 waves = 2 K-groups x 4 N-groups: a ring stage holds BK = 64 (one tap x
+//    64 input channels); K-group g runs the MFMAs of the stage's g-th 32-deep
+//    half on its own accumulators (TM x TN tiles, 0.45 LDS reads per MFMA),
+//    two waves per SIMD hide each other's fragment reads; the two partial sums
+//    meet once, through LDS, in the epilogue;
+//  * LDS-DMA ring of 3 stages, fixed DMA count per wave and stage (missing
+//    rows go to a trash KiB, out-of-image im2col rows read a zero block), so
+//    the wait for stage ks is a compile-time vmcnt; issued from asm (the
+//    compiler never drains the ring in front of a fragment read);
+//  * 128-B LDS rows, chunk c of row r at c ^ (r & 7) (v1's conflict-free
+//    swizzle), applied to the DMA source (a DMA instruction writes 1 KiB
+//    contiguously: 8 rows);
+//  * epilogue: K-group 1 adds its accumulators through an fp32 LDS tile, then
+//    bias -> 16-bit staging tile -> residual + ReLU with 16-B coalesced rows.
+// Requires Cin % 64 == 0 and Cout % BN == 0.
+// ===========================================================================
+namespace cv3 {
+constexpr int NS = 3;
+__device__ __forceinline__ uint32_t toff(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ (row & 7)) << 4)); }
+template <int TM, int TN>
+struct Geo {
+  static constexpr int BM = 16 * TM, BN = 64 * TN;
+  static constexpr int NIA = BM / 8, NIB = BN / 8, NI = NIA + NIB;
+  static constexpr int PER = (NI + 7) / 8;              // DMA wave-instructions per wave per stage
+  static constexpr int STAGE = (BM + BN) * 128;
+  static constexpr int TRASH = NS * STAGE;
+  static constexpr int PSTR = BN + 4;                    // fp32 row stride of the K-group sum tile
+  static constexpr int EPI = BM * PSTR * 4 + BM * BN * 2;
+  static constexpr int LDS = (TRASH + 1024) > EPI ? (TRASH + 1024) : EPI;
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+}  // namespace cv3
+
+template <int N>
+__device__ __forceinline__ void c3_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int TM, int TN, bool F16 = false>
+__global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
+  using namespace cv3;
+  using G = Geo<TM, TN>;
+  constexpr int BM = G::BM, BN = G::BN, PER = G::PER;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kg = wave >> 2, wn = wave & 3;
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = bid % p.tiles_n, tm = bid / p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int K = p.KH * p.KW * p.Cin;
+
+  // this lane's row of each of the wave's PER DMA instructions (instruction
+  // j = wave + 8 m: A rows 8 j .. 8 j + 7, then B rows, then trash)
+  int a_hi0[PER], a_wi0[PER];
+  uint32_t a_pix[PER];            // n * H * W (image base, pixels)
+  const bf16* b_src[PER];
+  uint32_t dst[PER];
+  int kind[PER];                  // 0 A, 1 B, 2 trash (wave-uniform)
+  uint32_t coff[PER];             // this lane's source chunk offset (elements)
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const int j = wave + 8 * m;
+    const int sub = lane >> 3, pos = lane & 7;
+    a_hi0[m] = -(1 << 28); a_wi0[m] = 0; a_pix[m] = 0; b_src[m] = p.W; coff[m] = 0;
+    if (j < G::NIA) {
+      kind[m] = 0;
+      const int row = 8 * j + sub;
+      const int pix = m0 + row;
+      coff[m] = (uint32_t)((pos ^ (row & 7)) * 8);
+      dst[m] = (uint32_t)(j * 1024);
+      if (pix < p.M) {
+        const int wo = pix % p.Wo, t = pix / p.Wo, ho = t % p.Ho, n = t / p.Ho;
+        a_hi0[m] = ho * p.stride - p.pad;
+        a_wi0[m] = wo * p.stride - p.pad;
+        a_pix[m] = (uint32_t)(n * p.H * p.Wd);
+      }
+    } else if (j < G::NI) {
+      kind[m] = 1;
+      const int row = 8 * (j - G::NIA) + sub;
+      b_src[m] = p.W + (size_t)(n0 + row) * K + (pos ^ (row & 7)) * 8;
+      dst[m] = (uint32_t)(BM * 128 + (j - G::NIA) * 1024);
+    } else {
+      kind[m] = 2;
+      dst[m] = (uint32_t)G::TRASH;
+    }
+  }
+  const int cpt = p.Cin / 64;
+  const int nk = p.KH * p.KW * cpt;
+  const bf16* zero = (const bf16*)&g_zero16;
+
+  auto issue = [&](int ks, int buf) {
+    const int tap = ks / cpt, c0 = (ks - tap * cpt) * 64;
+    const int dh = tap / p.KW, dw = tap - dh * p.KW;
+    char* sb = smem + buf * G::STAGE;
+#pragma unroll
+    for (int m = 0; m < PER; ++m) {
+      const bf16* src = zero;
+      uint32_t d = dst[m];
+      if (kind[m] == 0) {
+        const int hi = a_hi0[m] + dh, wi = a_wi0[m] + dw;
+        const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.Wd;
+        const bf16* a = p.X + ((size_t)a_pix[m] + (size_t)(ok ? hi : 0) * p.Wd + (ok ? wi : 0)) * p.Cin + c0 + coff[m];
+        src = ok ? a : zero;
+        d += buf * G::STAGE;
+      } else if (kind[m] == 1) {
+        src = b_src[m] + tap * p.Cin + c0;
+        d += buf * G::STAGE;
+      }
+      dma16_lds(src, smem + d);
+    }
+    (void)sb;
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int kc = kg * 4 + fq;      // this lane's 16-B chunk of the 64-deep stage
+  int buf = 0;
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk) c3_wait_barrier<PER>();   // stage ks landed; ks + 1 may still fly
+    else c3_wait_barrier<0>();
+    if (ks + NS - 1 < nk) issue(ks + NS - 1, (buf + NS - 1) % NS);   // into the buffer consumed at ks - 1
+    const char* As = smem + buf * G::STAGE;
+    const char* Bs = As + BM * 128;
+    bf16x8 af[TM], bfv[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = lds_read16(As, toff(i * 16 + fr, kc));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfv[j] = lds_read16(Bs, toff(wn * TN * 16 + j * 16 + fr, kc));
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = mfma16t<F16>(__builtin_bit_cast(u32x4, af[i]), __builtin_bit_cast(u32x4, bfv[j]), acc[i][j]);
+    buf = (buf + 1 == NS) ? 0 : buf + 1;
+  }
+  __syncthreads();   // every fragment read done (and every DMA landed: the last wait was vmcnt(0))
+
+  // K-group sum through LDS, then bias -> 16-bit staging tile [BM][BN]
+  float* P = (float*)smem;
+  uint16_t* S = (uint16_t*)(smem + BM * G::PSTR * 4);
+  if (kg == 1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[(i * 16 + 4 * fq + r) * G::PSTR + wn * TN * 16 + j * 16 + fr] = acc[i][j][r];
+  }
+  __syncthreads();
+  if (kg == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * TN * 16 + j * 16 + fr;
+      const float b = p.bias[n0 + col];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + 4 * fq + r;
+          S[row * BN + col] = f2s16<F16>(acc[i][j][r] + P[row * G::PSTR + col] + b);
+        }
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  const uint16_t* R = (const uint16_t*)p.R;
+  uint16_t* Y = (uint16_t*)p.Y;
+  for (int c = threadIdx.x; c < BM * CPR; c += 512) {
+    const int row = c / CPR, cc = c - row * CPR;
+    const int pix = m0 + row;
+    if (pix < p.M) {
+      const u32x4 tv = *(const u32x4*)(S + row * BN + cc * 8);
+      const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
+      u32x4 rv = {0u, 0u, 0u, 0u};
+      if (R) rv = *(const u32x4*)(R + o);
+      u32x4 out;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v = s162f<F16>((uint16_t)(tv[e] >> (16 * h)));
+          if (R) v = s162f<F16>(f2s16<F16>(v + s162f<F16>((uint16_t)(rv[e] >> (16 * h)))));
+          if (p.relu) v = fmaxf(v, 0.f);
+          w |= (uint32_t)f2s16<F16>(v) << (16 * h);
+        }
+        out[e] = w;
+      }
+      *(u32x4*)(Y + o) = out;
+    }
+  }
+}
+
+// number of CUs of the current device (cached per device)
+static int c3_num_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+template <int TM, int TN>
+static void c3_launch1(bool f16, dim3 g, dim3 b, hipStream_t stream, const Conv2dArgs& p) {
+  const size_t lds = (size_t)cv3::Geo<TM, TN>::LDS;
+  if (f16) hipLaunchKernelGGL((conv2d_nhwc_v3_kernel<TM, TN, true>), g, b, lds, stream, p);
+  else hipLaunchKernelGGL((conv2d_nhwc_v3_kernel<TM, TN, false>), g, b, lds, stream, p);
+}
+template <int TN>
+static void c3_launch(int tm, bool f16, dim3 g, dim3 b, hipStream_t stream, const Conv2dArgs& p) {
+  if (tm == 3) c3_launch1<3, TN>(f16, g, b, stream, p);
+  else if (tm == 4) c3_launch1<4, TN>(f16, g, b, stream, p);
+  else if (tm == 5) c3_launch1<5, TN>(f16, g, b, stream, p);
+  else c3_launch1<6, TN>(f16, g, b, stream, p);
+}
+
+// v3 tile rows: BM = 16 TM minimising (rounds of one workgroup per CU) x BM,
+// ties to the larger tile (fewer weight re-reads).  Returns TM, or 0 when v3
+// does not apply (Cout % BN, Cin % 64).
+static int c3_pick_tm(int M, int Cout, int Cin, int TN, int ncu, long long* cost) {
+  if (Cin % 64 || Cout % (64 * TN)) return 0;
+  const int tn = Cout / (64 * TN);
+  int best = 0;
+  long long bc = 0;
+  for (int tm = 3; tm <= 6; ++tm) {
+    if (TN == 4 && 16 * tm * (64 * TN + 4) * 4 + 16 * tm * 64 * TN * 2 > 160 * 1024) continue;
+    const long long tiles = (long long)cdiv(M, 16 * tm) * tn;
+    const long long c = cdiv((int)((tiles + 0) > 0x7fffffff ? 0x7fffffff : tiles), ncu) * (long long)(16 * tm);
+    if (!best || c < bc || (c == bc && tm > best)) { best = tm; bc = c; }
+  }
+  if (cost) *cost = bc;
+  return best;
+}
+
 }  // namespace ncnet
 
 using namespace ncnet;
@@ -358,6 +615,19 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
   // NCNET_CONV2D_VARIANT=1 / 2 forces v1 / the DMA ring (with 128-row tiles
   // unless NCNET_CONV2D_BIG is set or the grid is large).
   const int variant = tuning().conv2d_variant;
+  if (variant == 3) {
+    // one round of workgroups sized to the chip (conv2d_nhwc_v3)
+    const int TNv = (Cout % 256 == 0) ? 4 : 2;
+    const int tm = c3_pick_tm(p.M, Cout, Cin, TNv, c3_num_cus(), nullptr);
+    if (tm) {
+      p.tiles_n = Cout / (64 * TNv);
+      p.tiles_m = cdiv(p.M, 16 * tm);
+      dim3 g3((unsigned)(p.tiles_m * p.tiles_n)), b3(512);
+      if (TNv == 4) c3_launch<4>(tm, f16, g3, b3, stream, p);
+      else c3_launch<2>(tm, f16, g3, b3, stream, p);
+      return (int)hipGetLastError();
+    }
+  }
   const int t256 = cdiv(p.M, 256) * p.tiles_n;
   const bool big = BN == 128 && (variant == 0 ? t256 >= 384 : (t256 >= 512 || (t256 >= 256 && tuning().conv2d_big)));
   if (big && variant != 1) {

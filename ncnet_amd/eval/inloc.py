@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from ..data.transforms import normalize_image, resize_bilinear
+from ..ops.neigh_consensus import pin_fp8_weights
 from .point_tnf import corr_to_matches
 
 SCALE_FACTOR = 0.0625  # feature stride 1/16 (eval_inloc.py:77)
@@ -150,7 +151,10 @@ class PairMatcher:
     def __call__(self, fa, hwa, fb, hwb):
         if not (self.use_graph and torch.is_tensor(fa) and fa.is_cuda):
             return self._eager(fa, hwa, fb, hwb)
-        key = (tuple(fa.shape), tuple(fb.shape), fa.dtype, tuple(hwa), tuple(hwb))
+        # the graph bakes in the NC weights it was captured with (e.g. the
+        # cached fp8 quantisation): a weight update must re-capture
+        wver = tuple((id(p), p._version) for p in self.model.parameters())
+        key = (tuple(fa.shape), tuple(fb.shape), fa.dtype, tuple(hwa), tuple(hwb), wver)
         ent = self._graphs.get(key)
         if ent is None:
             try:
@@ -162,9 +166,12 @@ class PairMatcher:
                         self._eager(sa, hwa, sb, hwb)
                 torch.cuda.current_stream(fa.device).wait_stream(side)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with pin_fp8_weights() as pins, torch.cuda.graph(g):
                     res = self._eager(sa, hwa, sb, hwb)
-                ent = self._graphs[key] = (g, sa, sb, res)
+                # stale shapes / weight versions are dropped with their graphs;
+                # `pins` keeps the cached weight buffers the graph reads alive
+                self._graphs = {k: v for k, v in self._graphs.items() if k[:5] != key[:5]}
+                ent = self._graphs[key] = (g, sa, sb, res, pins)
             except RuntimeError as err:      # capture unsupported -> eager from now on (loudly)
                 import traceback
                 import warnings
@@ -172,7 +179,7 @@ class PairMatcher:
                 warnings.warn(f"PairMatcher: HIP graph capture disabled ({err})")
                 self.use_graph = False
                 return self._eager(fa, hwa, fb, hwb)
-        g, sa, sb, res = ent
+        g, sa, sb, res, _ = ent
         if sa.data_ptr() != fa.data_ptr():
             sa.copy_(fa)
         sb.copy_(fb)

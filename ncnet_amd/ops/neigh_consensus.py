@@ -37,6 +37,7 @@ import os as _os
 
 import numpy as np
 import torch
+import torch.utils.weak as _weak
 
 from .. import config as _config
 from . import _ext
@@ -1057,24 +1058,50 @@ def _fp8_weights(packed_bf16: torch.Tensor):
     return (packed_bf16.float() * 2.0 ** e).to(FP8), 2.0 ** -e
 
 
-_FP8_W_CACHE: dict = {}
+# weight tensor -> {kind: (version, shape, (fp8 fragments, 1/scale))}.  Keyed by
+# the tensor OBJECT (entries die with it), never by its address: a new weight
+# tensor the caching allocator places where a freed one lived must not inherit
+# its fp8 weights.
+_FP8_W_CACHE = _weak.WeakIdKeyDictionary()
+_FP8_PINS: list | None = None
+
+
+class pin_fp8_weights:
+    """Collects every cached fp8 weight tensor used inside the block (returned
+    by ``__enter__``): a HIP graph captured there replays those exact buffers,
+    so its owner keeps them alive for as long as the graph exists
+    (eval/inloc.py PairMatcher)."""
+
+    def __enter__(self):
+        global _FP8_PINS
+        self._prev, _FP8_PINS = _FP8_PINS, []
+        return _FP8_PINS
+
+    def __exit__(self, *exc):
+        global _FP8_PINS
+        _FP8_PINS = self._prev
+        return False
 
 
 def _fp8_weights_of(w_ref: torch.Tensor, kind: str):
     """Quantised fp8 fragments of one layer's weights, cached per weight tensor
-    version: the amax -> scale step reads the max on the host, which must not
-    happen per pair (it serialises the stream and is illegal inside the
-    InLoc PairMatcher HIP-graph capture)."""
-    key = (w_ref.data_ptr(), w_ref._version, tuple(w_ref.shape), kind)
-    hit = _FP8_W_CACHE.get(key)
-    if hit is None:
+    and version: the amax -> scale step reads the max on the host, which must
+    not happen per pair (it serialises the stream and is illegal inside the
+    InLoc PairMatcher HIP-graph capture).  Pass the weight Parameter itself
+    (``Conv4d.weight`` with ``pre_permuted_filters=True``, the default) for the
+    cache to hit across calls; a fresh tensor per call is re-quantised."""
+    per = _FP8_W_CACHE.get(w_ref)
+    if per is None:
+        per = _FP8_W_CACHE[w_ref] = {}
+    ent = per.get(kind)
+    if ent is None or ent[0] != w_ref._version or ent[1] != tuple(w_ref.shape):
         w = _std(w_ref)
         packed = {"1in": lambda: pack_w16_planes(ij_in_weights(w)), "16": lambda: pack_w16(w),
                   "1out": lambda: pack_w16_planes(ij_out_weights(w))}[kind]()
-        if len(_FP8_W_CACHE) > 64:
-            _FP8_W_CACHE.clear()
-        hit = _FP8_W_CACHE[key] = _fp8_weights(packed)
-    return hit
+        ent = per[kind] = (w_ref._version, tuple(w_ref.shape), _fp8_weights(packed))
+    if _FP8_PINS is not None:
+        _FP8_PINS.append(ent[2][0])
+    return ent[2]
 
 
 def _stack_fwd_fp8(x0: torch.Tensor, ws, bs, kinds) -> torch.Tensor:

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -138,6 +139,8 @@ class GradBucket:
         self.ctx = ctx
         self.inplace = getattr(optimizer, "flat_grad", None) is not None
         self._work = None
+        self._hooks = []            # post-accumulate hook handles of the early segment
+        self._armed = False
         self._early = []            # in-flight early segment all-reduces
         self._early_seg = None      # (lo, hi) flat range reduced early, or None
         if self.inplace:
@@ -167,26 +170,44 @@ class GradBucket:
         self._early_seg = (lo, hi)
         self._pending = set()
         ids = {id(p) for p in early}
+        me = weakref.ref(self)      # the parameters must not keep a dropped bucket alive
 
         def hook(p):
-            if id(p) not in ids or self._early_seg is None:
+            b = me()
+            if b is None or not b._armed or id(p) not in ids or b._early_seg is None:
                 return
-            self._pending.discard(id(p))
-            if not self._pending and not self._early:
-                self._early.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
-                self.early_launches += 1
+            b._pending.discard(id(p))
+            if not b._pending and not b._early:
+                b._early.append(dist.all_reduce(b.flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+                b.early_launches += 1
 
         self._ids = ids
         self.early_launches = 0
-        for p in early:
-            p.register_post_accumulate_grad_hook(hook)
+        self._hooks = [p.register_post_accumulate_grad_hook(hook) for p in early]
         self.reset()
 
     def reset(self):
-        """Arm the early segment for the next backward (Trainer: before backward)."""
+        """Arm the early segment for the next backward (Trainer: before backward).
+        Hooks fire only between ``reset`` and ``finish``: a backward that this
+        bucket does not own launches nothing."""
         if self._early_seg is not None:
             self._pending = set(self._ids)
             self._early = []
+            self._armed = True
+
+    def close(self):
+        """Remove the early-segment hooks (a replacement bucket on the same
+        parameters must not find this one's hooks still firing)."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self._armed = False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover  (interpreter teardown)
+            pass
 
     def start(self):
         """Launch the (async) all-reduce (packing the grads first unless in place)."""
@@ -214,6 +235,7 @@ class GradBucket:
 
     def finish(self):
         """Wait (and, for a private bucket, scatter the averaged gradients back)."""
+        self._armed = False
         if not self.ctx.enabled or self._work is None:
             return
         for w in (self._work if isinstance(self._work, list) else [self._work]) + self._early:

@@ -48,7 +48,7 @@ def main():
               ("l3.n1", 3, 1024, 256, 1, 1, 3), ("l3.n2", 3, 256, 256, 3, 1, 3), ("l3.n3", 3, 256, 1024, 1, 1, 3),
               ("l3.nd", 3, 512, 1024, 1, 2, 2), ("l3.n2s", 3, 256, 256, 3, 2, 2)]
     print(f"{'layer':8s} {'M':>8s} {'N':>5s} {'K':>5s}  {'native v1':>16s}  {'native v2':>16s}  {'v2 big':>16s}"
-          f"  {'hipBLASLt/MIOpen':>18s}")
+          f"  {'v3 (chip round)':>16s}  {'auto':>16s}  {'hipBLASLt/MIOpen':>18s}")
     for name, _, cin, cout, k, s, lin in shapes:
         H, W = hw[lin]
         x = torch.randn(n, cin, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
@@ -66,7 +66,10 @@ def main():
         C.set_tuning("conv2d_big", 1)
         t_b = timeit(run)
         C.set_tuning("conv2d_big", 0)
+        C.set_tuning("conv2d_variant", 3)
+        t_3 = timeit(run)
         C.set_tuning("conv2d_variant", 0)
+        t_a = timeit(run)
         if k == 1 and s == 1:
             x2 = x.permute(0, 2, 3, 1).reshape(M, cin)
             w2 = w.reshape(cout, cin)
@@ -77,7 +80,8 @@ def main():
             t_o = timeit(lambda: torch.relu_(torch.nn.functional.conv2d(x, wb, b.to(torch.bfloat16), s, k // 2)))
         print(f"{name:8s} {M:8d} {cout:5d} {K:5d}  {t_1 * 1e3:7.1f} us {fl / t_1 / 1e9:5.0f} TF  "
               f"{t_n * 1e3:7.1f} us {fl / t_n / 1e9:5.0f} TF  {t_b * 1e3:7.1f} us {fl / t_b / 1e9:5.0f} TF  "
-              f"{t_o * 1e3:7.1f} us {fl / t_o / 1e9:5.0f} TF")
+              f"{t_3 * 1e3:7.1f} us {fl / t_3 / 1e9:5.0f} TF  {t_a * 1e3:7.1f} us {fl / t_a / 1e9:5.0f} TF  "
+              f"{t_o * 1e3:7.1f} us {fl / t_o / 1e9:5.0f} TF", flush=True)
 
 
 if __name__ == "__main__":

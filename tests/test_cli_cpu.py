@@ -90,6 +90,11 @@ def test_inloc_localize_parallel_cached(workdir):
     stamp = {os.path.join(d, f): os.path.getmtime(os.path.join(d, f)) for d, _, fs in os.walk(cache) for f in fs}
     est3, _ = inloc_localize.main(base + ["--workers", "2", "--cache_dir", cache])
     assert stamp == {os.path.join(d, f): os.path.getmtime(os.path.join(d, f)) for d, _, fs in os.walk(cache) for f in fs}
+    # a rerun with another threshold must not reuse the cached poses / scores
+    inloc_localize.main(base + ["--workers", "1", "--cache_dir", cache, "--thr", "0.5"])
+    # (PV scores are keyed by the pose they scored: reused only for an identical P)
+    pnp = [k for k in stamp if os.sep + "pnp" + os.sep in k]
+    assert len(pnp) == 6 and all(os.path.getmtime(k) != stamp[k] for k in pnp)
     for e in (est2, est3):
         assert est1.keys() == e.keys()
         for k in est1:

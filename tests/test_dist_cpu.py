@@ -256,7 +256,20 @@ def _overlap_worker(rank, world, port, out_dir, early):
     for step in range(2):
         tr.train_step(_batch(10 * step + rank))
     launches = getattr(tr.bucket, "early_launches", 0) if early else 0
-    torch.save({"params": [p.detach().clone() for p in params], "early_launches": launches},
+    snap = [p.detach().clone() for p in params]
+    stale = 0
+    if early:
+        # a second trainer on the same parameters (a restart in-process): the
+        # first bucket's hooks must stay silent (disarmed after its finish)
+        old = tr.bucket
+        tr2 = Trainer(m, make_adam(params, 5e-4), ctx)
+        tr2.train_step(_batch(99 + rank))
+        stale = old.early_launches - launches
+        assert tr2.bucket.early_launches == 1
+        old.close()
+        tr2.bucket.close()
+        assert not old._hooks and not tr2.bucket._hooks
+    torch.save({"params": snap, "early_launches": launches, "stale": stale},
                os.path.join(out_dir, f"{'e' if early else 's'}{rank}.pt"))
     destroy(ctx)
 
@@ -272,5 +285,6 @@ def test_early_nc_allreduce_matches_serial(tmp_path):
         e = torch.load(str(tmp_path / f"e{r}.pt"), weights_only=True)
         s = torch.load(str(tmp_path / f"s{r}.pt"), weights_only=True)
         assert e["early_launches"] == 2                            # one per step, from the hook
+        assert e["stale"] == 0                                     # the replaced bucket launched nothing
         for a, b in zip(e["params"], s["params"]):
             assert torch.equal(a, b)

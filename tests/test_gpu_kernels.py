@@ -68,7 +68,8 @@ def test_conv16v4_matches_v3_bitwise(epi, shape, monkeypatch, tune):
     V, I, J, K, L = shape
     x = torch.rand(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
     m = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
-    w = pack_w16(torch.randn(16, 16, 5, 5, 5, 5, device=DEV) * 0.05)
+    w_std = torch.randn(16, 16, 5, 5, 5, 5, device=DEV) * 0.05
+    w = pack_w16(w_std)
     b = torch.randn(16, device=DEV) * 0.1
     outs = []
     for v3 in ("0", "1"):
@@ -78,6 +79,17 @@ def test_conv16v4_matches_v3_bitwise(epi, shape, monkeypatch, tune):
         outs.append(y)
     assert torch.isfinite(outs[0].float()).all()
     assert torch.equal(outs[0], outs[1])
+    # and v4 itself against the fp64 oracle on the same bf16 operands: bias +
+    # ReLU (forward) or the ReLU mask of the previous activation (the data
+    # gradient's EPI_MASK epilogue)
+    z = ref.conv4d(x.double().permute(0, 5, 1, 2, 3, 4), ref.conv4d_weight_from_std(bf(w_std)), None)
+    if epi == 1:
+        want = torch.relu(z + b.double().view(1, 16, 1, 1, 1, 1))
+    else:
+        want = z * (m.double().permute(0, 5, 1, 2, 3, 4) > 0)
+    got = outs[0].permute(0, 5, 1, 2, 3, 4)
+    # the only difference is the final bf16 rounding of the stored output (2^-9)
+    assert relerr(got, want) < 4e-3, relerr(got, want)
 
 
 @pytest.mark.parametrize("ks,shape,cin,relu", [(5, (4, 25, 25, 25, 25), 16, 1), (5, (1, 6, 5, 26, 29), 16, 0),
@@ -618,6 +630,38 @@ def test_conv2d_nhwc_kernel(cin, cout, k, stride, pad, res, relu, shape):
     assert relerr(y, yr) < 1e-2
 
 
+@pytest.mark.parametrize("cin,cout,k,stride,pad,res,relu,shape,dt", [
+    (256, 256, 3, 1, 1, False, True, (4, 25, 25), torch.bfloat16),     # layer-3 3x3 at the training size
+    (1024, 256, 1, 1, 0, False, True, (3, 25, 25), torch.bfloat16),    # layer-3 reduce 1x1
+    (256, 1024, 1, 1, 0, True, True, (2, 25, 25), torch.bfloat16),     # layer-3 expand 1x1 + residual
+    (256, 256, 3, 2, 1, False, True, (2, 50, 50), torch.bfloat16),     # stride-2 3x3
+    (512, 1024, 1, 2, 0, False, False, (2, 50, 50), torch.bfloat16),   # stride-2 downsample
+    (128, 128, 3, 1, 1, True, True, (3, 23, 19), torch.bfloat16),      # Cout 128: the 128-column tile
+    (256, 256, 3, 1, 1, True, True, (3, 25, 25), torch.float16)])     # IEEE half operands
+def test_conv2d_nhwc_v3(cin, cout, k, stride, pad, res, relu, shape, dt, tune):
+    """conv2d_nhwc_v3 (one round of chip-sized workgroups: 16 TM x 64 TN tiles,
+    8 waves as 2 K-groups x 4 N-groups, LDS-DMA ring, K-group sum in the
+    epilogue) vs F.conv2d in fp64 on 16-bit inputs: ragged M, stride 2, residual."""
+    C = _ext.ext()
+    tune("conv2d_variant", "3")
+    torch.manual_seed(18)
+    cl = torch.channels_last
+    x = torch.randn(shape[0], cin, shape[1], shape[2], device=DEV).to(dt).contiguous(memory_format=cl)
+    w = (torch.randn(cout, cin, k, k, device=DEV) * 0.05).to(dt).contiguous(memory_format=cl)
+    b = torch.randn(cout, device=DEV)
+    yr = torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride, pad)
+    r = None
+    if res:
+        r = torch.randn(yr.shape, device=DEV).to(dt).contiguous(memory_format=cl)
+        yr = yr + r.double()
+    if relu:
+        yr = torch.relu(yr)
+    y = torch.full(yr.shape, float("nan"), dtype=dt, device=DEV).contiguous(memory_format=cl)
+    C.conv2d_nhwc(x, w, b, r, y, stride, pad, 1 if relu else 0)
+    assert torch.isfinite(y.float()).all()
+    assert relerr(y, yr) < 1e-2, relerr(y, yr)
+
+
 @pytest.mark.parametrize("ks,shape", [(5, (2, 6, 7, 25, 25)), (3, (1, 4, 9, 30, 27)), (5, (1, 3, 12, 9, 7))])
 def test_group_plane_conv_multitile_bitwise(ks, shape, monkeypatch, tune):
     """The multi-tile group-plane conv16v2 (NCNET_GP_TPW consecutive j-tiles per
@@ -925,6 +969,79 @@ def test_neigh_consensus_fast1x_matches_ij_path(monkeypatch, symmetric):
         ea, eb = rel_l2(a, r), rel_l2(b, r)
         assert ea < max(2 * eb, 2e-2), (n, ea, eb)
         assert rel_l2(a, b) < 5e-2, (n, rel_l2(a, b))
+
+
+def _fast1x_vs_quantized_oracle(symmetric, perturb=None, seed=31):
+    """The 5,5,5 / 16,16,1 stack at 25^4 on the padded-plane fast path vs the
+    quantized fp64 oracle (engine/quantized_oracle.py: bf16 rounding exactly at
+    the stored activations, weights and pre-activation gradients).  Returns
+    {name: rel L2 error}.  ``perturb``: a function applied to the first layer's
+    packed weights (a mutation the check must catch)."""
+    import importlib
+    from ncnet_amd.engine import quantized_oracle as qo
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    torch.manual_seed(seed)
+    V = 2
+    x = torch.rand(V, 1, 25, 25, 25, 25, device=DEV).to(torch.bfloat16).float()
+    ws, bs, cin = [], [], 1
+    for k, c in zip((5, 5, 5), (16, 16, 1)):
+        ws.append((torch.randn(k, c, cin, k, k, k, device=DEV) * 0.05).to(torch.bfloat16).float())
+        bs.append(0.2 + torch.rand(c, device=DEV) * 0.1)
+        cin = c
+    g = torch.randn(V, 1, 25, 25, 25, 25, device=DEV)
+    xx = x.clone().requires_grad_(True)
+    pw = [w.clone().requires_grad_(True) for w in ws]
+    pb = [b.clone().requires_grad_(True) for b in bs]
+    assert nc.fast1x_ok(["1in", "16", "1out"], [16, 16, 1], [5, 5, 5], xx, symmetric)
+    orig = nc.pack_w1x
+    if perturb is not None:
+        calls = []
+
+        def mutated(w_std):
+            p = orig(w_std)
+            if not calls:                 # the first layer's forward packing only
+                p = perturb(p)
+            calls.append(1)
+            return p
+        nc.pack_w1x = mutated
+    try:
+        y = nc.neigh_consensus(xx, pw, pb, [16, 16, 1], symmetric=symmetric)
+        (y * g).sum().backward()
+    finally:
+        nc.pack_w1x = orig
+    got = [y.detach(), xx.grad] + [p.grad for p in pw + pb]
+    xr = x.double().requires_grad_(True)
+    wr = [ref.conv4d_weight_to_std(w.double()).requires_grad_(True) for w in ws]
+    br = [b.double().requires_grad_(True) for b in bs]
+    yr = qo.neigh_consensus(xr, wr, br, symmetric=symmetric)
+    (yr * g.double()).sum().backward()
+    want = [yr, xr.grad] + [ref.conv4d_weight_from_std(p.grad) for p in wr] + [p.grad for p in br]
+    names = ["y", "gx", "gw0", "gw1", "gw2", "gb0", "gb1", "gb2"]
+    return {n: rel_l2(a, r) for n, a, r in zip(names, got, want)}
+
+
+@pytest.mark.parametrize("symmetric", [True, False])
+def test_fast1x_stack_vs_quantized_oracle(symmetric):
+    """Output and every gradient of the fast training stack (conv1x16,
+    conv16v4 forward / data gradient, wgrad16v4, wgrad1x16, the Cout=1 block
+    forward) within 1e-3 of the quantized fp64 oracle: what remains is fp32
+    accumulation order and the rare bf16 rounding-boundary flip."""
+    errs = _fast1x_vs_quantized_oracle(symmetric)
+    print("fast1x vs quantized oracle:", {k: f"{v:.1e}" for k, v in errs.items()})
+    assert max(errs.values()) < 1e-3, errs
+
+
+def test_fast1x_oracle_check_catches_one_tap():
+    """Mutation check of the test above: one (dk, dl) tap of one plane offset of
+    the first layer's conv1x16 weights, scaled by 1.5 in the packed operand the
+    kernel reads, must push the forward error far past the 1e-3 tolerance."""
+    def perturb(p):                       # p [k*k planes, 64 lanes, 8]
+        p = p.clone()
+        p[12, 0:16, 3] *= 1.5             # plane (2, 2), tap 3, all 16 output channels
+        return p
+    errs = _fast1x_vs_quantized_oracle(True, perturb=perturb)
+    print("mutated conv1x16 tap:", {k: f"{v:.1e}" for k, v in errs.items()})
+    assert errs["y"] > 1e-2, errs
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])

@@ -42,25 +42,27 @@ def test_x3_fused_matches_fp64(ks, ch, shape):
     from ncnet_amd.ops.neigh_consensus import neigh_consensus
     torch.manual_seed(7)
     ws, bs = _params(ks, ch, 11, masked=True)
-    x = torch.rand(shape, device="cuda")
+    # x requires grad: the input gradient (three split data-gradient convs and
+    # the symmetric fold gx[:V] + gx[V:]^T) runs with --fe_finetune_params
+    x = torch.rand(shape, device="cuda").requires_grad_(True)
     n0 = _ext.DISPATCH["nc_x3_fused"]
     y = neigh_consensus(x, ws, bs, list(ch), symmetric=True, precision="fp32")
     assert _ext.DISPATCH["nc_x3_fused"] == n0 + 1
     gy = torch.rand_like(y)
     (y * gy).sum().backward()
-    got = []
+    got = [x.grad.clone()]
     for w, b in zip(ws, bs):
         got += [w.grad.clone(), b.grad.clone()]
-    xr = x.double()
+    xr = x.detach().double().requires_grad_(True)
     wd = [w.detach().double().requires_grad_(True) for w in ws]
     bd = [b.detach().double().requires_grad_(True) for b in bs]
     yr = ref.neigh_consensus(xr, wd, bd, True)
     (yr * gy.double()).sum().backward()
-    want = []
+    want = [xr.grad]
     for w, b in zip(wd, bd):
         want += [w.grad, b.grad]
     errs = {"y": rl2(y, yr)}
-    errs.update({f"g{i}": rl2(a, b) for i, (a, b) in enumerate(zip(got, want))})
+    errs.update({("gx" if i == 0 else f"g{i - 1}"): rl2(a, b) for i, (a, b) in enumerate(zip(got, want))})
     print("x3 fused errors:", {k: f"{v:.1e}" for k, v in errs.items()})
     # bf16x3 keeps ~16 mantissa bits per operand: ~1e-5 relative, vs ~1e-2 for bf16
     assert max(errs.values()) < 2e-4, errs
@@ -119,7 +121,7 @@ def test_x3_fused_matches_per_conv_path():
     ks, ch = (5, 5, 5), (16, 16, 1)
     ws, bs = _params(ks, ch, 11)
     torch.manual_seed(7)
-    x = torch.rand(2, 1, 9, 7, 9, 7, device="cuda")
+    x = torch.rand(2, 1, 9, 7, 9, 7, device="cuda").requires_grad_(True)
     kinds = tuple(layer_kinds(list(ch), list(ks)))
     params = []
     for w, b in zip(ws, bs):
@@ -129,9 +131,10 @@ def test_x3_fused_matches_per_conv_path():
                lambda t: NeighConsensusX3Fn.apply(t, True, kinds, ch, *params)):
         for p in params:
             p.grad = None
+        x.grad = None
         y = fn(x)
         torch.manual_seed(8)
         (y * torch.randn_like(y)).sum().backward()
-        outs.append([y.detach()] + [p.grad.clone() for p in params])
+        outs.append([y.detach(), x.grad.clone()] + [p.grad.clone() for p in params])
     errs = [rl2(a, b) for a, b in zip(*outs)]
     assert max(errs) < 1e-4, errs
