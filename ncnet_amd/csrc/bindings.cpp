@@ -24,6 +24,10 @@ int ncnet_ijsum(const float*, const float*, float*, int, int, int, int, int, int
 int ncnet_bias_act(void*, const float*, long long, int, int, int, hipStream_t);
 int ncnet_maxpool_bias_act(const void*, void*, const float*, int, int, int, int, int, int, int, int, int, int, int,
                            hipStream_t);
+int ncnet_conv2d_nhwc_x3(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_stem_im2col_x3(const float*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_maxpool_x3(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_x3_to_f32(const void*, float*, long long, int, hipStream_t);
 int ncnet_conv2d_nhwc(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, void*, int, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
@@ -683,6 +687,63 @@ void conv2d_nhwc(Tensor X, Tensor W, Tensor bias, c10::optional<Tensor> R, Tenso
      "conv2d_nhwc");
 }
 
+// bf16x3 (fp32-accurate) trunk, csrc/conv2d.hip conv2d_nhwc_v3 X3 + csrc/epilogue.hip:
+// activations are contiguous [N, H, W, 2C] bf16 = [hi | lo] channel pairs.
+// W3 [Cout, KH, KW, 3 Cin] = [W_hi | W_hi | W_lo]; bias fp32 [Cout].
+void conv2d_nhwc_x3(Tensor X, Tensor W3, Tensor bias, c10::optional<Tensor> R, Tensor Y, int64_t stride, int64_t pad,
+                    int64_t relu) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(W3, "W3", at::kBFloat16); check(Y, "Y", at::kBFloat16);
+  check(bias, "bias", at::kFloat);
+  TORCH_CHECK(X.dim() == 4 && X.size(3) % 128 == 0, "conv2d_nhwc_x3: X must be [N,H,W,2 Cin], Cin % 64 == 0");
+  const int64_t N = X.size(0), H = X.size(1), Wd = X.size(2), Cin = X.size(3) / 2;
+  TORCH_CHECK(W3.dim() == 4 && W3.size(3) == 3 * Cin, "conv2d_nhwc_x3: W3 must be [Cout,KH,KW,3 Cin]");
+  const int64_t Cout = W3.size(0), KH = W3.size(1), KW = W3.size(2);
+  TORCH_CHECK(Cout % 64 == 0, "conv2d_nhwc_x3: Cout % 64");
+  check_shape(bias, "bias", {Cout});
+  const int64_t Ho = (H + 2 * pad - KH) / stride + 1, Wo = (Wd + 2 * pad - KW) / stride + 1;
+  check_shape(Y, "Y", {N, Ho, Wo, 2 * Cout});
+  if (R.has_value()) { check(*R, "R", at::kBFloat16); check_shape(*R, "R", {N, Ho, Wo, 2 * Cout}); }
+  TORCH_CHECK(N * Ho * Wo < (1LL << 31) && N * H * Wd * 2 * Cin < (1LL << 40), "conv2d_nhwc_x3: sizes exceed int32");
+  ok(ncnet_conv2d_nhwc_x3(X.data_ptr(), W3.data_ptr(), (const float*)bias.data_ptr(),
+                          R.has_value() ? R->data_ptr() : nullptr, Y.data_ptr(), N, H, Wd, Cin, Cout, KH, KW, stride,
+                          pad, relu ? 1 : 0, cur_stream(X)),
+     "conv2d_nhwc_x3");
+}
+
+// fp32 NHWC image (an [N,C,H,W] channels-last tensor) -> stem im2col pairs A [N*Ho*Wo, 2 KP].
+void stem_im2col_x3(Tensor X, Tensor A, int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  TORCH_CHECK(X.is_cuda() && X.scalar_type() == at::kFloat && X.dim() == 4 &&
+                  X.is_contiguous(at::MemoryFormat::ChannelsLast), "stem_im2col_x3: X must be fp32 channels-last");
+  check(A, "A", at::kBFloat16);
+  const int64_t N = X.size(0), C = X.size(1), H = X.size(2), W = X.size(3);
+  const int64_t Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(A.dim() == 2 && A.size(0) == N * Ho * Wo && A.size(1) % 16 == 0 && A.size(1) / 2 >= KH * KW * C,
+              "stem_im2col_x3: A must be [N*Ho*Wo, 2 KP], KP % 8 == 0, KP >= KH*KW*C");
+  ok(ncnet_stem_im2col_x3((const float*)X.data_ptr(), A.data_ptr(), N, H, W, C, KH, KW, stride, pad, Ho, Wo,
+                          A.size(1) / 2, cur_stream(X)),
+     "stem_im2col_x3");
+}
+
+void maxpool_x3(Tensor X, Tensor Y, int64_t k, int64_t stride, int64_t pad) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(Y, "Y", at::kBFloat16);
+  TORCH_CHECK(X.dim() == 4 && X.size(3) % 16 == 0, "maxpool_x3: X must be [N,H,W,2C], C % 8 == 0");
+  const int64_t N = X.size(0), H = X.size(1), W = X.size(2), C = X.size(3) / 2;
+  const int64_t Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  check_shape(Y, "Y", {N, Ho, Wo, 2 * C});
+  ok(ncnet_maxpool_x3(X.data_ptr(), Y.data_ptr(), N, H, W, C, Ho, Wo, k, stride, pad, cur_stream(X)), "maxpool_x3");
+}
+
+void x3_to_f32(Tensor X, Tensor Y) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(Y, "Y", at::kFloat);
+  const int64_t C = Y.size(-1);
+  TORCH_CHECK(X.size(-1) == 2 * C && X.numel() == 2 * Y.numel() && C % 8 == 0, "x3_to_f32: X [..., 2C] -> Y [..., C]");
+  ok(ncnet_x3_to_f32(X.data_ptr(), (float*)Y.data_ptr(), Y.numel() / C, C, cur_stream(X)), "x3_to_f32");
+}
+
 // Guarded flat Adam (csrc/optim.hip).  g may be longer than p (trailing
 // loss-indicator slot); count / skipped int32 [1], step fp32 [1].
 void nonfinite_count(Tensor g, Tensor count) {
@@ -744,6 +805,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pad_geom", &pad_geom);
   m.def("pad_planes", &pad_planes);
   m.def("conv1x16", &conv1x16);
+  m.def("conv2d_nhwc_x3", &conv2d_nhwc_x3);
+  m.def("stem_im2col_x3", &stem_im2col_x3);
+  m.def("maxpool_x3", &maxpool_x3);
+  m.def("x3_to_f32", &x3_to_f32);
   m.def("wgrad1x16", &wgrad1x16);
   m.def("conv16_blk_fwd", &conv16_blk_fwd);
   m.def("conv16_fwd_x3", &conv16_fwd_x3);

@@ -198,7 +198,7 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
       if (kk < NT) {
         const int dk = kk / KS, dl = kk - dk * KS;
         t = (dk - P) * LP + (dl - P);
-        c = (4 - (((t % 4) + 4) % 4)) & 3;
+        c = (4 - ((C::F0 + t) & 3)) & 3;        // re-aligns element F0 + t (+ 16 w + 4 p) to 8 bytes
       }
       rowoff[h] = (uint32_t)(C::XOFF + c * C::COPYB + (C::F0 + 16 * wave + t + c + C::delta(c) + 4 * p) * 2);
     }
@@ -375,7 +375,7 @@ struct W1X {
   static constexpr int XDMA2 = (QN * 2 - 1024) / 16;          // lanes of an X1 plane's second DMA
   static_assert(QN * 2 > 1024 && QN * 2 <= 2048, "two DMA wave-instructions per X1 plane");
   static_assert(L * 32 % 16 == 0 && L * 2 <= 64, "one DMA wave-instruction per D row");
-  static_assert(NT * 32 * 16 * 4 + 64 <= KS * NCOL * XS, "reduction scratch fits the X1 ring");
+  static_assert(NT * 32 * 16 * 4 + 64 <= LDS, "reduction scratch fits the staging buffers");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restric
 
   // lane constants: combo rows of the two groups, K group, transposed-read row/column
   const int kg = lane >> 4, li = lane & 15;
-  const int c0 = li, c1 = (16 + li < NT) ? 16 + li : 16;      // rows >= NT repeat combo 16 (broadcast)
+  const int c0 = (li < NT) ? li : 0, c1 = (16 + li < NT) ? 16 + li : (NT > 16 ? 16 : 0);   // rows >= NT repeat a valid combo
   const int di0 = c0 / KS, dj0 = c0 - di0 * KS, di1 = c1 / KS, dj1 = c1 - di1 * KS;
   const uint32_t gl = (uint32_t)((C::GM + 4 * kg + (li >> 2)) * 32 + 8 * (li & 3) + cq * 1024 - 32 * C::GM);
 
@@ -460,8 +460,10 @@ __global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restric
       constexpr int u = decltype(uc)::value;
       constexpr int chunk = CQ + 4 * u;
       if constexpr (chunk < C::NQC) {
+        constexpr bool TWO = NT > 16;     // a second 16-combo row group (KS 5: 25 combos; KS 3: 9)
         const u32x4 A0 = cat4u(*(const u32x2*)(smem + xa0 + 256 * u), *(const u32x2*)(smem + xa0 + 256 * u + 32));
-        const u32x4 A1 = cat4u(*(const u32x2*)(smem + xa1 + 256 * u), *(const u32x2*)(smem + xa1 + 256 * u + 32));
+        u32x4 A1 = A0;
+        if constexpr (TWO) A1 = cat4u(*(const u32x2*)(smem + xa1 + 256 * u), *(const u32x2*)(smem + xa1 + 256 * u + 32));
         xstatic_for<0, C::NTW>([&](auto tc) {
           constexpr int tt = decltype(tc)::value;
           constexpr int tap = C::NTW * TH + tt;
@@ -470,7 +472,7 @@ __global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restric
             constexpr uint32_t off = 4096u * u + 32u * (C::GM - s);
             const u32x4 B = cat4u(lds_read_tr16u(smem, ga + off), lds_read_tr16u(smem, ga + off + 512));
             acc[tt][0] = mfma16u(A0, B, acc[tt][0]);
-            acc[tt][1] = mfma16u(A1, B, acc[tt][1]);
+            if constexpr (TWO) acc[tt][1] = mfma16u(A1, B, acc[tt][1]);
             if constexpr (BIAS && TH == 0 && tt == 0) accb = mfma16u(ones, B, accb);
           }
         });
@@ -480,7 +482,7 @@ __global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restric
 
   // the whole persistent loop per wave specialisation (one dispatch, so each
   // body's register allocation is its own)
-  float* red = (float*)(smem + C::XOFF);                      // [NT][32][16] + bias [16]
+  float* red = (float*)smem;                                  // [NT][32][16] + bias [16], over the drained buffers
   auto run = [&](auto thc, auto cqc) {
     constexpr int TH = decltype(thc)::value;
     for (int t = t0; t < t1; ++t) {
@@ -573,44 +575,68 @@ extern "C" int ncnet_pad_planes(const void* x, int x_is_bf16, void* y, int V, in
   return (int)hipGetLastError();
 }
 
-// conv1x16 at the training plane (K = L = 25, KS = 5): returns -1 when the
-// shape has no instantiation (the caller keeps the ij-packed path).
-extern "C" int ncnet_conv1x16(const void* Xp, const void* Wa, const float* bias, const void* M, void* Y, int V, int I,
-                              int J, int K, int L, int KS, int epi, int nt_store, hipStream_t s) {
-  if (!(KS == 5 && K == 25 && L == 25)) return -1;
-  if (epi != EPI1X_BIAS_RELU && epi != EPI1X_MASK) return -3;
-  constexpr int R = 5;
-  using C = C1X<5, 25, 25>;
+// conv1x16 / wgrad1x16 are instantiated for the training planes whose padded
+// geometry fits their two-DMA-per-copy staging: KS 5 at 25 x 25 (400 px) and
+// 20 x 20 (320 px), KS 3 at 25 x 25 (the IVD recipe, NC 3,3 / 16,1).  Mirrored
+// in ops/neigh_consensus.py FAST1X_SHAPES.
+static int c1x_num_cus() {
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
     hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
+  return ncu;
+}
+
+template <int KS, int K, int L>
+static void c1x_launch(int epi, int V, int I, int J, const bf16* x, const u32x4* w, const float* bias, const bf16* m,
+                       bf16* y, int nt_store, hipStream_t s) {
+  constexpr int R = 5;
+  using C = C1X<KS, K, L>;
   const int nitems = V * I * cdiv(J, R);
-  dim3 grid((unsigned)std::min(nitems, ncu)), block(512);   // persistent: one workgroup per CU
-  const bf16* x = (const bf16*)Xp; const u32x4* w = (const u32x4*)Wa; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
+  dim3 grid((unsigned)std::min(nitems, c1x_num_cus())), block(512);   // persistent: one workgroup per CU
+  const size_t lds = (size_t)C::lds(R + KS - 1, 1);
   if (epi == EPI1X_BIAS_RELU)
-    hipLaunchKernelGGL((conv1x16_kernel<5, R, EPI1X_BIAS_RELU, 25, 25>), grid, block, (size_t)C::lds(R + 4, 1), s, x, w, bias, m, y, V, I, J, nt_store);
+    hipLaunchKernelGGL((conv1x16_kernel<KS, R, EPI1X_BIAS_RELU, K, L>), grid, block, lds, s, x, w, bias, m, y, V, I, J, nt_store);
   else
-    hipLaunchKernelGGL((conv1x16_kernel<5, R, EPI1X_MASK, 25, 25>), grid, block, (size_t)C::lds(R + 4, 1), s, x, w, bias, m, y, V, I, J, nt_store);
+    hipLaunchKernelGGL((conv1x16_kernel<KS, R, EPI1X_MASK, K, L>), grid, block, lds, s, x, w, bias, m, y, V, I, J, nt_store);
+}
+
+// returns -1 when the shape has no instantiation
+extern "C" int ncnet_conv1x16(const void* Xp, const void* Wa, const float* bias, const void* M, void* Y, int V, int I,
+                              int J, int K, int L, int KS, int epi, int nt_store, hipStream_t s) {
+  if (epi != EPI1X_BIAS_RELU && epi != EPI1X_MASK) return -3;
+  const bf16* x = (const bf16*)Xp; const u32x4* w = (const u32x4*)Wa; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
+  if (KS == 5 && K == 25 && L == 25) c1x_launch<5, 25, 25>(epi, V, I, J, x, w, bias, m, y, nt_store, s);
+  else if (KS == 5 && K == 20 && L == 20) c1x_launch<5, 20, 20>(epi, V, I, J, x, w, bias, m, y, nt_store, s);
+  else if (KS == 3 && K == 25 && L == 25) c1x_launch<3, 25, 25>(epi, V, I, J, x, w, bias, m, y, nt_store, s);
+  else return -1;
   return (int)hipGetLastError();
 }
 
-// wgrad1x16 at the training plane (K = L = 25, KS = 5): D bf16 [V,I,J,K,L,16],
-// X1 padded planes [V*I*J][PPL]; part fp32 [G][KS*KS taps][32 combos][16] (one
-// partial per workgroup, G <= the CU count), partb fp32 [G][16] (sum of D; null: none).  Returns -1 for shapes without an instantiation.
-extern "C" int ncnet_wgrad1x16(const void* Dp, const void* X1p, float* part, float* partb, int G, int V, int I, int J,
-                               int K, int L, int KS, hipStream_t s) {
-  if (!(KS == 5 && K == 25 && L == 25)) return -1;
-  using C = W1X<5, 25, 25>;
-  if (G < 1) return -2;
-  const bf16* d = (const bf16*)Dp; const bf16* x = (const bf16*)X1p;
+template <int KS, int K, int L>
+static void w1x_launch(int G, int V, int I, int J, const bf16* d, const bf16* x, float* part, float* partb,
+                       hipStream_t s) {
+  using C = W1X<KS, K, L>;
   if (partb)
-    hipLaunchKernelGGL((wgrad1x16_kernel<5, 25, 25, true>), dim3((unsigned)G), dim3(512), (size_t)C::LDS, s, d, x, part,
+    hipLaunchKernelGGL((wgrad1x16_kernel<KS, K, L, true>), dim3((unsigned)G), dim3(512), (size_t)C::LDS, s, d, x, part,
                        partb, V, I, J);
   else
-    hipLaunchKernelGGL((wgrad1x16_kernel<5, 25, 25, false>), dim3((unsigned)G), dim3(512), (size_t)C::LDS, s, d, x,
+    hipLaunchKernelGGL((wgrad1x16_kernel<KS, K, L, false>), dim3((unsigned)G), dim3(512), (size_t)C::LDS, s, d, x,
                        part, partb, V, I, J);
+}
+
+// wgrad1x16: D bf16 [V,I,J,K,L,16], X1 padded planes [V*I*J][PPL]; part fp32
+// [G][KS*KS taps][32 combos][16] (one partial per workgroup, G <= the CU count),
+// partb fp32 [G][16] (sum of D; null: none).  Returns -1 for shapes without an instantiation.
+extern "C" int ncnet_wgrad1x16(const void* Dp, const void* X1p, float* part, float* partb, int G, int V, int I, int J,
+                               int K, int L, int KS, hipStream_t s) {
+  if (G < 1) return -2;
+  const bf16* d = (const bf16*)Dp; const bf16* x = (const bf16*)X1p;
+  if (KS == 5 && K == 25 && L == 25) w1x_launch<5, 25, 25>(G, V, I, J, d, x, part, partb, s);
+  else if (KS == 5 && K == 20 && L == 20) w1x_launch<5, 20, 20>(G, V, I, J, d, x, part, partb, s);
+  else if (KS == 3 && K == 25 && L == 25) w1x_launch<3, 25, 25>(G, V, I, J, d, x, part, partb, s);
+  else return -1;
   return (int)hipGetLastError();
 }

@@ -30,6 +30,9 @@ struct Conv2dArgs {
   const bf16* X; const bf16* W; const float* bias; const bf16* R; bf16* Y;
   int N, H, Wd, Cin, Cout, KH, KW, stride, pad, Ho, Wo;
   int M, tiles_m, tiles_n, relu;
+  // conv2d_nhwc_v3 only: X pixel stride Cx and GEMM channels per tap Ck (Cin,
+  // Cin for a plain conv; 2 Cin, 3 Cin for the bf16x3 split, see below)
+  int Cx, Ck;
 };
 
 // Epilogue shared by both kernels, staged through LDS so the global writes
@@ -377,7 +380,13 @@ __device__ __forceinline__ void c3_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int TM, int TN, bool F16 = false>
+// X3 (fp32-accurate "bf16x3" trunk, FrozenResNetPlan dtype float32): X, R, Y
+// hold [hi | lo] bf16 channel pairs (Cx = 2 Cin), the GEMM runs Ck = 3 Cin
+// channels per tap, channel c >= 2 Cin reading X channel c - 2 Cin (hi again),
+// against W = [W_hi | W_hi | W_lo]: acc = X_hi W_hi + X_lo W_hi + X_hi W_lo
+// (fp32 to ~2^-16 relative); the epilogue adds bias and the hi + lo residual
+// in fp32 and writes the output split again.
+template <int TM, int TN, bool F16 = false, bool X3 = false>
 __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
   using namespace cv3;
   using G = Geo<TM, TN>;
@@ -389,7 +398,7 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
   uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tn = bid % p.tiles_n, tm = bid / p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int K = p.KH * p.KW * p.Cin;
+  const int K = p.KH * p.KW * p.Ck;
 
   // this lane's row of each of the wave's PER DMA instructions (instruction
   // j = wave + 8 m: A rows 8 j .. 8 j + 7, then B rows, then trash)
@@ -426,12 +435,13 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
       dst[m] = (uint32_t)G::TRASH;
     }
   }
-  const int cpt = p.Cin / 64;
+  const int cpt = p.Ck / 64;
   const int nk = p.KH * p.KW * cpt;
   const bf16* zero = (const bf16*)&g_zero16;
 
   auto issue = [&](int ks, int buf) {
     const int tap = ks / cpt, c0 = (ks - tap * cpt) * 64;
+    const int cs = c0 >= p.Cx ? c0 - p.Cx : c0;      // X3: the W_lo third reads X_hi again
     const int dh = tap / p.KW, dw = tap - dh * p.KW;
     char* sb = smem + buf * G::STAGE;
 #pragma unroll
@@ -441,11 +451,11 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
       if (kind[m] == 0) {
         const int hi = a_hi0[m] + dh, wi = a_wi0[m] + dw;
         const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.Wd;
-        const bf16* a = p.X + ((size_t)a_pix[m] + (size_t)(ok ? hi : 0) * p.Wd + (ok ? wi : 0)) * p.Cin + c0 + coff[m];
+        const bf16* a = p.X + ((size_t)a_pix[m] + (size_t)(ok ? hi : 0) * p.Wd + (ok ? wi : 0)) * p.Cx + cs + coff[m];
         src = ok ? a : zero;
         d += buf * G::STAGE;
       } else if (kind[m] == 1) {
-        src = b_src[m] + tap * p.Cin + c0;
+        src = b_src[m] + tap * p.Ck + c0;
         d += buf * G::STAGE;
       }
       dma16_lds(src, smem + d);
@@ -486,6 +496,7 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
   __syncthreads();   // every fragment read done (and every DMA landed: the last wait was vmcnt(0))
 
   // K-group sum through LDS, then bias -> 16-bit staging tile [BM][BN]
+  // (X3: the fp32 sum tile itself is the staging tile)
   float* P = (float*)smem;
   uint16_t* S = (uint16_t*)(smem + BM * G::PSTR * 4);
   if (kg == 1) {
@@ -507,7 +518,9 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = i * 16 + 4 * fq + r;
-          S[row * BN + col] = f2s16<F16>(acc[i][j][r] + P[row * G::PSTR + col] + b);
+          const float v = acc[i][j][r] + P[row * G::PSTR + col] + b;
+          if constexpr (X3) P[row * G::PSTR + col] = v;
+          else S[row * BN + col] = f2s16<F16>(v);
         }
     }
   }
@@ -518,7 +531,37 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
   for (int c = threadIdx.x; c < BM * CPR; c += 512) {
     const int row = c / CPR, cc = c - row * CPR;
     const int pix = m0 + row;
-    if (pix < p.M) {
+    if (pix >= p.M) continue;
+    if constexpr (X3) {
+      // 8 channels: fp32 sum (+ residual hi + lo), ReLU, split into hi / lo
+      const f32x4 v0 = *(const f32x4*)(P + row * G::PSTR + cc * 8);
+      const f32x4 v1 = *(const f32x4*)(P + row * G::PSTR + cc * 8 + 4);
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const size_t o = (size_t)pix * (2 * p.Cout) + n0 + cc * 8;
+      if (R) {
+        const u32x4 rh = *(const u32x4*)(R + o), rl = *(const u32x4*)(R + o + p.Cout);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[e] += s162f<false>((uint16_t)(rh[e >> 1] >> (16 * (e & 1)))) +
+                  s162f<false>((uint16_t)(rl[e >> 1] >> (16 * (e & 1))));
+      }
+      u32x4 oh, ol;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        uint32_t wh = 0, wl = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float x = v[2 * e + h];
+          if (p.relu) x = fmaxf(x, 0.f);
+          const uint16_t hb = f2s16<false>(x);
+          wh |= (uint32_t)hb << (16 * h);
+          wl |= (uint32_t)f2s16<false>(x - s162f<false>(hb)) << (16 * h);
+        }
+        oh[e] = wh; ol[e] = wl;
+      }
+      *(u32x4*)(Y + o) = oh;
+      *(u32x4*)(Y + o + p.Cout) = ol;
+    } else {
       const u32x4 tv = *(const u32x4*)(S + row * BN + cc * 8);
       const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
       u32x4 rv = {0u, 0u, 0u, 0u};
@@ -554,18 +597,35 @@ static int c3_num_cus() {
   return cache[dev];
 }
 
+static int c3_pick_tm(int M, int Cout, int Cin, int TN, int ncu, long long* cost);
+static int c3_num_cus();
+// mode 0: bf16, 1: IEEE half, 2: bf16x3
 template <int TM, int TN>
-static void c3_launch1(bool f16, dim3 g, dim3 b, hipStream_t stream, const Conv2dArgs& p) {
+static void c3_launch1(int mode, dim3 g, dim3 b, hipStream_t stream, const Conv2dArgs& p) {
   const size_t lds = (size_t)cv3::Geo<TM, TN>::LDS;
-  if (f16) hipLaunchKernelGGL((conv2d_nhwc_v3_kernel<TM, TN, true>), g, b, lds, stream, p);
-  else hipLaunchKernelGGL((conv2d_nhwc_v3_kernel<TM, TN, false>), g, b, lds, stream, p);
+  if (mode == 1) hipLaunchKernelGGL((conv2d_nhwc_v3_kernel<TM, TN, true, false>), g, b, lds, stream, p);
+  else if (mode == 2) hipLaunchKernelGGL((conv2d_nhwc_v3_kernel<TM, TN, false, true>), g, b, lds, stream, p);
+  else hipLaunchKernelGGL((conv2d_nhwc_v3_kernel<TM, TN, false, false>), g, b, lds, stream, p);
 }
 template <int TN>
-static void c3_launch(int tm, bool f16, dim3 g, dim3 b, hipStream_t stream, const Conv2dArgs& p) {
-  if (tm == 3) c3_launch1<3, TN>(f16, g, b, stream, p);
-  else if (tm == 4) c3_launch1<4, TN>(f16, g, b, stream, p);
-  else if (tm == 5) c3_launch1<5, TN>(f16, g, b, stream, p);
-  else c3_launch1<6, TN>(f16, g, b, stream, p);
+static void c3_launch(int tm, int mode, dim3 g, dim3 b, hipStream_t stream, const Conv2dArgs& p) {
+  if (tm == 3) c3_launch1<3, TN>(mode, g, b, stream, p);
+  else if (tm == 4) c3_launch1<4, TN>(mode, g, b, stream, p);
+  else if (tm == 5) c3_launch1<5, TN>(mode, g, b, stream, p);
+  else c3_launch1<6, TN>(mode, g, b, stream, p);
+}
+// launch v3 with its tile choice; false when it does not apply
+static bool c3_run(Conv2dArgs& p, int mode, hipStream_t stream) {
+  const int TNv = (p.Cout % 256 == 0) ? 4 : (p.Cout % 128 == 0) ? 2 : 1;
+  const int tm = c3_pick_tm(p.M, p.Cout, p.Ck, TNv, c3_num_cus(), nullptr);
+  if (!tm || p.Cx % 64) return false;
+  p.tiles_n = p.Cout / (64 * TNv);
+  p.tiles_m = cdiv(p.M, 16 * tm);
+  dim3 g3((unsigned)(p.tiles_m * p.tiles_n)), b3(512);
+  if (TNv == 4) c3_launch<4>(tm, mode, g3, b3, stream, p);
+  else if (TNv == 2) c3_launch<2>(tm, mode, g3, b3, stream, p);
+  else c3_launch<1>(tm, mode, g3, b3, stream, p);
+  return true;
 }
 
 // v3 tile rows: BM = 16 TM minimising (rounds of one workgroup per CU) x BM,
@@ -577,9 +637,8 @@ static int c3_pick_tm(int M, int Cout, int Cin, int TN, int ncu, long long* cost
   int best = 0;
   long long bc = 0;
   for (int tm = 3; tm <= 6; ++tm) {
-    if (TN == 4 && 16 * tm * (64 * TN + 4) * 4 + 16 * tm * 64 * TN * 2 > 160 * 1024) continue;
     const long long tiles = (long long)cdiv(M, 16 * tm) * tn;
-    const long long c = cdiv((int)((tiles + 0) > 0x7fffffff ? 0x7fffffff : tiles), ncu) * (long long)(16 * tm);
+    const long long c = ((tiles + ncu - 1) / ncu) * (long long)(16 * tm);
     if (!best || c < bc || (c == bc && tm > best)) { best = tm; bc = c; }
   }
   if (cost) *cost = bc;
@@ -602,6 +661,7 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
   p.Wo = (Wd + 2 * pad - KW) / stride + 1;
   p.M = N * p.Ho * p.Wo;
   p.relu = relu;
+  p.Cx = Cin; p.Ck = Cin;
   const int BN = (Cout % 128 == 0) ? 128 : 64;
   p.tiles_n = Cout / BN;
   // 128-row tiles unless that leaves fewer than two workgroups per CU
@@ -615,21 +675,15 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
   // NCNET_CONV2D_VARIANT=1 / 2 forces v1 / the DMA ring (with 128-row tiles
   // unless NCNET_CONV2D_BIG is set or the grid is large).
   const int variant = tuning().conv2d_variant;
-  if (variant == 3) {
-    // one round of workgroups sized to the chip (conv2d_nhwc_v3)
-    const int TNv = (Cout % 256 == 0) ? 4 : 2;
-    const int tm = c3_pick_tm(p.M, Cout, Cin, TNv, c3_num_cus(), nullptr);
-    if (tm) {
-      p.tiles_n = Cout / (64 * TNv);
-      p.tiles_m = cdiv(p.M, 16 * tm);
-      dim3 g3((unsigned)(p.tiles_m * p.tiles_n)), b3(512);
-      if (TNv == 4) c3_launch<4>(tm, f16, g3, b3, stream, p);
-      else c3_launch<2>(tm, f16, g3, b3, stream, p);
-      return (int)hipGetLastError();
-    }
-  }
+  // v3 (one round of chip-sized tiles) where measured faster (scripts/conv_bench.py,
+  // profiles/r4/trunk): the N <= 256 convs with a deep K (layer-3 3x3 convs
+  // at the training size: 48.7 -> 37.7 us, their reduce 1x1: 27.0 -> 21.9 us)
   const int t256 = cdiv(p.M, 256) * p.tiles_n;
   const bool big = BN == 128 && (variant == 0 ? t256 >= 384 : (t256 >= 512 || (t256 >= 256 && tuning().conv2d_big)));
+  // (grids big enough for the 256 x 128 DMA-ring tile keep it: InLoc 3200 px
+  // layer 3, 467 us v2 vs 707 us v3)
+  const bool v3_auto = variant == 0 && !big && Cout <= 256 && KH * KW * Cin >= 1024;
+  if ((variant == 3 || v3_auto) && c3_run(p, f16 ? 1 : 0, stream)) return (int)hipGetLastError();
   if (big && variant != 1) {
     p.tiles_m = cdiv(p.M, 256);
     dim3 g2((unsigned)(p.tiles_m * p.tiles_n)), b2(512);
@@ -654,3 +708,22 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
 #undef LC2
   return (int)hipGetLastError();
 }
+
+// bf16x3 (fp32-accurate) conv: X [N,H,W,2 Cin] = [hi | lo] bf16 pairs, W [Cout][KH][KW][3 Cin]
+// = [W_hi | W_hi | W_lo], R / Y [.., 2 Cout] pairs, bias fp32 (conv2d_nhwc_v3 X3).
+extern "C" int ncnet_conv2d_nhwc_x3(const void* X, const void* W, const float* bias, const void* R, void* Y, int N,
+                                    int H, int Wd, int Cin, int Cout, int KH, int KW, int stride, int pad, int relu,
+                                    hipStream_t stream) {
+  if (Cin % 64 || Cout % 64 || stride < 1) return -1;
+  Conv2dArgs p;
+  p.X = (const bf16*)X; p.W = (const bf16*)W; p.bias = bias; p.R = (const bf16*)R; p.Y = (bf16*)Y;
+  p.N = N; p.H = H; p.Wd = Wd; p.Cin = Cin; p.Cout = Cout; p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad;
+  p.Ho = (H + 2 * pad - KH) / stride + 1;
+  p.Wo = (Wd + 2 * pad - KW) / stride + 1;
+  p.M = N * p.Ho * p.Wo;
+  p.relu = relu;
+  p.Cx = 2 * Cin; p.Ck = 3 * Cin;
+  if (!c3_run(p, 2, stream)) return -1;
+  return (int)hipGetLastError();
+}
+

@@ -716,7 +716,11 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
 #pragma unroll
     for (int m = 0; m < RPW; ++m) {
       const uint32_t d = xld[m] == (uint32_t)TRASH ? (uint32_t)TRASH : xld[m] + boff;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + d), 16, xvo[m], 0, 0, 0);
+      // a row instruction covers 32 voxels: with RS < 32 (planes narrower than
+      // 25) the lanes past the row stride would overwrite the next row's first
+      // voxels, so they stay off (the instruction, and the vmcnt count, remain)
+      if (RS >= 32 || (lane >> 1) < RS)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, LDS_PTR(void, smem + d), 16, xvo[m], 0, 0, 0);
     }
   };
   // weight slot dj <- (di, dj) fragments of step dv; WPW DMAs per wave, always
@@ -1026,6 +1030,39 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
 
 using namespace ncnet;
 
+// conv16v4 at the compile-time whole-plane tiles it is instantiated for: the
+// --image_size 240 / 320 / 400 training planes (15, 20, 25) at KS 5 and KS 3.
+template <int KS, int T>
+static void v4_launch1(int epi, dim3 grid, dim3 block, hipStream_t stream, const bf16* x, const u32x4* w,
+                       const float* bias, const bf16* m, bf16* y, const ConvGeom& g) {
+  constexpr int R = 5, NQ = (KS * KS + 1) / 2;
+  const size_t lds = 3 * (size_t)(T + KS - 1) * (T + ((KS - 1 + 7) / 8) * 8) * 32 + (size_t)KS * NQ * 1024 + 1024;
+#define L16V4(EPIV) hipLaunchKernelGGL((conv16v4_fwd_kernel<KS, R, EPIV, T, T>), grid, block, lds, stream, x, w, bias, m, y, g)
+  if (epi == EPI_BIAS_RELU) L16V4(EPI_BIAS_RELU);
+  else if (epi == EPI_MASK) L16V4(EPI_MASK);
+  else if (epi == (EPI_BIAS_RELU | EPI_X3)) L16V4(EPI_BIAS_RELU | EPI_X3);
+  else L16V4(EPI_MASK | EPI_X3);
+#undef L16V4
+}
+static bool v4_launch(int KS, int K, int epi, dim3 grid, dim3 block, hipStream_t stream, const bf16* x,
+                      const u32x4* w, const float* bias, const bf16* m, bf16* y, const ConvGeom& g) {
+  if (KS == 5) {
+    if (K == 25) v4_launch1<5, 25>(epi, grid, block, stream, x, w, bias, m, y, g);
+    else if (K == 20) v4_launch1<5, 20>(epi, grid, block, stream, x, w, bias, m, y, g);
+    else if (K == 15) v4_launch1<5, 15>(epi, grid, block, stream, x, w, bias, m, y, g);
+    else return false;
+    return true;
+  }
+  if (KS == 3) {
+    if (K == 25) v4_launch1<3, 25>(epi, grid, block, stream, x, w, bias, m, y, g);
+    else if (K == 20) v4_launch1<3, 20>(epi, grid, block, stream, x, w, bias, m, y, g);
+    else if (K == 15) v4_launch1<3, 15>(epi, grid, block, stream, x, w, bias, m, y, g);
+    else return false;
+    return true;
+  }
+  return false;
+}
+
 // Tile choice: the whole (k,l) plane when it fits (<= 25 x 25 output), else
 // 25 x 25 tiles (InLoc-size planes).
 static void pick_tile(int K, int L, int& tk, int& tl) {
@@ -1077,17 +1114,8 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
     const int njb1 = g.njb;
     g.njb = cdiv(J, R);
     dim3 grid3((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block3(512);
-    if (tk == 25 && tl == 25 && KS == 5 && !tuning().conv_v3) {
-      // compile-time 25 x 25 tile: pipelined fragments, triple-buffered planes
-      size_t lds4 = 3 * (size_t)(25 + 4) * 33 * 32 + (size_t)5 * nq * 1024 + 1024;
-#define L16V4(EPIV) hipLaunchKernelGGL((conv16v4_fwd_kernel<5, R, EPIV, 25, 25>), grid3, block3, lds4, stream, x, w, bias, m, y, g)
-      if (epi == EPI_BIAS_RELU) L16V4(EPI_BIAS_RELU);
-      else if (epi == EPI_MASK) L16V4(EPI_MASK);
-      else if (epi == (EPI_BIAS_RELU | EPI_X3)) L16V4(EPI_BIAS_RELU | EPI_X3);
-      else L16V4(EPI_MASK | EPI_X3);
-#undef L16V4
+    if (tk == K && tl == L && !tuning().conv_v3 && v4_launch(KS, K, epi, grid3, block3, stream, x, w, bias, m, y, g))
       return (int)hipGetLastError();
-    }
     g.njb = njb1;
     if (x3) goto v2_x3;   // other shapes: the v2 kernel's phases
     g.njb = cdiv(J, R);

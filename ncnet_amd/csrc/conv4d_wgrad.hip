@@ -602,7 +602,8 @@ __device__ __forceinline__ void wgrad16v4_body(const bf16* __restrict__ X, const
 #pragma unroll
     for (int m = 0; m < RPW; ++m) {
       const int r = wave + NW * m;
-      bdma16_lds(rs, xvo[m], r < PR ? xb + (uint32_t)(r * RS * 32) : lds0 + C::TRASH);
+      // lanes past a row stride RS < 32 would overwrite the next row: off (count unchanged)
+      if (RS >= 32 || (lane >> 1) < RS) bdma16_lds(rs, xvo[m], r < PR ? xb + (uint32_t)(r * RS * 32) : lds0 + C::TRASH);
     }
     ++xl_n;
     if (++xl_ii == g.I) {
@@ -985,6 +986,25 @@ extern "C" int ncnet_wgrad16p(const void* X, const void* G, float* part, float* 
   return (int)hipGetLastError();
 }
 
+template <int KS, int T>
+static void w4_launch1(dim3 grid, dim3 block, hipStream_t stream, const bf16* x, const bf16* gg, float* part,
+                       float* partb, const W3Geom& g) {
+  using C = W4C<KS, T, T>;
+  const size_t lds = (size_t)C::LDS;
+  hipLaunchKernelGGL((wgrad16v4_kernel<KS, T, T>), grid, block, lds, stream, x, gg, part, partb, g);
+}
+static bool w4_launch(int KS, int K, dim3 grid, dim3 block, hipStream_t stream, const bf16* x, const bf16* gg,
+                      float* part, float* partb, const W3Geom& g) {
+  if (KS == 5 && K == 25) w4_launch1<5, 25>(grid, block, stream, x, gg, part, partb, g);
+  else if (KS == 5 && K == 20) w4_launch1<5, 20>(grid, block, stream, x, gg, part, partb, g);
+  else if (KS == 5 && K == 15) w4_launch1<5, 15>(grid, block, stream, x, gg, part, partb, g);
+  else if (KS == 3 && K == 25) w4_launch1<3, 25>(grid, block, stream, x, gg, part, partb, g);
+  else if (KS == 3 && K == 20) w4_launch1<3, 20>(grid, block, stream, x, gg, part, partb, g);
+  else if (KS == 3 && K == 15) w4_launch1<3, 15>(grid, block, stream, x, gg, part, partb, g);
+  else return false;
+  return true;
+}
+
 // v3: ngroups column groups per dj (grid = ngroups * KS).
 // Tile rule (mirrored in ops/neigh_consensus.py wgrad_v3_groups):
 // ntl = ceil(K*L / 320), VT = roundup(ceil(K*L / ntl), 64).
@@ -1003,14 +1023,22 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
   g.flags = tuning().wgrad_flags;
   if (g.RW > 32) return -1;                 // one wave-instruction per staged row
   if (g.VT > 384) return -1;                // <= 6 chunks per half
-  {
-    if (KS == 5 && K == 25 && L == 25 && !tuning().wgrad_v3) {
-      using C = W4C<5, 25, 25>;
-      dim3 grid((unsigned)(KS * ngroups)), block(512);
-      hipLaunchKernelGGL((wgrad16v4_kernel<5, 25, 25>), grid, block, (size_t)C::LDS, stream, (const bf16*)X,
-                         (const bf16*)G, part, partb, g);
-      return (int)hipGetLastError();
+  if (K == L && !tuning().wgrad_v3 && w4_launch(KS, K, dim3((unsigned)(KS * ngroups)), dim3(512), stream,
+                                                 (const bf16*)X, (const bf16*)G, part, partb, g))
+    return (int)hipGetLastError();   // compile-time planes of the training sizes (--image_size 240 / 320 / 400)
+  // wgrad16v3<5, NCH> spills at NCH 3, 4, 6 (256 VGPRs of accumulators and
+  // double-buffered fragments): split the plane into more, smaller tiles until
+  // the chunk count is 1, 2 or 5 (mirrored in ops/neigh_consensus.py wgrad_v3_ntl)
+  if (KS == 5) {
+    while (true) {
+      const int nch = ((cdiv(KL, g.ntl) + 63) / 64);
+      if (nch == 1 || nch == 2 || nch == 5) break;
+      ++g.ntl;
     }
+    g.VT = ((cdiv(KL, g.ntl) + 63) / 64) * 64;
+    g.PR = (g.VT - 1) / L + 2 + KS - 1;
+    g.ncols = V * J * g.ntl;
+    g.cpg = cdiv(g.ncols, ngroups);
   }
   size_t lds = 2 * (size_t)g.PR * g.RS * 32 + (size_t)(KS + 2) * g.VT * 32;
   if (lds > 160 * 1024) return -1;
@@ -1020,8 +1048,10 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
 #define W3N(KSV, N) hipLaunchKernelGGL((wgrad16v3_kernel<KSV, N>), grid, block, lds, stream, x, gg, part, partb, g)
 #define W3(KSV) do { switch (nch) { case 1: W3N(KSV, 1); break; case 2: W3N(KSV, 2); break; case 3: W3N(KSV, 3); break; \
                                     case 4: W3N(KSV, 4); break; case 5: W3N(KSV, 5); break; default: W3N(KSV, 6); } } while (0)
-  if (KS == 5) W3(5);
-  else if (KS == 3) W3(3);
+  if (KS == 5) {
+    // only the spill-free chunk counts are instantiated (the tile rule above)
+    switch (nch) { case 1: W3N(5, 1); break; case 2: W3N(5, 2); break; case 5: W3N(5, 5); break; default: return -3; }
+  } else if (KS == 3) W3(3);
   else return -2;
 #undef W3
 #undef W3N

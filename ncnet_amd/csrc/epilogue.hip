@@ -87,6 +87,122 @@ __global__ __launch_bounds__(256) void maxpool_bias_act_kernel(const uint16_t* _
   *(u32x4*)(Y + e * 8) = out;
 }
 
+// ---------------------------------------------------------------------------
+// bf16x3 (fp32-accurate) trunk helpers (FrozenResNetPlan in float32): the
+// activations are [N, H, W, 2C] bf16 with hi = bf16(x) in channels [0, C) and
+// lo = bf16(x - hi) in [C, 2C); the convs run on conv2d_nhwc_v3's X3 mode.
+
+// Stem im2col: fp32 NHWC image [N, H, W, Cin] -> A [N*Ho*Wo, 2 KP] pairs with
+// k = (kh * KW + kw) * Cin + c (the channels-last weight order), zero for
+// padding taps and k >= KH*KW*Cin (KP % 8 == 0).  One thread = 8 k.
+__global__ __launch_bounds__(256) void stem_im2col_x3_kernel(const float* __restrict__ X, uint16_t* __restrict__ A,
+                                                             int N, int H, int W, int Cin, int KH, int KW, int st,
+                                                             int pad, int Ho, int Wo, int KP) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int kp8 = KP / 8;
+  const long long total = (long long)N * Ho * Wo * kp8;
+  if (e >= total) return;
+  const int k0 = (int)(e % kp8) * 8;
+  long long r = e / kp8;
+  const int wo = (int)(r % Wo); r /= Wo;
+  const int ho = (int)(r % Ho);
+  const int n = (int)(r / Ho);
+  const int K = KH * KW * Cin;
+  u32x4 oh, ol;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t wh = 0, wl = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = k0 + 2 * q + h;
+      float v = 0.f;
+      if (k < K) {
+        const int c = k % Cin, t = k / Cin, kw = t % KW, kh = t / KW;
+        const int hi = ho * st - pad + kh, wi = wo * st - pad + kw;
+        if (hi >= 0 && hi < H && wi >= 0 && wi < W) v = X[(((size_t)n * H + hi) * W + wi) * Cin + c];
+      }
+      const uint16_t hb = f2s16<false>(v);
+      wh |= (uint32_t)hb << (16 * h);
+      wl |= (uint32_t)f2s16<false>(v - s162f<false>(hb)) << (16 * h);
+    }
+    oh[q] = wh; ol[q] = wl;
+  }
+  const size_t row = ((size_t)n * Ho + ho) * Wo + wo;
+  *(u32x4*)(A + row * 2 * KP + k0) = oh;
+  *(u32x4*)(A + row * 2 * KP + KP + k0) = ol;
+}
+
+// k x k / stride max-pool of hi/lo pairs (the value is hi + lo in fp32;
+// padded taps skipped as MaxPool2d's -inf padding), X [N,H,W,2C] -> Y [N,Ho,Wo,2C].
+__global__ __launch_bounds__(256) void maxpool_x3_kernel(const uint16_t* __restrict__ X, uint16_t* __restrict__ Y,
+                                                         int N, int H, int W, int C, int Ho, int Wo, int k, int st,
+                                                         int pad) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int C8 = C / 8;
+  const long long total = (long long)N * Ho * Wo * C8;
+  if (e >= total) return;
+  const int c8 = (int)(e % C8);
+  long long r = e / C8;
+  const int wo = (int)(r % Wo); r /= Wo;
+  const int ho = (int)(r % Ho);
+  const int n = (int)(r / Ho);
+  float m[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) m[q] = -INFINITY;
+  const int h0 = ho * st - pad, w0 = wo * st - pad;
+  for (int dh = 0; dh < k; ++dh) {
+    const int h = h0 + dh;
+    if (h < 0 || h >= H) continue;
+    for (int dw = 0; dw < k; ++dw) {
+      const int w = w0 + dw;
+      if (w < 0 || w >= W) continue;
+      const uint16_t* px = X + (((size_t)n * H + h) * W + w) * 2 * C + c8 * 8;
+      const u32x4 vh = *(const u32x4*)px, vl = *(const u32x4*)(px + C);
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        m[q] = fmaxf(m[q], s162f<false>((uint16_t)(vh[q >> 1] >> (16 * (q & 1)))) +
+                               s162f<false>((uint16_t)(vl[q >> 1] >> (16 * (q & 1)))));
+    }
+  }
+  u32x4 oh, ol;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t wh = 0, wl = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float v = m[2 * q + h];
+      const uint16_t hb = f2s16<false>(v);
+      wh |= (uint32_t)hb << (16 * h);
+      wl |= (uint32_t)f2s16<false>(v - s162f<false>(hb)) << (16 * h);
+    }
+    oh[q] = wh; ol[q] = wl;
+  }
+  uint16_t* py = Y + (((size_t)n * Ho + ho) * Wo + wo) * 2 * C + c8 * 8;
+  *(u32x4*)py = oh;
+  *(u32x4*)(py + C) = ol;
+}
+
+// hi/lo pairs [rows, 2C] -> fp32 [rows, C] (hi + lo)
+__global__ __launch_bounds__(256) void x3_to_f32_kernel(const uint16_t* __restrict__ X, float* __restrict__ Y,
+                                                        long long rows, int C) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int C8 = C / 8;
+  if (e >= rows * C8) return;
+  const long long r = e / C8;
+  const int c8 = (int)(e % C8);
+  const uint16_t* px = X + r * 2 * C + c8 * 8;
+  const u32x4 vh = *(const u32x4*)px, vl = *(const u32x4*)(px + C);
+  f32x4 a, b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a[q] = s162f<false>((uint16_t)(vh[q >> 1] >> (16 * (q & 1)))) + s162f<false>((uint16_t)(vl[q >> 1] >> (16 * (q & 1))));
+    b[q] = s162f<false>((uint16_t)(vh[2 + (q >> 1)] >> (16 * (q & 1)))) +
+           s162f<false>((uint16_t)(vl[2 + (q >> 1)] >> (16 * (q & 1))));
+  }
+  *(f32x4*)(Y + r * C + c8 * 8) = a;
+  *(f32x4*)(Y + r * C + c8 * 8 + 4) = b;
+}
+
 // Sanitizer-tier self test: out[0] = 1 in release; in the debug build the
 // check fails on purpose (n >= 0), prints its NCNET_CHECK line and out[0] = 0.
 __global__ void debug_selftest_kernel(int* out, int n) {
@@ -134,3 +250,33 @@ extern "C" int ncnet_maxpool_bias_act(const void* X, void* Y, const float* b, in
 #undef MPB
   return (int)hipGetLastError();
 }
+
+extern "C" int ncnet_stem_im2col_x3(const float* X, void* A, int N, int H, int W, int Cin, int KH, int KW, int stride,
+                                    int pad, int Ho, int Wo, int KP, hipStream_t stream) {
+  if (KP % 8 || KP < KH * KW * Cin) return -1;
+  const long long total = (long long)N * Ho * Wo * (KP / 8);
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(stem_im2col_x3_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, X,
+                     (uint16_t*)A, N, H, W, Cin, KH, KW, stride, pad, Ho, Wo, KP);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ncnet_maxpool_x3(const void* X, void* Y, int N, int H, int W, int C, int Ho, int Wo, int k, int stride,
+                                int pad, hipStream_t stream) {
+  if (C % 8 || k < 1 || stride < 1 || pad < 0 || 2 * pad > k) return -1;
+  const long long total = (long long)N * Ho * Wo * (C / 8);
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(maxpool_x3_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
+                     (const uint16_t*)X, (uint16_t*)Y, N, H, W, C, Ho, Wo, k, stride, pad);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ncnet_x3_to_f32(const void* X, float* Y, long long rows, int C, hipStream_t stream) {
+  if (C % 8) return -1;
+  const long long total = rows * (C / 8);
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(x3_to_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
+                     (const uint16_t*)X, Y, rows, C);
+  return (int)hipGetLastError();
+}
+

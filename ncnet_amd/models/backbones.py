@@ -488,3 +488,142 @@ class FrozenResNetPlan(nn.Module):
                 out = torch.addmm(idt, self._rows(y2), p["w3t"])                # x W3 + identity
                 x = self._nchw(self._bias_act(out, p["b3"], True), n2, h2, w2)
         return x
+
+
+class FrozenResNetPlanX3(nn.Module):
+    """fp32-accurate plan of a frozen (BN-folded) ResNet trunk on the bf16
+    matrix cores: the "bf16x3" split of every conv (the reference runs the
+    trunk in fp32, lib/model.py:84; ``ImMatchNet(nc_precision='fp32')``).
+
+    Activations are [N, H, W, 2C] bf16 holding hi = bf16(x) and lo = bf16(x -
+    hi) (x to ~2^-16 relative); every conv is conv2d_nhwc_v3's X3 mode
+    (csrc/conv2d.hip: acc = X_hi W_hi + X_lo W_hi + X_hi W_lo in fp32, bias,
+    the hi + lo residual and ReLU in fp32, output split again), the 7x7 stem a
+    GEMM over an im2col of the fp32 image (K = 147 padded to 192), the stem
+    max-pool compares hi + lo.  Three bf16 MFMA passes per conv instead of the
+    MIOpen fp32 implicit GEMMs (1/16 of the bf16 rate on CDNA4); the output
+    is fp32 NCHW (channels-last).  The whole trunk replays as one HIP graph
+    per input shape.
+    """
+
+    KP_ALIGN = 64
+
+    def __init__(self, folded: nn.Sequential):
+        super().__init__()
+        self.steps = []
+
+        def split3(w_cl: torch.Tensor) -> torch.Tensor:
+            """[Cout, ..., Cin] fp32 -> [Cout, ..., 3 Cin] bf16 = [W_hi | W_hi | W_lo]."""
+            hi = w_cl.to(torch.bfloat16)
+            lo = (w_cl - hi.float()).to(torch.bfloat16)
+            return torch.cat((hi, hi, lo), -1).contiguous()
+
+        def conv_w(c: nn.Conv2d) -> torch.Tensor:
+            return split3(c.weight.detach().float().permute(0, 2, 3, 1))      # [Cout, KH, KW, 3 Cin]
+
+        def bias(c: nn.Conv2d) -> torch.Tensor:
+            if c.bias is None:
+                return torch.zeros(c.out_channels, device=c.weight.device)
+            return c.bias.detach().float().contiguous()
+
+        mods = list(folded.children())
+        for idx, m in enumerate(mods):
+            if isinstance(m, nn.Conv2d):
+                relu = any(isinstance(n, nn.ReLU) for n in mods[idx + 1: idx + 3])
+                co, ci, kh, kw = m.weight.shape
+                k = kh * kw * ci
+                kp = -(-k // self.KP_ALIGN) * self.KP_ALIGN
+                w = m.weight.detach().float().permute(0, 2, 3, 1).reshape(co, k)
+                w = torch.cat((w, w.new_zeros(co, kp - k)), 1)
+                self.steps.append(("stem", dict(w3=split3(w).reshape(co, 1, 1, 3 * kp), b=bias(m), kh=kh, kw=kw,
+                                                stride=m.stride[0], pad=m.padding[0], kp=kp, relu=relu)))
+            elif isinstance(m, nn.MaxPool2d):
+                k, st, pad = FrozenResNetPlan._pool_args((m.kernel_size, m.stride, m.padding))
+                self.steps.append(("maxpool", (k, st, pad)))
+            elif isinstance(m, nn.Sequential):
+                for blk in m:
+                    if not isinstance(blk, Bottleneck):
+                        raise TypeError("FrozenResNetPlanX3 expects Bottleneck layers")
+                    dn = None
+                    if blk.downsample is not None:
+                        dc = blk.downsample[0]
+                        dn = (conv_w(dc), bias(dc), dc.stride[0], 0)
+                    self.steps.append(("bottleneck", dict(
+                        n1=(conv_w(blk.conv1), bias(blk.conv1), 1, 0),
+                        n2=(conv_w(blk.conv2), bias(blk.conv2), blk.conv2.stride[0], 1),
+                        n3=(conv_w(blk.conv3), bias(blk.conv3), 1, 0), nd=dn)))
+            elif isinstance(m, (nn.ReLU, nn.Identity)):
+                pass
+            else:
+                raise TypeError(f"FrozenResNetPlanX3: unsupported module {type(m).__name__}")
+        import os
+        self.use_graphs = os.environ.get("NCNET_TRUNK_GRAPH", "1") != "0"
+        self._graphs = {}
+
+    @staticmethod
+    def _conv(x: torch.Tensor, p, relu: bool, res: torch.Tensor | None = None) -> torch.Tensor:
+        from ..ops import _ext
+        w3, b, stride, pad = p
+        n, h, wd, _ = x.shape
+        co, kh, kw, _ = w3.shape
+        ho, wo = (h + 2 * pad - kh) // stride + 1, (wd + 2 * pad - kw) // stride + 1
+        y = torch.empty((n, ho, wo, 2 * co), dtype=torch.bfloat16, device=x.device)
+        _ext.ext().conv2d_nhwc_x3(x, w3, b, res, y, stride, pad, 1 if relu else 0)
+        return y
+
+    def _run(self, img: torch.Tensor) -> torch.Tensor:
+        from ..ops import _ext
+        C = _ext.ext()
+        x = img.float().contiguous(memory_format=torch.channels_last)
+        for kind, p in self.steps:
+            if kind == "stem":
+                n, _, h, w = x.shape
+                ho = (h + 2 * p["pad"] - p["kh"]) // p["stride"] + 1
+                wo = (w + 2 * p["pad"] - p["kw"]) // p["stride"] + 1
+                a = torch.empty((n * ho * wo, 2 * p["kp"]), dtype=torch.bfloat16, device=x.device)
+                C.stem_im2col_x3(x, a, p["kh"], p["kw"], p["stride"], p["pad"])
+                x = self._conv(a.view(n, ho, wo, 2 * p["kp"]), (p["w3"], p["b"], 1, 0), p["relu"])
+            elif kind == "maxpool":
+                k, st, pad = p
+                n, h, w, c2 = x.shape
+                y = torch.empty((n, (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1, c2),
+                                dtype=torch.bfloat16, device=x.device)
+                C.maxpool_x3(x, y, k, st, pad)
+                x = y
+            else:
+                y1 = self._conv(x, p["n1"], True)
+                y2 = self._conv(y1, p["n2"], True)
+                idt = x if p["nd"] is None else self._conv(x, p["nd"], False)
+                x = self._conv(y2, p["n3"], True, idt)
+        n, h, w, c2 = x.shape
+        out = torch.empty((n, h, w, c2 // 2), dtype=torch.float32, device=x.device)
+        C.x3_to_f32(x, out)
+        return out.permute(0, 3, 1, 2)          # NCHW view, channels-last memory
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not self.use_graphs:
+            return self._run(x)
+        key = (tuple(x.shape), x.dtype, x.device)
+        ent = self._graphs.get(key)
+        if ent is None:
+            try:
+                static_in = x.clone()
+                side = torch.cuda.Stream(device=x.device)
+                side.wait_stream(torch.cuda.current_stream(x.device))
+                with torch.cuda.stream(side):
+                    self._run(static_in)
+                torch.cuda.current_stream(x.device).wait_stream(side)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    static_out = self._run(static_in)
+            except RuntimeError as err:            # capture unsupported -> stay eager (loudly)
+                import warnings
+                warnings.warn(f"FrozenResNetPlanX3: HIP graph capture disabled ({err})")
+                self.use_graphs = False
+                return self._run(x)
+            ent = self._graphs[key] = (graph, static_in, static_out)
+        graph, static_in, static_out = ent
+        static_in.copy_(x)
+        graph.replay()
+        return static_out.clone(memory_format=torch.channels_last)

@@ -34,10 +34,18 @@ from ..ops.neigh_consensus import neigh_consensus
 _nc_ops = importlib.import_module("ncnet_amd.ops.neigh_consensus")
 _ext_count = _ext_mod.count
 from ..utils.timing import segment
-from .backbones import FrozenResNetPlan, build_trunk, fold_frozen_bn
+from .backbones import FrozenResNetPlan, FrozenResNetPlanX3, build_trunk, fold_frozen_bn
 
 # Frozen bf16 trunk: pre-cast execution plan (default) or autocast (NCNET_TRUNK_PLAN=0).
 _TRUNK_PLAN = os.environ.get("NCNET_TRUNK_PLAN", "1") != "0"
+# fp32 trunk (nc_precision / corr_dtype 'fp32') as the bf16x3 plan (default) or
+# MIOpen fp32 convs (NCNET_TRUNK_X3=0)
+_TRUNK_X3 = os.environ.get("NCNET_TRUNK_X3", "1") != "0"
+
+
+def _ext_available() -> bool:
+    from ..ops import _ext
+    return _ext.available()
 
 
 def featureL2Norm(feature: torch.Tensor) -> torch.Tensor:  # noqa: N802 (reference name)
@@ -83,6 +91,9 @@ class FeatureExtraction(nn.Module):
         if frozen and not self.training and x.is_cuda and self.feature_extraction_cnn.startswith("resnet"):
             if dtype in (torch.bfloat16, torch.float16) and _TRUNK_PLAN:
                 return self._plan(dtype)(x)
+            if dtype == torch.float32 and _TRUNK_PLAN and _TRUNK_X3 and _ext_available():
+                # fp32-accurate trunk as bf16x3 splits on the native MFMA convs
+                return self._plan(torch.float32)(x)
             net = self._folded_trunk()
         else:
             net = self.model
@@ -102,7 +113,10 @@ class FeatureExtraction(nn.Module):
         ver = sum(p._version for p in self.model.parameters()) + sum(b._version for b in self.model.buffers())
         key = (ver, dtype, _TRUNK_PLAN)
         if getattr(self, "_plan_key", None) != key:
-            self._plan_obj = FrozenResNetPlan(self._folded_trunk(), dtype)
+            if dtype == torch.float32:
+                self._plan_obj = FrozenResNetPlanX3(self._folded_trunk())
+            else:
+                self._plan_obj = FrozenResNetPlan(self._folded_trunk(), dtype)
             self._plan_key = key
         return self._plan_obj
 

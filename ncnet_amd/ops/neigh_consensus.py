@@ -74,11 +74,26 @@ def wgrad_v3_ok(shape, ks: int) -> bool:
     return ks in (3, 5) and shape[4] + ks - 1 <= 32
 
 
+_V4_PLANES = {5: (15, 20, 25), 3: (15, 20, 25)}     # wgrad16v4 instantiations (K == L)
+
+
+def wgrad_v3_ntl(K: int, L: int, ks: int) -> int:
+    """(k, l) tiles per plane of wgrad16v3 / v4 (mirrors ncnet_wgrad16v3): ~320
+    voxels per tile; on the k = 5 fallback kernel, more tiles until the 64-voxel
+    chunk count per half-tile is 1, 2 or 5 (the instantiations that do not spill)."""
+    kl = K * L
+    ntl = -(-kl // 320)
+    if ks == 5 and not (K == L and K in _V4_PLANES[5]):
+        while (-(-(-(-kl // ntl)) // 64)) not in (1, 2, 5):
+            ntl += 1
+    return ntl
+
+
 def wgrad_v3_groups(shape, ks: int) -> int:
     """Column groups per dj for wgrad16v3: ~2 workgroups per CU, never more
     than the columns (v, j, tile).  Tile rule mirrors ncnet_wgrad16v3."""
     V, I, J, K, L = shape[:5]
-    ntl = -(-(K * L) // 320)
+    ntl = wgrad_v3_ntl(K, L, ks)
     ncols = V * J * ntl
     target = max(1, 512 // ks)
     return max(1, min(target, ncols))
@@ -311,6 +326,9 @@ def _gather(outs, f32: bool, cout: int):
 # conv1x16, both weight gradients on wgrad1x16.
 
 FAST1X = True    # module attribute (A/B tests, scripts/kbench.py); no environment knob
+# (kernel size, K, L) with conv1x16 / wgrad1x16 instantiations (csrc/conv1x.hip):
+# --image_size 400 and 320 at k = 5, and the IVD recipe's k = 3 at 400 px
+FAST1X_SHAPES = frozenset({(5, 25, 25), (5, 20, 20), (3, 25, 25)})
 
 
 def fast1x_ok(kinds, channels, kernel_sizes, x: torch.Tensor, symmetric: bool) -> bool:
@@ -318,12 +336,10 @@ def fast1x_ok(kinds, channels, kernel_sizes, x: torch.Tensor, symmetric: bool) -
         return False
     if any(k != "16" for k in kinds[1:-1]) or any(c != 16 for c in channels[:-1]):
         return False
-    if kernel_sizes[0] != 5 or kernel_sizes[-1] != 5:
-        return False
     _, _, I, J, K, L = x.shape
     if symmetric and (I, J) != (K, L):
         return False
-    return (K, L) == (25, 25)
+    return (kernel_sizes[0], K, L) in FAST1X_SHAPES and (kernel_sizes[-1], K, L) in FAST1X_SHAPES
 
 
 @functools.lru_cache(maxsize=None)
@@ -590,14 +606,15 @@ class NeighConsensusFn(torch.autograd.Function):
             # the 1-channel input as padded planes, both branches in one batch
             # (pad_planes trans=1 writes the swapped branch's planes directly)
             x3 = x.reshape(V, R, Cc)
+            k0 = ws[0].shape[0]
             if symmetric:
-                _, ppl = _ext.ext().pad_geom(K, L, 5)
+                _, ppl = _ext.ext().pad_geom(K, L, k0)
                 xp = torch.zeros((2 * V * R, ppl), dtype=torch.bfloat16, device=x.device)
-                _pad_1ch(x3, K, L, 5, 0, out=xp[:V * R])
-                _pad_1ch(x3, I, J, 5, 1, out=xp[V * R:])
+                _pad_1ch(x3, K, L, k0, 0, out=xp[:V * R])
+                _pad_1ch(x3, I, J, k0, 1, out=xp[V * R:])
                 z = _stack_fwd(None, ws, bs, kinds, saved_layers, xp=xp, shp=(2 * V, I, J, K, L))
             else:
-                z = _stack_fwd(None, ws, bs, kinds, saved_layers, xp=_pad_1ch(x3, K, L, 5, 0), shp=(V, I, J, K, L))
+                z = _stack_fwd(None, ws, bs, kinds, saved_layers, xp=_pad_1ch(x3, K, L, k0, 0), shp=(V, I, J, K, L))
             branches = [saved_layers]
         elif symmetric:
             xb = x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous()

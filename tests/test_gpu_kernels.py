@@ -92,6 +92,58 @@ def test_conv16v4_matches_v3_bitwise(epi, shape, monkeypatch, tune):
     assert relerr(got, want) < 4e-3, relerr(got, want)
 
 
+@pytest.mark.parametrize("ks,T", [(5, 20), (5, 15), (3, 25), (3, 20), (3, 15)])
+@pytest.mark.parametrize("epi", [1, 2])
+def test_conv16v4_other_planes(ks, T, epi, tune):
+    """conv16v4 at the other compile-time training planes (--image_size 320 /
+    240, and k = 3): bit-identical to the general conv16v3 and within the final
+    bf16 rounding of the fp64 oracle."""
+    from ncnet_amd.ops.packing import pack_w16
+    torch.manual_seed(2)
+    V, I, J = 2, 7, 11
+    x = torch.rand(V, I, J, T, T, 16, device=DEV).to(torch.bfloat16)
+    m = torch.randn(V, I, J, T, T, 16, device=DEV).to(torch.bfloat16)
+    w_std = torch.randn(16, 16, ks, ks, ks, ks, device=DEV) * 0.05
+    w = pack_w16(w_std)
+    b = torch.randn(16, device=DEV) * 0.1
+    outs = []
+    for v3 in ("0", "1"):
+        tune("conv_v3", v3)
+        y = torch.full_like(x, float("nan"))
+        _ext.ext().conv16_fwd(x, w, b if epi == 1 else None, m if epi == 2 else None, y, ks, epi)
+        outs.append(y)
+    assert torch.isfinite(outs[0].float()).all()
+    z = ref.conv4d(x.double().permute(0, 5, 1, 2, 3, 4), ref.conv4d_weight_from_std(bf(w_std)), None)
+    want = torch.relu(z + b.double().view(1, 16, 1, 1, 1, 1)) if epi == 1 else z * (m.double().permute(0, 5, 1, 2, 3, 4) > 0)
+    e4, e3 = relerr(outs[0].permute(0, 5, 1, 2, 3, 4), want), relerr(outs[1].permute(0, 5, 1, 2, 3, 4), want)
+    print(f"conv16v4 k{ks} {T}x{T}: v4 {e4:.2e} v3 {e3:.2e} bitwise {torch.equal(outs[0], outs[1])}")
+    assert e4 < 4e-3 and e3 < 4e-3, (e4, e3)
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("ks,T", [(5, 20), (5, 15), (3, 25), (3, 20), (3, 15)])
+def test_wgrad16v4_other_planes(ks, T, tune):
+    """wgrad16v4 at the other compile-time planes vs the general wgrad16v3 and
+    the fp64 weight gradient."""
+    from ncnet_amd.ops.neigh_consensus import wgrad16_partials, _reduce_wgrad16
+    torch.manual_seed(9)
+    V, I, J = 2, 6, 9
+    x = torch.randn(V, I, J, T, T, 16, device=DEV).to(torch.bfloat16)
+    g = torch.randn(V, I, J, T, T, 16, device=DEV).to(torch.bfloat16)
+    res = []
+    for v3 in ("0", "1"):
+        tune("wgrad_v3", v3)
+        s, sb = wgrad16_partials(_ext.ext(), x, g, ks, False)
+        res.append((_reduce_wgrad16(s, ks, 16, 16), sb))
+    w = torch.zeros(ks, 16, 16, ks, ks, ks, device=DEV, dtype=torch.float64, requires_grad=True)
+    y = ref.conv4d(x.double().permute(0, 5, 1, 2, 3, 4), w, None)
+    (y * g.double().permute(0, 5, 1, 2, 3, 4)).sum().backward()
+    want = ref.conv4d_weight_to_std(w.grad)
+    for dw, db in res:
+        assert relerr(dw, want) < 1e-4, relerr(dw, want)
+        assert relerr(db, g.double().sum(dim=(0, 1, 2, 3, 4))) < 1e-4
+
+
 @pytest.mark.parametrize("ks,shape,cin,relu", [(5, (4, 25, 25, 25, 25), 16, 1), (5, (1, 6, 5, 26, 29), 16, 0),
                                                (3, (2, 7, 9, 11, 13), 10, 1), (3, (1, 3, 2, 30, 27), 16, 1),
                                                (7, (1, 9, 8, 25, 25), 16, 1), (1, (2, 5, 6, 25, 25), 16, 0),
@@ -862,9 +914,11 @@ def _pad_1ch(x5, ks, trans=False):
     return y
 
 
-@pytest.mark.parametrize("shape", [(2, 25, 25, 25, 25), (1, 6, 7, 25, 25), (1, 3, 11, 25, 25)])
+@pytest.mark.parametrize("ks,shape", [(5, (2, 25, 25, 25, 25)), (5, (1, 6, 7, 25, 25)), (5, (1, 3, 11, 25, 25)),
+                                      (5, (2, 20, 20, 20, 20)), (5, (1, 7, 3, 20, 20)), (3, (2, 25, 25, 25, 25)),
+                                      (3, (1, 4, 9, 25, 25))])
 @pytest.mark.parametrize("epi", [1, 2])
-def test_conv1x16_vs_oracle(shape, epi):
+def test_conv1x16_vs_oracle(ks, shape, epi):
     """1 -> 16 Conv4d on zero-padded 1-channel planes (csrc/conv1x.hip: taps
     gathered by ds_read_b64_tr_b16 from 4 element-shifted LDS copies of each
     plane) vs the fp64 oracle: bias + ReLU forward, and the ReLU-mask epilogue
@@ -873,11 +927,11 @@ def test_conv1x16_vs_oracle(shape, epi):
     torch.manual_seed(3)
     V, I, J, K, L = shape
     x = torch.rand(V, I, J, K, L, device=DEV).to(torch.bfloat16)
-    w = torch.randn(16, 1, 5, 5, 5, 5, device=DEV) * 0.05
+    w = torch.randn(16, 1, ks, ks, ks, ks, device=DEV) * 0.05
     b = torch.randn(16, device=DEV) * 0.1
     m = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
     y = torch.full((V, I, J, K, L, 16), float("nan"), dtype=torch.bfloat16, device=DEV)
-    ran = _ext.ext().conv1x16(_pad_1ch(x, 5), pack_w1x(w), b if epi == 1 else None, m if epi == 2 else None, y, 5, epi)
+    ran = _ext.ext().conv1x16(_pad_1ch(x, ks), pack_w1x(w), b if epi == 1 else None, m if epi == 2 else None, y, ks, epi)
     assert ran
     z = ref.conv4d(x.double().unsqueeze(1), ref.conv4d_weight_from_std(bf(w)), None)   # [V, 16, I, J, K, L]
     if epi == 1:
@@ -897,10 +951,12 @@ def test_pad_planes_transposed():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("shape,G", [((2, 25, 25, 25, 25), 256), ((1, 6, 7, 25, 25), 7), ((1, 3, 11, 25, 25), 64),
-                                     ((1, 5, 5, 25, 25), 1)])
+@pytest.mark.parametrize("ks,shape,G", [(5, (2, 25, 25, 25, 25), 256), (5, (1, 6, 7, 25, 25), 7),
+                                        (5, (1, 3, 11, 25, 25), 64), (5, (1, 5, 5, 25, 25), 1),
+                                        (5, (2, 20, 20, 20, 20), 256), (5, (1, 4, 9, 20, 20), 13),
+                                        (3, (2, 25, 25, 25, 25), 256), (3, (1, 5, 7, 25, 25), 9)])
 @pytest.mark.parametrize("bias", [True, False])
-def test_wgrad1x16_vs_oracle(shape, G, bias):
+def test_wgrad1x16_vs_oracle(ks, shape, G, bias):
     """Weight gradient with a 1-channel operand straight from padded planes
     (csrc/conv1x.hip wgrad1x16: tap shift moved into the transposed D read, one
     partial per persistent workgroup, item starts at arbitrary (v, i, j) steps)
@@ -911,22 +967,23 @@ def test_wgrad1x16_vs_oracle(shape, G, bias):
     V, I, J, K, L = shape
     x1 = torch.rand(V, I, J, K, L, device=DEV).to(torch.bfloat16)
     d = torch.randn(V, I, J, K, L, 16, device=DEV).to(torch.bfloat16)
-    part = torch.full((G, 25, 32, 16), float("nan"), device=DEV)
+    nt = ks * ks
+    part = torch.full((G, nt, 32, 16), float("nan"), device=DEV)
     partb = torch.full((G, 16), float("nan"), device=DEV) if bias else None
-    assert _ext.ext().wgrad1x16(d, _pad_1ch(x1, 5), part, partb, 5)
-    R = part.sum(0)[:, :25, :]                                   # [tap, combo, c]
+    assert _ext.ext().wgrad1x16(d, _pad_1ch(x1, ks), part, partb, ks)
+    R = part.sum(0)[:, :nt, :]                                   # [tap, combo, c]
     # first layer: y[co] = conv(x1; W[co, 0]), dL/dy = d  ->  dW[co, 0, di, dj, dk, dl]
-    wr = torch.zeros(5, 16, 1, 5, 5, 5, device=DEV, dtype=torch.float64, requires_grad=True)
+    wr = torch.zeros(ks, 16, 1, ks, ks, ks, device=DEV, dtype=torch.float64, requires_grad=True)
     yr = ref.conv4d(x1.double().unsqueeze(1), wr, None)
     (yr * d.double().permute(0, 5, 1, 2, 3, 4)).sum().backward()
-    want = ref.conv4d_weight_to_std(wr.grad)[:, 0].reshape(16, 25, 25)      # [co, combo, tap]
+    want = ref.conv4d_weight_to_std(wr.grad)[:, 0].reshape(16, nt, nt)      # [co, combo, tap]
     assert relerr(R.permute(2, 1, 0), want) < 1e-4
     # last layer: y = conv(d; W[0, ci]), dL/dy = x1  ->  dW[0, ci, t] = R[2P - t][ci]
-    w3 = torch.zeros(5, 1, 16, 5, 5, 5, device=DEV, dtype=torch.float64, requires_grad=True)
+    w3 = torch.zeros(ks, 1, 16, ks, ks, ks, device=DEV, dtype=torch.float64, requires_grad=True)
     y3 = ref.conv4d(d.double().permute(0, 5, 1, 2, 3, 4), w3, None)
     (y3 * x1.double().unsqueeze(1)).sum().backward()
     want3 = ref.conv4d_weight_to_std(w3.grad)[0]                               # [ci, di, dj, dk, dl]
-    got3 = R.permute(2, 1, 0).reshape(16, 5, 5, 5, 5).flip(1, 2, 3, 4)
+    got3 = R.permute(2, 1, 0).reshape(16, ks, ks, ks, ks).flip(1, 2, 3, 4)
     assert relerr(got3, want3) < 1e-4
     if bias:
         assert relerr(partb.sum(0), d.double().sum(dim=(0, 1, 2, 3, 4))) < 1e-4
@@ -971,28 +1028,41 @@ def test_neigh_consensus_fast1x_matches_ij_path(monkeypatch, symmetric):
         assert rel_l2(a, b) < 5e-2, (n, rel_l2(a, b))
 
 
-def _fast1x_vs_quantized_oracle(symmetric, perturb=None, seed=31):
-    """The 5,5,5 / 16,16,1 stack at 25^4 on the padded-plane fast path vs the
-    quantized fp64 oracle (engine/quantized_oracle.py: bf16 rounding exactly at
-    the stored activations, weights and pre-activation gradients).  Returns
+def _fast1x_vs_quantized_oracle(symmetric, perturb=None, seed=31, ks=(5, 5, 5), ch=(16, 16, 1), T=25, V=2):
+    """The fast training stack on the padded-plane kernels vs the quantized
+    fp64 oracle (engine/quantized_oracle.py: bf16 rounding exactly at the
+    stored activations, weights and pre-activation gradients).  Returns
     {name: rel L2 error}.  ``perturb``: a function applied to the first layer's
-    packed weights (a mutation the check must catch)."""
+    packed weights (a mutation the check must catch).
+
+    The data are small multiples of powers of two (x in {0, 1}, weights and
+    biases k / 8 .. k / 32, |k| <= 2, output gradient k / 16) so every
+    pre-activation and every pre-activation gradient is EXACT in fp32: the
+    kernels and the oracle then round the same values to bf16 and take the
+    same ReLU masks.  With continuous random data a relative error of ~1e-6 in
+    fp32 flips ~1e-4 of the masks, and every flip moves a gradient element by
+    its full value (an L2 error of sqrt(1e-4) = 1e-2 whatever the kernels do)."""
     import importlib
     from ncnet_amd.engine import quantized_oracle as qo
     nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
-    torch.manual_seed(seed)
-    V = 2
-    x = torch.rand(V, 1, 25, 25, 25, 25, device=DEV).to(torch.bfloat16).float()
+    gen = torch.Generator(device=DEV).manual_seed(seed)
+
+    def ints(shape, lo, hi, scale):
+        return torch.randint(lo, hi + 1, shape, device=DEV, generator=gen).float() * scale
+
+    x = ints((V, 1, T, T, T, T), 0, 1, 1.0)
     ws, bs, cin = [], [], 1
-    for k, c in zip((5, 5, 5), (16, 16, 1)):
-        ws.append((torch.randn(k, c, cin, k, k, k, device=DEV) * 0.05).to(torch.bfloat16).float())
-        bs.append(0.2 + torch.rand(c, device=DEV) * 0.1)
+    for li, (k, c) in enumerate(zip(ks, ch)):
+        sc = 2.0 ** (-3 if li == 0 else -5)
+        ws.append(ints((k, c, cin, k, k, k), -2, 2, sc))
+        bs.append(ints((c,), -2, 2, sc))
         cin = c
-    g = torch.randn(V, 1, 25, 25, 25, 25, device=DEV)
+    g = ints((V, 1, T, T, T, T), -1, 1, 2.0 ** -4)
     xx = x.clone().requires_grad_(True)
     pw = [w.clone().requires_grad_(True) for w in ws]
     pb = [b.clone().requires_grad_(True) for b in bs]
-    assert nc.fast1x_ok(["1in", "16", "1out"], [16, 16, 1], [5, 5, 5], xx, symmetric)
+    kinds = nc.layer_kinds(list(ch), list(ks))
+    assert nc.fast1x_ok(kinds, list(ch), list(ks), xx, symmetric)
     orig = nc.pack_w1x
     if perturb is not None:
         calls = []
@@ -1005,7 +1075,7 @@ def _fast1x_vs_quantized_oracle(symmetric, perturb=None, seed=31):
             return p
         nc.pack_w1x = mutated
     try:
-        y = nc.neigh_consensus(xx, pw, pb, [16, 16, 1], symmetric=symmetric)
+        y = nc.neigh_consensus(xx, pw, pb, list(ch), symmetric=symmetric)
         (y * g).sum().backward()
     finally:
         nc.pack_w1x = orig
@@ -1016,8 +1086,27 @@ def _fast1x_vs_quantized_oracle(symmetric, perturb=None, seed=31):
     yr = qo.neigh_consensus(xr, wr, br, symmetric=symmetric)
     (yr * g.double()).sum().backward()
     want = [yr, xr.grad] + [ref.conv4d_weight_from_std(p.grad) for p in wr] + [p.grad for p in br]
-    names = ["y", "gx", "gw0", "gw1", "gw2", "gb0", "gb1", "gb2"]
+    names = ["y", "gx"] + [f"gw{i}" for i in range(len(ws))] + [f"gb{i}" for i in range(len(ws))]
+    # (diagnostic) the unrounded fp64 reference: the quantized oracle must sit
+    # ~1e-3 (y) .. ~1e-1 (gradients) from it, the kernels ~1e-3 from the oracle
+    x2 = x.double().requires_grad_(True)
+    w2 = [w.double().requires_grad_(True) for w in ws]
+    b2 = [b.double().requires_grad_(True) for b in bs]
+    y2 = ref.neigh_consensus(x2, w2, b2, symmetric=symmetric)
+    (y2 * g.double()).sum().backward()
+    plain = [y2, x2.grad] + [p.grad for p in w2 + b2]
+    print("kernels vs fp64 ref:", {n: f"{rel_l2(a, r):.1e}" for n, a, r in zip(names, got, plain)},
+          "oracle vs fp64 ref:", {n: f"{rel_l2(a, r):.1e}" for n, a, r in zip(names, want, plain)})
     return {n: rel_l2(a, r) for n, a, r in zip(names, got, want)}
+
+
+@pytest.mark.parametrize("ks,ch,T,V", [((5, 5, 5), (16, 16, 1), 20, 2), ((3, 3), (16, 1), 25, 2)])
+def test_fast1x_other_configs_vs_quantized_oracle(ks, ch, T, V):
+    """The fast training stack at --image_size 320 (20^4 volumes) and the IVD
+    recipe (NC 3,3 / 16,1 at 400 px) vs the quantized fp64 oracle."""
+    errs = _fast1x_vs_quantized_oracle(True, ks=ks, ch=ch, T=T, V=V)
+    print(f"fast1x {ks}/{ch} at {T}^4 vs quantized oracle:", {k: f"{v:.1e}" for k, v in errs.items()})
+    assert max(errs.values()) < 1e-3, errs
 
 
 @pytest.mark.parametrize("symmetric", [True, False])

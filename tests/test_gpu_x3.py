@@ -138,3 +138,70 @@ def test_x3_fused_matches_per_conv_path():
         outs.append([y.detach(), x.grad.clone()] + [p.grad.clone() for p in params])
     errs = [rl2(a, b) for a, b in zip(*outs)]
     assert max(errs) < 1e-4, errs
+
+
+def _pairs(t_nhwc):
+    """fp32 [N, H, W, C] -> bf16 [N, H, W, 2C] = [hi | lo]."""
+    hi = t_nhwc.to(torch.bfloat16)
+    lo = (t_nhwc - hi.float()).to(torch.bfloat16)
+    return torch.cat((hi, lo), -1).contiguous()
+
+
+def _unpair(p):
+    c = p.shape[-1] // 2
+    return p[..., :c].double() + p[..., c:].double()
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,pad,res,relu,shape", [
+    (256, 256, 3, 1, 1, False, True, (3, 25, 25)), (1024, 256, 1, 1, 0, False, True, (2, 25, 25)),
+    (256, 1024, 1, 1, 0, True, True, (2, 25, 25)), (64, 64, 3, 1, 1, False, True, (2, 37, 29)),
+    (128, 128, 3, 2, 1, False, True, (2, 50, 50)), (512, 1024, 1, 2, 0, False, False, (1, 50, 50))])
+def test_conv2d_x3_vs_fp64(cin, cout, k, stride, pad, res, relu, shape):
+    """conv2d_nhwc_v3 X3 mode: [hi | lo] bf16 pairs in and out, acc = X_hi W_hi +
+    X_lo W_hi + X_hi W_lo, fp32 bias / residual / ReLU: the fp32 conv to ~1e-5."""
+    C = _ext.ext()
+    torch.manual_seed(5)
+    n, h, w = shape
+    x = torch.randn(n, h, w, cin, device="cuda")
+    wt = torch.randn(cout, cin, k, k, device="cuda") * (1.0 / (cin * k * k) ** 0.5)
+    b = torch.randn(cout, device="cuda") * 0.1
+    wcl = wt.permute(0, 2, 3, 1)
+    whi = wcl.to(torch.bfloat16)
+    w3 = torch.cat((whi, whi, (wcl - whi.float()).to(torch.bfloat16)), -1).contiguous()
+    xp = _pairs(x)
+    want = torch.nn.functional.conv2d(_unpair(xp).permute(0, 3, 1, 2), wt.double(), b.double(), stride, pad)
+    want = want.permute(0, 2, 3, 1)
+    r = None
+    if res:
+        rr = torch.randn(want.shape, device="cuda")
+        r = _pairs(rr)
+        want = want + _unpair(r)
+    if relu:
+        want = torch.relu(want)
+    y = torch.full(tuple(want.shape[:3]) + (2 * cout,), float("nan"), dtype=torch.bfloat16, device="cuda")
+    C.conv2d_nhwc_x3(xp, w3, b, r, y, stride, pad, 1 if relu else 0)
+    err = rl2(_unpair(y), want)
+    print("conv2d x3 error", err)
+    assert err < 3e-5, err
+
+
+def test_trunk_x3_plan_vs_fp64():
+    """The bf16x3 trunk plan (FrozenResNetPlanX3: stem im2col GEMM, split
+    max-pool, every bottleneck conv on the X3 kernel) against the folded trunk
+    evaluated in fp64: fp32-class agreement, and no MIOpen fp32 conv involved."""
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.models.backbones import FrozenResNetPlanX3
+    torch.manual_seed(0)
+    m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], nc_precision="fp32").cuda().eval()
+    fe = m.FeatureExtraction
+    x = torch.randn(2, 3, 160, 192, device="cuda")
+    with torch.no_grad():
+        got = fe.trunk_forward(x, torch.float32)
+        assert isinstance(fe._plan_obj, FrozenResNetPlanX3)
+        got2 = fe.trunk_forward(x, torch.float32)           # graph replay
+        want = fe._folded_trunk().double()(x.double())
+        fe._folded = None                                    # (the fp64 copy is not the cached trunk)
+    err = rl2(got, want)
+    print("x3 trunk vs fp64:", err, "bf16 trunk would be ~1e-2")
+    assert torch.equal(got, got2)
+    assert err < 1e-4, err

@@ -15,18 +15,21 @@ from ncnet_amd import kernel_resources as kr
 
 # (kernel name prefix, template-argument string or None for every instantiation)
 HOT = [
-    ("conv16v4_fwd_kernel", "5, 5, 1, 25, 25"),     # 16->16 forward (training)
-    ("conv16v4_fwd_kernel", "5, 5, 2, 25, 25"),     # 16->16 data gradient (training)
+    ("conv16v4_fwd_kernel", "5, 5, 1, 25, 25"),     # 16->16 forward (training, 400 px)
+    ("conv16v4_fwd_kernel", "5, 5, 2, 25, 25"),     # 16->16 data gradient (training, 400 px)
+    ("conv16v4_fwd_kernel", None),                  # every compile-time plane: 15 / 20 / 25, k = 3 / 5, x3
     ("wgrad16v4_kernel", "5, 25, 25"),              # 16->16 weight gradient (training)
+    ("wgrad16v4_kernel", None),                     # every compile-time plane, k = 3 / 5
+    ("wgrad16v3_kernel", None),                     # general-shape 16->16 weight gradient (fallback)
     ("conv16v3_fwd_kernel", None),                  # general-shape 16->16 (k = 3, 5; fwd / dgrad)
     ("conv16v2_fwd_kernel", None),                  # 1-channel layers (group-plane / block modes)
     ("wgrad16v2_kernel", None),
     ("wgrad16p_kernel", None),
-    ("conv1x16_kernel", None),                      # 1 -> 16 on padded 1-channel planes
+    ("conv1x16_kernel", None),                      # 1 -> 16 on padded 1-channel planes (k 5: 20, 25; k 3: 25)
     ("wgrad1x16_kernel", None),                     # 1-channel-operand weight gradients
     ("corr_gemm", None),                            # correlation GEMMs (bf16 v1 / v2, MX-fp8)
     ("nc_fused_k3_kernel", None),                   # fused InLoc NC
-    ("conv2d_nhwc", None),                          # native trunk convs
+    ("conv2d_nhwc", None),                          # native trunk convs (v1, v2, v3 incl. the bf16x3 mode)
     ("l2norm_rows_kernel", None),
     ("mm_apply_kernel", None),
     ("stats_rows_kernel", None),
