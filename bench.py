@@ -96,6 +96,67 @@ def _inloc_secondary():
     return out
 
 
+def train_tflop_per_pair(size: int, ks=(5, 5, 5), ch=(16, 16, 1)) -> float:
+    """Useful FLOPs of one training pair at ``size`` px (BASELINE.md's
+    accounting): ResNet-101 to layer3 on the 2 images (44.6 GFLOP at 400 px,
+    scaling with the pixel count), the positive and rolled-negative
+    correlations, and per volume (positive and negative, both symmetric
+    branches) every Conv4d forward, data gradient (not for the first layer:
+    no gradient flows into the frozen trunk) and weight gradient."""
+    n = size // 16
+    trunk = 2 * 44.6e9 * (size / 400.0) ** 2
+    corr = 2 * 2.0 * n ** 4 * 1024
+    fwd, bwd, cin = 0.0, 0.0, 1
+    for li, (k, c) in enumerate(zip(ks, ch)):
+        f = 2.0 * n ** 4 * cin * c * k ** 4
+        fwd += f
+        bwd += f * (1 if li == 0 else 2)
+        cin = c
+    return (trunk + corr + 2 * 2 * (fwd + bwd)) / 1e12
+
+
+def _train_secondary(batch: int, size: int, ks=(5, 5, 5), ch=(16, 16, 1), steps: int = 5, warmup: int = 2):
+    """The headline step (Trainer.train_step, trunk prefetch) at another
+    ``--image_size`` or NeighConsensus recipe (the reference trains the IVD /
+    InLoc model with --ncons_kernel_sizes 3 3 --ncons_channels 16 1,
+    /root/reference/README.md:41-49); reports pairs/s and useful TFLOP/s."""
+    from ncnet_amd.engine.trainer import Trainer, make_adam
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.ops import _ext
+    from ncnet_amd.parallel.dist import DistContext
+    dev = torch.device("cuda")
+    torch.manual_seed(4)
+    model = ImMatchNet(ncons_kernel_sizes=list(ks), ncons_channels=list(ch), dtype="bf16").to(dev)
+    model.train()
+    params = [p for p in model.parameters() if p.requires_grad]
+    trainer = Trainer(model, make_adam(params, 5e-4), DistContext(device=dev))
+    g = torch.Generator(device=dev).manual_seed(97)
+    pool = [{"source_image": torch.randn(batch, 3, size, size, device=dev, generator=g),
+             "target_image": torch.randn(batch, 3, size, size, device=dev, generator=g)} for _ in range(2)]
+    for w in range(warmup):
+        trainer.train_step(pool[w % 2], pool[(w + 1) % 2])
+    torch.cuda.synchronize()
+    d0 = dict(_ext.DISPATCH)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = trainer.train_step(pool[(warmup + i) % 2], pool[(warmup + i + 1) % 2])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    pps = batch * steps / dt
+    tf = train_tflop_per_pair(size, ks, ch)
+    from ncnet_amd.ops.neigh_consensus import fast1x_ok, layer_kinds
+    n = size // 16
+    fast = fast1x_ok(layer_kinds(list(ch), list(ks)), list(ch), list(ks),
+                     torch.empty(1, 1, n, n, n, n, device=dev), True)
+    out = {"pairs_per_s": round(pps, 3), "ms_per_step": round(1e3 * dt / steps, 3), "image_size": size,
+           "ncons": [list(ks), list(ch)], "tflop_per_pair": round(tf, 4), "useful_tflops": round(pps * tf, 1),
+           "fast_1ch_path": bool(fast), "final_loss": float(loss.detach()),
+           "nc_paths": {k: v - d0.get(k, 0) for k, v in _ext.DISPATCH.items() if v != d0.get(k, 0)}}
+    del trainer, model
+    torch.cuda.empty_cache()
+    return out
+
+
 def _nc_precision_secondary(batch: int, size: int, nc_precision: str, steps: int = 5, warmup: int = 2):
     """The headline step with ``ImMatchNet(nc_precision=...)``: 'fp32' runs every
     NeighConsensus conv, data gradient and weight gradient as a bf16x3 split
@@ -217,7 +278,8 @@ def main(argv=None):
     ap.add_argument("--ref-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--profile", type=str, default="", help="write a torch.profiler trace to this dir")
     ap.add_argument("--only-secondary", type=str, default="",
-                    help="debug: skip the headline and print one secondary record (nc_fp32 | fe_finetune)")
+                    help="debug: skip the headline and print one secondary record "
+                         "(nc_fp32 | fe_finetune | train | train_ivd, at --image-size)")
     ap.add_argument("--inloc", type=int, default=1,
                     help="1: after the timed training steps of a 1-GPU run, also time the InLoc inference configs "
                          "(BASELINE configs 3-5: 1600 px bf16, 3200 px bf16, 3200 px fp8) into config.secondary")
@@ -226,7 +288,10 @@ def main(argv=None):
         return _self_launch(args, argv)
     if args.only_secondary:
         fn = {"nc_fp32": lambda: _nc_precision_secondary(args.batch, args.image_size, "fp32", args.steps, args.warmup),
-              "fe_finetune": lambda: _fe_finetune_secondary(args.batch, args.image_size, args.steps, args.warmup)}
+              "fe_finetune": lambda: _fe_finetune_secondary(args.batch, args.image_size, args.steps, args.warmup),
+              "train": lambda: _train_secondary(args.batch, args.image_size, steps=args.steps, warmup=args.warmup),
+              "train_ivd": lambda: _train_secondary(args.batch, args.image_size, (3, 3), (16, 1), args.steps,
+                                                    args.warmup)}
         print(json.dumps({"secondary": args.only_secondary, **fn[args.only_secondary]()}), flush=True)
         return 0
 
@@ -336,6 +401,15 @@ def main(argv=None):
             secondary["train_nc_fp32"] = _nc_precision_secondary(args.batch, s, "fp32")
         except Exception as e:  # the headline record must still print
             secondary["train_nc_fp32"] = {"error": repr(e)}
+        # the training step at the other --image_size values and the IVD recipe
+        for name, size, ks, ch in (("train_320", 320, (5, 5, 5), (16, 16, 1)),
+                                   ("train_480", 480, (5, 5, 5), (16, 16, 1)),
+                                   ("train_ivd_400", 400, (3, 3), (16, 1))):
+            try:
+                secondary[name] = _train_secondary(args.batch, size, ks, ch)
+            except Exception as e:  # the headline record must still print
+                secondary[name] = {"error": repr(e)}
+        secondary["headline_useful_tflops"] = round(pairs_per_s / ctx.world_size * train_tflop_per_pair(s), 1)
     if ctx.is_main:
         rec = {
             "metric": "image-pairs/sec fwd+bwd, ResNet-101+NC-Net(5,5,5) 400x400 bf16",

@@ -175,6 +175,7 @@ struct NcnetTuning {
   int conv2d_big;      // NCNET_CONV2D_BIG: allow the 256 x 128 tile on smaller grids (0)
   int corr_v2;         // NCNET_CORR_V2: -1 auto, 0 / 1 force the correlation GEMM variant
   int corr_ns;         // NCNET_CORR_NS: 3 or 4 ring stages of corr_gemm_v2
+  int conv2d_v3;       // NCNET_CONV2D_V3: chip-round v3 tiles where the auto rule picks them (1)
 };
 __host__ inline int ncnet_tuning_env(const char* k, int d) {
   const char* e = getenv(k);
@@ -185,7 +186,7 @@ __host__ inline NcnetTuning& tuning() {
                           ncnet_tuning_env("NCNET_CONV_V3", 0),     ncnet_tuning_env("NCNET_WGRAD_V3", 0),
                           ncnet_tuning_env("NCNET_WGRAD_FLAGS", 0), ncnet_tuning_env("NCNET_CONV2D_VARIANT", 0),
                           ncnet_tuning_env("NCNET_CONV2D_BIG", 0),  ncnet_tuning_env("NCNET_CORR_V2", -1),
-                          ncnet_tuning_env("NCNET_CORR_NS", 3) == 4 ? 4 : 3};
+                          ncnet_tuning_env("NCNET_CORR_NS", 3) == 4 ? 4 : 3, ncnet_tuning_env("NCNET_CONV2D_V3", 1)};
   return t;
 }
 __host__ inline int* tuning_slot(const char* name) {
@@ -199,5 +200,6 @@ __host__ inline int* tuning_slot(const char* name) {
   if (!strcmp(name, "conv2d_big")) return &t.conv2d_big;
   if (!strcmp(name, "corr_v2")) return &t.corr_v2;
   if (!strcmp(name, "corr_ns")) return &t.corr_ns;
+  if (!strcmp(name, "conv2d_v3")) return &t.conv2d_v3;
   return nullptr;
 }

@@ -682,7 +682,7 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
   const bool big = BN == 128 && (variant == 0 ? t256 >= 384 : (t256 >= 512 || (t256 >= 256 && tuning().conv2d_big)));
   // (grids big enough for the 256 x 128 DMA-ring tile keep it: InLoc 3200 px
   // layer 3, 467 us v2 vs 707 us v3)
-  const bool v3_auto = variant == 0 && !big && Cout <= 256 && KH * KW * Cin >= 1024;
+  const bool v3_auto = variant == 0 && tuning().conv2d_v3 && !big && Cout <= 256 && KH * KW * Cin >= 1024;
   if ((variant == 3 || v3_auto) && c3_run(p, f16 ? 1 : 0, stream)) return (int)hipGetLastError();
   if (big && variant != 1) {
     p.tiles_m = cdiv(p.M, 256);
