@@ -28,6 +28,8 @@ class RuntimeConfig:
     bwd_overlap: bool = True         # NCNET_BWD_OVERLAP: NC weight gradients on a side stream
     trunk_prefetch: bool = True      # NCNET_TRUNK_PREFETCH: next batch's frozen backbone on a side stream
     nc_fused: bool = True            # NCNET_NC_FUSED: fused (3,3)/(<=16,1) inference NeighConsensus kernel
+    step_priority: bool = False      # NCNET_STEP_PRIORITY: training step on high-priority streams, the
+                                     # prefetched trunk at default priority (fills gaps instead of time-slicing)
 
     @classmethod
     def from_env(cls, env=None) -> "RuntimeConfig":
@@ -41,7 +43,8 @@ class RuntimeConfig:
                    nt_store=e.get("NCNET_NT_STORE", "1") != "0",
                    bwd_overlap=e.get("NCNET_BWD_OVERLAP", "1") == "1",
                    trunk_prefetch=e.get("NCNET_TRUNK_PREFETCH", "1") == "1",
-                   nc_fused=e.get("NCNET_NC_FUSED", "1") != "0")
+                   nc_fused=e.get("NCNET_NC_FUSED", "1") != "0",
+                   step_priority=e.get("NCNET_STEP_PRIORITY", "0") == "1")
 
     def as_dict(self) -> dict:
         return dataclasses.asdict(self)

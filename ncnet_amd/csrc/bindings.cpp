@@ -54,8 +54,7 @@ int ncnet_resize_norm_u8(const void*, const long long*, float*, int, int, int, c
 int ncnet_debug_selftest(int*, hipStream_t);
 int ncnet_pad_geom(int, int, int, int*, int*);
 int ncnet_pad_planes(const void*, int, void*, int, int, int, int, int, int, int, hipStream_t);
-int ncnet_conv1x16(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int,
-                   hipStream_t);
+int ncnet_conv1x16(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, long long, long long, hipStream_t);
 int ncnet_wgrad1x16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_nc_fused_k3(const void*, const void*, const float*, const void*, const float*, float*, int, int, int, int,
                       int, int, int, int, int, int, hipStream_t);
@@ -125,17 +124,24 @@ bool conv1x16(Tensor Xp, Tensor Wa, c10::optional<Tensor> bias, c10::optional<Te
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(Xp.device());
   check(Xp, "Xp", at::kBFloat16); check(Wa, "Wa", at::kBFloat16); check(Y, "Y", at::kBFloat16);
   check_ks(ks);
-  TORCH_CHECK(Y.dim() == 6 && Y.size(5) == 16, "Y must be [V,I,J,K,L,16]");
-  const int64_t V = Y.size(0), I = Y.size(1), J = Y.size(2), K = Y.size(3), L = Y.size(4);
+  // epi 1 / 2; | 4: the bf16x3 layer -- Xp [2, N, PPL] (hi, lo planes), Wa [2, ks^2, 64, 8]
+  // (hi, lo fragments), Y [2, V,I,J,K,L,16] (hi, lo)
+  const bool x3 = (epi & 4) != 0;
+  const int e = (int)(epi & 3);
+  TORCH_CHECK(e == 1 || e == 2, "conv1x16: epi must be 1 or 2 (| 4 for bf16x3)");
+  const Tensor Y1 = x3 ? Y[0] : Y;
+  TORCH_CHECK(!x3 || (Y.dim() == 7 && Y.size(0) == 2), "conv1x16 x3: Y must be [2,V,I,J,K,L,16]");
+  TORCH_CHECK(Y1.dim() == 6 && Y1.size(5) == 16, "Y must be [V,I,J,K,L,16]");
+  const int64_t V = Y1.size(0), I = Y1.size(1), J = Y1.size(2), K = Y1.size(3), L = Y1.size(4);
   const auto g = pad_geom(K, L, ks);
-  check_shape(Xp, "Xp", {V * I * J, g[1]});
-  check_shape(Wa, "Wa", {ks * ks, 64, 8});
-  TORCH_CHECK(epi == 1 || epi == 2, "conv1x16: epi must be 1 or 2");
-  if (epi == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
-  if (epi == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", {V, I, J, K, L, 16}); }
+  if (x3) { check_shape(Xp, "Xp", {2, V * I * J, g[1]}); check_shape(Wa, "Wa", {2, ks * ks, 64, 8}); }
+  else { check_shape(Xp, "Xp", {V * I * J, g[1]}); check_shape(Wa, "Wa", {ks * ks, 64, 8}); }
+  if (e == 1) { TORCH_CHECK(bias.has_value()); check(*bias, "bias", at::kFloat); check_shape(*bias, "bias", {16}); }
+  if (e == 2) { TORCH_CHECK(M.has_value()); check(*M, "M", at::kBFloat16); check_shape(*M, "M", {V, I, J, K, L, 16}); }
   const int nt = ncnet_set_tuning("nt_store", 0, 0);
+  const long long xlo = x3 ? (long long)V * I * J * g[1] : 0, ylo = x3 ? (long long)Y1.numel() : 0;
   const int r = ncnet_conv1x16(Xp.data_ptr(), Wa.data_ptr(), opt_ptr<float>(bias), opt_ptr<void>(M), Y.data_ptr(),
-                               (int)V, (int)I, (int)J, (int)K, (int)L, (int)ks, (int)epi, nt, cur_stream(Xp));
+                               (int)V, (int)I, (int)J, (int)K, (int)L, (int)ks, (int)epi, nt, xlo, ylo, cur_stream(Xp));
   TORCH_CHECK(r != -1, "conv1x16: no kernel instantiation for ks=", ks, " K=", K, " L=", L, " epi=", epi);
   ok(r, "conv1x16");
   return true;

@@ -48,7 +48,11 @@ __device__ __forceinline__ void xstatic_for(F&& f) {
   }
 }
 
-enum Epi1x { EPI1X_BIAS_RELU = 1, EPI1X_MASK = 2 };
+// EPI1X_X3 (| with either): the fp32-accurate bf16x3 layer of nc_precision='fp32'
+// training: three phases per item, (X_hi, W_hi), (X_lo, W_hi), (X_hi, W_lo),
+// into the same accumulators (X_lo = Xp + xlo, Wa = [hi set; lo set]); the
+// epilogue splits the fp32 result into Y (hi) and Y + ylo (lo).
+enum Epi1x { EPI1X_BIAS_RELU = 1, EPI1X_MASK = 2, EPI1X_X3 = 4 };
 
 template <int KS, int K, int L>
 struct C1X {
@@ -128,10 +132,16 @@ __global__ __launch_bounds__(256) void pad_planes_kernel(const T* __restrict__ x
 template <int KS, int R, int EPI, int K, int L>
 __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict__ Xp, const u32x4* __restrict__ Wa,
                                                           const float* __restrict__ bias, const bf16* __restrict__ M,
-                                                          bf16* __restrict__ Y, int V, int I, int J, int nt_store) {
+                                                          bf16* __restrict__ Y, int V, int I, int J, int nt_store,
+                                                          long long xlo, long long ylo) {
 #if defined(__HIP_DEVICE_COMPILE__)   // device-only body (asm DMA); the host pass keeps the stub
   using C = C1X<KS, K, L>;
   constexpr int P = C::P, NT = C::NT, NW = C::NW, LP = C::LP, PPL = C::PPL, MAXT = C::MAXT;
+  constexpr bool X3 = (EPI & EPI1X_X3) != 0;
+  constexpr int EP = EPI & ~EPI1X_X3;                 // EPI1X_BIAS_RELU or EPI1X_MASK
+  constexpr int PH = X3 ? 3 : 1;                      // phases per item
+  constexpr int SPI = KS * PH;                        // steps per item
+  constexpr int XOFF = PH == 3 ? 2 * NT * 1024 : C::XOFF;   // both weight sets precede the planes
   constexpr int S = R + KS - 1;          // input j-planes per di = one step
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
@@ -145,24 +155,25 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
   const int G = gridDim.x;
   const int bid = blockIdx.x;
   const int my_items = bid < nitems ? (nitems - 1 - bid) / G + 1 : 0;
-  const int nsteps = my_items * KS;
+  const int nsteps = my_items * SPI;
 
   // weights (one KiB per plane offset) by LDS-DMA, before the first plane
-  for (int q = wave; q < NT; q += NW) dma16_lds(Wa + q * 64 + lane, smem + C::WOFF + q * 1024);
+  for (int q = wave; q < (X3 ? 2 : 1) * NT; q += NW) dma16_lds(Wa + q * 64 + lane, smem + C::WOFF + q * 1024);
 
   // step n: item bid + G (n / KS), di = n % KS; its S planes -> ring slot n % 2;
   // wave w DMAs copy w >> 1, half w & 1 of each plane
   const int cpy = wave >> 1, hlf = wave & 1;
   const uint32_t dvo = (uint32_t)((hlf * 64 + lane) * 16 - 2 * (cpy + C::delta(cpy)));   // element e -> e + c + delta
   auto issue = [&](int n) {
-    const int it = bid + G * (n / KS), di = n % KS;
+    const int it = bid + G * (n / SPI), di = (n % SPI) % KS;
     int b = it;
     const int jb = b % njb; b /= njb;
     const int ti = b % I, tv = b / I;
     const int ii = ti + di - P;
     const bool iv = n < nsteps && ii >= 0 && ii < I;
-    const bf16* xrow = Xp + ((size_t)(tv * I + (iv ? ii : 0)) * J) * PPL;
-    const uint32_t slot = lds0 + C::XOFF + (uint32_t)((n & 1) * S * C::SLOTB + cpy * C::COPYB + hlf * 1024);
+    const bf16* xsrc = (X3 && (n % SPI) / KS == 1) ? Xp + xlo : Xp;        // phase 1 reads X_lo
+    const bf16* xrow = xsrc + ((size_t)(tv * I + (iv ? ii : 0)) * J) * PPL;
+    const uint32_t slot = lds0 + XOFF + (uint32_t)((n & 1) * S * C::SLOTB + cpy * C::COPYB + hlf * 1024);
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       const int jp = jb * R - P + u;
@@ -200,7 +211,7 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
         t = (dk - P) * LP + (dl - P);
         c = (4 - ((C::F0 + t) & 3)) & 3;        // re-aligns element F0 + t (+ 16 w + 4 p) to 8 bytes
       }
-      rowoff[h] = (uint32_t)(C::XOFF + c * C::COPYB + (C::F0 + 16 * wave + t + c + C::delta(c) + 4 * p) * 2);
+      rowoff[h] = (uint32_t)(XOFF + c * C::COPYB + (C::F0 + 16 * wave + t + c + C::delta(c) + 4 * p) * 2);
     }
   }
   f32x4 acc[R][MAXT];
@@ -211,11 +222,13 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
 
   const size_t KLs = (size_t)K * L;
   const int co0 = 4 * (lane >> 4);
-  u32x2 mreg[EPI == EPI1X_MASK ? R : 1][EPI == EPI1X_MASK ? MAXT : 1];
+  u32x2 mreg[EP == EPI1X_MASK ? R : 1][EP == EPI1X_MASK ? MAXT : 1];
   f32x4 bv = {0.f, 0.f, 0.f, 0.f};   // this lane's 4 channels' bias, loaded once (not per store)
-  if constexpr (EPI == EPI1X_BIAS_RELU) bv = *(const f32x4*)(bias + co0);
+  if constexpr (EP == EPI1X_BIAS_RELU) bv = *(const f32x4*)(bias + co0);
   for (int n = 0; n < nsteps; ++n) {
-    const int it = bid + G * (n / KS), di = n % KS;
+    const int it = bid + G * (n / SPI), di = (n % SPI) % KS;
+    const bool last = (n % SPI) == SPI - 1;             // the item's last step (last phase, di = KS - 1)
+    const int wset = (X3 && (n % SPI) / KS == 2) ? NT : 0;   // phase 2 multiplies W_lo
     int b = it;
     const int jb = b % njb; b /= njb;
     const int ti = b % I, tv = b / I;
@@ -223,11 +236,11 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
     // this step's planes landed (issued one step ago); the previous step's reads are done
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     issue(n + 1);
-    if constexpr (EPI == EPI1X_MASK) {
+    if constexpr (EP == EPI1X_MASK) {
       // the item's last step: fetch the ReLU mask of its outputs now, so the
       // loads land under this step's MFMAs instead of stalling the epilogue
       // (issued after the DMA: in-order completion keeps the DMA count exact)
-      if (di == KS - 1) {
+      if (last) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int j = j0 + r;
@@ -250,7 +263,7 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
     if (ii >= 0 && ii < I) {
       bf16x8 A[KS];
 #pragma unroll
-      for (int dj = 0; dj < KS; ++dj) A[dj] = lds_read16(smem, C::WOFF + (di * KS + dj) * 1024 + lane * 16);
+      for (int dj = 0; dj < KS; ++dj) A[dj] = lds_read16(smem, C::WOFF + (wset + di * KS + dj) * 1024 + lane * 16);
       const uint32_t sb = (uint32_t)((n & 1) * S * C::SLOTB);
       xstatic_for<0, S>([&](auto sc) {
         constexpr int s = decltype(sc)::value;   // plane j' = j0 - P + s
@@ -281,7 +294,7 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
         }
       });
     }
-    if (di == KS - 1) {
+    if (last) {
       // item done: epilogue (stores are not waited for; the next item's planes are in flight)
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -298,10 +311,10 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               float x = acc[r][tt][q];
-              if constexpr (EPI == EPI1X_BIAS_RELU) x = fmaxf(x + bv[q], 0.f);
+              if constexpr (EP == EPI1X_BIAS_RELU) x = fmaxf(x + bv[q], 0.f);
               o[q] = x;
             }
-            if constexpr (EPI == EPI1X_MASK) {
+            if constexpr (EP == EPI1X_MASK) {
               const bf16x4 m = __builtin_bit_cast(bf16x4, mreg[r][tt]);
 #pragma unroll
               for (int q = 0; q < 4; ++q) o[q] = ((float)m[q] > 0.f) ? o[q] : 0.f;
@@ -311,6 +324,12 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
             for (int q = 0; q < 4; ++q) out[q] = f2bf(o[q]);
             if (nt_store) __builtin_nontemporal_store(__builtin_bit_cast(u32x2, out), (u32x2*)(Y + vox * 16 + co0));
             else *(bf16x4*)(Y + vox * 16 + co0) = out;
+            if constexpr (X3) {
+              bf16x4 lo;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) lo[q] = f2bf(o[q] - bf2f(out[q]));
+              *(bf16x4*)(Y + ylo + vox * 16 + co0) = lo;
+            }
           }
           acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
@@ -589,29 +608,42 @@ static int c1x_num_cus() {
   return ncu;
 }
 
-template <int KS, int K, int L>
+template <int KS, int K, int L, int R = 5>
 static void c1x_launch(int epi, int V, int I, int J, const bf16* x, const u32x4* w, const float* bias, const bf16* m,
-                       bf16* y, int nt_store, hipStream_t s) {
-  constexpr int R = 5;
+                       bf16* y, int nt_store, long long xlo, long long ylo, hipStream_t s) {
   using C = C1X<KS, K, L>;
   const int nitems = V * I * cdiv(J, R);
   dim3 grid((unsigned)std::min(nitems, c1x_num_cus())), block(512);   // persistent: one workgroup per CU
-  const size_t lds = (size_t)C::lds(R + KS - 1, 1);
-  if (epi == EPI1X_BIAS_RELU)
-    hipLaunchKernelGGL((conv1x16_kernel<KS, R, EPI1X_BIAS_RELU, K, L>), grid, block, lds, s, x, w, bias, m, y, V, I, J, nt_store);
-  else
-    hipLaunchKernelGGL((conv1x16_kernel<KS, R, EPI1X_MASK, K, L>), grid, block, lds, s, x, w, bias, m, y, V, I, J, nt_store);
+  // X3: both weight sets ahead of the planes
+  const size_t lds = (size_t)C::lds(R + KS - 1, 1) + ((epi & EPI1X_X3) ? (size_t)C::NT * 1024 : 0);
+#define C1L(E) hipLaunchKernelGGL((conv1x16_kernel<KS, R, E, K, L>), grid, block, lds, s, x, w, bias, m, y, V, I, J, nt_store, xlo, ylo)
+  if (epi == EPI1X_BIAS_RELU) C1L(EPI1X_BIAS_RELU);
+  else if (epi == EPI1X_MASK) C1L(EPI1X_MASK);
+  else if (epi == (EPI1X_BIAS_RELU | EPI1X_X3)) C1L(EPI1X_BIAS_RELU | EPI1X_X3);
+  else C1L(EPI1X_MASK | EPI1X_X3);
+#undef C1L
 }
 
-// returns -1 when the shape has no instantiation
+// returns -1 when the shape has no instantiation.  epi | 4 (EPI1X_X3): the
+// bf16x3 layer (X_lo = Xp + xlo, Wa = [hi; lo] fragment sets, Y_lo = Y + ylo,
+// elements); it runs 3 output j-planes per item (both weight sets in LDS).
 extern "C" int ncnet_conv1x16(const void* Xp, const void* Wa, const float* bias, const void* M, void* Y, int V, int I,
-                              int J, int K, int L, int KS, int epi, int nt_store, hipStream_t s) {
-  if (epi != EPI1X_BIAS_RELU && epi != EPI1X_MASK) return -3;
+                              int J, int K, int L, int KS, int epi, int nt_store, long long xlo, long long ylo,
+                              hipStream_t s) {
+  const int e = epi & ~EPI1X_X3;
+  const bool x3 = (epi & EPI1X_X3) != 0;
+  if (e != EPI1X_BIAS_RELU && e != EPI1X_MASK) return -3;
   const bf16* x = (const bf16*)Xp; const u32x4* w = (const u32x4*)Wa; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
-  if (KS == 5 && K == 25 && L == 25) c1x_launch<5, 25, 25>(epi, V, I, J, x, w, bias, m, y, nt_store, s);
-  else if (KS == 5 && K == 20 && L == 20) c1x_launch<5, 20, 20>(epi, V, I, J, x, w, bias, m, y, nt_store, s);
-  else if (KS == 3 && K == 25 && L == 25) c1x_launch<3, 25, 25>(epi, V, I, J, x, w, bias, m, y, nt_store, s);
-  else return -1;
+  if (KS == 5 && K == 25 && L == 25) {
+    if (x3) c1x_launch<5, 25, 25, 3>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
+    else c1x_launch<5, 25, 25>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
+  } else if (KS == 5 && K == 20 && L == 20) {
+    if (x3) c1x_launch<5, 20, 20, 3>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
+    else c1x_launch<5, 20, 20>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
+  } else if (KS == 3 && K == 25 && L == 25) {
+    if (x3) c1x_launch<3, 25, 25, 3>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
+    else c1x_launch<3, 25, 25>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
+  } else return -1;
   return (int)hipGetLastError();
 }
 

@@ -23,6 +23,8 @@ import time
 import numpy as np
 import torch
 
+from .. import config as _config
+
 from ..ops.loss import weak_loss_from_corr
 from ..parallel.dist import DistContext, GradBucket, all_reduce_mean
 from ..utils.timing import active as active_timer, segment
@@ -150,6 +152,12 @@ class Trainer:
         self.fault_step = fault_step if fault_step is not None else int(os.environ.get("NCNET_FAULT_STEP", "-1"))
         self.prefetch = TrunkPrefetcher(model)
         self.batch_to_device = None       # optional hook: host batch -> device batch (train.py: GPU resize)
+        # NCNET_STEP_PRIORITY: the step's kernels on a high-priority stream, so
+        # the prefetched trunk (default priority) is dispatched only where the
+        # step leaves the chip idle instead of time-slicing its kernels
+        self.hp_stream = None
+        if _config.RUNTIME.step_priority and self.prefetch.enabled:
+            self.hp_stream = torch.cuda.Stream(device=ctx.device, priority=-1)
 
     def _move(self, batch):
         if self.batch_to_device is not None:
@@ -171,6 +179,17 @@ class Trainer:
     def train_step(self, batch, next_batch=None) -> torch.Tensor:
         """One step on ``batch``; ``next_batch`` (already on the device) gets
         its backbone pass queued behind this step (TrunkPrefetcher)."""
+        if self.hp_stream is None:
+            return self._train_step(batch, next_batch)
+        cur = torch.cuda.current_stream(self.hp_stream.device)
+        self.hp_stream.wait_stream(cur)
+        with torch.cuda.stream(self.hp_stream):
+            loss = self._train_step(batch, next_batch)
+        cur.wait_stream(self.hp_stream)
+        loss.record_stream(cur)
+        return loss
+
+    def _train_step(self, batch, next_batch=None) -> torch.Tensor:
         if self.fault_step >= 0 and self.global_step == self.fault_step:
             raise RuntimeError(f"injected fault at step {self.global_step} (NCNET_FAULT_STEP)")
         self.opt.zero_grad(set_to_none=True)

@@ -413,7 +413,9 @@ _SIDE_STREAMS: dict = {}
 def _side_stream(dev: torch.device):
     st = _SIDE_STREAMS.get(dev.index)
     if st is None:
-        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+        # with NCNET_STEP_PRIORITY the whole training step runs at high priority
+        # (engine/trainer.py), its weight-gradient side stream too
+        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev, priority=-1 if _config.RUNTIME.step_priority else 0)
     return st
 
 
@@ -937,6 +939,35 @@ def _split_bf16(t: torch.Tensor, out: torch.Tensor):
     return out
 
 
+def _x3_fast1x_layer(C, ctx, li, kind, w, xin, g, dws, dbs, main, side, shp, ks, cin, cout):
+    """Backward of a 1-channel layer of the fused bf16x3 stack on the padded-plane
+    kernels: the weight gradient as the three wgrad1x16 products (X_hi G_hi +
+    X_hi G_lo + X_lo G_hi), the last layer's data gradient as conv1x16's
+    bf16x3 mode with the ReLU mask of its input.  ``g`` [2, 2V, ...(, 16)]: the
+    hi / lo gradient w.r.t. the layer's pre-activation.  Returns the next
+    (lower) layer's pre-activation gradient, or None after the first layer."""
+    V, I, J, K, L = ctx.dims
+    if kind == "1out":
+        n = g.shape[1]
+        gp = torch.zeros((2, n * I * J) + (C.pad_geom(K, L, ks)[1],), dtype=torch.bfloat16, device=g.device)
+        for h in range(2):
+            _pad_1ch(g[h].reshape(n, I * J, K * L), K, L, ks, 0, out=gp[h])
+        with _OnSide(main, side, (xin, g, gp)):
+            R = sum(_wgrad1x(C, xin[a], gp[b], ks, False)[0] for a, b in ((0, 0), (0, 1), (1, 0)))
+            Rf = R[:, :, :cin].reshape((ks,) * 4 + (cin,)).flip(0, 1, 2, 3)
+            dws[li] = Rf.permute(2, 4, 3, 0, 1).unsqueeze(1).contiguous()
+            dbs[li] = (g[0].sum(dtype=torch.float32) + g[1].sum(dtype=torch.float32)).reshape(1)
+        gn = torch.empty((2,) + tuple(shp) + (16,), dtype=torch.bfloat16, device=g.device)
+        C.conv1x16(gp, _pack2(pack_w1x, transpose_for_dgrad(w)), None, xin[0], gn, ks, 2 | 4)
+        return gn
+    # first layer: xin = padded planes of the NC input [2, N, PPL]; g [2, 2V, ..., 16]
+    parts = [_wgrad1x(C, g[a], xin[b], ks, b == 0) for a, b in ((0, 0), (1, 0), (0, 1))]
+    R = parts[0][0] + parts[1][0] + parts[2][0]
+    dws[li] = R[:, :, :cout].reshape((ks,) * 4 + (cout,)).permute(2, 4, 3, 0, 1).unsqueeze(2).contiguous()
+    dbs[li] = (parts[0][1] + parts[1][1])[:cout]
+    return None
+
+
 class NeighConsensusX3FusedFn(torch.autograd.Function):
     """fp32-accurate TRAINING NeighConsensus (symmetric, square volumes) on the
     fused bf16x3 kernels; same math as NeighConsensusX3Fn."""
@@ -948,18 +979,33 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
         bs = params[1::2]
         V, _, I, J, K, L = x.shape
         R, Cc = I * J, K * L
-        x0 = x.reshape(V, I, J, K, L).float()
-        x0 = torch.cat((x0, x0.permute(0, 3, 4, 1, 2)), 0)      # both symmetric branches
-        shp = tuple(x0.shape)
-        dev = x.device
-        xsp = torch.empty((2,) + shp, dtype=torch.bfloat16, device=dev)
-        _split_bf16(x0, xsp)
-        del x0
         ks0 = ws[0].shape[-1]
-        xs = torch.empty((2, ij_groups(ks0)) + shp + (16,), dtype=torch.bfloat16, device=dev)
-        C.ijpack(xsp[0], xs[0], ks0, 1)
-        C.ijpack(xsp[1], xs[1], ks0, 1)
-        del xsp
+        dev = x.device
+        fast = fast1x_ok(kinds, channels, [w.shape[-1] for w in ws], x, True)
+        if fast:
+            # padded 1-channel planes of hi and lo, both branches (the swapped
+            # one written by pad_planes trans=1): the conv1x16 / wgrad1x16 path
+            x3 = x.reshape(V, R, Cc).float()
+            hi = x3.to(torch.bfloat16)
+            lo = (x3 - hi.float()).to(torch.bfloat16)
+            _, ppl = C.pad_geom(K, L, ks0)
+            xs = torch.zeros((2, 2 * V * R, ppl), dtype=torch.bfloat16, device=dev)
+            for t, part in ((hi, xs[0]), (lo, xs[1])):
+                _pad_1ch(t, K, L, ks0, 0, out=part[:V * R])
+                _pad_1ch(t, I, J, ks0, 1, out=part[V * R:])
+            del x3, hi, lo
+            shp = (2 * V, I, J, K, L)
+        else:
+            x0 = x.reshape(V, I, J, K, L).float()
+            x0 = torch.cat((x0, x0.permute(0, 3, 4, 1, 2)), 0)      # both symmetric branches
+            shp = tuple(x0.shape)
+            xsp = torch.empty((2,) + shp, dtype=torch.bfloat16, device=dev)
+            _split_bf16(x0, xsp)
+            del x0
+            xs = torch.empty((2, ij_groups(ks0)) + shp + (16,), dtype=torch.bfloat16, device=dev)
+            C.ijpack(xsp[0], xs[0], ks0, 1)
+            C.ijpack(xsp[1], xs[1], ks0, 1)
+            del xsp
         saved = [xs]
         h = None
         for li, kind in enumerate(kinds):
@@ -972,7 +1018,9 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
                 h = y
                 break
             a = torch.empty((2,) + shp + (16,), dtype=torch.bfloat16, device=dev)
-            if kind == "1in":
+            if kind == "1in" and fast:
+                C.conv1x16(xs, _pack2(pack_w1x, w), _pad_bias(b, 16), None, a, ks, 1 | 4)
+            elif kind == "1in":
                 C.conv16_fwd_x3(xs[0], xs[1], _pack2(lambda t: pack_w16_planes(ij_in_weights(t)), w),
                                 _pad_bias(b, 16), None, a[0], a[1], ks, 1)
             else:
@@ -982,7 +1030,7 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
         z = h                                                      # [2V, I, J, K, L] fp32 (ReLU'd)
         y = torch.empty((V, I, J, K, L), dtype=torch.float32, device=dev)
         C.combine_fwd(z.reshape(-1), y, R, Cc)
-        ctx.kinds, ctx.channels, ctx.dims = kinds, channels, (V, I, J, K, L)
+        ctx.kinds, ctx.channels, ctx.dims, ctx.fast1x = kinds, channels, (V, I, J, K, L), fast
         ctx.save_for_backward(z, *params, *saved)
         return y.reshape(V, 1, I, J, K, L)
 
@@ -1015,6 +1063,17 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
             cin = 1 if li == 0 else channels[li - 1]
             xin = xs if li == 0 else acts[li - 1]                     # [2, (G,) 2V, ..., 16]
             gs = None
+            if ctx.fast1x and kind in ("1in", "1out"):
+                gn = _x3_fast1x_layer(C, ctx, li, kind, w, xin, g, dws, dbs, main, side, shp, ks, cin, cout)
+                if li == 0:
+                    if ctx.needs_input_grad[0]:
+                        wt = transpose_for_dgrad(w)
+                        gx = (conv_layer(g[0:1], _wsplit(wt)[0], cout, 1, relu=False)
+                              + conv_layer(g[0:1], _wsplit(wt)[1], cout, 1, relu=False)
+                              + conv_layer(g[1:2], _wsplit(wt)[0], cout, 1, relu=False))
+                    break
+                g = gn
+                continue
             if kind == "1out":
                 gs = torch.empty((2, ij_groups(ks)) + shp + (16,), dtype=torch.bfloat16, device=dev)
                 C.ijpack(g[0], gs[0], ks, -1)

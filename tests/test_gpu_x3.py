@@ -35,6 +35,8 @@ def _params(ks, ch, seed, masked=False):
 
 
 @pytest.mark.parametrize("ks,ch,shape", [((5, 5, 5), (16, 16, 1), (1, 1, 25, 25, 25, 25)),
+                                         ((5, 5, 5), (16, 16, 1), (1, 1, 20, 20, 20, 20)),
+                                         ((3, 3), (16, 1), (1, 1, 25, 25, 25, 25)),
                                          ((5, 5, 5), (16, 16, 1), (2, 1, 9, 7, 9, 7)),
                                          ((3, 3), (16, 1), (2, 1, 8, 11, 8, 11)),
                                          ((3, 3, 3), (10, 10, 1), (1, 1, 6, 6, 6, 6))])
@@ -46,6 +48,7 @@ def test_x3_fused_matches_fp64(ks, ch, shape):
     # the symmetric fold gx[:V] + gx[V:]^T) runs with --fe_finetune_params
     x = torch.rand(shape, device="cuda").requires_grad_(True)
     n0 = _ext.DISPATCH["nc_x3_fused"]
+    # 25 x 25 / 20 x 20 planes: the 1-channel layers on conv1x16's bf16x3 mode and wgrad1x16
     y = neigh_consensus(x, ws, bs, list(ch), symmetric=True, precision="fp32")
     assert _ext.DISPATCH["nc_x3_fused"] == n0 + 1
     gy = torch.rand_like(y)
