@@ -153,7 +153,7 @@ class PairMatcher:
             return self._eager(fa, hwa, fb, hwb)
         # the graph bakes in the NC weights it was captured with (e.g. the
         # cached fp8 quantisation): a weight update must re-capture
-        wver = tuple((id(p), p._version) for p in self.model.parameters())
+        wver = tuple((id(p), 0 if p.is_inference() else p._version) for p in self.model.parameters())
         key = (tuple(fa.shape), tuple(fb.shape), fa.dtype, tuple(hwa), tuple(hwb), wver)
         ent = self._graphs.get(key)
         if ent is None:

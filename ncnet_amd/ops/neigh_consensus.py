@@ -1170,11 +1170,12 @@ def _fp8_weights_of(w_ref: torch.Tensor, kind: str):
     if per is None:
         per = _FP8_W_CACHE[w_ref] = {}
     ent = per.get(kind)
-    if ent is None or ent[0] != w_ref._version or ent[1] != tuple(w_ref.shape):
+    ver = 0 if w_ref.is_inference() else w_ref._version      # inference tensors are immutable
+    if ent is None or ent[0] != ver or ent[1] != tuple(w_ref.shape):
         w = _std(w_ref)
         packed = {"1in": lambda: pack_w16_planes(ij_in_weights(w)), "16": lambda: pack_w16(w),
                   "1out": lambda: pack_w16_planes(ij_out_weights(w))}[kind]()
-        ent = per[kind] = (w_ref._version, tuple(w_ref.shape), _fp8_weights(packed))
+        ent = per[kind] = (ver, tuple(w_ref.shape), _fp8_weights(packed))
     if _FP8_PINS is not None:
         _FP8_PINS.append(ent[2][0])
     return ent[2]
