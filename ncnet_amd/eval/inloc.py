@@ -136,6 +136,7 @@ class PairMatcher:
         self.kw = dict(do_softmax=do_softmax, both_dirs=both_dirs, flip=flip)
         self.use_graph = (os.environ.get("NCNET_PAIR_GRAPH", "1") != "0") if use_graph is None else use_graph
         self._graphs = {}
+        self._nc_params = None
         self.capture_error = None
 
     @property
@@ -153,7 +154,10 @@ class PairMatcher:
             return self._eager(fa, hwa, fb, hwb)
         # the graph bakes in the NC weights it was captured with (e.g. the
         # cached fp8 quantisation): a weight update must re-capture
-        wver = tuple((id(p), 0 if p.is_inference() else p._version) for p in self.model.parameters())
+        # (only the NeighConsensus weights enter the graph; ~6 tensors, cheap per pair)
+        if self._nc_params is None:
+            self._nc_params = list(self.model.NeighConsensus.parameters())
+        wver = tuple(0 if p.is_inference() else p._version for p in self._nc_params)
         key = (tuple(fa.shape), tuple(fb.shape), fa.dtype, tuple(hwa), tuple(hwb), wver)
         ent = self._graphs.get(key)
         if ent is None:
