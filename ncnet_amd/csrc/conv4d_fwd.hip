@@ -1030,42 +1030,49 @@ static ConvGeom make_geom(int V, int I, int J, int K, int L, int KS, int tk, int
 
 using namespace ncnet;
 
-// conv16v4 at the compile-time whole-plane tiles it is instantiated for: the
-// --image_size 240 / 320 / 400 training planes (15, 20, 25) at KS 5 and KS 3.
-template <int KS, int T>
+// conv16v4 at the compile-time tiles it is instantiated for: the
+// --image_size 240 / 320 / 400 training planes (15, 20, 25: one whole-plane
+// tile) and 480 (30 x 30: two 30 x 15 tiles) at KS 5 and KS 3.
+template <int KS, int TK, int TL>
 static void v4_launch1(int epi, dim3 grid, dim3 block, hipStream_t stream, const bf16* x, const u32x4* w,
                        const float* bias, const bf16* m, bf16* y, const ConvGeom& g) {
   constexpr int R = 5, NQ = (KS * KS + 1) / 2;
-  const size_t lds = 3 * (size_t)(T + KS - 1) * (T + ((KS - 1 + 7) / 8) * 8) * 32 + (size_t)KS * NQ * 1024 + 1024;
-#define L16V4(EPIV) hipLaunchKernelGGL((conv16v4_fwd_kernel<KS, R, EPIV, T, T>), grid, block, lds, stream, x, w, bias, m, y, g)
-  if (epi == EPI_BIAS_RELU) L16V4(EPI_BIAS_RELU);
-  else if (epi == EPI_MASK) L16V4(EPI_MASK);
-  else if (epi == (EPI_BIAS_RELU | EPI_X3)) L16V4(EPI_BIAS_RELU | EPI_X3);
-  else L16V4(EPI_MASK | EPI_X3);
-#undef L16V4
+  const size_t lds = 3 * (size_t)(TK + KS - 1) * (TL + ((KS - 1 + 7) / 8) * 8) * 32 + (size_t)KS * NQ * 1024 + 1024;
+  auto go = [&](auto ec) {
+    constexpr int E = decltype(ec)::value;
+    hipLaunchKernelGGL((conv16v4_fwd_kernel<KS, R, E, TK, TL>), grid, block, lds, stream, x, w, bias, m, y, g);
+  };
+  if (epi == EPI_BIAS_RELU) go(std::integral_constant<int, EPI_BIAS_RELU>{});
+  else if (epi == EPI_MASK) go(std::integral_constant<int, EPI_MASK>{});
+  else if (epi == (EPI_BIAS_RELU | EPI_X3)) go(std::integral_constant<int, EPI_BIAS_RELU | EPI_X3>{});
+  else go(std::integral_constant<int, EPI_MASK | EPI_X3>{});
 }
-static bool v4_launch(int KS, int K, int epi, dim3 grid, dim3 block, hipStream_t stream, const bf16* x,
-                      const u32x4* w, const float* bias, const bf16* m, bf16* y, const ConvGeom& g) {
-  if (KS == 5) {
-    if (K == 25) v4_launch1<5, 25>(epi, grid, block, stream, x, w, bias, m, y, g);
-    else if (K == 20) v4_launch1<5, 20>(epi, grid, block, stream, x, w, bias, m, y, g);
-    else if (K == 15) v4_launch1<5, 15>(epi, grid, block, stream, x, w, bias, m, y, g);
-    else return false;
-    return true;
-  }
-  if (KS == 3) {
-    if (K == 25) v4_launch1<3, 25>(epi, grid, block, stream, x, w, bias, m, y, g);
-    else if (K == 20) v4_launch1<3, 20>(epi, grid, block, stream, x, w, bias, m, y, g);
-    else if (K == 15) v4_launch1<3, 15>(epi, grid, block, stream, x, w, bias, m, y, g);
-    else return false;
-    return true;
-  }
+template <int KS>
+static bool v4_launch_ks(int K, int L, int tk, int tl, int epi, dim3 grid, dim3 block, hipStream_t stream,
+                         const bf16* x, const u32x4* w, const float* bias, const bf16* m, bf16* y, const ConvGeom& g) {
+  if (K != L) return false;
+  if (K == 25 && tk == 25 && tl == 25) v4_launch1<KS, 25, 25>(epi, grid, block, stream, x, w, bias, m, y, g);
+  else if (K == 20 && tk == 20 && tl == 20) v4_launch1<KS, 20, 20>(epi, grid, block, stream, x, w, bias, m, y, g);
+  else if (K == 15 && tk == 15 && tl == 15) v4_launch1<KS, 15, 15>(epi, grid, block, stream, x, w, bias, m, y, g);
+  else if (K == 30 && tk == 30 && tl == 15) v4_launch1<KS, 30, 15>(epi, grid, block, stream, x, w, bias, m, y, g);
+  else return false;
+  return true;
+}
+static bool v4_launch(int KS, int K, int L, int tk, int tl, int epi, dim3 grid, dim3 block, hipStream_t stream,
+                      const bf16* x, const u32x4* w, const float* bias, const bf16* m, bf16* y, const ConvGeom& g) {
+  if (KS == 5) return v4_launch_ks<5>(K, L, tk, tl, epi, grid, block, stream, x, w, bias, m, y, g);
+  if (KS == 3) return v4_launch_ks<3>(K, L, tk, tl, epi, grid, block, stream, x, w, bias, m, y, g);
   return false;
 }
 
-// Tile choice: the whole (k,l) plane when it fits (<= 25 x 25 output), else
-// 25 x 25 tiles (InLoc-size planes).
+// Tile choice: the whole (k,l) plane when it fits (<= 25 x 25 output); planes
+// up to 32 x 32 (--image_size 480: 30 x 30) split into two K x ceil(L / 2)
+// tiles (a 25 x 25 tile on a 30 x 30 plane left 4 tiles of 2500 voxel slots
+// for 900 voxels); else 25 x 25 tiles (InLoc-size planes).
 static void pick_tile(int K, int L, int& tk, int& tl) {
+  if (K > 25 || L > 25) {
+    if (K <= 32 && L <= 32) { tk = K; tl = (L + 1) / 2; return; }
+  }
   tk = K <= 25 ? K : 25;
   tl = L <= 25 ? L : 25;
   // keep TK*TL <= 640 (MAXT * 8 waves * 16 voxels)
@@ -1114,7 +1121,7 @@ extern "C" int ncnet_conv16_fwd(const void* X, const void* Wp, const float* bias
     const int njb1 = g.njb;
     g.njb = cdiv(J, R);
     dim3 grid3((unsigned)(V * I * g.njb * g.nkt * g.nlt)), block3(512);
-    if (tk == K && tl == L && !tuning().conv_v3 && v4_launch(KS, K, epi, grid3, block3, stream, x, w, bias, m, y, g))
+    if (!tuning().conv_v3 && v4_launch(KS, K, L, tk, tl, epi, grid3, block3, stream, x, w, bias, m, y, g))
       return (int)hipGetLastError();
     g.njb = njb1;
     if (x3) goto v2_x3;   // other shapes: the v2 kernel's phases

@@ -513,11 +513,12 @@ struct W4C {
   static constexpr int NS = 2 * P + 3;                   // G ring slots (2 steps ahead)
   static constexpr int GOFF = 0, ZOFF = NS * GB, XOFF = ZOFF + GB, TRASH = XOFF + 3 * XB;
   static constexpr int LDS = TRASH + 1024;
-  static constexpr int RPW = (PR + NW - 1) / NW;         // X row DMAs per wave per step
+  static constexpr int RPW = (PR + NW - 1) / NW;         // X rows per wave per step
+  static constexpr int XI = (RW + 31) / 32;              // DMA wave-instructions per row (32 voxels each)
   static constexpr int GQ = GB / 1024;                   // 1-KiB G chunks per tile
   static constexpr int GPW = (GQ + NW - 1) / NW;         // G DMAs per wave per step
   static_assert((NT - 1) % 4 == 0, "NT must be 1 mod 4");
-  static_assert(RW <= 32, "one DMA wave-instruction per staged row");
+  static_assert(XI <= 2, "at most two DMA wave-instructions per staged row");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -574,15 +575,19 @@ __device__ __forceinline__ void wgrad16v4_body(const bf16* __restrict__ X, const
 
   // ---- loaders ------------------------------------------------------------
   const int gq = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-  // X: rows kf - P .. kf - P + PR - 1 of plane (v, ii, jj), col 0 <-> l = -P
-  uint32_t xvo[RPW];
+  // X: rows kf - P .. kf - P + PR - 1 of plane (v, ii, jj), col 0 <-> l = -P;
+  // instruction h of a row covers its voxels 32 h .. 32 h + 31
+  constexpr int XI = C::XI;
+  uint32_t xvo[RPW][XI];
   auto set_xvo = [&](int kf) {
 #pragma unroll
-    for (int m = 0; m < RPW; ++m) {
-      const int r = wave + NW * m, kg = kf - P + r, l = (lane >> 1) - P;
-      const bool ok = r < PR && kg >= 0 && kg < K && l >= 0 && l < L && (lane >> 1) < C::RW;
-      xvo[m] = ok ? (uint32_t)(((kg * L + l) * 16 + (lane & 1) * 8) * 2) : 0x7ffffff0u;
-    }
+    for (int m = 0; m < RPW; ++m)
+#pragma unroll
+      for (int h = 0; h < XI; ++h) {
+        const int r = wave + NW * m, kg = kf - P + r, c = (lane >> 1) + 32 * h, l = c - P;
+        const bool ok = r < PR && kg >= 0 && kg < K && l >= 0 && l < L && c < C::RW;
+        xvo[m][h] = ok ? (uint32_t)(((kg * L + l) * 16 + (lane & 1) * 8) * 2) : 0x7ffffff0u;
+      }
   };
   // loader cursors keep their column decoded (a plane pointer at ii = 0 and the
   // plane stride): the runtime divisions run once per column, not per step
@@ -602,8 +607,11 @@ __device__ __forceinline__ void wgrad16v4_body(const bf16* __restrict__ X, const
 #pragma unroll
     for (int m = 0; m < RPW; ++m) {
       const int r = wave + NW * m;
-      // lanes past a row stride RS < 32 would overwrite the next row: off (count unchanged)
-      if (RS >= 32 || (lane >> 1) < RS) bdma16_lds(rs, xvo[m], r < PR ? xb + (uint32_t)(r * RS * 32) : lds0 + C::TRASH);
+      // lanes past the row stride would overwrite the next row: off (count unchanged)
+#pragma unroll
+      for (int h = 0; h < XI; ++h)
+        if (RS >= 32 * (h + 1) || (lane >> 1) + 32 * h < RS)
+          bdma16_lds(rs, xvo[m][h], r < PR ? xb + (uint32_t)((r * RS + 32 * h) * 32) : lds0 + C::TRASH);
     }
     ++xl_n;
     if (++xl_ii == g.I) {
@@ -671,7 +679,7 @@ __device__ __forceinline__ void wgrad16v4_body(const bf16* __restrict__ X, const
   for (int n = 0; n < nsteps; ++n) {
     // plane n and G tile n + P landed (issued two steps ago); only the previous
     // step's RPW + GPW DMAs may still be in flight; previous step's reads done
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(RPW + GPW) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(RPW * XI + GPW) : "memory");
     issue_x();
     issue_g();
     const uint32_t xb = (uint32_t)(C::XOFF + (n % 3) * XB);
@@ -1001,6 +1009,8 @@ static bool w4_launch(int KS, int K, dim3 grid, dim3 block, hipStream_t stream, 
   else if (KS == 3 && K == 25) w4_launch1<3, 25>(grid, block, stream, x, gg, part, partb, g);
   else if (KS == 3 && K == 20) w4_launch1<3, 20>(grid, block, stream, x, gg, part, partb, g);
   else if (KS == 3 && K == 15) w4_launch1<3, 15>(grid, block, stream, x, gg, part, partb, g);
+  else if (KS == 5 && K == 30) w4_launch1<5, 30>(grid, block, stream, x, gg, part, partb, g);   // rows of 34 voxels: 2 DMAs
+  else if (KS == 3 && K == 30) w4_launch1<3, 30>(grid, block, stream, x, gg, part, partb, g);
   else return false;
   return true;
 }
@@ -1021,11 +1031,11 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
   g.ncols = V * J * g.ntl;
   g.cpg = cdiv(g.ncols, ngroups);
   g.flags = tuning().wgrad_flags;
-  if (g.RW > 32) return -1;                 // one wave-instruction per staged row
   if (g.VT > 384) return -1;                // <= 6 chunks per half
   if (K == L && !tuning().wgrad_v3 && w4_launch(KS, K, dim3((unsigned)(KS * ngroups)), dim3(512), stream,
                                                  (const bf16*)X, (const bf16*)G, part, partb, g))
-    return (int)hipGetLastError();   // compile-time planes of the training sizes (--image_size 240 / 320 / 400)
+    return (int)hipGetLastError();   // compile-time planes of the training sizes (--image_size 240 / 320 / 400 / 480)
+  if (g.RW > 32) return -1;                 // v3: one wave-instruction per staged row
   // wgrad16v3<5, NCH> spills at NCH 3, 4, 6 (256 VGPRs of accumulators and
   // double-buffered fragments): split the plane into more, smaller tiles until
   // the chunk count is 1, 2 or 5 (mirrored in ops/neigh_consensus.py wgrad_v3_ntl)

@@ -69,12 +69,17 @@ def layer_kinds(channels, kernel_sizes):
     return kinds
 
 
+_V4_PLANES = {5: (15, 20, 25, 30), 3: (15, 20, 25, 30)}     # wgrad16v4 instantiations (K == L)
+
+
 def wgrad_v3_ok(shape, ks: int) -> bool:
-    """wgrad16v3 (sliding G ring): KS 3/5, full-width X rows L + ks - 1 <= 32."""
-    return ks in (3, 5) and shape[4] + ks - 1 <= 32
-
-
-_V4_PLANES = {5: (15, 20, 25), 3: (15, 20, 25)}     # wgrad16v4 instantiations (K == L)
+    """wgrad16v3 (sliding G ring): KS 3/5, full-width X rows L + ks - 1 <= 32;
+    or a compile-time wgrad16v4 plane (30 x 30 stages its 34-voxel rows with
+    two DMA instructions)."""
+    if ks not in (3, 5):
+        return False
+    K, L = shape[3], shape[4]
+    return L + ks - 1 <= 32 or (K == L and K in _V4_PLANES[ks])
 
 
 def wgrad_v3_ntl(K: int, L: int, ks: int) -> int:
