@@ -77,7 +77,8 @@ struct C1X {
   // reads for real voxels stay inside their copy; junk columns / tiles may read
   // past it into the next copy (finite data) or into the LDS tail pad
   static_assert(FN - 1 + P * LP + P + 3 + 44 < COPYB / 2, "real-voxel tap reads stay inside one copy");
-  static_assert(COPYB > 1024 && COPYB <= 2048, "two DMA wave-instructions per copy");
+  static constexpr int NCH = (COPYB + 1023) / 1024;           // DMA wave-instructions per copy (2 or 3)
+  static_assert(COPYB > 1024 && COPYB <= 3072, "two or three DMA wave-instructions per copy");
 };
 
 // zero-padded planes (see the file comment): Y[n][(k+P)*LP + l + P] = X[n][k][l]
@@ -161,9 +162,20 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
   for (int q = wave; q < (X3 ? 2 : 1) * NT; q += NW) dma16_lds(Wa + q * 64 + lane, smem + C::WOFF + q * 1024);
 
   // step n: item bid + G (n / KS), di = n % KS; its S planes -> ring slot n % 2;
-  // wave w DMAs copy w >> 1, half w & 1 of each plane
-  const int cpy = wave >> 1, hlf = wave & 1;
-  const uint32_t dvo = (uint32_t)((hlf * 64 + lane) * 16 - 2 * (cpy + C::delta(cpy)));   // element e -> e + c + delta
+  // a plane is 4 copies x NCH KiB-chunks; wave w DMAs chunks w, w + 8, ... of
+  // each plane (NCH 2: copy w >> 1, half w & 1)
+  constexpr int NCH = C::NCH, NJ = 4 * NCH, JPW = (NJ + NW - 1) / NW;
+  uint32_t dvo[JPW], doff[JPW];
+  bool jon[JPW];
+#pragma unroll
+  for (int m = 0; m < JPW; ++m) {
+    const int jb = wave + NW * m, cpy = jb / NCH, prt = jb - cpy * NCH;
+    dvo[m] = (uint32_t)((prt * 64 + lane) * 16 - 2 * (cpy + C::delta(cpy)));   // element e -> e + c + delta
+    doff[m] = (uint32_t)(cpy * C::COPYB + prt * 1024);
+    // the last KiB of a copy is partial: its lanes past the copy stay off
+    // (exec never empty, so the instruction -- and the vmcnt count -- is fixed)
+    jon[m] = jb < NJ && (prt < NCH - 1 || lane < C::COPYB / 16 - 64 * (NCH - 1));
+  }
   auto issue = [&](int n) {
     const int it = bid + G * (n / SPI), di = (n % SPI) % KS;
     int b = it;
@@ -173,7 +185,7 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
     const bool iv = n < nsteps && ii >= 0 && ii < I;
     const bf16* xsrc = (X3 && (n % SPI) / KS == 1) ? Xp + xlo : Xp;        // phase 1 reads X_lo
     const bf16* xrow = xsrc + ((size_t)(tv * I + (iv ? ii : 0)) * J) * PPL;
-    const uint32_t slot = lds0 + XOFF + (uint32_t)((n & 1) * S * C::SLOTB + cpy * C::COPYB + hlf * 1024);
+    const uint32_t slot = lds0 + XOFF + (uint32_t)((n & 1) * S * C::SLOTB);
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       const int jp = jb * R - P + u;
@@ -185,13 +197,14 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
       rs[1] = (int)((uint32_t)(pb >> 32) & 0xffffu);
       rs[2] = pv ? PPL * 2 : 0;
       rs[3] = 0x00020000;
-      const uint32_t d = slot + (uint32_t)(u * C::SLOTB);
-      // the second KiB of a copy is partial: its lanes past the copy stay off
-      // (exec never empty, so the instruction -- and the vmcnt count -- is fixed)
-      if (hlf == 0 || lane < C::COPYB / 16 - 64)
-        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(dvo), "s"(rs),
-                     "s"(d)
-                     : "memory", "m0");
+#pragma unroll
+      for (int m = 0; m < JPW; ++m) {
+        const uint32_t d = slot + (uint32_t)(u * C::SLOTB) + doff[m];
+        if (jon[m])
+          asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(dvo[m]), "s"(rs),
+                       "s"(d)
+                       : "memory", "m0");
+      }
     }
   };
   issue(0);
@@ -391,8 +404,9 @@ struct W1X {
   static constexpr int LDS = XOFF + KS * NCOL * XS;
   static constexpr int NTW = (NT + 1) / 2;                    // taps per wave half
   static constexpr int NU = (NQC + 3) / 4;                    // chunks per wave (upper bound)
-  static constexpr int XDMA2 = (QN * 2 - 1024) / 16;          // lanes of an X1 plane's second DMA
-  static_assert(QN * 2 > 1024 && QN * 2 <= 2048, "two DMA wave-instructions per X1 plane");
+  static constexpr int NXD = (QN * 2 + 1023) / 1024;          // DMA wave-instructions per X1 plane (2 or 3)
+  static constexpr int XDMAL = (QN * 2 - (NXD - 1) * 1024) / 16;   // lanes of an X1 plane's last DMA
+  static_assert(QN * 2 > 1024 && QN * 2 <= 3072, "two or three DMA wave-instructions per X1 plane");
   static_assert(L * 32 % 16 == 0 && L * 2 <= 64, "one DMA wave-instruction per D row");
   static_assert(NT * 32 * 16 * 4 + 64 <= LDS, "reduction scratch fits the staging buffers");
   static_assert(LDS <= 160 * 1024, "LDS");
@@ -428,7 +442,7 @@ __global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restric
     const uint32_t d = __builtin_amdgcn_readfirstlane(
         lds0 + (uint32_t)(C::XOFF + (di * NCOL + (jc + P + NCOL) % NCOL) * C::XS + half * 1024));
     const uint32_t vo = (uint32_t)(half * 1024 + lane * 16);
-    if (half == 0 || lane < C::XDMA2)
+    if (half < C::NXD - 1 || lane < C::XDMAL)
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(vo), "s"(rs), "s"(d)
                    : "memory", "m0");
   };
@@ -443,14 +457,14 @@ __global__ __launch_bounds__(512, 1) void wgrad1x16_kernel(const bf16* __restric
   };
   auto issue_x_all = [&](int t) {                               // the KS x KS neighbourhood of step t
     const int vi = t / J, j = t - vi * J, v = vi / I, i = vi - v * I;
-    for (int e = wave; e < 2 * NT; e += NW) {
-      const int pl = e >> 1;
-      dma_x(v, i, pl / KS, j - P + pl % KS, e & 1);
+    for (int e = wave; e < C::NXD * NT; e += NW) {
+      const int pl = e / C::NXD;
+      dma_x(v, i, pl / KS, j - P + pl % KS, e - pl * C::NXD);
     }
   };
   auto issue_x_col = [&](int t) {                               // the new column j + P of step t
     const int vi = t / J, j = t - vi * J, v = vi / I, i = vi - v * I;
-    for (int e = wave; e < 2 * KS; e += NW) dma_x(v, i, e >> 1, j + P, e & 1);
+    for (int e = wave; e < C::NXD * KS; e += NW) dma_x(v, i, e / C::NXD, j + P, e % C::NXD);
   };
 
   // zero both D buffers once: margins, pad columns and the tail stay zero (the DMA writes rows only)
@@ -594,10 +608,11 @@ extern "C" int ncnet_pad_planes(const void* x, int x_is_bf16, void* y, int V, in
   return (int)hipGetLastError();
 }
 
-// conv1x16 / wgrad1x16 are instantiated for the training planes whose padded
-// geometry fits their two-DMA-per-copy staging: KS 5 at 25 x 25 (400 px) and
-// 20 x 20 (320 px), KS 3 at 25 x 25 (the IVD recipe, NC 3,3 / 16,1).  Mirrored
-// in ops/neigh_consensus.py FAST1X_SHAPES.
+// conv1x16 / wgrad1x16 are instantiated for the training planes: KS 5 at 25 x 25
+// (400 px), 20 x 20 (320 px) and 30 x 30 (480 px: three DMAs per staged copy,
+// 3 output j-planes per item -- 1 in the bf16x3 mode -- to fit LDS), KS 3 at
+// 25 x 25 (the IVD recipe, NC 3,3 / 16,1).  Mirrored in
+// ops/neigh_consensus.py FAST1X_SHAPES.
 static int c1x_num_cus() {
   static int ncu = 0;
   if (ncu == 0) {
@@ -608,20 +623,26 @@ static int c1x_num_cus() {
   return ncu;
 }
 
-template <int KS, int K, int L, int R = 5>
+template <int KS, int K, int L, int R, bool X3>
 static void c1x_launch(int epi, int V, int I, int J, const bf16* x, const u32x4* w, const float* bias, const bf16* m,
                        bf16* y, int nt_store, long long xlo, long long ylo, hipStream_t s) {
   using C = C1X<KS, K, L>;
   const int nitems = V * I * cdiv(J, R);
   dim3 grid((unsigned)std::min(nitems, c1x_num_cus())), block(512);   // persistent: one workgroup per CU
   // X3: both weight sets ahead of the planes
-  const size_t lds = (size_t)C::lds(R + KS - 1, 1) + ((epi & EPI1X_X3) ? (size_t)C::NT * 1024 : 0);
-#define C1L(E) hipLaunchKernelGGL((conv1x16_kernel<KS, R, E, K, L>), grid, block, lds, s, x, w, bias, m, y, V, I, J, nt_store, xlo, ylo)
-  if (epi == EPI1X_BIAS_RELU) C1L(EPI1X_BIAS_RELU);
-  else if (epi == EPI1X_MASK) C1L(EPI1X_MASK);
-  else if (epi == (EPI1X_BIAS_RELU | EPI1X_X3)) C1L(EPI1X_BIAS_RELU | EPI1X_X3);
-  else C1L(EPI1X_MASK | EPI1X_X3);
-#undef C1L
+  constexpr size_t lds = (size_t)C::lds(R + KS - 1, 1) + (X3 ? (size_t)C::NT * 1024 : 0);
+  static_assert(lds <= 160 * 1024, "LDS");
+  auto go = [&](auto ec) {
+    constexpr int E = decltype(ec)::value;
+    hipLaunchKernelGGL((conv1x16_kernel<KS, R, E, K, L>), grid, block, lds, s, x, w, bias, m, y, V, I, J, nt_store, xlo, ylo);
+  };
+  if constexpr (X3) {
+    if ((epi & ~EPI1X_X3) == EPI1X_BIAS_RELU) go(std::integral_constant<int, EPI1X_BIAS_RELU | EPI1X_X3>{});
+    else go(std::integral_constant<int, EPI1X_MASK | EPI1X_X3>{});
+  } else {
+    if (epi == EPI1X_BIAS_RELU) go(std::integral_constant<int, EPI1X_BIAS_RELU>{});
+    else go(std::integral_constant<int, EPI1X_MASK>{});
+  }
 }
 
 // returns -1 when the shape has no instantiation.  epi | 4 (EPI1X_X3): the
@@ -635,14 +656,17 @@ extern "C" int ncnet_conv1x16(const void* Xp, const void* Wa, const float* bias,
   if (e != EPI1X_BIAS_RELU && e != EPI1X_MASK) return -3;
   const bf16* x = (const bf16*)Xp; const u32x4* w = (const u32x4*)Wa; const bf16* m = (const bf16*)M; bf16* y = (bf16*)Y;
   if (KS == 5 && K == 25 && L == 25) {
-    if (x3) c1x_launch<5, 25, 25, 3>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
-    else c1x_launch<5, 25, 25>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
+    if (x3) c1x_launch<5, 25, 25, 3, true>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
+    else c1x_launch<5, 25, 25, 5, false>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
   } else if (KS == 5 && K == 20 && L == 20) {
-    if (x3) c1x_launch<5, 20, 20, 3>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
-    else c1x_launch<5, 20, 20>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
+    if (x3) c1x_launch<5, 20, 20, 3, true>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
+    else c1x_launch<5, 20, 20, 5, false>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
+  } else if (KS == 5 && K == 30 && L == 30) {
+    if (x3) c1x_launch<5, 30, 30, 1, true>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
+    else c1x_launch<5, 30, 30, 3, false>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
   } else if (KS == 3 && K == 25 && L == 25) {
-    if (x3) c1x_launch<3, 25, 25, 3>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
-    else c1x_launch<3, 25, 25>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
+    if (x3) c1x_launch<3, 25, 25, 3, true>(epi, V, I, J, x, w, bias, m, y, 0, xlo, ylo, s);
+    else c1x_launch<3, 25, 25, 5, false>(epi, V, I, J, x, w, bias, m, y, nt_store, 0, 0, s);
   } else return -1;
   return (int)hipGetLastError();
 }
@@ -668,6 +692,7 @@ extern "C" int ncnet_wgrad1x16(const void* Dp, const void* X1p, float* part, flo
   const bf16* d = (const bf16*)Dp; const bf16* x = (const bf16*)X1p;
   if (KS == 5 && K == 25 && L == 25) w1x_launch<5, 25, 25>(G, V, I, J, d, x, part, partb, s);
   else if (KS == 5 && K == 20 && L == 20) w1x_launch<5, 20, 20>(G, V, I, J, d, x, part, partb, s);
+  else if (KS == 5 && K == 30 && L == 30) w1x_launch<5, 30, 30>(G, V, I, J, d, x, part, partb, s);
   else if (KS == 3 && K == 25 && L == 25) w1x_launch<3, 25, 25>(G, V, I, J, d, x, part, partb, s);
   else return -1;
   return (int)hipGetLastError();

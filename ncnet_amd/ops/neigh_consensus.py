@@ -333,7 +333,7 @@ def _gather(outs, f32: bool, cout: int):
 FAST1X = True    # module attribute (A/B tests, scripts/kbench.py); no environment knob
 # (kernel size, K, L) with conv1x16 / wgrad1x16 instantiations (csrc/conv1x.hip):
 # --image_size 400 and 320 at k = 5, and the IVD recipe's k = 3 at 400 px
-FAST1X_SHAPES = frozenset({(5, 25, 25), (5, 20, 20), (3, 25, 25)})
+FAST1X_SHAPES = frozenset({(5, 25, 25), (5, 20, 20), (5, 30, 30), (3, 25, 25)})
 
 
 def fast1x_ok(kinds, channels, kernel_sizes, x: torch.Tensor, symmetric: bool) -> bool:

@@ -918,7 +918,7 @@ def _pad_1ch(x5, ks, trans=False):
 
 @pytest.mark.parametrize("ks,shape", [(5, (2, 25, 25, 25, 25)), (5, (1, 6, 7, 25, 25)), (5, (1, 3, 11, 25, 25)),
                                       (5, (2, 20, 20, 20, 20)), (5, (1, 7, 3, 20, 20)), (3, (2, 25, 25, 25, 25)),
-                                      (3, (1, 4, 9, 25, 25))])
+                                      (3, (1, 4, 9, 25, 25)), (5, (1, 30, 30, 30, 30)), (5, (1, 7, 4, 30, 30))])
 @pytest.mark.parametrize("epi", [1, 2])
 def test_conv1x16_vs_oracle(ks, shape, epi):
     """1 -> 16 Conv4d on zero-padded 1-channel planes (csrc/conv1x.hip: taps
@@ -956,7 +956,8 @@ def test_pad_planes_transposed():
 @pytest.mark.parametrize("ks,shape,G", [(5, (2, 25, 25, 25, 25), 256), (5, (1, 6, 7, 25, 25), 7),
                                         (5, (1, 3, 11, 25, 25), 64), (5, (1, 5, 5, 25, 25), 1),
                                         (5, (2, 20, 20, 20, 20), 256), (5, (1, 4, 9, 20, 20), 13),
-                                        (3, (2, 25, 25, 25, 25), 256), (3, (1, 5, 7, 25, 25), 9)])
+                                        (3, (2, 25, 25, 25, 25), 256), (3, (1, 5, 7, 25, 25), 9),
+                                        (5, (1, 30, 30, 30, 30), 256), (5, (1, 4, 9, 30, 30), 13)])
 @pytest.mark.parametrize("bias", [True, False])
 def test_wgrad1x16_vs_oracle(ks, shape, G, bias):
     """Weight gradient with a 1-channel operand straight from padded planes
@@ -1102,10 +1103,11 @@ def _fast1x_vs_quantized_oracle(symmetric, perturb=None, seed=31, ks=(5, 5, 5), 
     return {n: rel_l2(a, r) for n, a, r in zip(names, got, want)}
 
 
-@pytest.mark.parametrize("ks,ch,T,V", [((5, 5, 5), (16, 16, 1), 20, 2), ((3, 3), (16, 1), 25, 2)])
+@pytest.mark.parametrize("ks,ch,T,V", [((5, 5, 5), (16, 16, 1), 20, 2), ((3, 3), (16, 1), 25, 2),
+                                       ((5, 5, 5), (16, 16, 1), 30, 1)])
 def test_fast1x_other_configs_vs_quantized_oracle(ks, ch, T, V):
-    """The fast training stack at --image_size 320 (20^4 volumes) and the IVD
-    recipe (NC 3,3 / 16,1 at 400 px) vs the quantized fp64 oracle."""
+    """The fast training stack at --image_size 320 (20^4 volumes), 480 (30^4)
+    and the IVD recipe (NC 3,3 / 16,1 at 400 px) vs the quantized fp64 oracle."""
     errs = _fast1x_vs_quantized_oracle(True, ks=ks, ch=ch, T=T, V=V)
     print(f"fast1x {ks}/{ch} at {T}^4 vs quantized oracle:", {k: f"{v:.1e}" for k, v in errs.items()})
     assert max(errs.values()) < 1e-3, errs

@@ -36,6 +36,7 @@ def _params(ks, ch, seed, masked=False):
 
 @pytest.mark.parametrize("ks,ch,shape", [((5, 5, 5), (16, 16, 1), (1, 1, 25, 25, 25, 25)),
                                          ((5, 5, 5), (16, 16, 1), (1, 1, 20, 20, 20, 20)),
+                                         ((5, 5, 5), (16, 16, 1), (1, 1, 30, 30, 30, 30)),
                                          ((3, 3), (16, 1), (1, 1, 25, 25, 25, 25)),
                                          ((5, 5, 5), (16, 16, 1), (2, 1, 9, 7, 9, 7)),
                                          ((3, 3), (16, 1), (2, 1, 8, 11, 8, 11)),
