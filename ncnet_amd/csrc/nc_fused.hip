@@ -71,10 +71,14 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   char* S = smem;
   char* H = S + SR * SRS * 32;
   float* ring = (float*)(H + HR * HRS * 32);
-  u32x4* wl = (u32x4*)(ring + 3 * GR * TK * TL);   // [2 layers][5 tap pairs][64 lanes] fragments
+  // ring + 64 trash words (one per lane), rounded to 16 B; then the weight fragments [2 layers][5 tap pairs][64 lanes]
+  u32x4* wl = (u32x4*)(ring + ((3 * GR * TK * TL + 64 + 3) & ~3));
   const int nvox = TK * TL;
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index made wave-uniform (an SGPR): the per-wave tile-count checks are
+  // then scalar branches, not exec-mask save / restore sequences
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_assume(wave >= 0 && wave < NCF_NW);   // static tile counts fold the per-wave checks
   uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
   const int lt = bid % g.nlt; bid /= g.nlt;
   const int kt = bid % g.nkt; bid /= g.nkt;
@@ -101,14 +105,17 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     const int e = threadIdx.x;
     const int r = e / SW, c = e - r * SW;
     const int kg = k0 - 2 + r, lg = l0 - 2 + c;
-    s_lds = (e < SR * SW) ? (r * SRS + c) * 32 : -1;
+    // threads past the S tile write to column SW of row 0, a padding voxel no
+    // layer-1 read touches (taps reach column TL + 3 < SW <= SRS - 1): the
+    // S write is branch-free
+    s_lds = (e < SR * SW) ? (r * SRS + c) * 32 : SW * 32;
     s_in = e < SR * SW && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
     s_goff = s_in ? (kg * g.L + lg) * 2 : 0x7ffffff0;   // byte offset in the plane / out of range
   }
   // layer-1 tiles: h ext voxels e = tile*16 + (lane & 15) over HR x HW
   const int nt1 = (HR * HW + 15) >> 4;
   uint32_t b1off[NCF_MAXT1], h_wr[NCF_MAXT1];
-  bool h_in[NCF_MAXT1], h_ok[NCF_MAXT1];
+  bool h_in[NCF_MAXT1];
 #pragma unroll
   for (int t = 0; t < NCF_MAXT1; ++t) {
     int e = (wave + NCF_NW * t) * 16 + (lane & 15);
@@ -116,9 +123,10 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     if (!ok) e = 0;
     const int r = e / HW, c = e - r * HW;
     b1off[t] = (uint32_t)((r * SRS + c) * 32 + ((lane >> 4) & 1) * 16);
-    h_wr[t] = (uint32_t)((r * HRS + c) * 32 + 8 * (lane >> 4));
+    // lanes past the h region write to column HW of row 0 (padding no layer-2
+    // read touches: taps reach column TL + 1 < HW <= HRS - 1): branch-free
+    h_wr[t] = (uint32_t)(((ok ? r * HRS + c : HW)) * 32 + 8 * (lane >> 4));
     const int kg = k0 - 1 + r, lg = l0 - 1 + c;
-    h_ok[t] = ok;    // lanes past the h region of the last tile must not write (their e was clamped to 0)
     h_in[t] = ok && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
   }
   // layer-2 tiles: output voxels vi = tile*16 + (lane & 15) over TK x TL
@@ -165,35 +173,71 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   // set was written out, so no plane waits for its own gather.
   // plane byte offsets: one multiply per gather, the 9 combos differ by constants
   const int pstride = KLi * 2, rstride = g.J * KLi * 2;
+  // every load is issued (branch-free: a combo outside the volume gets the
+  // scalar offset nrec, past the buffer's range -> 0); a conditional load let
+  // the compiler merge the loads of both gather paths behind a VGPR phi of
+  // the offset, i.e. a readfirstlane waterfall loop around each load
+  const int nrec = (int)((size_t)g.I * g.J * KL * 2);
   auto gather = [&](int ih, int jh, uint32_t (&raw)[9]) {
     const int base = (ih * g.J + jh) * pstride;
     const bool iok[3] = {ih >= 1, true, ih + 1 < g.I}, jok[3] = {jh >= 1, true, jh + 1 < g.J};   // wave-uniform
 #pragma unroll
     for (int c = 0; c < 9; ++c) {
       const int di = c / 3, dj = c % 3;
-      raw[c] = (iok[di] && jok[dj])
-                   ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(xr, s_goff, base + (di - 1) * rstride + (dj - 1) * pstride, 0)
-                   : 0u;
+      const int so = (iok[di] && jok[dj]) ? base + (di - 1) * rstride + (dj - 1) * pstride : nrec;
+      raw[c] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(xr, s_goff, __builtin_amdgcn_readfirstlane(so), 0);
+    }
+  };
+  // sliding gather: plane (ih, jh) shares its combo columns dj = 0, 1 with
+  // columns dj = 1, 2 of plane (ih, jh - 1), still in the other register set
+  // (`prev`, that plane is one step younger): only the 3 values of the new
+  // column jh + 1 are loaded (was 9 buffer_load_ushort per S voxel per plane)
+  auto gather_slide = [&](int ih, int jh, uint32_t (&raw)[9], const uint32_t (&prev)[9]) {
+    const int base = (ih * g.J + jh) * pstride;
+    const bool iok[3] = {ih >= 1, true, ih + 1 < g.I};
+    const bool jok = jh + 1 < g.J;
+    // loads first, register moves last: the two gather paths then end in
+    // different instructions and are not tail-merged into one phi'd load
+#pragma unroll
+    for (int di = 0; di < 3; ++di) {
+      const int so = (iok[di] && jok) ? base + (di - 1) * rstride + pstride : nrec;
+      raw[di * 3 + 2] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(xr, s_goff, __builtin_amdgcn_readfirstlane(so), 0);
+    }
+#pragma unroll
+    for (int di = 0; di < 3; ++di) {
+      raw[di * 3 + 0] = prev[di * 3 + 1];
+      raw[di * 3 + 1] = prev[di * 3 + 2];
     }
   };
   auto write_s = [&](const uint32_t (&raw)[9]) {
-    if (s_lds < 0) return;
     *(u32x4*)(S + s_lds) = u32x4{raw[0] | (raw[1] << 16), raw[2] | (raw[3] << 16), raw[4] | (raw[5] << 16),
                                  raw[6] | (raw[7] << 16)};
     *(u32x4*)(S + s_lds + 16) = u32x4{raw[8], 0u, 0u, 0u};
   };
 
-  auto flush = [&](int io) {   // output row io -> Y (this wave's voxels only)
+  // output voxel (kg, lg) offsets of this lane's layer-2 tiles (-1: none / outside the volume)
+  int yvox[NCF_MAXT2];
+#pragma unroll
+  for (int t = 0; t < NCF_MAXT2; ++t) {
+    const int vv = vo[t] < 0 ? 0 : vo[t];
+    const int kk = vv / TL, ll = vv - kk * TL;
+    const int kg = k0 + kk, lg = l0 + ll;
+    yvox[t] = (vo[t] >= 0 && kg < g.K && lg < g.L) ? kg * g.L + lg : -1;
+  }
+  // output row io -> Y (this wave's voxels; lane group lane >> 4 takes planes
+  // p = lane >> 4, + 4, ...: all 64 lanes store, not 16)
+  auto flush = [&](int io) {
     const int slot = io % 3;
+    float* yrow = Y + (((size_t)v * g.I + io) * g.J + j0) * KL;
+    const int pg = lane >> 4;
 #pragma unroll
     for (int t = 0; t < NCF_MAXT2; ++t) {
-      if (vo[t] < 0 || (lane >> 4) != 0) continue;
-      const int kk = vo[t] / TL, ll = vo[t] - kk * TL;
-      const int kg = k0 + kk, lg = l0 + ll;
-      const bool ok = kg < g.K && lg < g.L;
-      for (int p = 0; p < R; ++p) {
+      if (wave + NCF_NW * t >= nt2) continue;
+      if (vo[t] < 0) continue;     // padding lanes of the last tile own no ring entry
+      for (int p = pg; p < R; p += 4) {
         float* rp = ring + (slot * GR + p) * nvox + vo[t];
-        if (ok) Y[(((size_t)v * g.I + io) * g.J + j0 + p) * KL + (size_t)kg * g.L + lg] = fmaxf(*rp + bias2, 0.f);
+        const float val = fmaxf(*rp + bias2, 0.f);
+        if (yvox[t] >= 0) yrow[(size_t)p * KL + yvox[t]] = val;
         *rp = 0.f;
       }
     }
@@ -202,58 +246,94 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   // hidden plane (ih, jh = jh_lo + pj); its gather registers are refilled with
   // the plane two steps ahead (gih, gpj), advanced incrementally (no divisions)
   int ih = ih_lo, pj = 0, gih = ih_lo, gpj = 0;
+  int slot0 = (ih_lo + 1) % 3;         // ring slot of output row ih + 1 (row ih - r + 1 -> slot0 - r mod 3)
   auto advance = [&](int& a, int& b) {
     if (++b == nplane) { b = 0; ++a; }
   };
-  auto step = [&](uint32_t (&raw)[9]) {
+  auto step = [&](uint32_t (&raw)[9], const uint32_t (&other)[9]) {
     const int jh = jh_lo + pj;
     // no barrier here: every wave already passed the previous step's "h
     // complete" barrier, i.e. all layer-1 reads of S are done, and h is next
     // written only after the "S complete" barrier below, i.e. after all
     // layer-2 reads of the previous plane (ring entries are wave-private)
     write_s(raw);
-    if (gih < ih_hi) gather(gih, jh_lo + gpj, raw);
+    if (gih < ih_hi) {
+      // `other` holds plane (gih, gpj - 1) when gpj >= 1 (same row, one plane back)
+      if (gpj >= 1) gather_slide(gih, jh_lo + gpj, raw, other);
+      else gather(gih, jh_lo + gpj, raw);
+    }
     advance(gih, gpj);
     __syncthreads();                   // S complete
     // ---- B: layer 1 -> h (bf16, zero outside the volume) ----
+    // K-step-major: each weight fragment is read from LDS once per plane and
+    // feeds every tile of this wave (was: once per tile and K-step, i.e. an
+    // LDS read of A beside every LDS read of B)
+    f32x4 acc1[NCF_MAXT1];
+#pragma unroll
+    for (int u = 0; u < NCF_MAXT1; ++u) acc1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const u32x4 a = wl[q * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < NCF_MAXT1; ++u)
+        if (wave + NCF_NW * u < nt1) acc1[u] = mfma16t<F16>(a, *(const u32x4*)(S + b1off[u] + toff1[q]), acc1[u]);
+    }
 #pragma unroll
     for (int u = 0; u < NCF_MAXT1; ++u) {
       if (wave + NCF_NW * u >= nt1) continue;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 acc = acc1[u];
+      // branch-free: ReLU, then a select for voxels outside the volume
+      float hv[4];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q)
-        acc = mfma16t<F16>(wl[q * 64 + lane], *(const u32x4*)(S + b1off[u] + toff1[q]), acc);
+      for (int r = 0; r < 4; ++r) {
+        const float t = fmaxf(acc[r] + bias1[r], 0.f);
+        hv[r] = h_in[u] ? t : 0.f;
+      }
       u32x2 o;
 #pragma unroll
       for (int r = 0; r < 2; ++r)
-        o[r] = (uint32_t)f2s16<F16>(h_in[u] ? fmaxf(acc[2 * r] + bias1[2 * r], 0.f) : 0.f) |
-               ((uint32_t)f2s16<F16>(h_in[u] ? fmaxf(acc[2 * r + 1] + bias1[2 * r + 1], 0.f) : 0.f) << 16);
-      if (h_ok[u]) *(u32x2*)(H + h_wr[u]) = o;
+        o[r] = (uint32_t)f2s16<F16>(hv[2 * r]) | ((uint32_t)f2s16<F16>(hv[2 * r + 1]) << 16);
+      *(u32x2*)(H + h_wr[u]) = o;
     }
     __syncthreads();                   // h complete
     // ---- C: layer 2 combos -> ring ----
     const int p2 = jh - dj2 + 1 - j0;         // output plane of this lane's combos
     const bool p_ok = dj2 < 3 && p2 >= 0 && p2 < R;
+    f32x4 acc2[NCF_MAXT2];
+#pragma unroll
+    for (int u = 0; u < NCF_MAXT2; ++u) acc2[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const u32x4 a = wl[(NQ + q) * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < NCF_MAXT2; ++u)
+        if (wave + NCF_NW * u < nt2) acc2[u] = mfma16t<F16>(a, *(const u32x4*)(H + b2off[u] + toff2[q]), acc2[u]);
+    }
 #pragma unroll
     for (int u = 0; u < NCF_MAXT2; ++u) {
       if (wave + NCF_NW * u >= nt2) continue;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < NQ; ++q)
-        acc = mfma16t<F16>(wl[(NQ + q) * 64 + lane], *(const u32x4*)(H + b2off[u] + toff2[q]), acc);
-      if (vo[u] < 0 || !p_ok) continue;
+      const f32x4 acc = acc2[u];
       // MFMA row 4 * dj2 + di2 <-> combo (di2, dj2): this lane's rows r share
-      // one output plane p2 and differ in the output row ih - r + 1 (uniform)
+      // one output plane p2 and differ in the output row ih - r + 1 (uniform).
+      // Lanes with no valid (voxel, plane) update a trash word past the ring
+      // (never an entry another lane owns: the RMW would race): no exec-mask
+      // branch around the update
+      const bool lok = vo[u] >= 0 && p_ok;
+      const int roff = p2 * nvox + vo[u];
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int io = ih - r + 1;
         if (io < i0 || io >= i1) continue;
-        ring[((io % 3) * GR + p2) * nvox + vo[u]] += acc[r];
+        const int slot = r == 0 ? slot0 : r == 1 ? (slot0 == 0 ? 2 : slot0 - 1) : (slot0 == 2 ? 0 : slot0 + 1);   // io % 3
+        float* rp = ring + (lok ? slot * GR * nvox + roff : 3 * GR * nvox + lane);   // trash: one word per lane
+        // read-add-write (lane-private entries); the LDS float atomic
+        // (ds_add_f32) measured 3.2x slower for the whole kernel
+        *rp += lok ? acc[r] : 0.f;
       }
     }
     // hidden row ih done: output row ih - 1 has all three contributions
     if (pj + 1 == nplane && ih - 1 >= i0 && ih - 1 < i1) flush(ih - 1);
-    advance(ih, pj);
+    if (++pj == nplane) { pj = 0; ++ih; slot0 = slot0 == 2 ? 0 : slot0 + 1; }
   };
 
   __syncthreads();                     // weights in LDS and the zeroed ring visible to every wave
@@ -263,8 +343,8 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   if (gih < ih_hi) gather(gih, jh_lo + gpj, rawB);
   advance(gih, gpj);
   for (int t = 0; t < nsteps; t += 2) {
-    step(rawA);
-    if (t + 1 < nsteps) step(rawB);
+    step(rawA, rawB);
+    if (t + 1 < nsteps) step(rawB, rawA);
   }
   // rows whose last contributing hidden row is past the volume / the segment
   for (int io = max(i0, ih_hi - 1); io < i1; ++io) flush(io);
@@ -290,7 +370,7 @@ extern "C" int ncnet_nc_fused_k3(const void* X, const void* W1p, const float* b1
   g.SRS = TL + 10;   // S rows: a layer-1 tile wrapping from column TL+1 to 0 jumps 9 voxels (one 256-B bank period + 1)
   g.HRS = TL + 8;    // h rows: a layer-2 tile wrapping from column TL-1 to 0 jumps 9 voxels
   if ((long long)I * J * K * L * 2 >= (1ll << 31)) return -4;   // buffer-resource byte offsets
-  size_t lds = (size_t)(TK + 4) * g.SRS * 32 + (size_t)(TK + 2) * g.HRS * 32 + (size_t)3 * R * TK * TL * 4 +
+  size_t lds = (size_t)(TK + 4) * g.SRS * 32 + (size_t)(TK + 2) * g.HRS * 32 + (size_t)((3 * R * TK * TL + 64 + 3) & ~3) * 4 +
                2 * 5 * 64 * 16;
   if (lds > 160 * 1024) return -3;
   dim3 grid((unsigned)((size_t)V * g.nib * g.njb * g.nkt * g.nlt)), block(512);

@@ -1241,7 +1241,7 @@ def neigh_consensus_fp8(x: torch.Tensor, weights, biases, kinds, symmetric: bool
 # inference.  The hidden activation stays in LDS; HBM sees the input and the
 # output volume once.  NCNET_NC_FUSED=0 falls back to the layer-by-layer path.
 FUSED = _config.RUNTIME.nc_fused
-_FUSED_LDS = 78 * 1024          # two workgroups per CU (160 KB LDS)
+_FUSED_LDS = 80 * 1024          # two workgroups per CU (160 KB LDS)
 
 
 def _cdiv(a: int, b: int) -> int:
@@ -1265,7 +1265,7 @@ def fused_tiles(V: int, I: int, J: int, K: int, L: int):
             if best is None or cost < best[0]:
                 best = (cost, tk, tl)
     _, tk, tl = best
-    fixed = (tk + 4) * (tl + 10) * 32 + (tk + 2) * (tl + 8) * 32 + 2 * 5 * 64 * 16
+    fixed = (tk + 4) * (tl + 10) * 32 + (tk + 2) * (tl + 8) * 32 + 2 * 5 * 64 * 16 + 268   # + ring trash / alignment
     r_max = max(1, (_FUSED_LDS - fixed) // (12 * tk * tl))
     base = V * _cdiv(K, tk) * _cdiv(L, tl)
 
