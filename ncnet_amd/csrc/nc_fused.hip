@@ -55,13 +55,18 @@ constexpr int NCF_MAXT2 = 3;       // layer-2 tiles per wave: TK*TL <= 384 voxel
 // tap offsets and ring indexing then fold into immediates -- the runtime
 // geometry kept ~50 SGPRs live (spilled to VGPR lanes) and cost ~10 SALU per
 // MFMA (profiles/r2_inloc/pmc_corr_ncfused_before.md).
-template <bool F16, int CTK = 0, int CTL = 0, int CR = 0>
-__global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ W1p,
+template <bool F16, int CTK = 0, int CTL = 0, int CR = 0, int NW = 8>
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 1) void nc_fused_k3_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ W1p,
                                                              const float* __restrict__ b1,
                                                              const u32x4* __restrict__ W2p,
                                                              const float* __restrict__ b2, float* __restrict__ Y,
                                                              NCFGeom g) {
   constexpr int NQ = 5;            // tap pairs of the 3x3 (dk, dl) taps
+  // NW = 8: two 512-thread workgroups per CU (<= 80 KB LDS each); NW = 16: one
+  // 1024-thread workgroup per CU with up to 160 KB (a deeper output ring: more
+  // planes per workgroup, less j halo) and half the tiles per wave per phase
+  constexpr int MT1 = 32 / NW;                 // layer-1 tiles per wave: (TK+2)(TL+2) <= 512
+  constexpr int MT2 = NW == 8 ? 3 : 2;         // layer-2 tiles per wave: TK*TL <= 16 NW MT2
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int TK = CTK ? CTK : g.TK, TL = CTL ? CTL : g.TL;
   const int GR = CR ? CR : g.R;                       // planes per workgroup (ring depth)
@@ -78,7 +83,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   // wave index made wave-uniform (an SGPR): the per-wave tile-count checks are
   // then scalar branches, not exec-mask save / restore sequences
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  __builtin_assume(wave >= 0 && wave < NCF_NW);   // static tile counts fold the per-wave checks
+  __builtin_assume(wave >= 0 && wave < NW);   // static tile counts fold the per-wave checks
   uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
   const int lt = bid % g.nlt; bid /= g.nlt;
   const int kt = bid % g.nkt; bid /= g.nkt;
@@ -114,11 +119,16 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   }
   // layer-1 tiles: h ext voxels e = tile*16 + (lane & 15) over HR x HW
   const int nt1 = (HR * HW + 15) >> 4;
-  uint32_t b1off[NCF_MAXT1], h_wr[NCF_MAXT1];
-  bool h_in[NCF_MAXT1];
+  uint32_t b1off[MT1], h_wr[MT1];
+  bool h_in[MT1];
+  // tap-pair read bases: lane half hh = lane >> 5 reads tap 2q + hh, which is
+  // the voxel after tap 2q (pairs 0, 2, 3), one row wrap after it (pair 1:
+  // taps (0,2) -> (1,0)) or the same voxel (pair 4: the padding tap); with the
+  // base per kind the tap offset of 2q is a compile-time immediate
+  const uint32_t hh = (uint32_t)(lane >> 5);
 #pragma unroll
-  for (int t = 0; t < NCF_MAXT1; ++t) {
-    int e = (wave + NCF_NW * t) * 16 + (lane & 15);
+  for (int t = 0; t < MT1; ++t) {
+    int e = (wave + NW * t) * 16 + (lane & 15);
     const bool ok = e < HR * HW;
     if (!ok) e = 0;
     const int r = e / HW, c = e - r * HW;
@@ -129,29 +139,25 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     const int kg = k0 - 1 + r, lg = l0 - 1 + c;
     h_in[t] = ok && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
   }
+  uint32_t a1c[MT1], a1w[MT1];
+#pragma unroll
+  for (int t = 0; t < MT1; ++t) { a1c[t] = b1off[t] + hh * 32u; a1w[t] = b1off[t] + hh * (uint32_t)(SRS - 2) * 32u; }
   // layer-2 tiles: output voxels vi = tile*16 + (lane & 15) over TK x TL
   const int nt2 = (nvox + 15) >> 4;
-  uint32_t b2off[NCF_MAXT2];
-  int vo[NCF_MAXT2];
+  uint32_t b2off[MT2];
+  int vo[MT2];
 #pragma unroll
-  for (int t = 0; t < NCF_MAXT2; ++t) {
-    int vi = (wave + NCF_NW * t) * 16 + (lane & 15);
+  for (int t = 0; t < MT2; ++t) {
+    int vi = (wave + NW * t) * 16 + (lane & 15);
     vo[t] = vi < nvox ? vi : -1;
     if (vi >= nvox) vi = 0;
     const int kk = vi / TL, ll = vi - kk * TL;
     b2off[t] = (uint32_t)((kk * HRS + ll) * 32 + ((lane >> 4) & 1) * 16);
   }
-  // tap offsets of the pair q: tap 2q + (lane >> 5) (the 10th tap is padding with zero weights)
-  uint32_t toff1[NQ], toff2[NQ];
+  uint32_t a2c[MT2], a2w[MT2];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    int tap = 2 * q + (lane >> 5);
-    if (tap > 8) tap = 8;
-    const int dk = tap / 3, dl = tap - dk * 3;
-    toff1[q] = (uint32_t)((dk * SRS + dl) * 32);
-    toff2[q] = (uint32_t)((dk * HRS + dl) * 32);
-  }
-  for (int o = threadIdx.x; o < NQ * 64; o += 512) { wl[o] = W1p[o]; wl[NQ * 64 + o] = W2p[o]; }
+  for (int t = 0; t < MT2; ++t) { a2c[t] = b2off[t] + hh * 32u; a2w[t] = b2off[t] + hh * (uint32_t)(HRS - 2) * 32u; }
+  for (int o = threadIdx.x; o < NQ * 64; o += NW * 64) { wl[o] = W1p[o]; wl[NQ * 64 + o] = W2p[o]; }
   const int co0 = 4 * (lane >> 4);
   const int dj2 = lane >> 4;                 // layer-2 combo column of this lane's MFMA rows
   float bias1[4];
@@ -160,7 +166,7 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   const float bias2 = b2[0];
 
   // zero the output ring (3 row slots x R planes x TK*TL)
-  for (int o = threadIdx.x; o < 3 * GR * nvox; o += 512) ring[o] = 0.f;
+  for (int o = threadIdx.x; o < 3 * GR * nvox; o += NW * 64) ring[o] = 0.f;
 
   const int ih_lo = max(0, i0 - 1), ih_hi = min(g.I, i1 + 1);   // hidden rows [lo, hi)
   const int jh_lo = max(0, j0 - 1), jh_hi = min(g.J, j0 + R + 1); // hidden planes [lo, hi)
@@ -209,6 +215,13 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
       raw[di * 3 + 1] = prev[di * 3 + 2];
     }
   };
+  // B fragment of tap pair q for tile u (S: layer 1, H: layer 2)
+  auto bread = [&](const char* buf, uint32_t c, uint32_t w, uint32_t z, int RS, int q) -> u32x4 {
+    const uint32_t t0 = q == 0 ? 0u : q == 1 ? 64u : q == 2 ? (uint32_t)(RS + 1) * 32u : q == 3 ? (uint32_t)(2 * RS) * 32u
+                                                                                    : (uint32_t)(2 * RS + 2) * 32u;
+    const uint32_t base = q == 1 ? w : q == 4 ? z : c;
+    return *(const u32x4*)(buf + base + t0);
+  };
   auto write_s = [&](const uint32_t (&raw)[9]) {
     *(u32x4*)(S + s_lds) = u32x4{raw[0] | (raw[1] << 16), raw[2] | (raw[3] << 16), raw[4] | (raw[5] << 16),
                                  raw[6] | (raw[7] << 16)};
@@ -216,9 +229,9 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
   };
 
   // output voxel (kg, lg) offsets of this lane's layer-2 tiles (-1: none / outside the volume)
-  int yvox[NCF_MAXT2];
+  int yvox[MT2];
 #pragma unroll
-  for (int t = 0; t < NCF_MAXT2; ++t) {
+  for (int t = 0; t < MT2; ++t) {
     const int vv = vo[t] < 0 ? 0 : vo[t];
     const int kk = vv / TL, ll = vv - kk * TL;
     const int kg = k0 + kk, lg = l0 + ll;
@@ -231,8 +244,8 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     float* yrow = Y + (((size_t)v * g.I + io) * g.J + j0) * KL;
     const int pg = lane >> 4;
 #pragma unroll
-    for (int t = 0; t < NCF_MAXT2; ++t) {
-      if (wave + NCF_NW * t >= nt2) continue;
+    for (int t = 0; t < MT2; ++t) {
+      if (wave + NW * t >= nt2) continue;
       if (vo[t] < 0) continue;     // padding lanes of the last tile own no ring entry
       for (int p = pg; p < R; p += 4) {
         float* rp = ring + (slot * GR + p) * nvox + vo[t];
@@ -268,50 +281,57 @@ __global__ __launch_bounds__(512, 2) void nc_fused_k3_kernel(const bf16* __restr
     // K-step-major: each weight fragment is read from LDS once per plane and
     // feeds every tile of this wave (was: once per tile and K-step, i.e. an
     // LDS read of A beside every LDS read of B)
-    f32x4 acc1[NCF_MAXT1];
+    f32x4 acc1[MT1];
 #pragma unroll
-    for (int u = 0; u < NCF_MAXT1; ++u) acc1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < MT1; ++u) acc1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const u32x4 a = wl[q * 64 + lane];
 #pragma unroll
-      for (int u = 0; u < NCF_MAXT1; ++u)
-        if (wave + NCF_NW * u < nt1) acc1[u] = mfma16t<F16>(a, *(const u32x4*)(S + b1off[u] + toff1[q]), acc1[u]);
+      for (int u = 0; u < MT1; ++u)
+        if (wave + NW * u < nt1) acc1[u] = mfma16t<F16>(a, bread(S, a1c[u], a1w[u], b1off[u], SRS, q), acc1[u]);
     }
 #pragma unroll
-    for (int u = 0; u < NCF_MAXT1; ++u) {
-      if (wave + NCF_NW * u >= nt1) continue;
+    for (int u = 0; u < MT1; ++u) {
+      if (wave + NW * u >= nt1) continue;
       const f32x4 acc = acc1[u];
-      // branch-free: ReLU, then a select for voxels outside the volume
+      // branch-free: bias + ReLU, packed conversion of channel pairs, then the
+      // zero of voxels outside the volume as one select per packed dword
       float hv[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float t = fmaxf(acc[r] + bias1[r], 0.f);
-        hv[r] = h_in[u] ? t : 0.f;
-      }
+      for (int r = 0; r < 4; ++r) hv[r] = fmaxf(acc[r] + bias1[r], 0.f);
       u32x2 o;
 #pragma unroll
-      for (int r = 0; r < 2; ++r)
-        o[r] = (uint32_t)f2s16<F16>(hv[2 * r]) | ((uint32_t)f2s16<F16>(hv[2 * r + 1]) << 16);
+      for (int r = 0; r < 2; ++r) {
+        uint32_t pk;
+        if constexpr (F16) {
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          pk = __builtin_bit_cast(uint32_t, h2{(_Float16)hv[2 * r], (_Float16)hv[2 * r + 1]});
+        } else {
+          typedef __bf16 b2t __attribute__((ext_vector_type(2)));
+          pk = __builtin_bit_cast(uint32_t, b2t{(__bf16)hv[2 * r], (__bf16)hv[2 * r + 1]});
+        }
+        o[r] = h_in[u] ? pk : 0u;
+      }
       *(u32x2*)(H + h_wr[u]) = o;
     }
     __syncthreads();                   // h complete
     // ---- C: layer 2 combos -> ring ----
     const int p2 = jh - dj2 + 1 - j0;         // output plane of this lane's combos
     const bool p_ok = dj2 < 3 && p2 >= 0 && p2 < R;
-    f32x4 acc2[NCF_MAXT2];
+    f32x4 acc2[MT2];
 #pragma unroll
-    for (int u = 0; u < NCF_MAXT2; ++u) acc2[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < MT2; ++u) acc2[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const u32x4 a = wl[(NQ + q) * 64 + lane];
 #pragma unroll
-      for (int u = 0; u < NCF_MAXT2; ++u)
-        if (wave + NCF_NW * u < nt2) acc2[u] = mfma16t<F16>(a, *(const u32x4*)(H + b2off[u] + toff2[q]), acc2[u]);
+      for (int u = 0; u < MT2; ++u)
+        if (wave + NW * u < nt2) acc2[u] = mfma16t<F16>(a, bread(H, a2c[u], a2w[u], b2off[u], HRS, q), acc2[u]);
     }
 #pragma unroll
-    for (int u = 0; u < NCF_MAXT2; ++u) {
-      if (wave + NCF_NW * u >= nt2) continue;
+    for (int u = 0; u < MT2; ++u) {
+      if (wave + NW * u >= nt2) continue;
       const f32x4 acc = acc2[u];
       // MFMA row 4 * dj2 + di2 <-> combo (di2, dj2): this lane's rows r share
       // one output plane p2 and differ in the output row ih - r + 1 (uniform).
@@ -363,26 +383,32 @@ extern "C" int ncnet_nc_fused_k3(const void* X, const void* W1p, const float* b1
   NCFGeom g{};
   g.V = V; g.I = I; g.J = J; g.K = K; g.L = L;
   g.TK = TK; g.TL = TL; g.R = R; g.IR = IR;
-  if ((TK + 2) * (TL + 2) > NCF_NW * NCF_MAXT1 * 16 || TK * TL > NCF_NW * NCF_MAXT2 * 16 ||
-      (TK + 4) * (TL + 4) > 512 || R < 1 || IR < 1)
-    return -2;
   g.nkt = cdiv(K, TK); g.nlt = cdiv(L, TL); g.njb = cdiv(J, R); g.nib = cdiv(I, IR);
   g.SRS = TL + 10;   // S rows: a layer-1 tile wrapping from column TL+1 to 0 jumps 9 voxels (one 256-B bank period + 1)
   g.HRS = TL + 8;    // h rows: a layer-2 tile wrapping from column TL-1 to 0 jumps 9 voxels
   if ((long long)I * J * K * L * 2 >= (1ll << 31)) return -4;   // buffer-resource byte offsets
   size_t lds = (size_t)(TK + 4) * g.SRS * 32 + (size_t)(TK + 2) * g.HRS * 32 + (size_t)((3 * R * TK * TL + 64 + 3) & ~3) * 4 +
                2 * 5 * 64 * 16;
+  // > 80 KB: one 16-wave workgroup per CU (NW = 16) instead of two 8-wave ones
+  const bool big = lds > 80 * 1024;
+  const int nw = big ? 16 : 8;
+  if ((TK + 2) * (TL + 2) > 512 || TK * TL > nw * (big ? 2 : 3) * 16 || (TK + 4) * (TL + 4) > nw * 64 || R < 1 ||
+      IR < 1)
+    return -2;
   if (lds > 160 * 1024) return -3;
-  dim3 grid((unsigned)((size_t)V * g.nib * g.njb * g.nkt * g.nlt)), block(512);
-#define NCF(H, A, B, C) hipLaunchKernelGGL((nc_fused_k3_kernel<H, A, B, C>), grid, block, lds, stream, (const bf16*)X, \
-                                           (const u32x4*)W1p, b1, (const u32x4*)W2p, b2, Y, g)
+  dim3 grid((unsigned)((size_t)V * g.nib * g.njb * g.nkt * g.nlt)), block(nw * 64);
+#define NCF(H, A, B, C, W) hipLaunchKernelGGL((nc_fused_k3_kernel<H, A, B, C, W>), grid, block, lds, stream, (const bf16*)X, \
+                                              (const u32x4*)W1p, b1, (const u32x4*)W2p, b2, Y, g)
   // the tiles ops/neigh_consensus.py fused_tiles picks at 3200 px (75x100 planes)
   // and 1600 px (37x50) get compile-time geometry; anything else the runtime one
   const bool t3200 = TK == 15 && TL == 20 && R == 10, t1600 = TK == 19 && TL == 17 && R == 8;
+  const bool t3200b = big && TK == 15 && TL == 20 && R == 20;
   if (f16) {
-    if (t3200) NCF(true, 15, 20, 10); else if (t1600) NCF(true, 19, 17, 8); else NCF(true, 0, 0, 0);
+    if (t3200b) NCF(true, 15, 20, 20, 16); else if (big) NCF(true, 0, 0, 0, 16);
+    else if (t3200) NCF(true, 15, 20, 10, 8); else if (t1600) NCF(true, 19, 17, 8, 8); else NCF(true, 0, 0, 0, 8);
   } else {
-    if (t3200) NCF(false, 15, 20, 10); else if (t1600) NCF(false, 19, 17, 8); else NCF(false, 0, 0, 0);
+    if (t3200b) NCF(false, 15, 20, 20, 16); else if (big) NCF(false, 0, 0, 0, 16);
+    else if (t3200) NCF(false, 15, 20, 10, 8); else if (t1600) NCF(false, 19, 17, 8, 8); else NCF(false, 0, 0, 0, 8);
   }
 #undef NCF
   return (int)hipGetLastError();

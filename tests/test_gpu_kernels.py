@@ -886,6 +886,28 @@ def test_nc_fused_k3_vs_quantized_oracle(cfg):
     assert relerr(y, yr.squeeze(1)) < 2e-3
 
 
+def test_nc_fused_k3_one_wide_workgroup():
+    """The > 80 KB configuration of the fused NC kernel (a 24-plane output
+    ring: one 16-wave workgroup per CU, csrc/nc_fused.hip NW = 16) against the
+    quantized fp64 oracle."""
+    import importlib
+    from ncnet_amd.engine import quantized_oracle as qo
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    torch.manual_seed(23)
+    V, I, J, K, L = 1, 6, 26, 17, 22
+    w1 = torch.randn(16, 1, 3, 3, 3, 3, device=DEV) * 0.2
+    w2 = torch.randn(1, 16, 3, 3, 3, 3, device=DEV) * 0.1
+    b1, b2 = torch.rand(16, device=DEV) * 0.1 - 0.03, torch.rand(1, device=DEV) * 0.1
+    x0 = torch.rand(V, I, J, K, L, device=DEV).to(torch.bfloat16)
+    wts = nc._fused_weights([ref.conv4d_weight_from_std(w1), ref.conv4d_weight_from_std(w2)], [b1, b2])
+    y = torch.full((V, I, J, K, L), float("nan"), device=DEV)
+    _ext.ext().nc_fused_k3(x0, *wts, y, 24, 4, 15, 20)      # R = 24, IR = 4, 15 x 20 tiles
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    yr = qo.nc_stack(x0.double().unsqueeze(1), [w1.double(), w2.double()], [b1.double(), b2.double()])
+    assert relerr(y, yr.squeeze(1)) < 2e-3
+
+
 def test_neigh_consensus_fused_symmetric_wrapper():
     """The symmetric InLoc NC (both branches through the fused kernel in one
     launch: cast + transpose into one [2V, ...] input, then the combine)
