@@ -37,6 +37,7 @@ int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, 
                           float, int, hipStream_t);
 int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, int, hipStream_t);
 int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, float*, int, int, hipStream_t);
+int ncnet_stats2d(const float*, float*, int*, float*, float*, int*, float*, int, int, int, float*, int, hipStream_t);
 int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, int, hipStream_t);
 int ncnet_mm_bwd(const float*, const float*, const float*, const int*, const float*, const int*, float*, float*, float*,
                  int, int, int, float, hipStream_t);
@@ -470,6 +471,34 @@ void stats_cols(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Te
      "stats_cols");
 }
 
+// x [V,R,C] fp32 -> row stats [V,R] and column stats [V,C] in one pass
+// (stats_rows + stats_cols); returns false (nothing written) if C % 4 != 0.
+bool stats2d(Tensor x, Tensor rmx, Tensor rarg, c10::optional<Tensor> rse, Tensor cmx, Tensor carg,
+             c10::optional<Tensor> cse, int64_t sum_kind) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  check(x, "x", at::kFloat);
+  TORCH_CHECK(x.dim() == 3);
+  const int64_t V = x.size(0), R = x.size(1), C = x.size(2);
+  if (C % 4 != 0) return false;
+  check(rmx, "rmx", at::kFloat); check_shape(rmx, "rmx", {V, R});
+  check(rarg, "rarg", at::kInt); check_shape(rarg, "rarg", {V, R});
+  check(cmx, "cmx", at::kFloat); check_shape(cmx, "cmx", {V, C});
+  check(carg, "carg", at::kInt); check_shape(carg, "carg", {V, C});
+  if (sum_kind) {
+    TORCH_CHECK(rse.has_value() && cse.has_value(), "stats2d: sum_kind needs rse and cse");
+    check(*rse, "rse", at::kFloat); check_shape(*rse, "rse", {V, R});
+    check(*cse, "cse", at::kFloat); check_shape(*cse, "cse", {V, C});
+  }
+  const int64_t nrt = (R + 63) / 64, nct = (C + 255) / 256;
+  Tensor work = at::empty({3 * V * (nct * R + nrt * C)}, x.options());
+  ok(ncnet_stats2d((float*)x.data_ptr(), (float*)rmx.data_ptr(), (int*)rarg.data_ptr(),
+                   sum_kind ? (float*)rse->data_ptr() : nullptr, (float*)cmx.data_ptr(), (int*)carg.data_ptr(),
+                   sum_kind ? (float*)cse->data_ptr() : nullptr, (int)V, (int)R, (int)C, (float*)work.data_ptr(),
+                   (int)sum_kind, cur_stream(x)),
+     "stats2d");
+  return true;
+}
+
 void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10::optional<Tensor> out_x,
               c10::optional<Tensor> out_xt, double eps) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
@@ -834,6 +863,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("corr_gemm_pool2", &corr_gemm_pool2);
   m.def("stats_rows", &stats_rows);
   m.def("stats_cols", &stats_cols);
+  m.def("stats2d", &stats2d);
   m.def("mm_apply", &mm_apply);
   m.def("mm_bwd", &mm_bwd);
   m.def("combine_fwd", &combine_fwd);

@@ -127,6 +127,104 @@ __global__ __launch_bounds__(256) void stats_cols_merge_kernel(const float* __re
 }
 
 // ---------------------------------------------------------------------------
+// stats2d: row AND column stats of [V, R, C] in ONE pass over the volume
+// (MutualMatching needs both maxima, the bidirectional match extraction both
+// softmax stats: two strided passes before, each at ~1 TB/s -- a wave per row
+// with 4-byte loads, and 64-column blocks walking rows).  Block = a 64-row x
+// 256-column tile, 4 waves x 16 rows, each lane 4 consecutive columns (one
+// 16-byte load per row, all 16 rows issued before any use): per-lane column
+// stats over the wave's rows are merged across the 4 waves in LDS into one
+// column partial per tile; each row's 256-column partial is a wave reduction.
+// Partials [V][tiles][n] are merged in tile order by stats2d_merge (ties keep
+// the smallest index either way).  Needs C % 4 == 0 (16-byte rows).
+// ---------------------------------------------------------------------------
+template <int WS>
+__global__ __launch_bounds__(256) void stats2d_tile_kernel(const float* __restrict__ x, int R, int C, int nrt, int nct,
+                                                           float* __restrict__ rpm, int* __restrict__ rpi,
+                                                           float* __restrict__ rps, float* __restrict__ cpm,
+                                                           int* __restrict__ cpi, float* __restrict__ cps) {
+  __shared__ float sm[4][256], ss[4][256];
+  __shared__ int si[4][256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int b = blockIdx.x;
+  const int ct = b % nct; b /= nct;
+  const int rt = b % nrt;
+  const int v = b / nrt;
+  const int c0 = ct * 256 + lane * 4;
+  const bool cok = c0 < C;
+  const int rbase = rt * 64 + wave * 16;
+  const float* xv = x + (size_t)v * R * C;
+  float4 val[16];
+#pragma unroll
+  for (int rr = 0; rr < 16; ++rr) {
+    const int r = rbase + rr;
+    val[rr] = (cok && r < R) ? *(const float4*)(xv + (size_t)r * C + c0) : float4{0.f, 0.f, 0.f, 0.f};
+  }
+  Stat col[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) col[k] = Stat{-INFINITY, 0.f, 0x7fffffff};
+#pragma unroll
+  for (int rr = 0; rr < 16; ++rr) {
+    const int r = rbase + rr;
+    if (r >= R) break;                                   // wave-uniform
+    const float e[4] = {val[rr].x, val[rr].y, val[rr].z, val[rr].w};
+    Stat rs{-INFINITY, 0.f, 0x7fffffff};
+    if (cok) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        col[k] = stat_push(col[k], e[k], r, WS);
+        rs = stat_push(rs, e[k], c0 + k, WS);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      Stat ot;
+      ot.m = __shfl_xor(rs.m, o, 64);
+      ot.s = __shfl_xor(rs.s, o, 64);
+      ot.idx = __shfl_xor(rs.idx, o, 64);
+      rs = stat_merge(rs, ot, WS);
+    }
+    if (lane == 0) {
+      const size_t o = ((size_t)v * nct + ct) * R + r;
+      rpm[o] = rs.m; rpi[o] = rs.idx;
+      if (WS) rps[o] = rs.s;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { sm[wave][lane * 4 + k] = col[k].m; ss[wave][lane * 4 + k] = col[k].s; si[wave][lane * 4 + k] = col[k].idx; }
+  __syncthreads();
+  const int cc = threadIdx.x;                           // one column of the tile per thread
+  const int c = ct * 256 + cc;
+  if (c < C) {
+    Stat a{sm[0][cc], ss[0][cc], si[0][cc]};
+#pragma unroll
+    for (int w = 1; w < 4; ++w) a = stat_merge(a, Stat{sm[w][cc], ss[w][cc], si[w][cc]}, WS);
+    const size_t o = ((size_t)v * nrt + rt) * C + c;
+    cpm[o] = a.m; cpi[o] = a.idx;
+    if (WS) cps[o] = a.s;
+  }
+}
+
+// merge [V][nt][n] partials -> [V][n]
+template <int WS>
+__global__ __launch_bounds__(256) void stats2d_merge_kernel(const float* __restrict__ pm, const int* __restrict__ pi,
+                                                            const float* __restrict__ ps, float* __restrict__ mx,
+                                                            int* __restrict__ arg, float* __restrict__ se, int V,
+                                                            int n, int nt) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)V * n) return;
+  const int v = (int)(e / n), i = (int)(e - (long long)v * n);
+  Stat a{-INFINITY, 0.f, 0x7fffffff};
+  for (int t = 0; t < nt; ++t) {
+    const size_t o = ((size_t)v * nt + t) * n + i;
+    a = stat_merge(a, Stat{pm[o], WS ? ps[o] : 0.f, pi[o]}, WS);
+  }
+  mx[e] = a.m;
+  if (arg) arg[e] = a.idx;
+  if (WS && se) se[e] = a.s;
+}
+
+// ---------------------------------------------------------------------------
 // MutualMatching apply, 64x64 tiles.  rmax: [V,R] (max over B for each A row),
 // cmax: [V,C] (max over A for each B column).
 //   out_f32 [V,R,C] (optional), out_x bf16 [V,R,C] at volume slot v (optional),
@@ -418,6 +516,25 @@ extern "C" int ncnet_stats_cols(const float* x, float* mx, int* arg, float* se, 
                      se ? ps : nullptr, R, C, nchunk, rpc, sum_kind);
   hipLaunchKernelGGL(stats_cols_merge_kernel, dim3((unsigned)cdiv(V * C, 256)), dim3(256), 0, s, pm, pi,
                      se ? ps : nullptr, mx, arg, se, V, C, nchunk, sum_kind);
+  return (int)hipGetLastError();
+}
+// stats2d: work = 3 * V * (nct * R + nrt * C) floats of partials (nrt = ceil(R / 64), nct = ceil(C / 256)).
+// sum_kind 0: max / argmax only (rse, cse ignored).  C % 4 == 0 (else -2).
+extern "C" int ncnet_stats2d(const float* x, float* rmx, int* rarg, float* rse, float* cmx, int* carg, float* cse,
+                             int V, int R, int C, float* work, int sum_kind, hipStream_t s) {
+  if (C % 4 != 0) return -2;
+  const int nrt = cdiv(R, 64), nct = cdiv(C, 256);
+  const size_t nr = (size_t)V * nct * R, nc = (size_t)V * nrt * C;
+  float* rpm = work; int* rpi = (int*)(work + nr); float* rps = work + 2 * nr;
+  float* cpm = work + 3 * nr; int* cpi = (int*)(cpm + nc); float* cps = cpm + 2 * nc;
+  const dim3 grid((unsigned)((size_t)V * nrt * nct)), blk(256);
+#define S2D(WSV) do { \
+    hipLaunchKernelGGL(stats2d_tile_kernel<WSV>, grid, blk, 0, s, x, R, C, nrt, nct, rpm, rpi, rps, cpm, cpi, cps); \
+    hipLaunchKernelGGL(stats2d_merge_kernel<WSV>, dim3((unsigned)cdiv(V * R, 256)), blk, 0, s, rpm, rpi, rps, rmx, rarg, rse, V, R, nct); \
+    hipLaunchKernelGGL(stats2d_merge_kernel<WSV>, dim3((unsigned)cdiv(V * C, 256)), blk, 0, s, cpm, cpi, cps, cmx, carg, cse, V, C, nrt); \
+  } while (0)
+  if (sum_kind == 1) S2D(1); else if (sum_kind == 2) S2D(2); else S2D(0);
+#undef S2D
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_mm_apply(const float* c, const float* rmax, const float* cmax, float* out_f32, void* out_x,

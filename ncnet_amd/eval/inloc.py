@@ -21,7 +21,7 @@ import torch
 
 from ..data.transforms import normalize_image, resize_bilinear
 from ..ops.neigh_consensus import pin_fp8_weights
-from .point_tnf import corr_to_matches
+from .point_tnf import best_both, corr_to_matches
 
 SCALE_FACTOR = 0.0625  # feature stride 1/16 (eval_inloc.py:77)
 
@@ -78,8 +78,9 @@ def pair_matches(corr4d, delta4d, k_size: int, do_softmax: bool = True, both_dir
     k = max(1, k_size)
     kw = dict(scale="positive", do_softmax=do_softmax, delta4d=delta4d, k_size=k, return_indices=True)
     if both_dirs:
-        r1 = corr_to_matches(corr4d, **kw)
-        r2 = corr_to_matches(corr4d, invert_matching_direction=True, **kw)
+        both = best_both(corr4d, do_softmax)            # one pass for both directions where it applies
+        r1 = corr_to_matches(corr4d, best=both[0] if both else None, **kw)
+        r2 = corr_to_matches(corr4d, invert_matching_direction=True, best=both[1] if both else None, **kw)
         xA, yA, xB, yB, sc, iA, jA, iB, jB = (torch.cat((a.reshape(-1), c.reshape(-1))) for a, c in zip(r1, r2))
         HA, WA, HB, WB = fs1 * k, fs2 * k, fs3 * k, fs4 * k
         key = ((jA.long() * HA + iA.long()) * WB + jB.long()) * HB + iB.long()  # lexicographic (xA,yA,xB,yB)

@@ -42,8 +42,31 @@ def _best(mat: torch.Tensor, dim: int, do_softmax: bool):
     return score, idx
 
 
+def best_both(corr4d, do_softmax: bool):
+    """The (score, index) of the best entry along both directions of the
+    volume in one pass (stats2d) -> ((score_B, idx_B), (score_A, idx_A)), or
+    None where stats2d does not apply (CPU, or rows not a 16-byte multiple)."""
+    b, _, fs1, fs2, fs3, fs4 = corr4d.shape
+    mat = corr4d.reshape(b, fs1 * fs2, fs3 * fs4)
+    if not (_ext.use_hip(mat) and mat.dtype == torch.float32):
+        return None
+    x = mat.contiguous()
+    R, C = x.shape[1], x.shape[2]
+    f = dict(dtype=torch.float32, device=x.device)
+    rmx, cmx = torch.empty((b, R), **f), torch.empty((b, C), **f)
+    rarg = torch.empty((b, R), dtype=torch.int32, device=x.device)
+    carg = torch.empty((b, C), dtype=torch.int32, device=x.device)
+    rse = torch.empty((b, R), **f) if do_softmax else None
+    cse = torch.empty((b, C), **f) if do_softmax else None
+    if not _ext.ext().stats2d(x, rmx, rarg, rse, cmx, carg, cse, 1 if do_softmax else 0):
+        return None
+    col = ((1.0 / cse) if do_softmax else cmx, carg.long())
+    row = ((1.0 / rse) if do_softmax else rmx, rarg.long())
+    return col, row
+
+
 def corr_to_matches(corr4d, delta4d=None, k_size=1, do_softmax=False, scale="centered", return_indices=False,
-                    invert_matching_direction=False):
+                    invert_matching_direction=False, best=None):
     """Matches from a [b,1,fs1,fs2,fs3,fs4] volume (lib/point_tnf.py:12-80).
 
     B->A (default): for each B cell the best A cell; A->B with
@@ -60,12 +83,12 @@ def corr_to_matches(corr4d, delta4d=None, k_size=1, do_softmax=False, scale="cen
     if mat.dtype != torch.float32:
         mat = mat.float()
     if invert_matching_direction:
-        score, idx = _best(mat, 2, do_softmax)           # per A cell, best B
+        score, idx = best if best is not None else _best(mat, 2, do_softmax)   # per A cell, best B
         ia = torch.arange(fs1 * fs2, device=dev).expand(b, -1)
         iA, jA = ia // fs2, ia % fs2
         iB, jB = idx // fs4, idx % fs4
     else:
-        score, idx = _best(mat, 1, do_softmax)           # per B cell, best A
+        score, idx = best if best is not None else _best(mat, 1, do_softmax)   # per B cell, best A
         ib = torch.arange(fs3 * fs4, device=dev).expand(b, -1)
         iB, jB = ib // fs4, ib % fs4
         iA, jA = idx // fs2, idx % fs2

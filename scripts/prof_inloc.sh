@@ -11,6 +11,6 @@ export TMPDIR=/tmp
 OUT="$ROOT/gpurun_out/prof_inloc$TAG"
 rm -rf "$OUT"
 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$OUT" -o run \
-  -- python3 "$ROOT/scripts/bench_inloc.py" --image-size "$SIZE" --pairs 3 --warmup 1 "$@" || exit $?
+  -- python3 "$ROOT/scripts/bench_inloc.py" --image-size "$SIZE" --pairs ${PAIRS:-3} --warmup 1 "$@" || exit $?
 f=$(find "$OUT" -name "*kernel_trace.csv" | head -1)
-python3 "$ROOT/scripts/prof_summary.py" "$f" --warmup 1 --steps 3 --out "$ROOT/gpurun_out/prof_inloc_$SIZE$TAG.md"
+python3 "$ROOT/scripts/prof_summary.py" "$f" --warmup 1 --steps ${PAIRS:-3} --out "$ROOT/gpurun_out/prof_inloc_$SIZE$TAG.md"

@@ -886,6 +886,39 @@ def test_nc_fused_k3_vs_quantized_oracle(cfg):
     assert relerr(y, yr.squeeze(1)) < 2e-3
 
 
+@pytest.mark.parametrize("shape", [(1, 7500, 7500), (3, 625, 400), (2, 130, 1852), (1, 64, 256)])
+@pytest.mark.parametrize("sum_kind", [0, 1, 2])
+def test_stats2d_matches_row_and_col_kernels(shape, sum_kind):
+    """One-pass row + column statistics (csrc/volume.hip stats2d) equal the
+    separate stats_rows / stats_cols kernels: max and first argmax exactly
+    (values drawn from a small set: many ties), the sums to fp32 rounding."""
+    V, R, C = shape
+    torch.manual_seed(31)
+    x = (torch.randint(0, 50, shape, device=DEV).float() / 7.0 - 3.0).contiguous()
+    E = _ext.ext()
+    f = dict(dtype=torch.float32, device=DEV)
+    out = []
+    for fused in (True, False):
+        rmx, cmx = torch.empty((V, R), **f), torch.empty((V, C), **f)
+        rarg, carg = (torch.empty((V, n), dtype=torch.int32, device=DEV) for n in (R, C))
+        rse, cse = torch.empty((V, R), **f), torch.empty((V, C), **f)
+        if fused:
+            assert E.stats2d(x, rmx, rarg, rse, cmx, carg, cse, sum_kind)
+        else:
+            E.stats_rows(x, rmx, rarg, rse if sum_kind else None, sum_kind)
+            E.stats_cols(x, cmx, carg, cse if sum_kind else None, sum_kind)
+        out.append((rmx, rarg, rse, cmx, carg, cse))
+    a, b = out
+    for i in (0, 1, 3, 4):
+        assert torch.equal(a[i], b[i]), i
+    if sum_kind:
+        for i in (2, 5):
+            assert torch.allclose(a[i], b[i], rtol=1e-5, atol=1e-5), (i, (a[i] - b[i]).abs().max())
+    # rows not a 16-byte multiple: stats2d declines and writes nothing
+    assert not E.stats2d(x[..., :C - 1].contiguous(), rmx, rarg, None, cmx[:, :C - 1].contiguous(),
+                         carg[:, :C - 1].contiguous(), None, 0) if C % 4 == 0 and C > 4 else True
+
+
 def test_nc_fused_k3_one_wide_workgroup():
     """The > 80 KB configuration of the fused NC kernel (a 24-plane output
     ring: one 16-wave workgroup per CU, csrc/nc_fused.hip NW = 16) against the
