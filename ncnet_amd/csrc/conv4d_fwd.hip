@@ -624,6 +624,14 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
   constexpr int NVOX = TK * TL;
   constexpr int NTILE = (NVOX + 15) / 16;
   constexpr int MAXT = (NTILE + NW - 1) / NW;
+  // SPLIT (the 20 x 20 plane: 25 tiles over 8 waves): the one tile past
+  // 8 x MT is not given whole to wave 0 (a 4th tile while the others hold 3,
+  // i.e. 22 % idle MFMA time) but split by output plane: wave w < R computes
+  // it for r = w only (one MFMA per K-step on the steps where dj = s - w is
+  // a live tap), with its own accumulator and per-K-step weight reads
+  constexpr bool SPLIT = NTILE % NW == 1 && NTILE > NW && R <= NW;
+  constexpr int MT = SPLIT ? NTILE / NW : MAXT;   // whole tiles per wave
+  constexpr int TS = NW * MT;                      // the split tile (SPLIT)
   constexpr int S = R + KS - 1;              // input j-planes per di
   constexpr int RS = TL + 8;                 // row stride (voxels): a wrapping tile jumps one 256-B bank period
   constexpr int PR = TK + KS - 1;            // staged rows
@@ -661,24 +669,28 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
   // padded last pair, whose half-1 weights are zero: it reads voxel ll + 5 of
   // the same DMA-written row), c2 = half 1 one row down with dl wrapped
   // (2q + 1 a multiple of KS)
-  uint32_t c1[MAXT], c2[MAXT];
+  uint32_t c1[MT], c2[MT];
+  uint32_t c1s = 0, c2s = 0;                       // the split tile's bases (SPLIT)
   {
     const uint32_t hh = (uint32_t)(lane >> 5);
-#pragma unroll
-    for (int tt = 0; tt < MAXT; ++tt) {
-      int vi = (wave + NW * tt) * 16 + (lane & 15);
+    auto bases = [&](int tile, uint32_t& a1, uint32_t& a2) {
+      int vi = tile * 16 + (lane & 15);
       if (vi >= NVOX) vi = 0;
       const int kk = vi / TL, ll = vi - kk * TL;
       const uint32_t b0 = (uint32_t)(XOFF + (kk * RS + ll) * 32 + ((lane >> 4) & 1) * 16);
-      c1[tt] = b0 + hh * 32u;
-      c2[tt] = b0 + hh * (uint32_t)((RS - KS + 1) * 32);
-    }
+      a1 = b0 + hh * 32u;
+      a2 = b0 + hh * (uint32_t)((RS - KS + 1) * 32);
+    };
+#pragma unroll
+    for (int tt = 0; tt < MT; ++tt) bases(wave + NW * tt, c1[tt], c2[tt]);
+    if constexpr (SPLIT) bases(TS, c1s, c2s);
   }
-  f32x4 acc[R][MAXT];
+  f32x4 acc[R][MT];
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
-    for (int tt = 0; tt < MAXT; ++tt) acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int tt = 0; tt < MT; ++tt) acc[r][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accs = {0.f, 0.f, 0.f, 0.f};               // split tile, output plane r = wave (SPLIT)
 
   // Plane DMA through a buffer resource over ONE (i, j) plane: every lane of a
   // row instruction writes its 16-B chunk (row voxel lane / 2 = l0 - P + lane / 2),
@@ -769,13 +781,13 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
       if (jp >= 0 && jp < g.J) {
         constexpr int dlo = (s - R + 1) > 0 ? (s - R + 1) : 0;
         constexpr int dhi = s < KS - 1 ? s : KS - 1;  // inclusive
-        // (q, tt) MFMA groups in order k = q * MAXT + tt; the weight fragments
+        // (q, tt) MFMA groups in order k = q * MT + tt; the weight fragments
         // of K-step q + 1 are read at group (q, 0) (double buffer), the X
         // fragment of group k + 2 at group k (three registers in rotation);
         // sched_group_barrier pins that order (the default scheduler sinks each
         // read to just before its MFMAs and waits lgkmcnt(0) there)
         constexpr int NDJ = dhi - dlo + 1;
-        constexpr int NK = NQ * MAXT;
+        constexpr int NK = NQ * MT;
         bf16x8 A[2][KS], Xr[3];
         auto load_a = [&](auto qc) {
           constexpr int q = decltype(qc)::value;
@@ -788,7 +800,7 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
         };
         auto load_x = [&](auto kc) {
           constexpr int k = decltype(kc)::value;
-          constexpr int q = k / MAXT, tt = k % MAXT;
+          constexpr int q = k / MT, tt = k % MT;
           constexpr int t0 = 2 * q;
           constexpr uint32_t T0 = (uint32_t)(((t0 / KS) * RS + t0 % KS) * 32);
           const uint32_t base = ((2 * q + 1) % KS == 0 && 2 * q + 1 < NT) ? c2[tt] : c1[tt];
@@ -800,7 +812,7 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
         __builtin_amdgcn_sched_group_barrier(0x100, NDJ + 2, 0);
         static_for<0, NK>([&](auto kc) {
           constexpr int k = decltype(kc)::value;
-          constexpr int q = k / MAXT, tt = k % MAXT;
+          constexpr int q = k / MT, tt = k % MT;
           constexpr bool LA = tt == 0 && q + 1 < NQ;
           constexpr bool LX = k + 2 < NK;
           if constexpr (LA) load_a(std::integral_constant<int, q + 1>{});
@@ -812,12 +824,37 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
           if constexpr (LA || LX) __builtin_amdgcn_sched_group_barrier(0x100, (LA ? NDJ : 0) + (LX ? 1 : 0), 0);
           __builtin_amdgcn_sched_group_barrier(0x008, NDJ, 0);
         });
+        if constexpr (SPLIT) {
+          // the split tile for output plane r = wave: tap slot dj = s - wave,
+          // one accumulation chain over the NQ K-steps (weights of slot dj and
+          // the tile's X fragment read one K-step ahead)
+          const int dj = s - wave;
+          if (wave < R && dj >= 0 && dj < KS) {
+            const uint32_t wdj = wb + (uint32_t)(dj * NQ * 1024);
+            bf16x8 As[2], Xs[2];
+            auto ld = [&](auto qc) {
+              constexpr int q = decltype(qc)::value;
+              constexpr int t0 = 2 * q;
+              constexpr uint32_t T0 = (uint32_t)(((t0 / KS) * RS + t0 % KS) * 32);
+              const uint32_t base = ((2 * q + 1) % KS == 0 && 2 * q + 1 < NT) ? c2s : c1s;
+              As[q & 1] = *(const bf16x8*)(smem + wdj + q * 1024);
+              Xs[q & 1] = *(const bf16x8*)(smem + base + T0);
+            };
+            ld(std::integral_constant<int, 0>{});
+            static_for<0, NQ>([&](auto qc) {
+              constexpr int q = decltype(qc)::value;
+              if constexpr (q + 1 < NQ) ld(std::integral_constant<int, q + 1>{});
+              accs = mfma16(As[q & 1], Xs[q & 1], accs);
+            });
+          }
+        }
       }
       // advance the X addresses to the next step's buffer ((n + 1) % 3)
       {
         const uint32_t adv = (n % 3 == 2) ? (uint32_t)(-2 * PLANE) : (uint32_t)PLANE;
 #pragma unroll
-        for (int tt = 0; tt < MAXT; ++tt) { c1[tt] += adv; c2[tt] += adv; }
+        for (int tt = 0; tt < MT; ++tt) { c1[tt] += adv; c2[tt] += adv; }
+        if constexpr (SPLIT) { c1s += adv; c2s += adv; }
       }
       ++n;
     });
@@ -825,9 +862,8 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 
   const size_t nvox_all = (size_t)g.V * g.I * g.J * g.K * g.L;
-  auto out_vox = [&](int r, int tt, size_t& vox) -> bool {
+  auto out_vox_t = [&](int r, int tile, size_t& vox) -> bool {
     const int j = j0 + r;
-    const int tile = wave + NW * tt;
     const int vi = tile * 16 + (lane & 15);
     const int kk = vi / TL, ll = vi - kk * TL;
     const int kg = k0 + kk, lg = l0 + ll;
@@ -835,32 +871,47 @@ __global__ __launch_bounds__(512, 1) void conv16v4_fwd_kernel(const bf16* __rest
     vox = ok ? plane_offset(g, tv, ti, j, 1) + (size_t)kg * g.L + lg : 0;
     return ok;
   };
+  auto out_vox = [&](int r, int tt, size_t& vox) -> bool { return out_vox_t(r, wave + NW * tt, vox); };
   // EPI_MASK: every ReLU-mask load of the item first (fixed count, out-of-range
   // voxels read voxel 0), then the stores: a load -> wait -> store sequence per
   // (r, tt) serialised 25 memory round trips (stores count in vmcnt here)
   constexpr bool MPF = (EPI & ~EPI_X3) == EPI_MASK;
-  u32x2 mreg[MPF ? R : 1][MPF ? MAXT : 1];
+  u32x2 mreg[MPF ? R : 1][MPF ? MT : 1];
+  u32x2 mregs = {0u, 0u};
   const f32x4 bv = lane_bias4<EPI>(bias, lane);
   if constexpr (MPF) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int tt = 0; tt < MAXT; ++tt) {
+      for (int tt = 0; tt < MT; ++tt) {
         size_t vox;
         out_vox(r, tt, vox);
         mreg[r][tt] = *(const u32x2*)(M + vox * 16 + 4 * (lane >> 4));
       }
+    if constexpr (SPLIT) {
+      size_t vox;
+      out_vox_t(wave < R ? wave : 0, TS, vox);
+      mregs = *(const u32x2*)(M + vox * 16 + 4 * (lane >> 4));
+    }
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
 #pragma unroll
-    for (int tt = 0; tt < MAXT; ++tt) {
+    for (int tt = 0; tt < MT; ++tt) {
       size_t vox;
       if (out_vox(r, tt, vox)) {
         const u32x2* mp = nullptr;
         if constexpr (MPF) mp = &mreg[r][tt];
         store16<EPI>(acc[r][tt], Y, M, bias, vox, 4 * (lane >> 4), nvox_all, g.nco, g.nt, g.ylo, mp, &bv);
       }
+    }
+  }
+  if constexpr (SPLIT) {
+    size_t vox;
+    if (wave < R && out_vox_t(wave, TS, vox)) {
+      const u32x2* mp = nullptr;
+      if constexpr (MPF) mp = &mregs;
+      store16<EPI>(accs, Y, M, bias, vox, 4 * (lane >> 4), nvox_all, g.nco, g.nt, g.ylo, mp, &bv);
     }
   }
 #endif

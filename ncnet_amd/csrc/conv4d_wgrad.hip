@@ -505,8 +505,13 @@ struct W4C {
   static constexpr int TPG = (NT - 1) / 4, EXP = (KS + 2) / 3;
   static constexpr int KL = K * L;
   static constexpr int NTL = (KL + 319) / 320;
-  static constexpr int VT = (((KL + NTL - 1) / NTL) + 63) / 64 * 64;
-  static constexpr int NCH = VT / 64;                    // 32-voxel chunks per half
+  // VT: a multiple of 32 voxels (was 64): the two wave halves take NCH0 and
+  // NCH1 32-voxel chunks (20 x 20 planes: 2 tiles of 224 = 4 + 3 chunks, 448
+  // voxel slots for 400 voxels, where 64-voxel rounding gave 512)
+  static constexpr int NC32 = (((KL + NTL - 1) / NTL) + 31) / 32;
+  static constexpr int VT = NC32 * 32;
+  static constexpr int NCH0 = (NC32 + 1) / 2, NCH1 = NC32 / 2;   // chunks of half 0 / half 1
+  static constexpr int NCH = NCH0;                       // the larger
   static constexpr int RS = L + 8, RW = L + KS - 1;
   static constexpr int PR = (VT - 1) / L + 2 + KS - 1;   // staged X rows
   static constexpr int XB = PR * RS * 32, GB = VT * 32;
@@ -539,12 +544,13 @@ __device__ __forceinline__ void bdma16_lds(const i32x4v& rs, uint32_t voff, uint
                : "memory", "m0");
 }
 
-template <int KS, int K, int L, int TG>
+template <int KS, int K, int L, int TG, int NCHH>
 __device__ __forceinline__ void wgrad16v4_body(const bf16* __restrict__ X, const bf16* __restrict__ G,
                                                float* __restrict__ part, float* __restrict__ partb, const W3Geom& g,
                                                int wave, int half, int dj, int grp) {
   using C = W4C<KS, K, L>;
-  constexpr int P = C::P, NT = C::NT, TPG = C::TPG, EXP = C::EXP, NCH = C::NCH, NS = C::NS, NW = C::NW;
+  constexpr int P = C::P, NT = C::NT, TPG = C::TPG, EXP = C::EXP, NS = C::NS, NW = C::NW;
+  constexpr int NCH = NCHH;                              // this wave's chunks (its half's share)
   constexpr int RS = C::RS, PR = C::PR, XB = C::XB, GB = C::GB;
   constexpr int RPW = C::RPW, GPW = C::GPW, GQ = C::GQ;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -660,7 +666,7 @@ __device__ __forceinline__ void wgrad16v4_body(const bf16* __restrict__ X, const
   issue_x(); issue_g();
 
   // ---- compute ------------------------------------------------------------
-  const int ch_lo = half * NCH;
+  const int ch_lo = half * C::NCH0;
   const uint32_t ga_base = (uint32_t)((ch_lo * 32 + gq * 4 + qq) * 32 + pp * 8);
   uint32_t pav0[NCH], pav1[NCH];
   auto set_tile = [&](int c) {
@@ -771,6 +777,20 @@ __device__ __forceinline__ void wgrad16v4_body(const bf16* __restrict__ X, const
   if (TG == 0 && center_blk && lane < 16) partb[row * 16 + lane] = accb[0];
 }
 
+// the body for this wave's half: one instantiation when both halves hold the
+// same chunk count, two otherwise
+template <int KS, int K, int L, int TG>
+__device__ __forceinline__ void w4_half(const bf16* __restrict__ X, const bf16* __restrict__ G, float* __restrict__ part,
+                                        float* __restrict__ partb, const W3Geom& g, int wave, int half, int dj, int grp) {
+  using C = W4C<KS, K, L>;
+  if constexpr (C::NCH0 == C::NCH1) {
+    wgrad16v4_body<KS, K, L, TG, C::NCH0>(X, G, part, partb, g, wave, half, dj, grp);
+  } else {
+    if (half == 0) wgrad16v4_body<KS, K, L, TG, C::NCH0>(X, G, part, partb, g, wave, half, dj, grp);
+    else wgrad16v4_body<KS, K, L, TG, C::NCH1>(X, G, part, partb, g, wave, half, dj, grp);
+  }
+}
+
 template <int KS, int K, int L>
 __global__ __launch_bounds__(512, 1) void wgrad16v4_kernel(const bf16* __restrict__ X, const bf16* __restrict__ G,
                                                            float* __restrict__ part, float* __restrict__ partb,
@@ -781,10 +801,10 @@ __global__ __launch_bounds__(512, 1) void wgrad16v4_kernel(const bf16* __restric
   const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
   const int dj = lb % KS, grp = lb / KS;
   switch (tg) {
-    case 0: wgrad16v4_body<KS, K, L, 0>(X, G, part, partb, g, wave, half, dj, grp); break;
-    case 1: wgrad16v4_body<KS, K, L, 1>(X, G, part, partb, g, wave, half, dj, grp); break;
-    case 2: wgrad16v4_body<KS, K, L, 2>(X, G, part, partb, g, wave, half, dj, grp); break;
-    default: wgrad16v4_body<KS, K, L, 3>(X, G, part, partb, g, wave, half, dj, grp); break;
+    case 0: w4_half<KS, K, L, 0>(X, G, part, partb, g, wave, half, dj, grp); break;
+    case 1: w4_half<KS, K, L, 1>(X, G, part, partb, g, wave, half, dj, grp); break;
+    case 2: w4_half<KS, K, L, 2>(X, G, part, partb, g, wave, half, dj, grp); break;
+    default: w4_half<KS, K, L, 3>(X, G, part, partb, g, wave, half, dj, grp); break;
   }
 #endif
 }
