@@ -38,6 +38,8 @@ int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, 
 int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, int, hipStream_t);
 int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, float*, int, int, hipStream_t);
 int ncnet_stats2d(const float*, float*, int*, float*, float*, int*, float*, int, int, int, float*, int, hipStream_t);
+int ncnet_match_candidates(const float*, const float*, const int*, const float*, const float*, const int*,
+                           const uint8_t*, int, int, int, int, int, float*, float*, long long*, hipStream_t);
 int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, int, hipStream_t);
 int ncnet_mm_bwd(const float*, const float*, const float*, const int*, const float*, const int*, float*, float*, float*,
                  int, int, int, float, hipStream_t);
@@ -499,6 +501,32 @@ bool stats2d(Tensor x, Tensor rmx, Tensor rarg, c10::optional<Tensor> rse, Tenso
   return true;
 }
 
+// one volume's bidirectional match candidates from its column (B cells) and
+// row (A cells) stats: m [N,5] fp32, sc [N] fp32, key [N] int64, N = R + C;
+// code: packed 2-bit offsets uint8 [R*C] (k = 2) or none
+void match_candidates(Tensor cmx, c10::optional<Tensor> cse, Tensor carg, Tensor rmx, c10::optional<Tensor> rse,
+                      Tensor rarg, c10::optional<Tensor> code, int64_t fs1, int64_t fs2, int64_t fs3, int64_t fs4,
+                      int64_t k, Tensor m, Tensor sc, Tensor key) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(cmx.device());
+  const int64_t R = fs1 * fs2, C = fs3 * fs4;
+  check(cmx, "cmx", at::kFloat); check_shape(cmx, "cmx", {C});
+  check(carg, "carg", at::kInt); check_shape(carg, "carg", {C});
+  check(rmx, "rmx", at::kFloat); check_shape(rmx, "rmx", {R});
+  check(rarg, "rarg", at::kInt); check_shape(rarg, "rarg", {R});
+  TORCH_CHECK(cse.has_value() == rse.has_value(), "match_candidates: both or neither softmax sums");
+  if (cse.has_value()) { check(*cse, "cse", at::kFloat); check_shape(*cse, "cse", {C}); check(*rse, "rse", at::kFloat); check_shape(*rse, "rse", {R}); }
+  if (code.has_value()) { check(*code, "code", at::kByte); TORCH_CHECK(code->numel() == R * C, "match_candidates: code size"); }
+  check(m, "m", at::kFloat); check_shape(m, "m", {R + C, 5});
+  check(sc, "sc", at::kFloat); check_shape(sc, "sc", {R + C});
+  check(key, "key", at::kLong); check_shape(key, "key", {R + C});
+  ok(ncnet_match_candidates((float*)cmx.data_ptr(), cse.has_value() ? (float*)cse->data_ptr() : nullptr,
+                            (int*)carg.data_ptr(), (float*)rmx.data_ptr(), rse.has_value() ? (float*)rse->data_ptr() : nullptr,
+                            (int*)rarg.data_ptr(), code.has_value() ? (uint8_t*)code->data_ptr() : nullptr, (int)fs1,
+                            (int)fs2, (int)fs3, (int)fs4, (int)k, (float*)m.data_ptr(), (float*)sc.data_ptr(),
+                            (long long*)key.data_ptr(), cur_stream(cmx)),
+     "match_candidates");
+}
+
 void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10::optional<Tensor> out_x,
               c10::optional<Tensor> out_xt, double eps) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
@@ -864,6 +892,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stats_rows", &stats_rows);
   m.def("stats_cols", &stats_cols);
   m.def("stats2d", &stats2d);
+  m.def("match_candidates", &match_candidates);
   m.def("mm_apply", &mm_apply);
   m.def("mm_bwd", &mm_bwd);
   m.def("combine_fwd", &combine_fwd);

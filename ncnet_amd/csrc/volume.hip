@@ -225,6 +225,57 @@ __global__ __launch_bounds__(256) void stats2d_merge_kernel(const float* __restr
 }
 
 // ---------------------------------------------------------------------------
+// match_candidates: the bidirectional match candidates of one volume
+// [R = fs1*fs2 A cells, C = fs3*fs4 B cells] from its row / column stats, in
+// one launch (lib/point_tnf.py:12-80 + eval_inloc.py:180-189): entry n < C is
+// B cell n with its best A cell (column stats), entry C + m is A cell m with
+// its best B cell (row stats); the 2-bit relocalization offsets of the matched
+// cell are decoded (packed codes, k = 2), the cells mapped onto the [0, 1]
+// linspace grids at full resolution and recentred to pixel centres.
+// Outputs: m [N][5] = (xA, yA, xB, yB, score), sc [N] score, key [N] int64 =
+// ((jA HA + iA) WB + jB) HB + iB (the lexicographic de-duplication key).
+// Arithmetic mirrors the PyTorch ops it replaces (linspace's two-sided
+// formula, recentre as mul -> div -> add with no contraction).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float lin01(int i, int n) {       // torch.linspace(0, 1, n)[i]
+  const float step = __fdiv_rn(1.f, (float)(n - 1));
+  return i < n / 2 ? __fmul_rn(step, (float)i) : __fsub_rn(1.f, __fmul_rn(step, (float)(n - i - 1)));
+}
+__device__ __forceinline__ float recentre(float y, int n) {
+  return __fadd_rn(__fdiv_rn(__fmul_rn(y, (float)(n - 1)), (float)n), (float)(0.5 / (double)n));
+}
+__global__ __launch_bounds__(256) void match_candidates_kernel(const float* __restrict__ cmx, const float* __restrict__ cse,
+                                                               const int* __restrict__ carg, const float* __restrict__ rmx,
+                                                               const float* __restrict__ rse, const int* __restrict__ rarg,
+                                                               const uint8_t* __restrict__ code, int fs1, int fs2, int fs3,
+                                                               int fs4, int k, float* __restrict__ m, float* __restrict__ sc,
+                                                               long long* __restrict__ key) {
+  const int R = fs1 * fs2, C = fs3 * fs4;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= R + C) return;
+  int a, b;
+  float s;
+  if (e < C) { b = e; a = carg[e]; s = cse ? __fdiv_rn(1.f, cse[e]) : cmx[e]; }
+  else { a = e - C; b = rarg[a]; s = rse ? __fdiv_rn(1.f, rse[a]) : rmx[a]; }
+  a = min(max(a, 0), R - 1);        // an all-NaN line leaves the argmax sentinel: keep the code read in range
+  b = min(max(b, 0), C - 1);
+  int iA = a / fs2, jA = a - (a / fs2) * fs2, iB = b / fs4, jB = b - (b / fs4) * fs4;
+  if (code) {
+    const int c = code[(size_t)a * C + b];
+    iA = iA * k + ((c >> 6) & 3); jA = jA * k + ((c >> 4) & 3);
+    iB = iB * k + ((c >> 2) & 3); jB = jB * k + (c & 3);
+  }   // no offsets: the indices stay at pooled resolution on the k-times grid (point_tnf.corr_to_matches)
+  const int HA = fs1 * k, WA = fs2 * k, HB = fs3 * k, WB = fs4 * k;
+  m[(size_t)e * 5 + 0] = recentre(lin01(jA, WA), WA);
+  m[(size_t)e * 5 + 1] = recentre(lin01(iA, HA), HA);
+  m[(size_t)e * 5 + 2] = recentre(lin01(jB, WB), WB);
+  m[(size_t)e * 5 + 3] = recentre(lin01(iB, HB), HB);
+  m[(size_t)e * 5 + 4] = s;
+  sc[e] = s;
+  key[e] = (((long long)jA * HA + iA) * WB + jB) * HB + iB;
+}
+
+// ---------------------------------------------------------------------------
 // MutualMatching apply, 64x64 tiles.  rmax: [V,R] (max over B for each A row),
 // cmax: [V,C] (max over A for each B column).
 //   out_f32 [V,R,C] (optional), out_x bf16 [V,R,C] at volume slot v (optional),
@@ -535,6 +586,14 @@ extern "C" int ncnet_stats2d(const float* x, float* rmx, int* rarg, float* rse, 
   } while (0)
   if (sum_kind == 1) S2D(1); else if (sum_kind == 2) S2D(2); else S2D(0);
 #undef S2D
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_match_candidates(const float* cmx, const float* cse, const int* carg, const float* rmx,
+                                      const float* rse, const int* rarg, const uint8_t* code, int fs1, int fs2, int fs3,
+                                      int fs4, int k, float* m, float* sc, long long* key, hipStream_t s) {
+  const int n = fs1 * fs2 + fs3 * fs4;
+  hipLaunchKernelGGL(match_candidates_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, cmx, cse, carg, rmx, rse,
+                     rarg, code, fs1, fs2, fs3, fs4, k, m, sc, key);
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_mm_apply(const float* c, const float* rmax, const float* cmax, float* out_f32, void* out_x,

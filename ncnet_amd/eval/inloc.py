@@ -21,6 +21,7 @@ import torch
 
 from ..data.transforms import normalize_image, resize_bilinear
 from ..ops.neigh_consensus import pin_fp8_weights
+from ..ops import _ext
 from .point_tnf import best_both, corr_to_matches
 
 SCALE_FACTOR = 0.0625  # feature stride 1/16 (eval_inloc.py:77)
@@ -67,6 +68,51 @@ def prepare_image(img_uint8_hwc: np.ndarray, image_size: int, k_size: int, devic
     return resize_bilinear(x, h, w).unsqueeze(0)
 
 
+def _fused_candidates(corr4d, delta4d, k: int, do_softmax: bool):
+    """Both directions' match candidates of a single volume in two HIP launches
+    (stats2d + match_candidates: the ~60 small index / gather / arithmetic ops
+    of two corr_to_matches calls, their concatenation and the recentre) ->
+    (m [N, 5] recentred, sc [N], key [N] int64) in the same order and values as
+    the op-by-op path, or None where it does not apply."""
+    b, _, fs1, fs2, fs3, fs4 = corr4d.shape
+    if b != 1 or not (_ext.use_hip(corr4d) and corr4d.dtype == torch.float32):
+        return None
+    if delta4d is not None and not (torch.is_tensor(delta4d) and delta4d.dtype == torch.uint8):
+        return None
+    R, C = fs1 * fs2, fs3 * fs4
+    x = corr4d.reshape(1, R, C).contiguous()
+    dev = x.device
+    f = dict(dtype=torch.float32, device=dev)
+    rmx, cmx = torch.empty((1, R), **f), torch.empty((1, C), **f)
+    rarg = torch.empty((1, R), dtype=torch.int32, device=dev)
+    carg = torch.empty((1, C), dtype=torch.int32, device=dev)
+    rse = torch.empty((1, R), **f) if do_softmax else None
+    cse = torch.empty((1, C), **f) if do_softmax else None
+    E = _ext.ext()
+    if not E.stats2d(x, rmx, rarg, rse, cmx, carg, cse, 1 if do_softmax else 0):
+        return None
+    m = torch.empty((R + C, 5), **f)
+    sc = torch.empty((R + C,), **f)
+    key = torch.empty((R + C,), dtype=torch.int64, device=dev)
+    code = delta4d.reshape(-1) if delta4d is not None else None
+    E.match_candidates(cmx[0], cse[0] if do_softmax else None, carg[0], rmx[0], rse[0] if do_softmax else None,
+                       rarg[0], code, fs1, fs2, fs3, fs4, k, m, sc, key)
+    return m, sc, key
+
+
+def _dedup(sc, key):
+    """Stable de-duplication order: by score (descending), then by key; the
+    first of equal keys is kept -> (idx, first)."""
+    order = torch.argsort(-sc, stable=True)
+    key_s = key[order]
+    order2 = torch.argsort(key_s, stable=True)
+    idx = order[order2]
+    ks_ = key[idx]
+    first = torch.ones_like(ks_, dtype=torch.bool)
+    first[1:] = ks_[1:] != ks_[:-1]
+    return idx, first
+
+
 def pair_matches(corr4d, delta4d, k_size: int, do_softmax: bool = True, both_dirs: bool = True,
                  flip: bool = False, static: bool = False):
     """Bidirectional, de-duplicated, recentred matches of one pair -> [Npts, 5] tensor.
@@ -78,6 +124,17 @@ def pair_matches(corr4d, delta4d, k_size: int, do_softmax: bool = True, both_dir
     k = max(1, k_size)
     kw = dict(scale="positive", do_softmax=do_softmax, delta4d=delta4d, k_size=k, return_indices=True)
     if both_dirs:
+        fc = _fused_candidates(corr4d, delta4d, k, do_softmax)
+        if fc is not None:
+            m_all, sc, key = fc
+            idx, first = _dedup(sc, key)
+            if static:
+                pos = torch.cumsum(first.to(torch.int64), 0) - 1
+                dst = torch.where(first, pos, torch.full_like(pos, idx.numel()))
+                out = torch.zeros((idx.numel() + 1, 5), dtype=m_all.dtype, device=m_all.device)
+                out.index_copy_(0, dst, m_all[idx])
+                return out[:-1], first.sum()
+            return m_all[idx[first]]
         both = best_both(corr4d, do_softmax)            # one pass for both directions where it applies
         r1 = corr_to_matches(corr4d, best=both[0] if both else None, **kw)
         r2 = corr_to_matches(corr4d, invert_matching_direction=True, best=both[1] if both else None, **kw)

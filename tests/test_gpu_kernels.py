@@ -919,6 +919,31 @@ def test_stats2d_matches_row_and_col_kernels(shape, sum_kind):
                          carg[:, :C - 1].contiguous(), None, 0) if C % 4 == 0 and C > 4 else True
 
 
+@pytest.mark.parametrize("k,packed,softmax", [(2, True, True), (2, True, False), (1, False, True), (2, False, True)])
+def test_fused_match_candidates_match_op_path(k, packed, softmax, monkeypatch):
+    """InLoc pair_matches through stats2d + match_candidates (one launch for
+    both directions' candidates, offsets decoded, recentred) against the
+    op-by-op corr_to_matches path: identical de-duplicated order and keys,
+    coordinates to 1e-6 (linspace rounding)."""
+    import ncnet_amd.eval.inloc as inl
+    torch.manual_seed(33)
+    fs = (9, 12, 9, 12)
+    corr = (torch.randint(0, 40, (1, 1) + fs, device=DEV).float() / 9.0).contiguous()
+    code = None
+    if packed:   # 2-bit fields, each an in-cell offset < k (as the fused pool writes them)
+        f4 = torch.randint(0, k, (4, 1, 1) + fs, device=DEV)
+        code = ((f4[0] << 6) | (f4[1] << 4) | (f4[2] << 2) | f4[3]).to(torch.uint8)
+    if k > 1 and not packed:
+        code = None
+    got, n_got = inl.pair_matches(corr, code, k, do_softmax=softmax, static=True)
+    monkeypatch.setattr(inl, "_fused_candidates", lambda *a, **kw: None)
+    want, n_want = inl.pair_matches(corr, code, k, do_softmax=softmax, static=True)
+    assert int(n_got) == int(n_want)
+    n = int(n_got)
+    assert torch.allclose(got[:n], want[:n], atol=1e-6, rtol=0), (got[:n] - want[:n]).abs().max()
+    assert torch.equal(got[:n, 4], want[:n, 4])
+
+
 def test_nc_fused_k3_one_wide_workgroup():
     """The > 80 KB configuration of the fused NC kernel (a 24-plane output
     ring: one 16-wave workgroup per CU, csrc/nc_fused.hip NW = 16) against the
