@@ -30,6 +30,8 @@ class RuntimeConfig:
     nc_fused: bool = True            # NCNET_NC_FUSED: fused (3,3)/(<=16,1) inference NeighConsensus kernel
     step_priority: bool = False      # NCNET_STEP_PRIORITY: training step on high-priority streams, the
                                      # prefetched trunk at default priority (fills gaps instead of time-slicing)
+    prefetch_at: int = 0             # NCNET_PREFETCH_AT: when the next batch's trunk is queued on its stream:
+                                     # 0 with the forward, 1 before the backward, 2 after the backward
 
     @classmethod
     def from_env(cls, env=None) -> "RuntimeConfig":
@@ -44,7 +46,8 @@ class RuntimeConfig:
                    bwd_overlap=e.get("NCNET_BWD_OVERLAP", "1") == "1",
                    trunk_prefetch=e.get("NCNET_TRUNK_PREFETCH", "1") == "1",
                    nc_fused=e.get("NCNET_NC_FUSED", "1") != "0",
-                   step_priority=e.get("NCNET_STEP_PRIORITY", "0") == "1")
+                   step_priority=e.get("NCNET_STEP_PRIORITY", "0") == "1",
+                   prefetch_at=int(e.get("NCNET_PREFETCH_AT", "0")))
 
     def as_dict(self) -> dict:
         return dataclasses.asdict(self)

@@ -194,12 +194,18 @@ class Trainer:
             raise RuntimeError(f"injected fault at step {self.global_step} (NCNET_FAULT_STEP)")
         self.opt.zero_grad(set_to_none=True)
         self.bucket.reset()
+        at = _config.RUNTIME.prefetch_at
         with segment("forward"):
             feats = self.prefetch.take(batch)
-            self.prefetch.submit(next_batch)
+            if at == 0:
+                self.prefetch.submit(next_batch)
             loss = weak_loss_from_features(self.model, feats, self.normalization)
         with segment("backward"):
+            if at == 1:
+                self.prefetch.submit(next_batch)
             loss.backward()
+            if at >= 2:
+                self.prefetch.submit(next_batch)
         if self.flat and self.nan_guard:
             # loss-finite indicator rides in the gradient bucket: every rank's
             # FlatAdam then skips the same (globally non-finite) step, with no host sync
