@@ -474,14 +474,13 @@ void stats_cols(Tensor x, Tensor mx, c10::optional<Tensor> arg, c10::optional<Te
 }
 
 // x [V,R,C] fp32 -> row stats [V,R] and column stats [V,C] in one pass
-// (stats_rows + stats_cols); returns false (nothing written) if C % 4 != 0.
+// (stats_rows + stats_cols); always true (kept boolean for the callers' fallbacks).
 bool stats2d(Tensor x, Tensor rmx, Tensor rarg, c10::optional<Tensor> rse, Tensor cmx, Tensor carg,
              c10::optional<Tensor> cse, int64_t sum_kind) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check(x, "x", at::kFloat);
   TORCH_CHECK(x.dim() == 3);
   const int64_t V = x.size(0), R = x.size(1), C = x.size(2);
-  if (C % 4 != 0) return false;
   check(rmx, "rmx", at::kFloat); check_shape(rmx, "rmx", {V, R});
   check(rarg, "rarg", at::kInt); check_shape(rarg, "rarg", {V, R});
   check(cmx, "cmx", at::kFloat); check_shape(cmx, "cmx", {V, C});

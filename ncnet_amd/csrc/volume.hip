@@ -136,9 +136,9 @@ __global__ __launch_bounds__(256) void stats_cols_merge_kernel(const float* __re
 // stats over the wave's rows are merged across the 4 waves in LDS into one
 // column partial per tile; each row's 256-column partial is a wave reduction.
 // Partials [V][tiles][n] are merged in tile order by stats2d_merge (ties keep
-// the smallest index either way).  Needs C % 4 == 0 (16-byte rows).
+// the smallest index either way).  C % 4 != 0: four scalar loads per lane and row.
 // ---------------------------------------------------------------------------
-template <int WS>
+template <int WS, bool VEC>
 __global__ __launch_bounds__(256) void stats2d_tile_kernel(const float* __restrict__ x, int R, int C, int nrt, int nct,
                                                            float* __restrict__ rpm, int* __restrict__ rpi,
                                                            float* __restrict__ rps, float* __restrict__ cpm,
@@ -152,13 +152,20 @@ __global__ __launch_bounds__(256) void stats2d_tile_kernel(const float* __restri
   const int v = b / nrt;
   const int c0 = ct * 256 + lane * 4;
   const bool cok = c0 < C;
+  const int nk = min(4, C - c0);                         // valid columns of this lane (C % 4 != 0: scalar loads)
   const int rbase = rt * 64 + wave * 16;
   const float* xv = x + (size_t)v * R * C;
   float4 val[16];
 #pragma unroll
   for (int rr = 0; rr < 16; ++rr) {
     const int r = rbase + rr;
-    val[rr] = (cok && r < R) ? *(const float4*)(xv + (size_t)r * C + c0) : float4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (VEC) {
+      val[rr] = (cok && r < R) ? *(const float4*)(xv + (size_t)r * C + c0) : float4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      const float* xr = xv + (size_t)(r < R ? r : 0) * C;
+      val[rr] = float4{cok && r < R ? xr[c0] : 0.f, nk > 1 && r < R ? xr[c0 + 1] : 0.f,
+                       nk > 2 && r < R ? xr[c0 + 2] : 0.f, nk > 3 && r < R ? xr[c0 + 3] : 0.f};
+    }
   }
   Stat col[4];
 #pragma unroll
@@ -172,8 +179,10 @@ __global__ __launch_bounds__(256) void stats2d_tile_kernel(const float* __restri
     if (cok) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        col[k] = stat_push(col[k], e[k], r, WS);
-        rs = stat_push(rs, e[k], c0 + k, WS);
+        if (VEC || k < nk) {
+          col[k] = stat_push(col[k], e[k], r, WS);
+          rs = stat_push(rs, e[k], c0 + k, WS);
+        }
       }
     }
 #pragma unroll
@@ -570,17 +579,18 @@ extern "C" int ncnet_stats_cols(const float* x, float* mx, int* arg, float* se, 
   return (int)hipGetLastError();
 }
 // stats2d: work = 3 * V * (nct * R + nrt * C) floats of partials (nrt = ceil(R / 64), nct = ceil(C / 256)).
-// sum_kind 0: max / argmax only (rse, cse ignored).  C % 4 == 0 (else -2).
+// sum_kind 0: max / argmax only (rse, cse ignored).
 extern "C" int ncnet_stats2d(const float* x, float* rmx, int* rarg, float* rse, float* cmx, int* carg, float* cse,
                              int V, int R, int C, float* work, int sum_kind, hipStream_t s) {
-  if (C % 4 != 0) return -2;
+  const bool vec = C % 4 == 0;   // 16-byte rows: one float4 per lane and row; else four scalar loads
   const int nrt = cdiv(R, 64), nct = cdiv(C, 256);
   const size_t nr = (size_t)V * nct * R, nc = (size_t)V * nrt * C;
   float* rpm = work; int* rpi = (int*)(work + nr); float* rps = work + 2 * nr;
   float* cpm = work + 3 * nr; int* cpi = (int*)(cpm + nc); float* cps = cpm + 2 * nc;
   const dim3 grid((unsigned)((size_t)V * nrt * nct)), blk(256);
 #define S2D(WSV) do { \
-    hipLaunchKernelGGL(stats2d_tile_kernel<WSV>, grid, blk, 0, s, x, R, C, nrt, nct, rpm, rpi, rps, cpm, cpi, cps); \
+    if (vec) hipLaunchKernelGGL((stats2d_tile_kernel<WSV, true>), grid, blk, 0, s, x, R, C, nrt, nct, rpm, rpi, rps, cpm, cpi, cps); \
+    else hipLaunchKernelGGL((stats2d_tile_kernel<WSV, false>), grid, blk, 0, s, x, R, C, nrt, nct, rpm, rpi, rps, cpm, cpi, cps); \
     hipLaunchKernelGGL(stats2d_merge_kernel<WSV>, dim3((unsigned)cdiv(V * R, 256)), blk, 0, s, rpm, rpi, rps, rmx, rarg, rse, V, R, nct); \
     hipLaunchKernelGGL(stats2d_merge_kernel<WSV>, dim3((unsigned)cdiv(V * C, 256)), blk, 0, s, cpm, cpi, cps, cmx, carg, cse, V, C, nrt); \
   } while (0)
