@@ -54,3 +54,6 @@ class RuntimeConfig:
 
 
 RUNTIME = RuntimeConfig.from_env()
+# one-pass row + column statistics (csrc/volume.hip stats2d) in MutualMatching
+# and the weak loss; NCNET_STATS2D=0 restores the separate row / column kernels (A/B)
+STATS2D = os.environ.get("NCNET_STATS2D", "1") != "0"

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import torch
 
+from .. import config as _config
 from . import _ext
 from . import reference as ref
 
@@ -27,7 +28,7 @@ def _stats(c3: torch.Tensor):
     cmax = torch.empty((V, Cc), dtype=torch.float32, device=c3.device)
     carg = torch.empty((V, Cc), dtype=torch.int32, device=c3.device)
     # both maxima in one pass over the volume (stats2d) when rows are 16-byte multiples
-    if not C.stats2d(c3, rmax, rarg, None, cmax, carg, None, 0):
+    if not (_config.STATS2D and C.stats2d(c3, rmax, rarg, None, cmax, carg, None, 0)):
         C.stats_rows(c3, rmax, rarg, None, 0)
         C.stats_cols(c3, cmax, carg, None, 0)
     return rmax, rarg, cmax, carg
