@@ -42,7 +42,7 @@ int ncnet_match_candidates(const float*, const float*, const int*, const float*,
                            const uint8_t*, int, int, int, int, int, float*, float*, long long*, hipStream_t);
 int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, int, hipStream_t);
 int ncnet_mm_bwd(const float*, const float*, const float*, const int*, const float*, const int*, float*, float*, float*,
-                 int, int, int, float, hipStream_t);
+                 int, int, int, float, float*, hipStream_t);
 int ncnet_combine_fwd(const float*, float*, int, int, int, hipStream_t);
 int ncnet_combine_bwd(const float*, const float*, void*, void*, int, int, int, hipStream_t);
 int ncnet_softmax_max_bwd(const float*, const float*, const int*, const float*, const float*, const int*, const float*,
@@ -546,7 +546,9 @@ void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10
      "mm_apply");
 }
 
-void mm_bwd(Tensor c, Tensor g, Tensor rmax, Tensor rarg, Tensor cmax, Tensor carg, Tensor gc, double eps) {
+// one_pass: both sums of the backward in one pass over (c, g) (default), else the separate row / column passes
+void mm_bwd(Tensor c, Tensor g, Tensor rmax, Tensor rarg, Tensor cmax, Tensor carg, Tensor gc, double eps,
+            bool one_pass) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
   check(c, "c", at::kFloat); check(g, "g", at::kFloat); check(gc, "gc", at::kFloat);
   check(rmax, "rmax", at::kFloat); check(cmax, "cmax", at::kFloat); check(rarg, "rarg", at::kInt); check(carg, "carg", at::kInt);
@@ -556,9 +558,12 @@ void mm_bwd(Tensor c, Tensor g, Tensor rmax, Tensor rarg, Tensor cmax, Tensor ca
   check_shape(cmax, "cmax", {V, C}); check_shape(carg, "carg", {V, C});
   auto rsum = torch::empty({V, R}, c.options());
   auto csum = torch::empty({V, C}, c.options());
+  Tensor work;
+  if (one_pass) work = torch::empty({V * (((C + 255) / 256) * R + ((R + 63) / 64) * C)}, c.options());
   ok(ncnet_mm_bwd((float*)c.data_ptr(), (float*)g.data_ptr(), (float*)rmax.data_ptr(), (int*)rarg.data_ptr(),
                   (float*)cmax.data_ptr(), (int*)carg.data_ptr(), (float*)rsum.data_ptr(), (float*)csum.data_ptr(),
-                  (float*)gc.data_ptr(), V, R, C, (float)eps, cur_stream(c)), "mm_bwd");
+                  (float*)gc.data_ptr(), V, R, C, (float)eps, one_pass ? (float*)work.data_ptr() : nullptr,
+                  cur_stream(c)), "mm_bwd");
 }
 
 // z [2*Vh, R, C] (second half stored as [C, R]) -> y [Vh, R, C]

@@ -372,6 +372,77 @@ __global__ __launch_bounds__(256) void mm_bwd_colsum_kernel(const float* __restr
   if (wave == 0 && k < C) csum[(size_t)v * C + k] = sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane];
 }
 
+// Both sums of the MutualMatching backward in ONE pass over (c, g) (the
+// separate row pass and the 64-column-block column pass read both volumes
+// twice; the column pass, V * C / 64 blocks walking rows, was also a long
+// tail on the critical path of the pipelined step).  Same 64 x 256 tiling as
+// stats2d: row partials by wave reduction, column partials merged in LDS over
+// the 4 waves; partials summed in tile order by sum_partials_kernel.
+template <bool VEC>
+__global__ __launch_bounds__(256) void mm_bwd_sums2d_kernel(const float* __restrict__ c, const float* __restrict__ g,
+                                                            const float* __restrict__ rmax, const float* __restrict__ cmax,
+                                                            int R, int C, int nrt, int nct, float* __restrict__ rp,
+                                                            float* __restrict__ cp, float eps) {
+  __shared__ float sh[4][256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int b = blockIdx.x;
+  const int ct = b % nct; b /= nct;
+  const int rt = b % nrt;
+  const int v = b / nrt;
+  const int c0 = ct * 256 + lane * 4;
+  const int nk = c0 < C ? min(4, C - c0) : 0;
+  const int rbase = rt * 64 + wave * 16;
+  const size_t vb = (size_t)v * R * C;
+  float cm[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) cm[k] = k < nk ? cmax[(size_t)v * C + c0 + k] + eps : 1.f;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int rr = 0; rr < 16; ++rr) {
+    const int r = rbase + rr;
+    if (r >= R) break;                                   // wave-uniform
+    const float ra = rmax[(size_t)v * R + r] + eps;
+    const float* cr = c + vb + (size_t)r * C + c0;
+    const float* gr = g + vb + (size_t)r * C + c0;
+    float xv[4], gv[4];
+    if constexpr (VEC) {
+      const float4 x4 = nk ? *(const float4*)cr : float4{0.f, 0.f, 0.f, 0.f};
+      const float4 g4 = nk ? *(const float4*)gr : float4{0.f, 0.f, 0.f, 0.f};
+      xv[0] = x4.x; xv[1] = x4.y; xv[2] = x4.z; xv[3] = x4.w;
+      gv[0] = g4.x; gv[1] = g4.y; gv[2] = g4.z; gv[3] = g4.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { xv[k] = k < nk ? cr[k] : 0.f; gv[k] = k < nk ? gr[k] : 0.f; }
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x = xv[k];
+      const float t = k < nk ? gv[k] * (x * ((x / ra) * (x / cm[k]))) : 0.f;
+      cs[k] += t;
+      rs += t;
+    }
+    rs = wave_sum(rs);
+    if (lane == 0) rp[((size_t)v * nct + ct) * R + r] = rs;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sh[wave][lane * 4 + k] = cs[k];
+  __syncthreads();
+  const int cc = threadIdx.x, col = ct * 256 + cc;
+  if (col < C) cp[((size_t)v * nrt + rt) * C + col] = sh[0][cc] + sh[1][cc] + sh[2][cc] + sh[3][cc];
+}
+
+// out [V][n] = sum over t of p [V][nt][n] (in t order)
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ p, float* __restrict__ out, int V,
+                                                           int n, int nt) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)V * n) return;
+  const int v = (int)(e / n), i = (int)(e - (long long)v * n);
+  float s = 0.f;
+  for (int t = 0; t < nt; ++t) s += p[((size_t)v * nt + t) * n + i];
+  out[e] = s;
+}
+
 __global__ __launch_bounds__(256) void mm_bwd_apply_kernel(const float* __restrict__ c, const float* __restrict__ g,
                                                            const float* __restrict__ rmax, const int* __restrict__ rarg,
                                                            const float* __restrict__ rsum,
@@ -616,14 +687,28 @@ extern "C" int ncnet_mm_apply(const float* c, const float* rmax, const float* cm
                        (uint16_t*)out_x, (uint16_t*)out_xt, R, C, eps);
   return (int)hipGetLastError();
 }
+// work: nullptr (separate row / column passes) or V * (ceil(C/256) * R + ceil(R/64) * C) floats (one pass)
 extern "C" int ncnet_mm_bwd(const float* c, const float* g, const float* rmax, const int* rarg, const float* cmax,
                             const int* carg, float* rsum, float* csum, float* gc, int V, int R, int C, float eps,
-                            hipStream_t s) {
+                            float* work, hipStream_t s) {
   long long rows = (long long)V * R;
-  hipLaunchKernelGGL(mm_bwd_rowsum_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, c, g, rmax, cmax, rsum,
-                     rows, R, C, eps);
-  hipLaunchKernelGGL(mm_bwd_colsum_kernel, dim3((unsigned)(V * cdiv(C, 64))), dim3(256), 0, s, c, g, rmax, cmax, csum,
-                     R, C, eps);
+  if (work) {
+    const int nrt = cdiv(R, 64), nct = cdiv(C, 256);
+    float* rp = work;
+    float* cp = work + (size_t)V * nct * R;
+    const dim3 grid((unsigned)((size_t)V * nrt * nct));
+    if (C % 4 == 0)
+      hipLaunchKernelGGL((mm_bwd_sums2d_kernel<true>), grid, dim3(256), 0, s, c, g, rmax, cmax, R, C, nrt, nct, rp, cp, eps);
+    else
+      hipLaunchKernelGGL((mm_bwd_sums2d_kernel<false>), grid, dim3(256), 0, s, c, g, rmax, cmax, R, C, nrt, nct, rp, cp, eps);
+    hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)cdiv(V * R, 256)), dim3(256), 0, s, rp, rsum, V, R, nct);
+    hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)cdiv(V * C, 256)), dim3(256), 0, s, cp, csum, V, C, nrt);
+  } else {
+    hipLaunchKernelGGL(mm_bwd_rowsum_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, c, g, rmax, cmax, rsum,
+                       rows, R, C, eps);
+    hipLaunchKernelGGL(mm_bwd_colsum_kernel, dim3((unsigned)(V * cdiv(C, 64))), dim3(256), 0, s, c, g, rmax, cmax, csum,
+                       R, C, eps);
+  }
   long long total = rows * C;
   hipLaunchKernelGGL(mm_bwd_apply_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, c, g, rmax, rarg,
                      rsum, cmax, carg, csum, gc, total, R, C, eps);

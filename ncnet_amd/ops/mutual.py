@@ -52,7 +52,7 @@ class MutualMatchingFn(torch.autograd.Function):
         c3, rmax, rarg, cmax, carg = ctx.saved_tensors
         g3 = g.reshape(c3.shape).float().contiguous()
         gc = torch.empty_like(c3)
-        _ext.ext().mm_bwd(c3, g3, rmax, rarg, cmax, carg, gc, EPS)
+        _ext.ext().mm_bwd(c3, g3, rmax, rarg, cmax, carg, gc, EPS, _config.STATS2D)   # one pass for both sums
         return gc.reshape(ctx.shape)
 
 

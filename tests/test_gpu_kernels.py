@@ -272,7 +272,7 @@ def test_neigh_consensus_autograd(ks, ch, shape):
     assert errs["y"] < 1e-2 and max(errs.values()) < 0.1, errs
 
 
-@pytest.mark.parametrize("shape", [(3, 1, 25, 25, 25, 25), (2, 1, 7, 9, 11, 5)])
+@pytest.mark.parametrize("shape", [(3, 1, 25, 25, 25, 25), (2, 1, 7, 9, 11, 5), (2, 1, 8, 10, 16, 20)])
 def test_mutual_matching(shape):
     from ncnet_amd.ops.mutual import mutual_matching
     torch.manual_seed(5)
