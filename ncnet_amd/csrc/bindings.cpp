@@ -37,6 +37,7 @@ int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, 
                           float, int, hipStream_t);
 int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, int, hipStream_t);
 int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, float*, int, int, hipStream_t);
+int ncnet_gather_bf16(const float*, const int*, void*, long long, hipStream_t);
 int ncnet_stats2d(const float*, float*, int*, float*, float*, int*, float*, int, int, int, float*, int, hipStream_t);
 int ncnet_match_candidates(const float*, const float*, const int*, const float*, const float*, const int*,
                            const uint8_t*, int, int, int, int, int, float*, float*, long long*, hipStream_t);
@@ -526,6 +527,15 @@ void match_candidates(Tensor cmx, c10::optional<Tensor> cse, Tensor carg, Tensor
      "match_candidates");
 }
 
+// out[i] = bf16(src[idx[i]]) (0 where idx < 0): src fp32 [N], idx int32 [M], out bf16 [M]
+void gather_bf16(Tensor src, Tensor idx, Tensor out) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
+  check(src, "src", at::kFloat); check(idx, "idx", at::kInt); check(out, "out", at::kBFloat16);
+  TORCH_CHECK(idx.numel() == out.numel(), "gather_bf16: idx / out size");
+  ok(ncnet_gather_bf16((float*)src.data_ptr(), (int*)idx.data_ptr(), out.data_ptr(), out.numel(), cur_stream(src)),
+     "gather_bf16");
+}
+
 void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10::optional<Tensor> out_x,
               c10::optional<Tensor> out_xt, double eps) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
@@ -896,6 +906,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stats_rows", &stats_rows);
   m.def("stats_cols", &stats_cols);
   m.def("stats2d", &stats2d);
+  m.def("gather_bf16", &gather_bf16);
   m.def("match_candidates", &match_candidates);
   m.def("mm_apply", &mm_apply);
   m.def("mm_bwd", &mm_bwd);

@@ -42,8 +42,9 @@ import torch.utils.weak as _weak
 from .. import config as _config
 from . import _ext
 from . import reference as ref
-from .packing import (blk_out_weights, ij_groups, ij_in_grad, ij_in_weights, ij_out_grad, ij_out_weights, pack_w16,
-                      pack_w1x, pack_w16_planes, plane_dgrad_weights, transpose_for_dgrad)
+from .packing import (_blk_packed, _w1x_dgrad, blk_out_weights, gather_pack, ij_groups, ij_in_grad, ij_in_weights,
+                      ij_out_grad, ij_out_weights, pack_w16, pack_w1x, pack_w16_planes, plane_dgrad_weights,
+                      transpose_for_dgrad)
 
 HIP_KS = (1, 3, 5, 7)
 # Cout=1 layers with <= 16 input channels run in output-plane-block mode
@@ -257,7 +258,7 @@ def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=N
         # output-plane blocks: the 16 MFMA rows are 4x4 output planes, no
         # combo-planar partials (2.5 GB at the training shape) and no ijsum
         y = torch.empty(shp, dtype=torch.float32, device=dev)
-        C.conv16_blk_fwd(h[0], pack_w16_planes(blk_out_weights(w_std)),
+        C.conv16_blk_fwd(h[0], gather_pack(_blk_packed, w_std),
                          None if bias is None else bias.float().reshape(1).contiguous(), y, ks, 1 if relu else 0)
         return y
     if cout == 1:                          # ij encoding: combo-planar partials, shift-summed by ijsum
@@ -270,8 +271,8 @@ def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=N
         C.ijsum(z, None if bias is None else _pad_bias(bias, 1), y, ks, 1 if relu else 0, 1)
         return y
     if nbi == 1:
-        outs = [_epilogue_call(C, h[0], pack_w16(w_std[_blk(w_std, b, cout), :16]), bias, b, cout, relu, mask, f32,
-                               shp, ks) for b in range(nbo)]
+        outs = [_epilogue_call(C, h[0], gather_pack(pack_w16, w_std[_blk(w_std, b, cout), :16]), bias, b, cout, relu,
+                               mask, f32, shp, ks) for b in range(nbo)]
         return _gather(outs, f32, cout)
     # several input blocks: fp32 partials per (out, in) block pair, summed before the activation
     outs = []
@@ -388,7 +389,7 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list, xp=None, shp=None):
         xs = None
         if li == 0 and xp is not None:      # padded-plane first layer (fast1x_ok)
             y = torch.empty(tuple(shp) + (16,), dtype=torch.bfloat16, device=xp.device)
-            C.conv1x16(xp, pack_w1x(w), _pad_bias(b, 16), None, y, ks, 1)
+            C.conv1x16(xp, gather_pack(pack_w1x, w), _pad_bias(b, 16), None, y, ks, 1)
             save.append(xp)
             h, cin = y.unsqueeze(0), cout
             continue
@@ -537,7 +538,7 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
                     db = g.sum(dtype=torch.float32).reshape(1)
                 if li > 0 or need_dx0:
                     gn = torch.empty((1,) + tuple(hin.shape[1:]), dtype=torch.bfloat16, device=g.device)
-                    C.conv1x16(gp, pack_w1x(transpose_for_dgrad(w)), None, hin[0], gn[0], ks, 2)
+                    C.conv1x16(gp, gather_pack(_w1x_dgrad, w), None, hin[0], gn[0], ks, 2)
                     g = gn
             else:                                    # first layer: xin = padded NC-input planes
                 R, sb = _wgrad1x(C, g[0], xin, ks, True)

@@ -55,13 +55,13 @@ def _as_std(w_std: torch.Tensor, cout: int, cin: int) -> torch.Tensor:
     return out
 
 
-def pack_w16(w_std: torch.Tensor) -> torch.Tensor:
+def pack_w16(w_std: torch.Tensor, out_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
     ks = w_std.shape[-1]
     w = _as_std(w_std, 16, 16).reshape(16, 16, ks * ks, ks * ks)
     co, ci, tap, valid = _idx16(ks, w.device)
     vals = w[co, ci, :, tap]                      # [nq, 64, 8, k*k]
     vals = vals * valid.unsqueeze(-1).to(vals.dtype)
-    return vals.permute(3, 0, 1, 2).contiguous().to(torch.bfloat16)
+    return vals.permute(3, 0, 1, 2).contiguous().to(out_dtype)
 
 
 # ---------------------------------------------------------------------------
@@ -168,7 +168,7 @@ def _idx1x(ks: int, device: str):
     return co.contiguous().to(device), torch.clamp(kk, max=ks * ks - 1).contiguous().to(device), valid.to(device)
 
 
-def pack_w1x(w_std: torch.Tensor) -> torch.Tensor:
+def pack_w1x(w_std: torch.Tensor, out_dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
     """[co<=16, 1, k, k, k, k] -> [k*k plane offsets, 64 lanes, 8] bf16:
     lane l of plane offset p = di*k + dj holds W[co = l&15, 0, di, dj, tap kk]
     for kk = 8 (l>>4) + j (taps dk*k + dl; zero for kk >= k*k or co >= Cout)."""
@@ -176,4 +176,61 @@ def pack_w1x(w_std: torch.Tensor) -> torch.Tensor:
     w = _as_std(w_std, 16, 1).reshape(16, ks * ks, ks * ks)      # [co, plane, tap]
     co, kk, valid = _idx1x(ks, str(w.device))
     vals = w[co, :, kk] * valid.unsqueeze(-1).to(w.dtype)          # [64, 8, plane]
-    return vals.permute(2, 0, 1).contiguous().to(torch.bfloat16)
+    return vals.permute(2, 0, 1).contiguous().to(out_dtype)
+
+
+# ---------------------------------------------------------------------------
+# Per-step packing as ONE gather launch.  Every pack above is a pure gather of
+# the standard-layout weight (plus zeros): run once per (pack, shape) on an
+# index-valued fp64 tensor, it yields the source element of every packed
+# slot; each training step then packs with a single `gather_bf16` launch
+# (csrc/epilogue.hip) instead of 4-5 small PyTorch kernels (index, multiply,
+# permute-copy, cast), which sat on the critical path of the pipelined step.
+# ---------------------------------------------------------------------------
+_GATHER_IDX: dict = {}
+_GATHER_ON = __import__("os").environ.get("NCNET_GATHER_PACK", "0") == "1"   # measured slower (profiles/r4/ab/gather_pack.txt): off
+
+
+def _gather_index(fn, shape, device):
+    key = (fn, tuple(shape), str(device))
+    ent = _GATHER_IDX.get(key)
+    if ent is None:
+        n = 1
+        for d in shape:
+            n *= d
+        wi = torch.arange(1, n + 1, dtype=torch.float64).reshape(shape)
+        v = fn(wi)
+        idx = (v.round().to(torch.int64) - 1).to(torch.int32)    # 0 (a zero slot) -> -1
+        ent = (idx.reshape(-1).to(device), tuple(v.shape))
+        _GATHER_IDX[key] = ent
+    return ent
+
+
+def gather_pack(fn, w_std: torch.Tensor) -> torch.Tensor:
+    """``fn(w_std)`` (a pure-gather pack to bf16) as one gather launch on GPU.
+    ``fn`` takes (w, out_dtype) or just (w) and must not depend on the values."""
+    from . import _ext
+    if not (_GATHER_ON and fn in _F64 and w_std.is_cuda and _ext.use_hip(w_std)):
+        return fn(w_std).to(torch.bfloat16)        # (unknown packs -- e.g. a test's mutated one -- run as they are)
+    idx, shape = _gather_index(_F64[fn], w_std.shape, w_std.device)
+    out = torch.empty(shape, dtype=torch.bfloat16, device=w_std.device)
+    _ext.ext().gather_bf16(w_std.detach().float().contiguous().reshape(-1), idx, out.reshape(-1))
+    return out
+
+
+def _blk_packed(w, out_dtype=torch.bfloat16):
+    return pack_w16_planes(blk_out_weights(w), out_dtype)
+
+
+def _w16_dgrad(w, out_dtype=torch.bfloat16):
+    return pack_w16(transpose_for_dgrad(w), out_dtype)
+
+
+def _w1x_dgrad(w, out_dtype=torch.bfloat16):
+    return pack_w1x(transpose_for_dgrad(w), out_dtype)
+
+
+# the index builders: the same packs with fp64 output (indices stay exact)
+_F64 = {pack_w16: lambda w: pack_w16(w, torch.float64), pack_w1x: lambda w: pack_w1x(w, torch.float64),
+        _blk_packed: lambda w: _blk_packed(w, torch.float64), _w16_dgrad: lambda w: _w16_dgrad(w, torch.float64),
+        _w1x_dgrad: lambda w: _w1x_dgrad(w, torch.float64)}
