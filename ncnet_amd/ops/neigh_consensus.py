@@ -33,6 +33,7 @@ kernels (even kernel sizes) raises unless NCNET_ALLOW_TORCH_FALLBACK=1.
 from __future__ import annotations
 
 import functools
+import os
 import os as _os
 
 import numpy as np
@@ -95,13 +96,18 @@ def wgrad_v3_ntl(K: int, L: int, ks: int) -> int:
     return ntl
 
 
+# workgroups of the 16 -> 16 weight gradient (grid = groups * ks; partials 2 *
+# groups x 160 K floats, summed afterwards); NCNET_WGRAD_WG (A/B)
+_WGRAD_WG_TARGET = int(os.environ.get("NCNET_WGRAD_WG", "512"))
+
+
 def wgrad_v3_groups(shape, ks: int) -> int:
     """Column groups per dj for wgrad16v3: ~2 workgroups per CU, never more
     than the columns (v, j, tile).  Tile rule mirrors ncnet_wgrad16v3."""
     V, I, J, K, L = shape[:5]
     ntl = wgrad_v3_ntl(K, L, ks)
     ncols = V * J * ntl
-    target = max(1, 512 // ks)
+    target = max(1, _WGRAD_WG_TARGET // ks)
     return max(1, min(target, ncols))
 
 
