@@ -77,7 +77,13 @@ def _fused_candidates(corr4d, delta4d, k: int, do_softmax: bool):
     b, _, fs1, fs2, fs3, fs4 = corr4d.shape
     if b != 1 or not (_ext.use_hip(corr4d) and corr4d.dtype == torch.float32):
         return None
-    if delta4d is not None and not (torch.is_tensor(delta4d) and delta4d.dtype == torch.uint8):
+    if delta4d is not None and not torch.is_tensor(delta4d):
+        # unpacked (di, dj, dk, dl) offsets -> the packed 2-bit code (same decode as the fused pool's codes)
+        if len(delta4d) != 4:
+            return None
+        d = [t.reshape(-1).to(torch.int32) for t in delta4d]
+        delta4d = ((d[0] << 6) | (d[1] << 4) | (d[2] << 2) | d[3]).to(torch.uint8)
+    elif delta4d is not None and delta4d.dtype != torch.uint8:
         return None
     R, C = fs1 * fs2, fs3 * fs4
     x = corr4d.reshape(1, R, C).contiguous()
