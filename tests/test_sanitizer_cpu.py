@@ -42,6 +42,8 @@ def _dummy(kind: str):
         return 1.0
     if "SupportsInt" in kind:
         return 3
+    if kind == "bool":
+        return True
     raise AssertionError(f"unhandled argument type {kind}")
 
 
