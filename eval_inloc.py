@@ -87,6 +87,8 @@ def main(argv=None):
     ap.add_argument("--query_path", type=str, default="datasets/inloc/query/iphone7/")
     ap.add_argument("--output_dir", type=str, default="matches/")
     ap.add_argument("--synthetic_queries", type=int, default=0)
+    ap.add_argument("--synthetic_hw", type=int, nargs=2, default=[768, 1024],
+                    help="height width of the --synthetic_queries images (default 768 1024, 4:3 landscape)")
     ap.add_argument("--ncons_kernel_sizes", nargs="+", type=int, default=[3, 3])
     ap.add_argument("--ncons_channels", nargs="+", type=int, default=[16, 1])
     ap.add_argument("--precision", choices=["fp16", "bf16", "fp8", "fp32"], default="fp16",
@@ -106,7 +108,7 @@ def main(argv=None):
     if args.synthetic_queries:
         tmp = tempfile.mkdtemp(prefix="ncnet_inloc_")
         args.inloc_shortlist, args.query_path, args.pano_path = make_synthetic_inloc(
-            tmp, args.synthetic_queries, args.n_panos)
+            tmp, args.synthetic_queries, args.n_panos, *args.synthetic_hw)
         args.n_queries = args.synthetic_queries
     torch.manual_seed(1)   # checkpoint-less (synthetic) runs: the same random NC weights on every launch
     model = ImMatchNet(use_cuda=ctx.device.type == "cuda", checkpoint=args.checkpoint or None,
@@ -139,7 +141,6 @@ def main(argv=None):
             path = os.path.join(out_dir, f"{q + 1}.mat")
             if os.path.exists(path):
                 continue
-            matches = np.zeros((1, args.n_panos, N, 5))
             src = prepare_image(read_image(os.path.join(args.query_path, queries[q])), args.image_size, args.k_size,
                                 ctx.device)
             npq = min(args.n_panos, len(panos[q]))
@@ -163,6 +164,7 @@ def main(argv=None):
                 else:
                     fq = model.extract(src)
                     fps = [model.extract(t) for t in tgts]
+            pair_ms = []
             for idx in range(npq):
                 if vp is not None:
                     out = vp.forward({"source_image": src, "target_image": tgts[idx]})
@@ -173,9 +175,20 @@ def main(argv=None):
                     # correlation .. match extraction as one HIP graph per shape
                     res, cnt = matcher(fq[0], fq[1], fps[idx][0], fps[idx][1])
                     m = res[:int(cnt)].double().cpu().numpy()
-                n = min(len(m), N)
-                matches[0, idx, :n] = m[:n]
+                pair_ms.append(m)
                 npairs += 1
+            # the reference's N (eval_inloc.py:116-118) is sized for 4:3 landscape
+            # images; a pair with more unique matches (square / other aspect ratios)
+            # grows the array instead of being truncated -- the MATLAB side squeezes
+            # it, so the row count is free -- and the reference itself would fail
+            # on the overflow (eval_inloc.py:197-203), never drop rows silently
+            nq_rows = max([N] + [len(m) for m in pair_ms])
+            if nq_rows > N:
+                print(f"query {q + 1}: {nq_rows} matches exceed N={N} (4:3 sizing); "
+                      f"writing {nq_rows} rows", file=sys.stderr, flush=True)
+            matches = np.zeros((1, args.n_panos, nq_rows, 5))
+            for idx, m in enumerate(pair_ms):
+                matches[0, idx, :len(m)] = m
             if vp is None or ctx.is_main:
                 save_query(path, matches, queries[q], pano_all)
             if ctx.is_main:

@@ -37,17 +37,20 @@ int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, 
                           float, int, hipStream_t);
 int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, int, hipStream_t);
 int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, float*, int, int, hipStream_t);
-int ncnet_gather_bf16(const float*, const int*, void*, long long, hipStream_t);
+int ncnet_gather_bf16(const float*, const int*, void*, long long, long long, hipStream_t);
 int ncnet_stats2d(const float*, float*, int*, float*, float*, int*, float*, int, int, int, float*, int, hipStream_t);
 int ncnet_match_candidates(const float*, const float*, const int*, const float*, const float*, const int*,
                            const uint8_t*, int, int, int, int, int, float*, float*, long long*, hipStream_t);
-int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, int, hipStream_t);
+int ncnet_mm_apply(const float*, const float*, const float*, float*, void*, void*, int, int, int, float, int, int, int, int,
+                   int, int, hipStream_t);
 int ncnet_mm_bwd(const float*, const float*, const float*, const int*, const float*, const int*, float*, float*, float*,
                  int, int, int, float, float*, hipStream_t);
 int ncnet_combine_fwd(const float*, float*, int, int, int, hipStream_t);
 int ncnet_combine_bwd(const float*, const float*, void*, void*, int, int, int, hipStream_t);
 int ncnet_softmax_max_bwd(const float*, const float*, const int*, const float*, const float*, const int*, const float*,
-                          const float*, const float*, float*, int, int, int, int, float, hipStream_t);
+                          const float*, const float*, float*, int, int, int, int, float, const float*, hipStream_t);
+int ncnet_score_sum(const float*, const float*, const float*, const float*, const float*, const float*, int, int, int, int,
+                    float, float*, hipStream_t);
 int ncnet_maxpool4d(const void*, int, float*, uint8_t*, int, int, int, int, int, int, hipStream_t);
 int ncnet_transpose(const void*, void*, int, int, int, int, hipStream_t);
 int ncnet_nonfinite_count(const float*, long long, int*, hipStream_t);
@@ -532,12 +535,15 @@ void gather_bf16(Tensor src, Tensor idx, Tensor out) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
   check(src, "src", at::kFloat); check(idx, "idx", at::kInt); check(out, "out", at::kBFloat16);
   TORCH_CHECK(idx.numel() == out.numel(), "gather_bf16: idx / out size");
-  ok(ncnet_gather_bf16((float*)src.data_ptr(), (int*)idx.data_ptr(), out.data_ptr(), out.numel(), cur_stream(src)),
+  ok(ncnet_gather_bf16((float*)src.data_ptr(), (int*)idx.data_ptr(), out.data_ptr(), out.numel(), src.numel(),
+                      cur_stream(src)),
      "gather_bf16");
 }
 
+// pad (ks, I2, J2): out_x / out_xt are the zero-padded bf16 planes of csrc/conv1x.hip ([V*R, PPL] /
+// [V*C, PPL], halos written too) of a square volume R = C = I2 * J2; else [V,R,C] / [V,C,R] bf16 or f16.
 void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10::optional<Tensor> out_x,
-              c10::optional<Tensor> out_xt, double eps) {
+              c10::optional<Tensor> out_xt, double eps, std::vector<int64_t> pad) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(c.device());
   check(c, "c", at::kFloat); check(rmax, "rmax", at::kFloat); check(cmax, "cmax", at::kFloat);
   TORCH_CHECK(c.dim() == 3);
@@ -548,11 +554,23 @@ void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10
   const bool h = (out_x.has_value() && out_x->scalar_type() == at::kHalf) ||
                  (out_xt.has_value() && out_xt->scalar_type() == at::kHalf);
   const auto xt = h ? at::kHalf : at::kBFloat16;
-  if (out_x.has_value()) { check(*out_x, "out_x", xt); check_shape(*out_x, "out_x", {V, R, C}); }
-  if (out_xt.has_value()) { check(*out_xt, "out_xt", xt); check_shape(*out_xt, "out_xt", {V, C, R}); }
+  int64_t pks = 0, I2 = 0, J2 = 0;
+  if (!pad.empty()) {
+    TORCH_CHECK(pad.size() == 3, "mm_apply: pad = (ks, I2, J2)");
+    pks = pad[0]; I2 = pad[1]; J2 = pad[2];
+    check_ks(pks);
+    TORCH_CHECK(!h && I2 * J2 == R && R == C, "mm_apply pad: bf16 planes of a square volume, I2 * J2 = R = C");
+    const auto g = pad_geom(I2, J2, pks);
+    if (out_x.has_value()) { check(*out_x, "out_x", xt); check_shape(*out_x, "out_x", {V * R, g[1]}); }
+    if (out_xt.has_value()) { check(*out_xt, "out_xt", xt); check_shape(*out_xt, "out_xt", {V * C, g[1]}); }
+  } else {
+    if (out_x.has_value()) { check(*out_x, "out_x", xt); check_shape(*out_x, "out_x", {V, R, C}); }
+    if (out_xt.has_value()) { check(*out_xt, "out_xt", xt); check_shape(*out_xt, "out_xt", {V, C, R}); }
+  }
   ok(ncnet_mm_apply((float*)c.data_ptr(), (float*)rmax.data_ptr(), (float*)cmax.data_ptr(),
                     out.has_value() ? (float*)out->data_ptr() : nullptr, out_x.has_value() ? out_x->data_ptr() : nullptr,
-                    out_xt.has_value() ? out_xt->data_ptr() : nullptr, V, R, C, (float)eps, h ? 1 : 0, cur_stream(c)),
+                    out_xt.has_value() ? out_xt->data_ptr() : nullptr, V, R, C, (float)eps, h ? 1 : 0, (int)pks,
+                    (int)I2, (int)J2, (int)I2, (int)J2, cur_stream(c)),
      "mm_apply");
 }
 
@@ -600,7 +618,7 @@ void combine_bwd(Tensor g, Tensor z, Tensor gz, int64_t R, int64_t C, c10::optio
 
 // norm: 1 'softmax', 2 'l1' (eps), 0 None -- rse / cse from stats with the matching sum_kind
 void softmax_max_bwd(Tensor x, Tensor rmax, Tensor rarg, Tensor rse, Tensor cmax, Tensor carg, Tensor cse, Tensor wr,
-                     Tensor wc, Tensor gx, int64_t norm, double eps) {
+                     Tensor wc, Tensor gx, int64_t norm, double eps, c10::optional<Tensor> gscale) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   check(x, "x", at::kFloat); check(gx, "gx", at::kFloat);
   TORCH_CHECK(x.dim() == 3 && gx.sizes() == x.sizes());
@@ -612,10 +630,27 @@ void softmax_max_bwd(Tensor x, Tensor rmax, Tensor rarg, Tensor rse, Tensor cmax
   check_shape(rmax, "rmax", {V, R}); check_shape(rse, "rse", {V, R}); check_shape(rarg, "rarg", {V, R});
   check_shape(cmax, "cmax", {V, C}); check_shape(cse, "cse", {V, C}); check_shape(carg, "carg", {V, C});
   check_shape(wr, "wr", {V}); check_shape(wc, "wc", {V});
+  if (gscale.has_value()) { check(*gscale, "gscale", at::kFloat); TORCH_CHECK(gscale->numel() == 1, "gscale: one element"); }
   ok(ncnet_softmax_max_bwd((float*)x.data_ptr(), (float*)rmax.data_ptr(), (int*)rarg.data_ptr(), (float*)rse.data_ptr(),
                            (float*)cmax.data_ptr(), (int*)carg.data_ptr(), (float*)cse.data_ptr(), (float*)wr.data_ptr(),
                            (float*)wc.data_ptr(), (float*)gx.data_ptr(), V, R, C, (int)norm, (float)eps,
-                           cur_stream(x)), "softmax_max_bwd");
+                           opt_ptr<float>(gscale), cur_stream(x)), "softmax_max_bwd");
+}
+
+// weak-loss score value out [] fp32 from the row / column stats (rse / cse: the sums of `norm`)
+void score_sum(Tensor rmax, Tensor rse, Tensor cmax, Tensor cse, Tensor wr, Tensor wc, Tensor out, int64_t norm,
+               double eps) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(rmax.device());
+  for (auto* t : {&rmax, &rse, &cmax, &cse, &wr, &wc, &out}) check(*t, "score_sum operand", at::kFloat);
+  TORCH_CHECK(norm >= 0 && norm <= 2, "score_sum: norm must be 0, 1 or 2");
+  TORCH_CHECK(rmax.dim() == 2 && cmax.dim() == 2 && rmax.size(0) == cmax.size(0), "score_sum: [V, R] / [V, C] stats");
+  const int64_t V = rmax.size(0), R = rmax.size(1), C = cmax.size(1);
+  check_shape(rse, "rse", {V, R}); check_shape(cse, "cse", {V, C});
+  check_shape(wr, "wr", {V}); check_shape(wc, "wc", {V});
+  TORCH_CHECK(out.numel() == 1, "score_sum: out must have one element");
+  ok(ncnet_score_sum((float*)rmax.data_ptr(), (float*)rse.data_ptr(), (float*)cmax.data_ptr(), (float*)cse.data_ptr(),
+                     (float*)wr.data_ptr(), (float*)wc.data_ptr(), (int)V, (int)R, (int)C, (int)norm, (float)eps,
+                     (float*)out.data_ptr(), cur_stream(rmax)), "score_sum");
 }
 
 void maxpool4d(Tensor x, Tensor y, Tensor code, int64_t ks) {
@@ -908,12 +943,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stats2d", &stats2d);
   m.def("gather_bf16", &gather_bf16);
   m.def("match_candidates", &match_candidates);
-  m.def("mm_apply", &mm_apply);
+  m.def("mm_apply", &mm_apply, py::arg("c"), py::arg("rmax"), py::arg("cmax"), py::arg("out"), py::arg("out_x"),
+        py::arg("out_xt"), py::arg("eps"), py::arg("pad") = std::vector<int64_t>{});
   m.def("mm_bwd", &mm_bwd);
   m.def("combine_fwd", &combine_fwd);
   m.def("combine_bwd", &combine_bwd, py::arg("g"), py::arg("z"), py::arg("gz"), py::arg("R"), py::arg("C"),
         py::arg("gzl") = py::none());
-  m.def("softmax_max_bwd", &softmax_max_bwd);
+  m.def("softmax_max_bwd", &softmax_max_bwd, py::arg("x"), py::arg("rmax"), py::arg("rarg"), py::arg("rse"),
+        py::arg("cmax"), py::arg("carg"), py::arg("cse"), py::arg("wr"), py::arg("wc"), py::arg("gx"), py::arg("norm"),
+        py::arg("eps"), py::arg("gscale") = py::none());
+  m.def("score_sum", &score_sum);
   m.def("maxpool4d", &maxpool4d);
   m.def("transpose", &transpose);
   m.def("nc_fused_k3", &nc_fused_k3);

@@ -282,14 +282,17 @@ extern "C" int ncnet_x3_to_f32(const void* X, float* Y, long long rows, int C, h
 
 // gather_bf16: out[i] = bf16(src[idx[i]]) (0 where idx[i] < 0) -- the per-step
 // weight packs as one launch (ops/packing.py gather_pack)
+// (an index past the source -- nsrc elements -- also reads as 0: never a fault)
 __global__ __launch_bounds__(256) void gather_bf16_kernel(const float* __restrict__ src, const int* __restrict__ idx,
-                                                          __bf16* __restrict__ out, long long n) {
+                                                          __bf16* __restrict__ out, long long n, long long nsrc) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const int j = idx[i];
-  out[i] = (__bf16)(j >= 0 ? src[j] : 0.f);
+  out[i] = (__bf16)(j >= 0 && j < nsrc ? src[j] : 0.f);
 }
-extern "C" int ncnet_gather_bf16(const float* src, const int* idx, void* out, long long n, hipStream_t s) {
-  hipLaunchKernelGGL(gather_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, idx, (__bf16*)out, n);
+extern "C" int ncnet_gather_bf16(const float* src, const int* idx, void* out, long long n, long long nsrc,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(gather_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, idx, (__bf16*)out, n,
+                     nsrc);
   return (int)hipGetLastError();
 }

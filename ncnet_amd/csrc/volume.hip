@@ -290,11 +290,33 @@ __global__ __launch_bounds__(256) void match_candidates_kernel(const float* __re
 //   out_f32 [V,R,C] (optional), out_x bf16 [V,R,C] at volume slot v (optional),
 //   out_xt bf16 [V,C,R] at volume slot v (optional; A<->B swapped copy).
 // F16: out_x / out_xt are IEEE half (the half_precision NC input).
-template <bool F16>
+// PAD (training NC input, csrc/conv1x.hip layout): out_x / out_xt are the
+// zero-padded bf16 planes of conv1x16 / wgrad1x16 instead -- out_x [V*R][PPL]
+// (plane (v, r) = the [K2, L2] row r), out_xt [V*C][PPL] (plane (v, c) = the
+// [I2, J2] column c of the swapped branch) -- halos included: block (tr, tc)
+// zeroes chunk tc of the halo of its 64 row planes and chunk tr of the halo of
+// its 64 column planes, so no separate fill and pad passes are needed.
+struct PadGeom { int K2, L2, I2, J2, P, LP, PPL; };
+
+// position of halo element h of a padded [K2, L2] plane (rows of LP, P-wide
+// margins, PPL - (K2 + 2P) LP tail elements)
+__device__ __forceinline__ int halo_pos(int h, int K2, int L2, int P, int LP) {
+  const int top = P * LP;
+  if (h < top) return h;
+  h -= top;
+  const int mid = K2 * 2 * P;
+  if (h < mid) {
+    const int row = h / (2 * P), side = h - row * 2 * P;
+    return (row + P) * LP + (side < P ? side : L2 + side);
+  }
+  return (K2 + P) * LP + (h - mid);   // bottom margin rows, then the tail
+}
+
+template <bool F16, bool PAD>
 __global__ __launch_bounds__(256) void mm_apply_kernel(const float* __restrict__ c, const float* __restrict__ rmax,
                                                        const float* __restrict__ cmax, float* __restrict__ out_f32,
                                                        uint16_t* __restrict__ out_x, uint16_t* __restrict__ out_xt,
-                                                       int R, int C, float eps) {
+                                                       int R, int C, float eps, PadGeom pg) {
   __shared__ float tile[64][65];
   const int ntr = (R + 63) / 64, ntc = (C + 63) / 64;
   int b = blockIdx.x;
@@ -305,6 +327,8 @@ __global__ __launch_bounds__(256) void mm_apply_kernel(const float* __restrict__
   const size_t vb = (size_t)v * R * C;
   const int cc = c0 + tx;
   const float cm = (cc < C) ? cmax[(size_t)v * C + cc] + eps : 1.f;
+  // padded position of this lane's column cc in a row plane (PAD)
+  const int pcol = PAD ? (cc / pg.L2 + pg.P) * pg.LP + cc % pg.L2 + pg.P : 0;
   for (int rr = ty; rr < 64; rr += 4) {
     int r = r0 + rr;
     float o = 0.f;
@@ -313,7 +337,10 @@ __global__ __launch_bounds__(256) void mm_apply_kernel(const float* __restrict__
       float ra = rmax[(size_t)v * R + r] + eps;
       o = x * ((x / ra) * (x / cm));
       if (out_f32) out_f32[vb + (size_t)r * C + cc] = o;
-      if (out_x) out_x[vb + (size_t)r * C + cc] = f2s16<F16>(o);
+      if (out_x) {
+        if constexpr (PAD) out_x[((size_t)v * R + r) * pg.PPL + pcol] = f2s16<F16>(o);
+        else out_x[vb + (size_t)r * C + cc] = f2s16<F16>(o);
+      }
     }
     tile[rr][tx] = o;
   }
@@ -321,9 +348,32 @@ __global__ __launch_bounds__(256) void mm_apply_kernel(const float* __restrict__
     __syncthreads();
     // write transposed: row = c, col = r
     const int rw = r0 + tx;
+    const int prow = PAD ? (rw / pg.J2 + pg.P) * pg.LP + rw % pg.J2 + pg.P : 0;
     for (int cl = ty; cl < 64; cl += 4) {
       int ccol = c0 + cl;
-      if (ccol < C && rw < R) out_xt[vb + (size_t)ccol * R + rw] = f2s16<F16>(tile[tx][cl]);
+      if (ccol < C && rw < R) {
+        if constexpr (PAD) out_xt[((size_t)v * C + ccol) * pg.PPL + prow] = f2s16<F16>(tile[tx][cl]);
+        else out_xt[vb + (size_t)ccol * R + rw] = f2s16<F16>(tile[tx][cl]);
+      }
+    }
+  }
+  if constexpr (PAD) {
+    const uint16_t zero = 0;
+    if (out_x) {   // chunk tc of the halos of row planes r0 .. r0 + 63
+      const int nh = pg.PPL - pg.K2 * pg.L2, ch = (nh + ntc - 1) / ntc;
+      const int h0 = tc * ch, h1 = min(nh, h0 + ch);
+      for (int e = threadIdx.x; e < 64 * (h1 - h0); e += 256) {
+        const int rr = e / (h1 - h0), h = h0 + e - rr * (h1 - h0);
+        if (r0 + rr < R) out_x[((size_t)v * R + r0 + rr) * pg.PPL + halo_pos(h, pg.K2, pg.L2, pg.P, pg.LP)] = zero;
+      }
+    }
+    if (out_xt) {  // chunk tr of the halos of column planes c0 .. c0 + 63
+      const int nh = pg.PPL - pg.I2 * pg.J2, ch = (nh + ntr - 1) / ntr;
+      const int h0 = tr * ch, h1 = min(nh, h0 + ch);
+      for (int e = threadIdx.x; e < 64 * (h1 - h0); e += 256) {
+        const int cl = e / (h1 - h0), h = h0 + e - cl * (h1 - h0);
+        if (c0 + cl < C) out_xt[((size_t)v * C + c0 + cl) * pg.PPL + halo_pos(h, pg.I2, pg.J2, pg.P, pg.LP)] = zero;
+      }
     }
   }
 }
@@ -543,7 +593,7 @@ __global__ __launch_bounds__(256) void softmax_max_bwd_kernel(const float* __res
                                                               const float* __restrict__ cse,
                                                               const float* __restrict__ wr, const float* __restrict__ wc,
                                                               float* __restrict__ gx, long long total, int R, int C,
-                                                              int norm, float eps) {
+                                                              int norm, float eps, const float* __restrict__ gscale) {
   long long e = (long long)blockIdx.x * 256 + threadIdx.x;
   if (e >= total) return;
   const int k = (int)(e % C);
@@ -566,7 +616,41 @@ __global__ __launch_bounds__(256) void softmax_max_bwd_kernel(const float* __res
   } else {
     gr = wr[v] * dr + wc[v] * dc;
   }
-  gx[e] = gr;
+  // gscale: the incoming gradient of the scalar score (autograd's g), read by
+  // every lane from one address (no separate volume-sized multiply pass)
+  gx[e] = gscale ? gr * gscale[0] : gr;
+}
+
+// Weak-loss score value from the row / column statistics, in one launch:
+//   out = sum_{v,r} wr[v] s(rmax, rse) + sum_{v,c} wc[v] s(cmax, cse)
+// with s = 1 / sum (norm 1 'softmax'), max / (sum + eps) (2 'l1'), max (0).
+// One 1024-thread workgroup (V (R + C) is ~40 K terms at the training shape);
+// replaces the reciprocal / multiply / two reductions / add of the PyTorch form.
+__global__ __launch_bounds__(1024) void score_sum_kernel(const float* __restrict__ rmax, const float* __restrict__ rse,
+                                                         const float* __restrict__ cmax, const float* __restrict__ cse,
+                                                         const float* __restrict__ wr, const float* __restrict__ wc,
+                                                         int V, int R, int C, int norm, float eps,
+                                                         float* __restrict__ out) {
+  __shared__ float part[16];
+  float acc = 0.f;
+  const long long nr = (long long)V * R, nc = (long long)V * C;
+  for (long long e = threadIdx.x; e < nr + nc; e += 1024) {
+    const bool row = e < nr;
+    const long long i = row ? e : e - nr;
+    const float mx = row ? rmax[i] : cmax[i];
+    const float sm = row ? rse[i] : cse[i];
+    const float w = row ? wr[i / R] : wc[i / C];
+    const float sc = norm == 1 ? 1.f / sm : norm == 2 ? mx / (sm + eps) : mx;
+    acc += w * sc;
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = threadIdx.x < 16 ? part[threadIdx.x] : 0.f;
+    t = wave_sum(t);
+    if (threadIdx.x == 0) out[0] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -624,6 +708,7 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ x,
 
 using namespace ncnet;
 
+extern "C" int ncnet_pad_geom(int K, int L, int KS, int* lp, int* ppl);   // csrc/conv1x.hip
 static unsigned tiles64(int V, int R, int C) { return (unsigned)((long long)V * cdiv(R, 64) * cdiv(C, 64)); }
 
 // sum_kind: 1 sum exp(x - max), 2 plain sum (only when se != nullptr)
@@ -677,14 +762,23 @@ extern "C" int ncnet_match_candidates(const float* cmx, const float* cse, const 
                      rarg, code, fs1, fs2, fs3, fs4, k, m, sc, key);
   return (int)hipGetLastError();
 }
+// pad_ks > 0: out_x / out_xt are padded bf16 planes for kernel size pad_ks (I2 x J2 = R, K2 x L2 = C)
 extern "C" int ncnet_mm_apply(const float* c, const float* rmax, const float* cmax, float* out_f32, void* out_x,
-                              void* out_xt, int V, int R, int C, float eps, int x_f16, hipStream_t s) {
-  if (x_f16)
-    hipLaunchKernelGGL(mm_apply_kernel<true>, dim3(tiles64(V, R, C)), dim3(256), 0, s, c, rmax, cmax, out_f32,
-                       (uint16_t*)out_x, (uint16_t*)out_xt, R, C, eps);
+                              void* out_xt, int V, int R, int C, float eps, int x_f16, int pad_ks, int I2, int J2,
+                              int K2, int L2, hipStream_t s) {
+  PadGeom pg = {K2, L2, I2, J2, 0, 0, 0};
+  if (pad_ks > 0) {
+    if (x_f16 || I2 * J2 != R || K2 * L2 != C || I2 != K2 || J2 != L2) return -1;
+    pg.P = pad_ks / 2;
+    ncnet_pad_geom(K2, L2, pad_ks, &pg.LP, &pg.PPL);
+    hipLaunchKernelGGL((mm_apply_kernel<false, true>), dim3(tiles64(V, R, C)), dim3(256), 0, s, c, rmax, cmax, out_f32,
+                       (uint16_t*)out_x, (uint16_t*)out_xt, R, C, eps, pg);
+  } else if (x_f16)
+    hipLaunchKernelGGL((mm_apply_kernel<true, false>), dim3(tiles64(V, R, C)), dim3(256), 0, s, c, rmax, cmax, out_f32,
+                       (uint16_t*)out_x, (uint16_t*)out_xt, R, C, eps, pg);
   else
-    hipLaunchKernelGGL(mm_apply_kernel<false>, dim3(tiles64(V, R, C)), dim3(256), 0, s, c, rmax, cmax, out_f32,
-                       (uint16_t*)out_x, (uint16_t*)out_xt, R, C, eps);
+    hipLaunchKernelGGL((mm_apply_kernel<false, false>), dim3(tiles64(V, R, C)), dim3(256), 0, s, c, rmax, cmax, out_f32,
+                       (uint16_t*)out_x, (uint16_t*)out_xt, R, C, eps, pg);
   return (int)hipGetLastError();
 }
 // work: nullptr (separate row / column passes) or V * (ceil(C/256) * R + ceil(R/64) * C) floats (one pass)
@@ -727,10 +821,15 @@ extern "C" int ncnet_combine_bwd(const float* g, const float* z, void* gz, void*
 extern "C" int ncnet_softmax_max_bwd(const float* x, const float* rmax, const int* rarg, const float* rse,
                                      const float* cmax, const int* carg, const float* cse, const float* wr,
                                      const float* wc, float* gx, int V, int R, int C, int norm, float eps,
-                                     hipStream_t s) {
+                                     const float* gscale, hipStream_t s) {
   long long total = (long long)V * R * C;
   hipLaunchKernelGGL(softmax_max_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, rmax, rarg, rse,
-                     cmax, carg, cse, wr, wc, gx, total, R, C, norm, eps);
+                     cmax, carg, cse, wr, wc, gx, total, R, C, norm, eps, gscale);
+  return (int)hipGetLastError();
+}
+extern "C" int ncnet_score_sum(const float* rmax, const float* rse, const float* cmax, const float* cse, const float* wr,
+                               const float* wc, int V, int R, int C, int norm, float eps, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(score_sum_kernel, dim3(1), dim3(1024), 0, s, rmax, rse, cmax, cse, wr, wc, V, R, C, norm, eps, out);
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_maxpool4d(const void* x, int x_is_bf16, float* y, uint8_t* code, int V, int I, int J, int K,

@@ -27,7 +27,8 @@ from ..ops.conv4d import Conv4d
 from ..ops.correlation import (correlation, correlation_pool2, correlation_x3, l2norm_pack, l2norm_pack_f16,
                                l2norm_pack_fp8, l2norm_pack_split, maxpool4d as _maxpool4d)
 from ..ops import _ext as _ext_mod
-from ..ops.mutual import mutual_matching, mutual_matching_nc_input as _mm_nc_input
+from ..ops.mutual import (mutual_matching, mutual_matching_nc_input as _mm_nc_input,
+                          mutual_matching_padded as _mm_padded)
 from ..ops.neigh_consensus import neigh_consensus
 
 # the module (the package re-exports the function under the same name)
@@ -169,12 +170,27 @@ class NeighConsensus(nn.Module):
     def conv_layers(self):
         return [m for m in self.conv if isinstance(m, Conv4d)]
 
-    def forward(self, x):
+    def forward(self, x, padded=None):
+        """``padded``: x's zero-padded bf16 planes of both symmetric branches
+        (ops/mutual.py mutual_matching_padded), used by the bf16 training stack."""
         layers = self.conv_layers()
         ws = [m.weight_ref() for m in layers]
         bs = [m.bias if m.bias is not None else torch.zeros(m.out_channels, device=x.device) for m in layers]
         return neigh_consensus(x, ws, bs, self.channels, symmetric=self.symmetric_mode,
-                               fp8=getattr(self, "fp8", False), precision=getattr(self, "precision", "bf16"))
+                               fp8=getattr(self, "fp8", False), precision=getattr(self, "precision", "bf16"),
+                               padded=padded)
+
+    def padded_input_ks(self, x) -> int:
+        """Kernel size of the first layer when the bf16 training stack will take
+        its padded-plane path on ``x`` (MutualMatching then writes the planes
+        directly), else 0."""
+        if not (self.symmetric_mode and x.is_cuda and getattr(self, "precision", "bf16") == "bf16"
+                and not getattr(self, "fp8", False) and torch.is_grad_enabled()):
+            return 0
+        kinds = _nc_ops.layer_kinds(self.channels, self.kernel_sizes)
+        if kinds is None or not _nc_ops.fast1x_ok(kinds, self.channels, self.kernel_sizes, x, True):
+            return 0
+        return self.kernel_sizes[0]
 
 
 def _load_reference_checkpoint(path: str):
@@ -317,10 +333,16 @@ class ImMatchNet(nn.Module):
                     [m.bias if m.bias is not None else torch.zeros(m.out_channels, device=x2.device) for m in layers])
             with segment("mutual_matching"):
                 return MutualMatching(corr4d)
+        pks = nc.padded_input_ks(corr4d) if _ext_mod.use_hip(corr4d) else 0
         with segment("mutual_matching"):
-            corr4d = MutualMatching(corr4d)
+            # training stack: MutualMatching also writes the NC input's padded planes
+            xp = None
+            if pks:
+                corr4d, xp = _mm_padded(corr4d, pks)
+            else:
+                corr4d = MutualMatching(corr4d)
         with segment("neigh_consensus"):
-            corr4d = self.NeighConsensus(corr4d)
+            corr4d = self.NeighConsensus(corr4d, padded=xp)
         with segment("mutual_matching"):
             return MutualMatching(corr4d)
 

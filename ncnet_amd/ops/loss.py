@@ -42,14 +42,6 @@ def _row_col_stats(x3: torch.Tensor, norm: int):
     return rmax, rarg, rse, cmax, carg, cse
 
 
-def _scores(norm: int, mx: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
-    if norm == 1:
-        return 1.0 / s
-    if norm == 2:
-        return mx / (s + ref.L1_EPS)
-    return mx
-
-
 class SoftmaxMaxScoreFn(torch.autograd.Function):
     """sum_v wr[v] * sum_rows s_row + wc[v] * sum_cols s_col, s = the max of the
     normalised row / column (norm 1 softmax, 2 l1, 0 None)."""
@@ -59,7 +51,10 @@ class SoftmaxMaxScoreFn(torch.autograd.Function):
         x3 = x3.float().contiguous()
         st = _row_col_stats(x3, norm)
         rmax, rarg, rse, cmax, carg, cse = st
-        val = (wr.view(-1, 1) * _scores(norm, rmax, rse)).sum() + (wc.view(-1, 1) * _scores(norm, cmax, cse)).sum()
+        # one launch for the weighted score sum (was 7 small PyTorch kernels on the step's critical path)
+        val = torch.empty((), dtype=torch.float32, device=x3.device)
+        _ext.ext().score_sum(rmax, rse, cmax, cse, wr.float().contiguous(), wc.float().contiguous(), val, norm,
+                             ref.L1_EPS)
         ctx.norm = norm
         ctx.save_for_backward(x3, wr, wc, *st)
         return val
@@ -68,9 +63,10 @@ class SoftmaxMaxScoreFn(torch.autograd.Function):
     def backward(ctx, g):
         x3, wr, wc, rmax, rarg, rse, cmax, carg, cse = ctx.saved_tensors
         gx = torch.empty_like(x3)
+        # the incoming gradient scales inside the kernel (no extra pass over the volume)
         _ext.ext().softmax_max_bwd(x3, rmax, rarg, rse, cmax, carg, cse, wr.float().contiguous(),
-                                   wc.float().contiguous(), gx, ctx.norm, ref.L1_EPS)
-        return gx * g, None, None, None
+                                   wc.float().contiguous(), gx, ctx.norm, ref.L1_EPS, g.float().contiguous().reshape(1))
+        return gx, None, None, None
 
 
 _WEIGHTS: dict = {}

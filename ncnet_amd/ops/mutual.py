@@ -36,24 +36,46 @@ def _stats(c3: torch.Tensor):
 
 class MutualMatchingFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, corr4d):
+    def forward(ctx, corr4d, pad_ks: int = 0):
         V, ch, I, J, K, L = corr4d.shape
         assert ch == 1
         c3 = corr4d.reshape(V, I * J, K * L).float().contiguous()
         rmax, rarg, cmax, carg = _stats(c3)
         out = torch.empty_like(c3)
-        _ext.ext().mm_apply(c3, rmax, cmax, out, None, None, EPS)
+        xp = None
+        if pad_ks:
+            # the padded bf16 NC-input planes of both symmetric branches in the same
+            # pass (csrc/volume.hip mm_apply PAD mode, halos included)
+            _, ppl = _ext.ext().pad_geom(K, L, pad_ks)
+            xp = torch.empty((2 * V * I * J, ppl), dtype=torch.bfloat16, device=c3.device)
+            _ext.ext().mm_apply(c3, rmax, cmax, out, xp[:V * I * J], xp[V * I * J:], EPS, [pad_ks, I, J])
+            ctx.mark_non_differentiable(xp)
+        else:
+            _ext.ext().mm_apply(c3, rmax, cmax, out, None, None, EPS)
         ctx.save_for_backward(c3, rmax, rarg, cmax, carg)
         ctx.shape = corr4d.shape
+        if xp is not None:
+            return out.reshape(corr4d.shape), xp
         return out.reshape(corr4d.shape)
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, *_):
         c3, rmax, rarg, cmax, carg = ctx.saved_tensors
         g3 = g.reshape(c3.shape).float().contiguous()
         gc = torch.empty_like(c3)
         _ext.ext().mm_bwd(c3, g3, rmax, rarg, cmax, carg, gc, EPS, _config.STATS2D)   # one pass for both sums
-        return gc.reshape(ctx.shape)
+        return gc.reshape(ctx.shape), None
+
+
+def mutual_matching_padded(corr4d: torch.Tensor, ks: int):
+    """MutualMatching (autograd) that also writes its output as the zero-padded
+    bf16 planes of both symmetric NeighConsensus branches for a first layer of
+    kernel size ``ks`` (the training stack's conv1x16 / wgrad1x16 operand,
+    ops/neigh_consensus.py fast1x path) -> (x [V,1,I,J,K,L] fp32, planes
+    [2 V I J, PPL] bf16).  Square volumes only."""
+    V, ch, I, J, K, L = corr4d.shape
+    assert ch == 1 and (I, J) == (K, L)
+    return MutualMatchingFn.apply(corr4d, ks)
 
 
 def mutual_matching_nc_input(corr4d: torch.Tensor, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:

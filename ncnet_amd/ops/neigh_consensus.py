@@ -43,9 +43,9 @@ import torch.utils.weak as _weak
 from .. import config as _config
 from . import _ext
 from . import reference as ref
-from .packing import (_blk_packed, _w1x_dgrad, blk_out_weights, gather_pack, ij_groups, ij_in_grad, ij_in_weights,
-                      ij_out_grad, ij_out_weights, pack_w16, pack_w1x, pack_w16_planes, plane_dgrad_weights,
-                      transpose_for_dgrad)
+from .packing import (_blk_packed, _w16_dgrad, _w1x_dgrad, blk_out_weights, gather_pack, ij_groups, ij_in_grad,
+                      ij_in_weights, ij_out_grad, ij_out_weights, pack_w16, pack_w1x, pack_w16_planes, packed_weights,
+                      plane_dgrad_weights, transpose_for_dgrad)
 
 HIP_KS = (1, 3, 5, 7)
 # Cout=1 layers with <= 16 input channels run in output-plane-block mode
@@ -229,7 +229,7 @@ def _ij_out_planes(w_std: torch.Tensor, nbi: int) -> torch.Tensor:
 
 
 def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=None, relu: bool = True,
-               mask=None, f32: bool = False, xs=None) -> torch.Tensor:
+               mask=None, f32: bool = False, xs=None, wp=None) -> torch.Tensor:
     """One "same" Conv4d on the HIP kernels, any channel counts.
 
     h: the 1-channel input [V,I,J,K,L] (bf16/fp32) when cin == 1, else bf16
@@ -238,7 +238,9 @@ def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=N
       f32=False: bf16 blocks [NBo, ...,16] (cout > 1) / fp32 [V,I,J,K,L] (cout == 1)
       f32=True : fp32 planar [cout, V,I,J,K,L] (cout > 1) / fp32 [V,I,J,K,L].
     ``mask`` (bf16 blocks like the output, cout > 1, f32=False only) replaces
-    bias/ReLU by the data-gradient epilogue y = acc * (mask > 0)."""
+    bias/ReLU by the data-gradient epilogue y = acc * (mask > 0).  ``wp``: the
+    layer's packed operand from ``packed_weights`` (single-block 16 -> 16 and
+    output-plane-block Cout=1 layers), else packed here."""
     C = _ext.ext()
     ks = w_std.shape[-1]
     shp = tuple(h.shape[:5]) if cin == 1 else tuple(h.shape[1:6])
@@ -264,7 +266,7 @@ def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=N
         # output-plane blocks: the 16 MFMA rows are 4x4 output planes, no
         # combo-planar partials (2.5 GB at the training shape) and no ijsum
         y = torch.empty(shp, dtype=torch.float32, device=dev)
-        C.conv16_blk_fwd(h[0], gather_pack(_blk_packed, w_std),
+        C.conv16_blk_fwd(h[0], wp if wp is not None else gather_pack(_blk_packed, w_std),
                          None if bias is None else bias.float().reshape(1).contiguous(), y, ks, 1 if relu else 0)
         return y
     if cout == 1:                          # ij encoding: combo-planar partials, shift-summed by ijsum
@@ -277,7 +279,8 @@ def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=N
         C.ijsum(z, None if bias is None else _pad_bias(bias, 1), y, ks, 1 if relu else 0, 1)
         return y
     if nbi == 1:
-        outs = [_epilogue_call(C, h[0], gather_pack(pack_w16, w_std[_blk(w_std, b, cout), :16]), bias, b, cout, relu,
+        outs = [_epilogue_call(C, h[0], wp if (wp is not None and nbo == 1) else
+                               gather_pack(pack_w16, w_std[_blk(w_std, b, cout), :16]), bias, b, cout, relu,
                                mask, f32, shp, ks) for b in range(nbo)]
         return _gather(outs, f32, cout)
     # several input blocks: fp32 partials per (out, in) block pair, summed before the activation
@@ -380,10 +383,11 @@ def _wgrad1x(C, d16: torch.Tensor, xp: torch.Tensor, ks: int, bias: bool):
     return part.sum(0)[:, : ks * ks], (partb.sum(0) if bias else None)
 
 
-def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list, xp=None, shp=None):
+def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list, xp=None, shp=None, packs=None):
     """x0: [V,I,J,K,L] bf16 -> last layer's ReLU output, fp32: [V,I,J,K,L] if it
     has one channel, else planar [C, V,I,J,K,L].  Appends, per layer, what its
-    backward reads: the ij-packed input (1-channel inputs) or the bf16 input blocks."""
+    backward reads: the ij-packed input (1-channel inputs) or the bf16 input blocks.
+    ``packs``: {("f", layer): packed forward operand} from ``_stack_packs``."""
     C = _ext.ext()
     h = x0
     nl = len(kinds)
@@ -395,7 +399,7 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list, xp=None, shp=None):
         xs = None
         if li == 0 and xp is not None:      # padded-plane first layer (fast1x_ok)
             y = torch.empty(tuple(shp) + (16,), dtype=torch.bfloat16, device=xp.device)
-            C.conv1x16(xp, gather_pack(pack_w1x, w), _pad_bias(b, 16), None, y, ks, 1)
+            C.conv1x16(xp, packs[("f", 0)] if packs else gather_pack(pack_w1x, w), _pad_bias(b, 16), None, y, ks, 1)
             save.append(xp)
             h, cin = y.unsqueeze(0), cout
             continue
@@ -405,7 +409,8 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list, xp=None, shp=None):
             save.append((xs, h) if li > 0 else xs)   # mid-stack 1-channel inputs also serve as ReLU masks
         else:
             save.append(h)
-        y = conv_layer(h, w, cin, cout, bias=b, relu=True, f32=last and cout > 1, xs=xs)
+        y = conv_layer(h, w, cin, cout, bias=b, relu=True, f32=last and cout > 1, xs=xs,
+                       wp=packs.get(("f", li)) if packs else None)
         if cout == 1 and not last:
             y = y.to(torch.bfloat16)
         h = y
@@ -506,7 +511,8 @@ def _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout):
     return ij_in_grad(torch.stack([p[0][0] for p in parts]), 1), parts[0][1][:1].clone()
 
 
-def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool, fast1x: bool = False):
+def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool, fast1x: bool = False,
+               packs=None):
     """g_last: grad w.r.t. the last conv's PRE-activation, bf16: [V,I,J,K,L] for
     a 1-channel output, else blocks [NB, V,I,J,K,L,16].
     Returns (dW list in checkpoint layout, db list, grad of x0 fp32 or None)."""
@@ -544,7 +550,8 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
                     db = g.sum(dtype=torch.float32).reshape(1)
                 if li > 0 or need_dx0:
                     gn = torch.empty((1,) + tuple(hin.shape[1:]), dtype=torch.bfloat16, device=g.device)
-                    C.conv1x16(gp, gather_pack(_w1x_dgrad, w), None, hin[0], gn[0], ks, 2)
+                    C.conv1x16(gp, packs[("b", li)] if packs else gather_pack(_w1x_dgrad, w), None, hin[0], gn[0],
+                               ks, 2)
                     g = gn
             else:                                    # first layer: xin = padded NC-input planes
                 R, sb = _wgrad1x(C, g[0], xin, ks, True)
@@ -580,7 +587,8 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
                 else:                                # mid-stack: the previous layer's ReLU mask
                     g = (gx * (hin > 0)).to(torch.bfloat16)
             else:                                    # "16": masked by the previous layer's ReLU output
-                g = conv_layer(g, transpose_for_dgrad(w), cout, cin, relu=False, mask=hin)
+                g = conv_layer(g, transpose_for_dgrad(w), cout, cin, relu=False, mask=hin,
+                               wp=packs.get(("b", li)) if packs else None)
         dws[li] = dw
         dbs[li] = db
     if side is not None:
@@ -588,6 +596,24 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
         for t in dws + dbs:          # produced on the side stream, consumed (and freed) on main
             t.record_stream(main)
     return [d if ref_layout[i] else ref.conv4d_weight_from_std(d) for i, d in enumerate(dws)], dbs, gx0
+
+
+def _stack_packs(ws, kinds):
+    """Every packed operand of the padded-plane training stack (fast1x_ok) --
+    conv1x16 weights of layer 0, conv16 weights of the 16 -> 16 layers and their
+    data-gradient (transposed, flipped) weights, the output-plane-block weights
+    of the Cout=1 layer and its conv1x16 data-gradient weights -- from ONE gather
+    launch (packing.packed_weights) -> {("f" | "b", layer): bf16 tensor}."""
+    specs, keys = [], []
+    nl = len(kinds)
+    for li, kind in enumerate(kinds):
+        if li == 0:
+            specs.append((0, pack_w1x)); keys.append(("f", 0))
+        elif li == nl - 1:
+            specs += [(li, _blk_packed), (li, _w1x_dgrad)]; keys += [("f", li), ("b", li)]
+        else:
+            specs += [(li, pack_w16), (li, _w16_dgrad)]; keys += [("f", li), ("b", li)]
+    return dict(zip(keys, packed_weights(list(ws), specs)))
 
 
 def _swap_flat(x: torch.Tensor, shape_ab):
@@ -609,6 +635,13 @@ def _combine_multi(z1: torch.Tensor, z2: torch.Tensor, dims) -> torch.Tensor:
 class NeighConsensusFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, symmetric, kinds, channels, *params):
+        return NeighConsensusFn._fwd(ctx, x, symmetric, kinds, channels, params)
+
+    @staticmethod
+    def _fwd(ctx, x, symmetric, kinds, channels, params, xp_in=None):
+        """``xp_in``: the padded bf16 planes of both symmetric branches, already
+        written by MutualMatching (mutual.mutual_matching_padded); only used
+        on the padded-plane path (fast1x_ok, symmetric, square)."""
         ws, bs = params[0::2], params[1::2]
         V, _, I, J, K, L = x.shape
         R, Cc = I * J, K * L
@@ -616,6 +649,7 @@ class NeighConsensusFn(torch.autograd.Function):
         saved_layers = []
         square = (I, J) == (K, L)
         fast = fast1x_ok(kinds, channels, [w.shape[0] for w in ws], x, symmetric)
+        packs = _stack_packs(ws, kinds) if fast and BLK_1OUT else None
         if fast:
             # the 1-channel input as padded planes, both branches in one batch
             # (pad_planes trans=1 writes the swapped branch's planes directly)
@@ -623,12 +657,16 @@ class NeighConsensusFn(torch.autograd.Function):
             k0 = ws[0].shape[0]
             if symmetric:
                 _, ppl = _ext.ext().pad_geom(K, L, k0)
-                xp = torch.zeros((2 * V * R, ppl), dtype=torch.bfloat16, device=x.device)
-                _pad_1ch(x3, K, L, k0, 0, out=xp[:V * R])
-                _pad_1ch(x3, I, J, k0, 1, out=xp[V * R:])
-                z = _stack_fwd(None, ws, bs, kinds, saved_layers, xp=xp, shp=(2 * V, I, J, K, L))
+                if xp_in is not None and tuple(xp_in.shape) == (2 * V * R, ppl) and xp_in.dtype == torch.bfloat16:
+                    xp = xp_in
+                else:
+                    xp = torch.zeros((2 * V * R, ppl), dtype=torch.bfloat16, device=x.device)
+                    _pad_1ch(x3, K, L, k0, 0, out=xp[:V * R])
+                    _pad_1ch(x3, I, J, k0, 1, out=xp[V * R:])
+                z = _stack_fwd(None, ws, bs, kinds, saved_layers, xp=xp, shp=(2 * V, I, J, K, L), packs=packs)
             else:
-                z = _stack_fwd(None, ws, bs, kinds, saved_layers, xp=_pad_1ch(x3, K, L, k0, 0), shp=(V, I, J, K, L))
+                z = _stack_fwd(None, ws, bs, kinds, saved_layers, xp=_pad_1ch(x3, K, L, k0, 0), shp=(V, I, J, K, L),
+                               packs=packs)
             branches = [saved_layers]
         elif symmetric:
             xb = x.reshape(V, I, J, K, L).to(torch.bfloat16).contiguous()
@@ -660,6 +698,7 @@ class NeighConsensusFn(torch.autograd.Function):
         else:
             y = z.reshape(V, 1, I, J, K, L) if cl == 1 else z.transpose(0, 1).contiguous()
         ctx.fast1x = fast
+        ctx.packs = packs
         ctx.symmetric = symmetric
         ctx.kinds = kinds
         ctx.channels = channels
@@ -682,6 +721,11 @@ class NeighConsensusFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        gx, grads = NeighConsensusFn._bwd(ctx, gy)
+        return (gx, None, None, None, *grads)
+
+    @staticmethod
+    def _bwd(ctx, gy):
         z, *rest = ctx.saved_tensors
         nparam = 2 * len(ctx.kinds)
         params, flat = rest[:nparam], list(rest[nparam:])
@@ -726,7 +770,8 @@ class NeighConsensusFn(torch.autograd.Function):
                           planar_to_blocks(gz2.reshape(cl, V, K, L, I, J))]
             else:
                 gl = [planar_to_blocks(g1 * (z > 0))]
-        res = [_stack_bwd(g, br, ws, ctx.kinds, ctx.channels, need_dx0, ctx.fast1x) for g, br in zip(gl, branches)]
+        res = [_stack_bwd(g, br, ws, ctx.kinds, ctx.channels, need_dx0, ctx.fast1x, ctx.packs)
+               for g, br in zip(gl, branches)]
         if len(res) == 1:            # one batched branch: no accumulation copies
             dws, dbs = res[0][0], res[0][1]
         else:
@@ -747,7 +792,22 @@ class NeighConsensusFn(torch.autograd.Function):
         grads = []
         for dw, db in zip(dws, dbs):
             grads += [dw, db]
-        return (gx, None, None, None, *grads)
+        return gx, grads
+
+
+class NeighConsensusPaddedFn(torch.autograd.Function):
+    """NeighConsensusFn with the padded NC-input planes supplied by the
+    MutualMatching that produced ``x`` (mm_apply's padded mode): the two
+    pad passes and the zero fill of the training step's forward disappear."""
+
+    @staticmethod
+    def forward(ctx, x, xp, symmetric, kinds, channels, *params):
+        return NeighConsensusFn._fwd(ctx, x, symmetric, kinds, channels, params, xp_in=xp)
+
+    @staticmethod
+    def backward(ctx, gy):
+        gx, grads = NeighConsensusFn._bwd(ctx, gy)
+        return (gx, None, None, None, None, *grads)
 
 
 # ---------------------------------------------------------------------------
@@ -1371,7 +1431,7 @@ def fp8_ok(kinds, channels) -> bool:
 
 
 def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool = True, fp8: bool = False,
-                    precision: str = "bf16") -> torch.Tensor:
+                    precision: str = "bf16", padded: torch.Tensor | None = None) -> torch.Tensor:
     """x: [V,1,I,J,K,L] fp32; weights in checkpoint layout [k, out, in, k, k, k].
     Returns [V, C_last, I, J, K, L] fp32.
 
@@ -1380,7 +1440,9 @@ def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool 
     (inference, other ``fp8_ok`` stacks) on the fp8 MFMA Conv4d kernels; ``precision='fp32'`` (inference) on the bf16x3
     kernels (fp32-accurate); everything else with odd kernel sizes <= 7 and
     any channel counts on the bf16 autograd stack.  ``_ext.DISPATCH`` records
-    which path ran."""
+    which path ran.  ``padded``: x's padded bf16 planes for both symmetric
+    branches from ``mutual.mutual_matching_padded`` (the bf16 training stack
+    uses them instead of padding x itself)."""
     kernel_sizes = [w.shape[0] for w in weights]
     kinds = layer_kinds(channels, kernel_sizes)
     if _ext.use_hip(x):
@@ -1414,5 +1476,8 @@ def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool 
             params = []
             for w, b in zip(weights, biases):
                 params += [w, b]
+            if padded is not None:
+                return NeighConsensusPaddedFn.apply(x.float().contiguous(), padded, symmetric, tuple(kinds),
+                                                    tuple(channels), *params)
             return NeighConsensusFn.apply(x.float().contiguous(), symmetric, tuple(kinds), tuple(channels), *params)
     return ref.neigh_consensus(x.float(), [w.float() for w in weights], [b.float() for b in biases], symmetric)

@@ -180,42 +180,98 @@ def pack_w1x(w_std: torch.Tensor, out_dtype: torch.dtype = torch.bfloat16) -> to
 
 
 # ---------------------------------------------------------------------------
-# Per-step packing as ONE gather launch.  Every pack above is a pure gather of
-# the standard-layout weight (plus zeros): run once per (pack, shape) on an
-# index-valued fp64 tensor, it yields the source element of every packed
-# slot; each training step then packs with a single `gather_bf16` launch
-# (csrc/epilogue.hip) instead of 4-5 small PyTorch kernels (index, multiply,
-# permute-copy, cast), which sat on the critical path of the pipelined step.
+# Per-step packing: every pack above is a pure gather of the standard-layout
+# weight (plus zeros).  ``packed_weights`` builds ALL the packs a NeighConsensus
+# stack needs in a step (forward and backward operands of every layer) with ONE
+# `gather_bf16` launch (csrc/epilogue.hip) from the parameters' storage: the
+# index of every packed slot is found once per (layout, pack list) by running
+# the packs on an index-valued fp64 tensor.  The packs of unchanged weights
+# (same storage, same version counters -- FlatAdam bumps them after its update)
+# are reused, so inference packs once.  Before this the ~22 small PyTorch
+# kernels of the packs (index, multiply, permute-copy, cast per pack) sat on the
+# critical path of the training step (profiles/r5/).
 # ---------------------------------------------------------------------------
-_GATHER_IDX: dict = {}
-_GATHER_ON = __import__("os").environ.get("NCNET_GATHER_PACK", "0") == "1"   # measured slower (profiles/r4/ab/gather_pack.txt): off
-
-
-def _gather_index(fn, shape, device):
-    key = (fn, tuple(shape), str(device))
-    ent = _GATHER_IDX.get(key)
-    if ent is None:
-        n = 1
-        for d in shape:
-            n *= d
-        wi = torch.arange(1, n + 1, dtype=torch.float64).reshape(shape)
-        v = fn(wi)
-        idx = (v.round().to(torch.int64) - 1).to(torch.int32)    # 0 (a zero slot) -> -1
-        ent = (idx.reshape(-1).to(device), tuple(v.shape))
-        _GATHER_IDX[key] = ent
-    return ent
 
 
 def gather_pack(fn, w_std: torch.Tensor) -> torch.Tensor:
-    """``fn(w_std)`` (a pure-gather pack to bf16) as one gather launch on GPU.
-    ``fn`` takes (w, out_dtype) or just (w) and must not depend on the values."""
+    """``fn(w_std)`` as bf16 (the un-batched path: general stacks, tests)."""
+    return fn(w_std).to(torch.bfloat16)
+
+
+_PLAN_CACHE: dict = {}
+_PACK_CACHE: dict = {}
+
+
+def _source(ws):
+    """(flat fp32 source, element offset of each weight) -- the parameters' own
+    storage when they all live in one (FlatAdam's flat buffer), else None."""
+    st = ws[0].untyped_storage()
+    if all(w.dtype == torch.float32 and w.is_contiguous() and w.untyped_storage().data_ptr() == st.data_ptr()
+           for w in ws):
+        flat = torch.empty(0, dtype=torch.float32, device=ws[0].device).set_(st)
+        return flat, [w.storage_offset() for w in ws]
+    return None
+
+
+def _plan(shapes, offsets, nsrc, specs, device):
+    """Index of every packed slot into the flat source (-1: a zero slot) and
+    each pack's shape.  ``specs``: (weight index, pack fn) pairs."""
+    from .reference import conv4d_weight_to_std
+    key = (shapes, tuple(offsets), nsrc, specs, str(device))
+    ent = _PLAN_CACHE.get(key)
+    if ent is None:
+        idx, shp = [], []
+        for wi, fn in specs:
+            n = 1
+            for d in shapes[wi]:
+                n *= d
+            w = (torch.arange(1, n + 1, dtype=torch.float64) + offsets[wi]).reshape(shapes[wi])
+            v = _F64[fn](conv4d_weight_to_std(w))
+            idx.append((v.round().to(torch.int64) - 1).reshape(-1))   # 0 (a zero slot) -> -1
+            shp.append(tuple(v.shape))
+        cat = torch.cat(idx)
+        if int(cat.max()) >= nsrc:
+            raise RuntimeError("packed_weights: index past the source (internal)")
+        ent = _PLAN_CACHE[key] = (cat.to(torch.int32).to(device), shp)
+    return ent
+
+
+def packed_weights(ws, specs):
+    """The packs ``[fn(std(ws[i])) for i, fn in specs]`` (bf16) with one gather
+    launch on the GPU (the weights in checkpoint layout, fp32)."""
     from . import _ext
-    if not (_GATHER_ON and fn in _F64 and w_std.is_cuda and _ext.use_hip(w_std)):
-        return fn(w_std).to(torch.bfloat16)        # (unknown packs -- e.g. a test's mutated one -- run as they are)
-    idx, shape = _gather_index(_F64[fn], w_std.shape, w_std.device)
-    out = torch.empty(shape, dtype=torch.bfloat16, device=w_std.device)
-    _ext.ext().gather_bf16(w_std.detach().float().contiguous().reshape(-1), idx, out.reshape(-1))
-    return out
+    specs = tuple(specs)
+    ws = [w.detach() for w in ws]
+    if not (ws[0].is_cuda and _ext.use_hip(ws[0]) and all(fn in _F64 for _, fn in specs)):
+        from .reference import conv4d_weight_to_std
+        return [gather_pack(fn, conv4d_weight_to_std(ws[i]).float()) for i, fn in specs]
+    src = _source(ws)
+    ver = tuple((w.untyped_storage().data_ptr(), w.storage_offset(), w._version) for w in ws)
+    ckey = (ver, specs)
+    hit = _PACK_CACHE.get(specs)
+    if hit is not None and hit[0] == ckey and not torch.cuda.is_current_stream_capturing():
+        return hit[1]
+    if src is None:
+        flat = torch.cat([w.float().reshape(-1) for w in ws])
+        offs, o = [], 0
+        for w in ws:
+            offs.append(o)
+            o += w.numel()
+    else:
+        flat, offs = src
+    idx, shp = _plan(tuple(tuple(w.shape) for w in ws), offs, flat.numel(), specs, ws[0].device)
+    out = torch.empty(idx.numel(), dtype=torch.bfloat16, device=ws[0].device)
+    _ext.ext().gather_bf16(flat, idx, out)
+    res, o = [], 0
+    for sh in shp:
+        n = 1
+        for d in sh:
+            n *= d
+        res.append(out[o:o + n].view(sh))
+        o += n
+    if not torch.cuda.is_current_stream_capturing():
+        _PACK_CACHE[specs] = (ckey, res)
+    return res
 
 
 def _blk_packed(w, out_dtype=torch.bfloat16):

@@ -53,6 +53,22 @@ def test_inloc_export_contract(workdir):
     assert rows == sorted(set(rows))
 
 
+def test_inloc_export_square_grows_n(workdir):
+    """A square query pools to an 8 x 8 grid at 256 px: more unique matches than
+    the reference's 4:3 N (2 * 8 * 6 = 96).  The export grows the array instead
+    of silently dropping rows (the reference raises on the overflow)."""
+    import eval_inloc
+    from scipy.io import loadmat
+    out = eval_inloc.main(["--synthetic_queries", "1", "--n_panos", "1", "--image_size", "256", "--k_size", "2",
+                           "--synthetic_hw", "512", "512", "--output_dir", "msq"])
+    m = loadmat(os.path.join(out, "1.mat"))["matches"]
+    used = m[0, 0, :, 4] > 0
+    n_ref = 2 * 8 * 6
+    assert used.sum() > n_ref and m.shape[2] == used.sum()
+    rows = [tuple(r) for r in m[0, 0, used, :4]]
+    assert rows == sorted(set(rows))
+
+
 def test_point_transfer_demo(workdir):
     import point_transfer_demo
     out = os.path.join(workdir, "demo.png")
