@@ -80,15 +80,13 @@ def _inloc_secondary():
             if "pair_graph_error" in r:
                 out[name]["pair_graph_error"] = r["pair_graph_error"]
         # the all-fp8 pipeline (fp8 Conv4d NC kernels instead of the fused bf16 stack)
-        os.environ["NCNET_NC_FP8"] = "1"
-        try:
+        from ncnet_amd import config as _config
+        with _config.override(nc_fp8=True):
             r = bench_inloc.run_single(3200, pairs=10, warmup=2, model=model, panos_per_query=10, precision="fp8")
             out["inloc_3200_fp8_nc_fp8"] = {"ms_per_pair": r["value"], "stages_ms": r["stages_ms"],
                                             "stages_ms_eager": r.get("stages_ms_eager"),
                                             "panos_per_query": 10, "dtype": r["dtype"],
                                             "pair_graph": r["pair_graph"]}
-        finally:
-            os.environ.pop("NCNET_NC_FP8", None)
         del model
     except Exception as e:  # the headline record must still print
         out["error"] = repr(e)
@@ -295,7 +293,7 @@ def main(argv=None):
         print(json.dumps({"secondary": args.only_secondary, **fn[args.only_secondary]()}), flush=True)
         return 0
 
-    from ncnet_amd.config import RuntimeConfig
+    from ncnet_amd import config as _config
     from ncnet_amd.engine.trainer import Trainer, make_adam
     from ncnet_amd.models import ImMatchNet
     from ncnet_amd.parallel.dist import (GradBucket, all_reduce_max_float, barrier, broadcast_module, comm_info,
@@ -434,7 +432,7 @@ def main(argv=None):
                        "optimizer": type(opt).__name__,
                        "hbm_peak_gb": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
                                        if dev.type == "cuda" else None),
-                       "runtime": RuntimeConfig.from_env().as_dict(),
+                       "runtime": _config.RUNTIME.as_dict(),
                        "secondary": secondary},
         }
         print(json.dumps(rec), flush=True)

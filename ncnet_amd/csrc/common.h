@@ -162,31 +162,24 @@ __device__ __noinline__ bool ncnet_check_fail(const char* cond, const char* file
 #endif
 
 // Launcher tuning switches -- A/B tests and scripts/kbench.py only.  ONE
-// process-wide table, seeded from the NCNET_* environment when a launcher
-// first runs and changed in-process through the set_tuning binding
-// (ncnet_set_tuning): no launch reads the environment.
+// process-wide table with the defaults below; the Python side pushes
+// ncnet_amd.config.RUNTIME's values (the NCNET_* environment, read once there)
+// through the set_tuning binding when the extension loads (ops/_ext.py
+// apply_tuning): no launcher reads the environment.
 struct NcnetTuning {
-  int nt_store;        // NCNET_NT_STORE: non-temporal Conv4d epilogue stores (1)
-  int gp_tpw;          // NCNET_GP_TPW: output j-tiles per group-plane workgroup (5)
-  int conv_v3;         // NCNET_CONV_V3: conv16v3 instead of conv16v4 at 25 x 25 (0)
-  int wgrad_v3;        // NCNET_WGRAD_V3: wgrad16v3 instead of wgrad16v4 at 25 x 25 (0)
-  int wgrad_flags;     // NCNET_WGRAD_FLAGS: wgrad16v3 ablation flags (0)
-  int conv2d_variant;  // NCNET_CONV2D_VARIANT: 0 auto, 1 register-staged, 2 DMA ring
-  int conv2d_big;      // NCNET_CONV2D_BIG: allow the 256 x 128 tile on smaller grids (0)
-  int corr_v2;         // NCNET_CORR_V2: -1 auto, 0 / 1 force the correlation GEMM variant
-  int corr_ns;         // NCNET_CORR_NS: 3 or 4 ring stages of corr_gemm_v2
-  int conv2d_v3;       // NCNET_CONV2D_V3: chip-round v3 tiles where the auto rule picks them (1)
+  int nt_store;        // non-temporal Conv4d epilogue stores (1)
+  int gp_tpw;          // output j-tiles per group-plane workgroup (5)
+  int conv_v3;         // conv16v3 instead of conv16v4 at the compile-time planes (0)
+  int wgrad_v3;        // wgrad16v3 instead of wgrad16v4 at the compile-time planes (0)
+  int wgrad_flags;     // wgrad16v3 ablation flags (0)
+  int conv2d_variant;  // 0 auto, 1 register-staged, 2 DMA ring
+  int corr_v2;         // -1 auto, 0 / 1 force the correlation GEMM variant
+  int corr_ns;         // 3 or 4 ring stages of corr_gemm_v2
+  int conv2d_v3;       // chip-round v3 tiles where the auto rule picks them (1)
+  int c1x_pd;          // conv1x16 transposed-read lookahead in tiles, 1, 2 or 3 (2)
 };
-__host__ inline int ncnet_tuning_env(const char* k, int d) {
-  const char* e = getenv(k);
-  return e ? atoi(e) : d;
-}
 __host__ inline NcnetTuning& tuning() {
-  static NcnetTuning t = {ncnet_tuning_env("NCNET_NT_STORE", 1),    ncnet_tuning_env("NCNET_GP_TPW", 5),
-                          ncnet_tuning_env("NCNET_CONV_V3", 0),     ncnet_tuning_env("NCNET_WGRAD_V3", 0),
-                          ncnet_tuning_env("NCNET_WGRAD_FLAGS", 0), ncnet_tuning_env("NCNET_CONV2D_VARIANT", 0),
-                          ncnet_tuning_env("NCNET_CONV2D_BIG", 0),  ncnet_tuning_env("NCNET_CORR_V2", -1),
-                          ncnet_tuning_env("NCNET_CORR_NS", 3) == 4 ? 4 : 3, ncnet_tuning_env("NCNET_CONV2D_V3", 1)};
+  static NcnetTuning t = {1, 5, 0, 0, 0, 0, -1, 3, 1, 2};
   return t;
 }
 __host__ inline int* tuning_slot(const char* name) {
@@ -197,9 +190,9 @@ __host__ inline int* tuning_slot(const char* name) {
   if (!strcmp(name, "wgrad_v3")) return &t.wgrad_v3;
   if (!strcmp(name, "wgrad_flags")) return &t.wgrad_flags;
   if (!strcmp(name, "conv2d_variant")) return &t.conv2d_variant;
-  if (!strcmp(name, "conv2d_big")) return &t.conv2d_big;
   if (!strcmp(name, "corr_v2")) return &t.corr_v2;
   if (!strcmp(name, "corr_ns")) return &t.corr_ns;
   if (!strcmp(name, "conv2d_v3")) return &t.conv2d_v3;
+  if (!strcmp(name, "c1x_pd")) return &t.c1x_pd;
   return nullptr;
 }

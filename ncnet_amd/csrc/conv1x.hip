@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void pad_planes_kernel(const T* __restrict__ x
 // (lane l: co = l & 15, K rows 8 (l >> 4) .. +7 = taps dk*KS+dl, >= NT zero);
 // Y: bf16 [V,I,J,K,L,16]; EPI1X_BIAS_RELU (bias [16]) or EPI1X_MASK (M bf16 [V,I,J,K,L,16]: y *= M > 0).
 // ---------------------------------------------------------------------------
-template <int KS, int R, int EPI, int K, int L>
+template <int KS, int R, int EPI, int K, int L, int PD = 1>
 __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict__ Xp, const u32x4* __restrict__ Wa,
                                                           const float* __restrict__ bias, const bf16* __restrict__ M,
                                                           bf16* __restrict__ Y, int V, int I, int J, int nt_store,
@@ -176,11 +176,21 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
     // (exec never empty, so the instruction -- and the vmcnt count -- is fixed)
     jon[m] = jb < NJ && (prt < NCH - 1 || lane < C::COPYB / 16 - 64 * (NCH - 1));
   }
-  auto issue = [&](int n) {
-    const int it = bid + G * (n / SPI), di = (n % SPI) % KS;
-    int b = it;
-    const int jb = b % njb; b /= njb;
-    const int ti = b % I, tv = b / I;
+  // the item of a step as mixed-radix digits (jb, ti, tv) of it = (tv I + ti) njb + jb,
+  // advanced by G per item with carries: no runtime-divisor division in the
+  // step loop (they were ~2 scalar-ALU instructions per MFMA, PMC profiles/r5/)
+  const int g_jb = G % njb, g_q = G / njb, g_ti = g_q % I, g_tv = g_q / I;
+  auto advance = [&](int& jb, int& ti, int& tv) {
+    jb += g_jb;
+    int c = jb >= njb ? 1 : 0;
+    jb -= c * njb;
+    ti += g_ti + c;
+    c = ti >= I ? 1 : 0;
+    ti -= c * I;
+    tv += g_tv + c;
+  };
+  auto issue = [&](int n, int jb, int ti, int tv) {
+    const int di = (n % SPI) % KS;
     const int ii = ti + di - P;
     const bool iv = n < nsteps && ii >= 0 && ii < I;
     const bf16* xsrc = (X3 && (n % SPI) / KS == 1) ? Xp + xlo : Xp;        // phase 1 reads X_lo
@@ -207,7 +217,8 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
       }
     }
   };
-  issue(0);
+  int c_jb = bid % njb, c_ti = (bid / njb) % I, c_tv = (bid / njb) / I;   // item of the current step
+  issue(0, c_jb, c_ti, c_tv);
 
   // per-lane transposed-read row offsets (h = 0, 1): K row kk = 8 g + 4 h + q of
   // lane (g = l >> 4, q = (l >> 2) & 3, p = l & 3): tap kk, 4 voxels from 4 p,
@@ -239,16 +250,16 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
   f32x4 bv = {0.f, 0.f, 0.f, 0.f};   // this lane's 4 channels' bias, loaded once (not per store)
   if constexpr (EP == EPI1X_BIAS_RELU) bv = *(const f32x4*)(bias + co0);
   for (int n = 0; n < nsteps; ++n) {
-    const int it = bid + G * (n / SPI), di = (n % SPI) % KS;
+    const int di = (n % SPI) % KS;
     const bool last = (n % SPI) == SPI - 1;             // the item's last step (last phase, di = KS - 1)
     const int wset = (X3 && (n % SPI) / KS == 2) ? NT : 0;   // phase 2 multiplies W_lo
-    int b = it;
-    const int jb = b % njb; b /= njb;
-    const int ti = b % I, tv = b / I;
+    const int jb = c_jb, ti = c_ti, tv = c_tv;
     const int j0 = jb * R;
+    int n_jb = c_jb, n_ti = c_ti, n_tv = c_tv;         // item of step n + 1
+    if (last) advance(n_jb, n_ti, n_tv);
     // this step's planes landed (issued one step ago); the previous step's reads are done
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    issue(n + 1);
+    issue(n + 1, n_jb, n_ti, n_tv);
     if constexpr (EP == EPI1X_MASK) {
       // the item's last step: fetch the ReLU mask of its outputs now, so the
       // loads land under this step's MFMAs instead of stalling the epilogue
@@ -286,22 +297,25 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
           constexpr int dhi = s < KS - 1 ? s : KS - 1;   // inclusive
           constexpr int NDJ = dhi - dlo + 1;
           const uint32_t a0 = rowoff[0] + sb + s * C::SLOTB, a1 = rowoff[1] + sb + s * C::SLOTB;
-          u32x4 B[2];
+          // B fragments read PD tiles ahead of their MFMAs (PD = 1: the round-4
+          // schedule; 2: a deeper lookahead for the planes that feed only one or
+          // two output planes, A/B via the c1x_pd tuning switch)
+          u32x4 B[PD + 1];
           auto load_b = [&](auto tc) {
             constexpr int tt = decltype(tc)::value;
-            B[tt & 1] = cat4u(lds_read_tr16u(smem, a0 + tt * NW * 32), lds_read_tr16u(smem, a1 + tt * NW * 32));
+            B[tt % (PD + 1)] = cat4u(lds_read_tr16u(smem, a0 + tt * NW * 32), lds_read_tr16u(smem, a1 + tt * NW * 32));
           };
-          load_b(std::integral_constant<int, 0>{});
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          xstatic_for<0, (PD < MAXT ? PD : MAXT)>([&](auto tc) { load_b(tc); });
+          __builtin_amdgcn_sched_group_barrier(0x100, 2 * (PD < MAXT ? PD : MAXT), 0);
           xstatic_for<0, MAXT>([&](auto tc) {
             constexpr int tt = decltype(tc)::value;
-            if constexpr (tt + 1 < MAXT) load_b(std::integral_constant<int, tt + 1>{});
+            if constexpr (tt + PD < MAXT) load_b(std::integral_constant<int, tt + PD>{});
             xstatic_for<dlo, dhi + 1>([&](auto dc) {
               constexpr int dj = decltype(dc)::value;
-              acc[s - dj][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[dj], __builtin_bit_cast(bf16x8, B[tt & 1]),
-                                                                        acc[s - dj][tt], 0, 0, 0);
+              acc[s - dj][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  A[dj], __builtin_bit_cast(bf16x8, B[tt % (PD + 1)]), acc[s - dj][tt], 0, 0, 0);
             });
-            if constexpr (tt + 1 < MAXT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            if constexpr (tt + PD < MAXT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
             __builtin_amdgcn_sched_group_barrier(0x008, NDJ, 0);
           });
         }
@@ -348,6 +362,7 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
         }
       }
     }
+    c_jb = n_jb; c_ti = n_ti; c_tv = n_tv;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 #endif
@@ -634,7 +649,20 @@ static void c1x_launch(int epi, int V, int I, int J, const bf16* x, const u32x4*
   static_assert(lds <= 160 * 1024, "LDS");
   auto go = [&](auto ec) {
     constexpr int E = decltype(ec)::value;
-    hipLaunchKernelGGL((conv1x16_kernel<KS, R, E, K, L>), grid, block, lds, s, x, w, bias, m, y, V, I, J, nt_store, xlo, ylo);
+    if constexpr (!X3 && KS == 5 && K == 25) {
+      if (tuning().c1x_pd == 2) {
+        hipLaunchKernelGGL((conv1x16_kernel<KS, R, E, K, L, 2>), grid, block, lds, s, x, w, bias, m, y, V, I, J,
+                           nt_store, xlo, ylo);
+        return;
+      }
+      if (tuning().c1x_pd == 3) {
+        hipLaunchKernelGGL((conv1x16_kernel<KS, R, E, K, L, 3>), grid, block, lds, s, x, w, bias, m, y, V, I, J,
+                           nt_store, xlo, ylo);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((conv1x16_kernel<KS, R, E, K, L>), grid, block, lds, s, x, w, bias, m, y, V, I, J, nt_store, xlo,
+                       ylo);
   };
   if constexpr (X3) {
     if ((epi & ~EPI1X_X3) == EPI1X_BIAS_RELU) go(std::integral_constant<int, EPI1X_BIAS_RELU | EPI1X_X3>{});

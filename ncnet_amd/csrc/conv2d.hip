@@ -679,7 +679,7 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
   // profiles/r4/trunk): the N <= 256 convs with a deep K (layer-3 3x3 convs
   // at the training size: 48.7 -> 37.7 us, their reduce 1x1: 27.0 -> 21.9 us)
   const int t256 = cdiv(p.M, 256) * p.tiles_n;
-  const bool big = BN == 128 && (variant == 0 ? t256 >= 384 : (t256 >= 512 || (t256 >= 256 && tuning().conv2d_big)));
+  const bool big = BN == 128 && (variant == 0 ? t256 >= 384 : t256 >= 512);
   // (grids big enough for the 256 x 128 DMA-ring tile keep it: InLoc 3200 px
   // layer 3, 467 us v2 vs 707 us v3)
   const bool v3_auto = variant == 0 && tuning().conv2d_v3 && !big && Cout <= 256 && KH * KW * Cin >= 1024;

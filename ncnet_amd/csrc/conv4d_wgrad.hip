@@ -1052,8 +1052,11 @@ extern "C" int ncnet_wgrad16v3(const void* X, const void* G, float* part, float*
   g.cpg = cdiv(g.ncols, ngroups);
   g.flags = tuning().wgrad_flags;
   if (g.VT > 384) return -1;                // <= 6 chunks per half
-  if (K == L && !tuning().wgrad_v3 && w4_launch(KS, K, dim3((unsigned)(KS * ngroups)), dim3(512), stream,
-                                                 (const bf16*)X, (const bf16*)G, part, partb, g))
+  // the wgrad_v3 A/B switch selects the general kernel only where it can stage the
+  // rows (RW <= 32); ops/neigh_consensus.py wgrad_v3_ntl mirrors the tile rule either way
+  if (K == L && (!tuning().wgrad_v3 || g.RW > 32) &&
+      w4_launch(KS, K, dim3((unsigned)(KS * ngroups)), dim3(512), stream, (const bf16*)X, (const bf16*)G, part,
+                partb, g))
     return (int)hipGetLastError();   // compile-time planes of the training sizes (--image_size 240 / 320 / 400 / 480)
   if (g.RW > 32) return -1;                 // v3: one wave-instruction per staged row
   // wgrad16v3<5, NCH> spills at NCH 3, 4, 6 (256 VGPRs of accumulators and

@@ -17,7 +17,6 @@ from __future__ import annotations
 
 import json
 import math
-import os
 import time
 
 import numpy as np
@@ -36,15 +35,13 @@ def make_adam(params, lr: float) -> torch.optim.Optimizer:
     Default: ``FlatAdam`` (engine/optim.py) -- flat parameter/gradient
     buffers, the gradient buffer doubles as the RCCL bucket, three HIP
     launches per step and an exact asynchronous NaN/Inf step skip.
-    NCNET_ADAM=torch selects torch.optim.Adam (foreach), NCNET_ADAM=fused its
-    fused kernel.  The state_dict layout is torch.optim.Adam's in every case,
-    so checkpoints interchange."""
+    config.RUNTIME.adam (NCNET_ADAM) = 'torch' selects torch.optim.Adam
+    (foreach), 'fused' its fused kernel.  The state_dict layout is
+    torch.optim.Adam's in every case, so checkpoints interchange."""
     from .optim import FlatAdam
 
     params = list(params)
-    kind = os.environ.get("NCNET_ADAM", "flat")
-    if os.environ.get("NCNET_FUSED_ADAM", "0") == "1":
-        kind = "fused"
+    kind = _config.RUNTIME.adam
     if kind == "flat" and params and all(p.dtype == torch.float32 for p in params) \
             and len({p.device for p in params}) == 1:
         return FlatAdam(params, lr=lr)
@@ -77,15 +74,15 @@ class TrunkPrefetcher:
     no backbone parameter is trainable (the reference default,
     ``--fe_finetune_params 0``): the features of batch t+1 must not depend on
     step t's update.  Disabled otherwise, on CPU, and with
-    NCNET_TRUNK_PREFETCH=0; then ``take`` just runs the backbone in place.
+    config.RUNTIME.trunk_prefetch off (NCNET_TRUNK_PREFETCH=0); then ``take``
+    just runs the backbone in place.
     """
 
     def __init__(self, model):
         self.model = model
         dev = next(model.parameters()).device
         fe_trainable = any(p.requires_grad for p in model.FeatureExtraction.parameters())
-        self.enabled = (dev.type == "cuda" and not fe_trainable
-                        and os.environ.get("NCNET_TRUNK_PREFETCH", "1") == "1")
+        self.enabled = dev.type == "cuda" and not fe_trainable and _config.RUNTIME.trunk_prefetch
         self.stream = torch.cuda.Stream(device=dev) if self.enabled else None
         self._pending = None
 
@@ -149,15 +146,9 @@ class Trainer:
             optimizer.guard = nan_guard   # nan_guard=False: FlatAdam applies every step unguarded
         self.metrics_path = metrics_path if ctx.is_main else None
         self.global_step = 0
-        self.fault_step = fault_step if fault_step is not None else int(os.environ.get("NCNET_FAULT_STEP", "-1"))
+        self.fault_step = fault_step if fault_step is not None else _config.RUNTIME.fault_step
         self.prefetch = TrunkPrefetcher(model)
         self.batch_to_device = None       # optional hook: host batch -> device batch (train.py: GPU resize)
-        # NCNET_STEP_PRIORITY: the step's kernels on a high-priority stream, so
-        # the prefetched trunk (default priority) is dispatched only where the
-        # step leaves the chip idle instead of time-slicing its kernels
-        self.hp_stream = None
-        if _config.RUNTIME.step_priority and self.prefetch.enabled:
-            self.hp_stream = torch.cuda.Stream(device=ctx.device, priority=-1)
 
     def _move(self, batch):
         if self.batch_to_device is not None:
@@ -178,34 +169,19 @@ class Trainer:
 
     def train_step(self, batch, next_batch=None) -> torch.Tensor:
         """One step on ``batch``; ``next_batch`` (already on the device) gets
-        its backbone pass queued behind this step (TrunkPrefetcher)."""
-        if self.hp_stream is None:
-            return self._train_step(batch, next_batch)
-        cur = torch.cuda.current_stream(self.hp_stream.device)
-        self.hp_stream.wait_stream(cur)
-        with torch.cuda.stream(self.hp_stream):
-            loss = self._train_step(batch, next_batch)
-        cur.wait_stream(self.hp_stream)
-        loss.record_stream(cur)
-        return loss
-
-    def _train_step(self, batch, next_batch=None) -> torch.Tensor:
+        its backbone pass queued with this step's forward (TrunkPrefetcher: it
+        fills the CUs the forward's kernels leave idle; queued later it only
+        competes with the backward's two streams, measured in round 4)."""
         if self.fault_step >= 0 and self.global_step == self.fault_step:
             raise RuntimeError(f"injected fault at step {self.global_step} (NCNET_FAULT_STEP)")
         self.opt.zero_grad(set_to_none=True)
         self.bucket.reset()
-        at = _config.RUNTIME.prefetch_at
         with segment("forward"):
             feats = self.prefetch.take(batch)
-            if at == 0:
-                self.prefetch.submit(next_batch)
+            self.prefetch.submit(next_batch)
             loss = weak_loss_from_features(self.model, feats, self.normalization)
         with segment("backward"):
-            if at == 1:
-                self.prefetch.submit(next_batch)
             loss.backward()
-            if at >= 2:
-                self.prefetch.submit(next_batch)
         if self.flat and self.nan_guard:
             # loss-finite indicator rides in the gradient bucket: every rank's
             # FlatAdam then skips the same (globally non-finite) step, with no host sync

@@ -19,6 +19,7 @@ import os
 import numpy as np
 import torch
 
+from .. import config as _config
 from ..data.transforms import normalize_image, resize_bilinear
 from ..ops.neigh_consensus import pin_fp8_weights
 from ..ops import _ext
@@ -198,7 +199,7 @@ class PairMatcher:
                  use_graph: bool | None = None):
         self.model, self.k = model, k_size
         self.kw = dict(do_softmax=do_softmax, both_dirs=both_dirs, flip=flip)
-        self.use_graph = (os.environ.get("NCNET_PAIR_GRAPH", "1") != "0") if use_graph is None else use_graph
+        self.use_graph = _config.RUNTIME.pair_graph if use_graph is None else use_graph
         self._graphs = {}
         self._nc_params = None
         self.capture_error = None

@@ -311,15 +311,15 @@ class FrozenResNetPlan(nn.Module):
             else:
                 raise TypeError(f"FrozenResNetPlan: unsupported module {type(m).__name__}")
         self._keep = keep
-        import os
-        self.use_graphs = os.environ.get("NCNET_TRUNK_GRAPH", "1") != "0"
+        from .. import config as _config
+        self.use_graphs = _config.RUNTIME.trunk_graph
         # "native": NHWC implicit-GEMM HIP kernels with fused bias/residual/ReLU
         # (csrc/conv2d.hip); "blas": hipBLASLt 1x1 GEMMs + MIOpen 3x3 + bias_act;
         # "auto" (default): native, except each bottleneck's first 1x1 conv
         # (bias + ReLU, no residual) goes to hipBLASLt's fused-epilogue GEMM
         # where that measured faster for this input shape (timed once per shape
         # in the eager warm-up before the graph capture)
-        self.conv_mode = os.environ.get("NCNET_TRUNK_CONV", "auto")
+        self.conv_mode = _config.RUNTIME.trunk_conv
         self._graphs = {}
         self._tuned = {}
 
@@ -556,8 +556,8 @@ class FrozenResNetPlanX3(nn.Module):
                 pass
             else:
                 raise TypeError(f"FrozenResNetPlanX3: unsupported module {type(m).__name__}")
-        import os
-        self.use_graphs = os.environ.get("NCNET_TRUNK_GRAPH", "1") != "0"
+        from .. import config as _config
+        self.use_graphs = _config.RUNTIME.trunk_graph
         self._graphs = {}
 
     @staticmethod

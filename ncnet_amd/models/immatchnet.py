@@ -15,7 +15,6 @@ Compute policy (MI355X):
 from __future__ import annotations
 
 import importlib
-import os
 from collections import OrderedDict
 
 import torch
@@ -37,11 +36,7 @@ _ext_count = _ext_mod.count
 from ..utils.timing import segment
 from .backbones import FrozenResNetPlan, FrozenResNetPlanX3, build_trunk, fold_frozen_bn
 
-# Frozen bf16 trunk: pre-cast execution plan (default) or autocast (NCNET_TRUNK_PLAN=0).
-_TRUNK_PLAN = os.environ.get("NCNET_TRUNK_PLAN", "1") != "0"
-# fp32 trunk (nc_precision / corr_dtype 'fp32') as the bf16x3 plan (default) or
-# MIOpen fp32 convs (NCNET_TRUNK_X3=0)
-_TRUNK_X3 = os.environ.get("NCNET_TRUNK_X3", "1") != "0"
+from .. import config as _config
 
 
 def _ext_available() -> bool:
@@ -82,6 +77,10 @@ class FeatureExtraction(nn.Module):
             self.model = self.model.cuda()
         self._folded = None
         self._folded_version = None
+        # the fp32 frozen trunk: 'x3' (bf16x3 plan, ~2^-16 relative, the fp32-accurate
+        # training mode) or 'miopen' (true fp32, the reference's evaluation numerics);
+        # ImMatchNet sets it from nc_precision / corr_dtype, config.RUNTIME.trunk_fp32 overrides
+        self.fp32_trunk = "miopen"
 
     def trunk_forward(self, images: torch.Tensor, dtype: torch.dtype | None = None) -> torch.Tensor:
         """Raw (un-normalised) trunk features, channels-last on GPU."""
@@ -90,9 +89,11 @@ class FeatureExtraction(nn.Module):
         if x.is_cuda:
             x = x.contiguous(memory_format=torch.channels_last)
         if frozen and not self.training and x.is_cuda and self.feature_extraction_cnn.startswith("resnet"):
-            if dtype in (torch.bfloat16, torch.float16) and _TRUNK_PLAN:
+            rt = _config.RUNTIME
+            if dtype in (torch.bfloat16, torch.float16) and rt.trunk_plan:
                 return self._plan(dtype)(x)
-            if dtype == torch.float32 and _TRUNK_PLAN and _TRUNK_X3 and _ext_available():
+            x3 = rt.trunk_fp32 == "x3" or (rt.trunk_fp32 == "auto" and self.fp32_trunk == "x3")
+            if dtype == torch.float32 and rt.trunk_plan and x3 and _ext_available():
                 # fp32-accurate trunk as bf16x3 splits on the native MFMA convs
                 return self._plan(torch.float32)(x)
             net = self._folded_trunk()
@@ -112,7 +113,7 @@ class FeatureExtraction(nn.Module):
 
     def _plan(self, dtype):
         ver = sum(p._version for p in self.model.parameters()) + sum(b._version for b in self.model.buffers())
-        key = (ver, dtype, _TRUNK_PLAN)
+        key = (ver, dtype)
         if getattr(self, "_plan_key", None) != key:
             if dtype == torch.float32:
                 self._plan_obj = FrozenResNetPlanX3(self._folded_trunk())
@@ -268,6 +269,10 @@ class ImMatchNet(nn.Module):
                                                    feature_extraction_model_file=feature_extraction_model_file or "",
                                                    last_layer=feature_extraction_last_layer,
                                                    normalization=normalize_features, use_cuda=self.use_cuda)
+        # fp32-accurate training runs its frozen trunk as bf16x3 splits (3x the bf16
+        # MFMA work instead of MIOpen's fp32 convs at 1/16 of the bf16 rate); fp32
+        # inference (corr_dtype='fp32', parity runs) keeps MIOpen's true fp32
+        self.FeatureExtraction.fp32_trunk = "x3" if nc_precision == "fp32" else "miopen"
         self.FeatureCorrelation = FeatureCorrelation(shape="4D", normalization=False)
         self.NeighConsensus = NeighConsensus(use_cuda=self.use_cuda, kernel_sizes=list(ncons_kernel_sizes),
                                              channels=list(ncons_channels))

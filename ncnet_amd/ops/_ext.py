@@ -4,16 +4,17 @@ Dispatch policy (used by every op in ``ncnet_amd.ops``):
 
 * GPU tensors run the hand-written gfx950 kernels.  If the extension cannot be
   imported on a machine with a GPU the op raises -- there is no silent eager
-  fallback (set ``NCNET_ALLOW_TORCH_FALLBACK=1`` to opt into the PyTorch
+  fallback (``NCNET_ALLOW_TORCH_FALLBACK=1`` / config.RUNTIME.allow_torch_fallback opts into the PyTorch
   oracle path explicitly, e.g. for A/B debugging).
 * CPU tensors run the pure-PyTorch oracles in ``ncnet_amd.ops.reference``.
 """
 from __future__ import annotations
 
 import collections
-import os
 
 import torch
+
+from .. import config as _config
 
 _C = None
 _ERR: Exception | None = None
@@ -26,12 +27,24 @@ def load():
     try:
         import importlib
 
-        variant = os.environ.get("NCNET_EXT", "release")   # build variants: ncnet_amd/build.py
+        variant = _config.RUNTIME.ext_variant   # build variants: ncnet_amd/build.py
         name = "ncnet_amd._C" if variant in ("", "release") else f"ncnet_amd._C_{variant}"
         _C = importlib.import_module(name)
     except Exception as e:  # pragma: no cover - depends on the build state
         _ERR = e
+    apply_tuning()
     return _C
+
+
+def apply_tuning() -> None:
+    """Push config.RUNTIME's launcher tuning fields into the extension's
+    process-wide table (csrc/common.h NcnetTuning; the C++ side reads no
+    environment)."""
+    m = _C
+    if m is None or not hasattr(m, "set_tuning"):
+        return
+    for k, v in _config.RUNTIME.tuning().items():
+        m.set_tuning(k, int(v))
 
 
 def available() -> bool:
@@ -39,14 +52,14 @@ def available() -> bool:
 
 
 def fallback_allowed() -> bool:
-    return os.environ.get("NCNET_ALLOW_TORCH_FALLBACK", "0") == "1"
+    return _config.RUNTIME.allow_torch_fallback
 
 
 def use_hip(t: torch.Tensor) -> bool:
     """True when ``t`` must go through the HIP kernels."""
     if not t.is_cuda:
         return False
-    if fallback_allowed() and os.environ.get("NCNET_FORCE_TORCH", "0") == "1":
+    if fallback_allowed() and _config.RUNTIME.force_torch:
         return False
     if load() is None:
         if fallback_allowed():

@@ -33,7 +33,7 @@ def _row_col_stats(x3: torch.Tensor, norm: int):
     carg = torch.empty((V, Cc), dtype=torch.int32, device=x3.device)
     sum_kind = {1: 1, 2: 2, 0: 0}[norm]
     # one pass for both directions when rows are 16-byte multiples (stats2d)
-    if not (_config.STATS2D and C.stats2d(x3, rmax, rarg, rse, cmax, carg, cse, sum_kind)):
+    if not (_config.RUNTIME.stats2d and C.stats2d(x3, rmax, rarg, rse, cmax, carg, cse, sum_kind)):
         C.stats_rows(x3, rmax, rarg, rse if sum_kind else None, sum_kind)
         C.stats_cols(x3, cmax, carg, cse if sum_kind else None, sum_kind)
     if not sum_kind:

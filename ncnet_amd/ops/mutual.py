@@ -28,7 +28,7 @@ def _stats(c3: torch.Tensor):
     cmax = torch.empty((V, Cc), dtype=torch.float32, device=c3.device)
     carg = torch.empty((V, Cc), dtype=torch.int32, device=c3.device)
     # both maxima in one pass over the volume (stats2d) when rows are 16-byte multiples
-    if not (_config.STATS2D and C.stats2d(c3, rmax, rarg, None, cmax, carg, None, 0)):
+    if not (_config.RUNTIME.stats2d and C.stats2d(c3, rmax, rarg, None, cmax, carg, None, 0)):
         C.stats_rows(c3, rmax, rarg, None, 0)
         C.stats_cols(c3, cmax, carg, None, 0)
     return rmax, rarg, cmax, carg
@@ -63,7 +63,7 @@ class MutualMatchingFn(torch.autograd.Function):
         c3, rmax, rarg, cmax, carg = ctx.saved_tensors
         g3 = g.reshape(c3.shape).float().contiguous()
         gc = torch.empty_like(c3)
-        _ext.ext().mm_bwd(c3, g3, rmax, rarg, cmax, carg, gc, EPS, _config.STATS2D)   # one pass for both sums
+        _ext.ext().mm_bwd(c3, g3, rmax, rarg, cmax, carg, gc, EPS, _config.RUNTIME.stats2d)   # one pass for both sums
         return gc.reshape(ctx.shape), None
 
 

@@ -28,13 +28,12 @@ MI355X design:
 * ``y = z1 + z2^T`` (the branch un-swap) and, in backward, its transpose plus
   the last layer's ReLU mask are single tiled kernels.
 There is no silent PyTorch fallback on the GPU: a configuration without HIP
-kernels (even kernel sizes) raises unless NCNET_ALLOW_TORCH_FALLBACK=1.
+kernels (even kernel sizes) raises unless config.RUNTIME.allow_torch_fallback
+(NCNET_ALLOW_TORCH_FALLBACK=1).
 """
 from __future__ import annotations
 
 import functools
-import os
-import os as _os
 
 import numpy as np
 import torch
@@ -86,19 +85,22 @@ def wgrad_v3_ok(shape, ks: int) -> bool:
 
 def wgrad_v3_ntl(K: int, L: int, ks: int) -> int:
     """(k, l) tiles per plane of wgrad16v3 / v4 (mirrors ncnet_wgrad16v3): ~320
-    voxels per tile; on the k = 5 fallback kernel, more tiles until the 64-voxel
-    chunk count per half-tile is 1, 2 or 5 (the instantiations that do not spill)."""
+    voxels per tile; on the k = 5 general kernel, more tiles until the 64-voxel
+    chunk count per half-tile is 1, 2 or 5 (the instantiations that do not spill).
+    The general kernel runs where no v4 plane exists or when the wgrad_v3 A/B
+    switch asks for it and the rows fit (L + ks - 1 <= 32)."""
     kl = K * L
     ntl = -(-kl // 320)
-    if ks == 5 and not (K == L and K in _V4_PLANES[5]):
+    v4 = K == L and K in _V4_PLANES[ks] and not (_config.RUNTIME.wgrad_v3 and L + ks - 1 <= 32)
+    if ks == 5 and not v4:
         while (-(-(-(-kl // ntl)) // 64)) not in (1, 2, 5):
             ntl += 1
     return ntl
 
 
 # workgroups of the 16 -> 16 weight gradient (grid = groups * ks; partials 2 *
-# groups x 160 K floats, summed afterwards); NCNET_WGRAD_WG (A/B)
-_WGRAD_WG_TARGET = int(os.environ.get("NCNET_WGRAD_WG", "512"))
+# groups x 160 K floats, summed afterwards); other targets measured within noise
+_WGRAD_WG_TARGET = 512
 
 
 def wgrad_v3_groups(shape, ks: int) -> int:
@@ -419,20 +421,17 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list, xp=None, shp=None, p
 
 
 # Weight gradients of the layers after the first on a second HIP stream
-# (NCNET_BWD_OVERLAP=0 disables, read by config.RUNTIME): they depend only on the layer input and the
+# (config.RUNTIME.bwd_overlap, NCNET_BWD_OVERLAP=0 disables): they depend only on the layer input and the
 # incoming gradient, so wgrad(l) runs while the data-gradient chain continues
 # on the main stream (dgrad(l) -> dgrad(l-1) -> ...).  The first layer's
 # weight gradient stays on the main stream, which is idle by then.
-BWD_OVERLAP = _config.RUNTIME.bwd_overlap
 _SIDE_STREAMS: dict = {}
 
 
 def _side_stream(dev: torch.device):
     st = _SIDE_STREAMS.get(dev.index)
     if st is None:
-        # with NCNET_STEP_PRIORITY the whole training step runs at high priority
-        # (engine/trainer.py), its weight-gradient side stream too
-        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev, priority=-1 if _config.RUNTIME.step_priority else 0)
+        st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
     return st
 
 
@@ -523,7 +522,7 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
     g = g_last
     gx0 = None
     main = side = None
-    if BWD_OVERLAP and g_last.is_cuda:
+    if _config.RUNTIME.bwd_overlap and g_last.is_cuda:
         main = torch.cuda.current_stream(g_last.device)
         side = _side_stream(g_last.device)
     for li in range(nl - 1, -1, -1):
@@ -1125,7 +1124,7 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
         dws, dbs = [None] * nl, [None] * nl
         gx = None
         main = side = None
-        if BWD_OVERLAP and z.is_cuda:
+        if _config.RUNTIME.bwd_overlap and z.is_cuda:
             main = torch.cuda.current_stream(dev)
             side = _side_stream(dev)
         for li in range(nl - 1, -1, -1):
@@ -1307,7 +1306,6 @@ def neigh_consensus_fp8(x: torch.Tensor, weights, biases, kinds, symmetric: bool
 # Fused InLoc NC (csrc/nc_fused.hip): kernel sizes (3, 3), channels (<=16, 1),
 # inference.  The hidden activation stays in LDS; HBM sees the input and the
 # output volume once.  NCNET_NC_FUSED=0 falls back to the layer-by-layer path.
-FUSED = _config.RUNTIME.nc_fused
 _FUSED_LDS = 80 * 1024          # two workgroups per CU (160 KB LDS)
 
 
@@ -1391,7 +1389,7 @@ def fused_applies(x: torch.Tensor, weights, channels, fp8: bool = False, precisi
     kernel_sizes = [w.shape[0] for w in weights]
     kinds = layer_kinds(channels, kernel_sizes)
     return (x.is_cuda and _ext.use_hip(x) and kinds is not None and precision != "fp32"
-            and _fused_ok(kinds, kernel_sizes, channels, x) and not (fp8 and _os.environ.get("NCNET_NC_FP8") == "1"))
+            and _fused_ok(kinds, kernel_sizes, channels, x) and not (fp8 and _config.RUNTIME.nc_fp8))
 
 
 def neigh_consensus_fused(x: torch.Tensor, weights, biases, symmetric: bool = True) -> torch.Tensor:
@@ -1420,7 +1418,7 @@ def neigh_consensus_fused(x: torch.Tensor, weights, biases, symmetric: bool = Tr
 
 
 def _fused_ok(kinds, kernel_sizes, channels, x) -> bool:
-    return (FUSED and not torch.is_grad_enabled() and list(kinds) == ["1in", "1out"] and channels[0] <= 16
+    return (_config.RUNTIME.nc_fused and not torch.is_grad_enabled() and list(kinds) == ["1in", "1out"] and channels[0] <= 16
             and list(kernel_sizes) == [3, 3] and x.shape[2] * x.shape[3] * x.shape[4] * x.shape[5] < 2 ** 30)
 
 
@@ -1436,7 +1434,7 @@ def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool 
     Returns [V, C_last, I, J, K, L] fp32.
 
     On the GPU: the (3,3)/(<=16,1) inference stack runs on the fused kernel
-    (hidden layer in LDS; also in fp8 mode unless NCNET_NC_FP8=1); ``fp8``
+    (hidden layer in LDS; also in fp8 mode unless config.RUNTIME.nc_fp8); ``fp8``
     (inference, other ``fp8_ok`` stacks) on the fp8 MFMA Conv4d kernels; ``precision='fp32'`` (inference) on the bf16x3
     kernels (fp32-accurate); everything else with odd kernel sizes <= 7 and
     any channel counts on the bf16 autograd stack.  ``_ext.DISPATCH`` records
@@ -1466,7 +1464,7 @@ def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool 
             # applies -- measured faster at InLoc 3200 px (5.5 vs 7.3 ms per pair:
             # the fused kernel never writes the hidden volume) -- unless
             # NCNET_NC_FP8=1 asks for the all-fp8 pipeline
-            if _fused_ok(kinds, kernel_sizes, channels, x) and not (fp8 and _os.environ.get("NCNET_NC_FP8") == "1"):
+            if _fused_ok(kinds, kernel_sizes, channels, x) and not (fp8 and _config.RUNTIME.nc_fp8):
                 _ext.count("nc_fused_k3")
                 return neigh_consensus_fused(x.float().contiguous(), weights, biases, symmetric)
             if fp8 and not torch.is_grad_enabled() and fp8_ok(kinds, channels):

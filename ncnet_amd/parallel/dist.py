@@ -52,7 +52,8 @@ def wants_process_group(world: int) -> bool:
     stays collective-free."""
     if world > 1:
         return True
-    if os.environ.get("NCNET_FORCE_PG", "0") == "1":
+    from .. import config as _config
+    if _config.RUNTIME.force_pg:
         return True
     return bool(os.environ.get("TORCHELASTIC_RUN_ID"))
 
@@ -62,11 +63,12 @@ def init_distributed(device: str | None = None, timeout_s: int | None = None) ->
     MASTER_*).  Without a launcher (``wants_process_group`` False) this is a
     single-process context with no process group.
 
-    ``timeout_s`` (default NCNET_PG_TIMEOUT_S or 600) is the rank-failure
+    ``timeout_s`` (default config.RUNTIME.pg_timeout_s: NCNET_PG_TIMEOUT_S or 600) is the rank-failure
     detector: a collective that a dead or hung rank never joins raises on the
     surviving ranks after that many seconds instead of hanging forever."""
+    from .. import config as _config
     if timeout_s is None:
-        timeout_s = int(os.environ.get("NCNET_PG_TIMEOUT_S", "600"))
+        timeout_s = _config.RUNTIME.pg_timeout_s
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -80,9 +82,9 @@ def init_distributed(device: str | None = None, timeout_s: int | None = None) ->
     if wants_process_group(world):
         os.environ.setdefault("MASTER_PORT", "29500")
         backend = "nccl" if use_gpu else "gloo"
-        # NCNET_DIST_BACKEND=gloo: rehearse the multi-rank GPU path with several
-        # ranks on ONE card (RCCL refuses two ranks per device)
-        backend = os.environ.get("NCNET_DIST_BACKEND", backend)
+        # config.RUNTIME.dist_backend (NCNET_DIST_BACKEND=gloo): rehearse the multi-rank
+        # GPU path with several ranks on ONE card (RCCL refuses two ranks per device)
+        backend = _config.RUNTIME.dist_backend or backend
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
             kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))

@@ -30,6 +30,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
+from ncnet_amd import config as _config  # noqa: E402
 from ncnet_amd.eval.inloc import n_matches, pair_matches, target_size  # noqa: E402
 from ncnet_amd.models import ImMatchNet  # noqa: E402
 from ncnet_amd.ops.correlation import correlation, correlation_pool2  # noqa: E402
@@ -65,7 +66,7 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
     fp8 = precision == "fp8"
     h, w = target_size(src_hw[0], src_hw[1], image_size, k)
     if pair_graph is None:
-        pair_graph = panos_per_query > 1 and os.environ.get("NCNET_PAIR_GRAPH", "1") != "0"
+        pair_graph = panos_per_query > 1 and _config.RUNTIME.pair_graph
     src = torch.randn(1, 3, h, w, device=dev)
     tgt = torch.randn(1, 3, h, w, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
@@ -180,7 +181,7 @@ def run_single(image_size: int = 1600, fp8: bool = False, pairs: int = 5, warmup
         "pairs_per_s": round(1e3 / ms, 3), "n_gpus": 1, "pairs": pairs, "warmup": warmup,
         "impl": impl,
         "dtype": ("fp32-backbone/fp16-volume" if impl == "reference" else
-                  (("fp8-corr+fp8-nc" if os.environ.get("NCNET_NC_FP8") == "1" else "fp8-corr+bf16-fused-nc")
+                  (("fp8-corr+fp8-nc" if _config.RUNTIME.nc_fp8 else "fp8-corr+bf16-fused-nc")
                    if fp8 else precision)),
         "data": "synthetic (random 4:3 images, random-init weights)",
         "config": {"image": [h, w], "features": [h // 16, w // 16], "volume": list(fs) * 2,

@@ -47,7 +47,7 @@ def main():
               ("l2.n1", 2, 512, 128, 1, 1, 2), ("l2.n2", 2, 128, 128, 3, 1, 2), ("l2.n3", 2, 128, 512, 1, 1, 2),
               ("l3.n1", 3, 1024, 256, 1, 1, 3), ("l3.n2", 3, 256, 256, 3, 1, 3), ("l3.n3", 3, 256, 1024, 1, 1, 3),
               ("l3.nd", 3, 512, 1024, 1, 2, 2), ("l3.n2s", 3, 256, 256, 3, 2, 2)]
-    print(f"{'layer':8s} {'M':>8s} {'N':>5s} {'K':>5s}  {'native v1':>16s}  {'native v2':>16s}  {'v2 big':>16s}"
+    print(f"{'layer':8s} {'M':>8s} {'N':>5s} {'K':>5s}  {'native v1':>16s}  {'native v2':>16s}"
           f"  {'v3 (chip round)':>16s}  {'auto':>16s}  {'hipBLASLt/MIOpen':>18s}")
     for name, _, cin, cout, k, s, lin in shapes:
         H, W = hw[lin]
@@ -63,9 +63,6 @@ def main():
         t_1 = timeit(run)
         C.set_tuning("conv2d_variant", 2)
         t_n = timeit(run)
-        C.set_tuning("conv2d_big", 1)
-        t_b = timeit(run)
-        C.set_tuning("conv2d_big", 0)
         C.set_tuning("conv2d_variant", 3)
         t_3 = timeit(run)
         C.set_tuning("conv2d_variant", 0)
@@ -79,7 +76,7 @@ def main():
             wb = w
             t_o = timeit(lambda: torch.relu_(torch.nn.functional.conv2d(x, wb, b.to(torch.bfloat16), s, k // 2)))
         print(f"{name:8s} {M:8d} {cout:5d} {K:5d}  {t_1 * 1e3:7.1f} us {fl / t_1 / 1e9:5.0f} TF  "
-              f"{t_n * 1e3:7.1f} us {fl / t_n / 1e9:5.0f} TF  {t_b * 1e3:7.1f} us {fl / t_b / 1e9:5.0f} TF  "
+              f"{t_n * 1e3:7.1f} us {fl / t_n / 1e9:5.0f} TF  "
               f"{t_3 * 1e3:7.1f} us {fl / t_3 / 1e9:5.0f} TF  {t_a * 1e3:7.1f} us {fl / t_a / 1e9:5.0f} TF  "
               f"{t_o * 1e3:7.1f} us {fl / t_o / 1e9:5.0f} TF", flush=True)
 

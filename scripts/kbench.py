@@ -21,20 +21,17 @@ from ncnet_amd.ops.neigh_consensus import wgrad_groups, wgrad_plane_groups, wgra
 from ncnet_amd.ops.packing import ij_groups, ij_in_weights, ij_out_weights, pack_w16, pack_w16_planes  # noqa: E402
 
 
-_TUNING = {"NCNET_CONV_V3": "conv_v3", "NCNET_WGRAD_V3": "wgrad_v3", "NCNET_GP_TPW": "gp_tpw",
+_TUNING = {"NCNET_C1X_PD": "c1x_pd", "NCNET_CONV_V3": "conv_v3", "NCNET_WGRAD_V3": "wgrad_v3", "NCNET_GP_TPW": "gp_tpw",
            "NCNET_NT_STORE": "nt_store", "NCNET_WGRAD_FLAGS": "wgrad_flags"}
 
 
 def with_env(key, val, fn):
     """Run fn with launcher tuning switch ``key`` (its NCNET_* name) set to val
-    (the set_tuning binding; the launchers never read the environment)."""
+    (config.override: the launchers never read the environment)."""
     def run():
-        C = _ext.ext()
-        old = C.set_tuning(_TUNING[key], int(val))
-        try:
+        from ncnet_amd import config
+        with config.override(**{_TUNING[key]: int(val)}):
             fn()
-        finally:
-            C.set_tuning(_TUNING[key], old)
     return run
 
 
@@ -129,6 +126,12 @@ def main():
         "pad_planes_t": (lambda: C.pad_planes(x1.reshape(V, S * S, S * S), xpad, S, S, ks, 1), None),
         "conv1x16_fwd": (lambda: C.conv1x16(xpad, w1x, b16, None, y16, ks, 1), fl1),
         "conv1x16_dgrad": (lambda: C.conv1x16(xpad, w1x, None, x16, y16, ks, 2), fl1),
+        "conv1x16_fwd_pd2": (with_env("NCNET_C1X_PD", "2", lambda: C.conv1x16(xpad, w1x, b16, None, y16, ks, 1)), fl1),
+        "conv1x16_dgrad_pd2": (with_env("NCNET_C1X_PD", "2", lambda: C.conv1x16(xpad, w1x, None, x16, y16, ks, 2)),
+                               fl1),
+        "conv1x16_fwd_pd3": (with_env("NCNET_C1X_PD", "3", lambda: C.conv1x16(xpad, w1x, b16, None, y16, ks, 1)), fl1),
+        "conv1x16_dgrad_pd3": (with_env("NCNET_C1X_PD", "3", lambda: C.conv1x16(xpad, w1x, None, x16, y16, ks, 2)),
+                               fl1),
         "wgrad1x16": (lambda: C.wgrad1x16(g16, xpad, p1x, p1xb, ks), fl1),
         "wgrad1x16_nobias": (lambda: C.wgrad1x16(x16, xpad, p1x, None, ks), fl1),
         "ij_1in_conv": (lambda: C.conv16_fwd(xs, wij, b16, None, y16, ks, 1), fl1),

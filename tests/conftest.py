@@ -9,6 +9,25 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def set_runtime(monkeypatch, **fields):
+    """Switch ncnet_amd.config.RUNTIME fields for one test (the op modules read
+    the configuration at call time; launcher tuning goes to the extension)."""
+    import dataclasses
+    from ncnet_amd import config
+    monkeypatch.setattr(config, "RUNTIME", dataclasses.replace(config.RUNTIME, **fields))
+    from ncnet_amd.ops import _ext
+    _ext.apply_tuning()
+
+
+@pytest.fixture
+def runtime(monkeypatch):
+    """``runtime(nc_fp8=True)`` inside a test: see set_runtime."""
+    yield lambda **kw: set_runtime(monkeypatch, **kw)
+    from ncnet_amd.ops import _ext
+    monkeypatch.undo()
+    _ext.apply_tuning()
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP kernels)")
     config.addinivalue_line("markers", "slow: long-running test")
@@ -42,16 +61,11 @@ def _ncnet_debug_kernel_checks(request):
 
 
 @pytest.fixture
-def tune():
-    """tune(name, value): set a launcher tuning switch (csrc/common.h
-    NcnetTuning, the set_tuning binding) for this test; restored afterwards."""
+def tune(monkeypatch):
+    """tune(name, value): set a launcher tuning field of config.RUNTIME (pushed
+    into csrc/common.h NcnetTuning by the set_tuning binding) for this test;
+    restored afterwards."""
     from ncnet_amd.ops import _ext
-    saved = {}
-
-    def set_(name, value):
-        old = _ext.ext().set_tuning(name, int(value))
-        saved.setdefault(name, old)
-
-    yield set_
-    for k, v in saved.items():
-        _ext.ext().set_tuning(k, v)
+    yield lambda name, value: set_runtime(monkeypatch, **{name: int(value)})
+    monkeypatch.undo()
+    _ext.apply_tuning()

@@ -99,7 +99,8 @@ def test_pair_matcher_graph_equals_eager(nc_fp8, monkeypatch):
     try:
         _train_one_step_like_bench()
         if nc_fp8:
-            monkeypatch.setenv("NCNET_NC_FP8", "1")
+            from tests.conftest import set_runtime
+            set_runtime(monkeypatch, nc_fp8=True)
         torch.manual_seed(3)
         m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], relocalization_k_size=2,
                        half_precision=True, corr_dtype="fp8" if nc_fp8 else "bf16").cuda().eval()

@@ -223,13 +223,13 @@ def test_conv4d_autograd(cin, cout, ks):
     assert relerr(b.grad, br.grad) < 1e-3
 
 
-def test_conv4d_even_kernel_raises_without_opt_in(monkeypatch):
+def test_conv4d_even_kernel_raises_without_opt_in(runtime):
     """No silent fallback: k = 4 has no HIP kernel, so the GPU op raises unless
     NCNET_ALLOW_TORCH_FALLBACK=1 opts into the PyTorch reference."""
     from ncnet_amd.ops.conv4d import conv4d
     x = torch.rand(1, 16, 4, 4, 4, 4, device=DEV)
     w = torch.randn(4, 16, 16, 4, 4, 4, device=DEV) * 0.05
-    monkeypatch.delenv("NCNET_ALLOW_TORCH_FALLBACK", raising=False)
+    runtime(allow_torch_fallback=False)
     with pytest.raises(NotImplementedError):
         conv4d(x, w, None, permute_filters=False)
 
@@ -596,12 +596,12 @@ def test_conv16_fp8_kernel(ks, shape):
     assert relerr(z, zr) < 1e-4
 
 
-def test_immatchnet_fp8_nc_path(monkeypatch):
+def test_immatchnet_fp8_nc_path(runtime):
     """corr_dtype='fp8' (fp8 correlation + fp8 Conv4d NC kernels, forced with
-    NCNET_NC_FP8=1: by default this (3,3)/(16,1) stack takes the faster fused
+    config nc_fp8 (NCNET_NC_FP8=1): by default this (3,3)/(16,1) stack takes the faster fused
     bf16 NC kernel) vs the bf16 path; the dispatch counters prove which NC
     implementation ran."""
-    monkeypatch.setenv("NCNET_NC_FP8", "1")
+    runtime(nc_fp8=True)
     from ncnet_amd.models import ImMatchNet
     torch.manual_seed(0)
     m = ImMatchNet(use_cuda=True, ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1],
@@ -620,7 +620,7 @@ def test_immatchnet_fp8_nc_path(monkeypatch):
         assert _ext.DISPATCH["nc_fp8"] == n_fp8 + 1                # fp8: the fp8 MFMA Conv4d path
     assert c8.shape == c16.shape
     assert rel_l2(c8, c16) < 0.15
-    monkeypatch.delenv("NCNET_NC_FP8")
+    runtime(nc_fp8=False)
     with torch.inference_mode():
         n_fused = _ext.DISPATCH["nc_fused_k3"]
         c8f, _ = m(batch)                                         # default fp8 mode: fp8 correlation + fused NC
@@ -787,8 +787,8 @@ def _pipeline_run(monkeypatch, prefetch: bool, overlap: bool, steps: int = 3):
 
     nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")   # the module, not the re-exported function
 
-    monkeypatch.setenv("NCNET_TRUNK_PREFETCH", "1" if prefetch else "0")
-    monkeypatch.setattr(nc, "BWD_OVERLAP", overlap)
+    from tests.conftest import set_runtime
+    set_runtime(monkeypatch, trunk_prefetch=prefetch, bwd_overlap=overlap)
     torch.manual_seed(0)
     model = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1], dtype="bf16").to(DEV)
     model.train()

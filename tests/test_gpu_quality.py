@@ -86,7 +86,8 @@ def deterministic_trunk(monkeypatch):
     """Pin the operating point: native trunk kernels only (no per-shape
     timing-based hipBLASLt choice) and no MIOpen benchmark-mode solver search
     for the stem, whatever earlier tests in the session switched on."""
-    monkeypatch.setenv("NCNET_TRUNK_CONV", "native")
+    from tests.conftest import set_runtime
+    set_runtime(monkeypatch, trunk_conv="native")
     old = torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic
     torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = False, True
     yield

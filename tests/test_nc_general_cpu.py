@@ -114,14 +114,14 @@ def test_conv4d_module_matches_oracle(emu, cin, cout, ks):
     assert max(errs.values()) < 2e-2, errs
 
 
-def test_even_kernel_raises_on_gpu_policy(monkeypatch):
+def test_even_kernel_raises_on_gpu_policy(runtime):
     """No silent fallback: an even kernel size has no HIP kernel; the GPU
     dispatcher must raise unless NCNET_ALLOW_TORCH_FALLBACK=1."""
     assert layer_kinds([16, 1], [4, 3]) is None
-    monkeypatch.delenv("NCNET_ALLOW_TORCH_FALLBACK", raising=False)
+    runtime(allow_torch_fallback=False)
     with pytest.raises(NotImplementedError):
         _ext.torch_fallback("test")
-    monkeypatch.setenv("NCNET_ALLOW_TORCH_FALLBACK", "1")
+    runtime(allow_torch_fallback=True)
     before = _ext.DISPATCH["torch_fallback"]
     _ext.torch_fallback("test")
     assert _ext.DISPATCH["torch_fallback"] == before + 1

@@ -35,7 +35,7 @@ def _variant_module():
 
 def _dummy(kind: str):
     if "Sequence" in kind:
-        return [0.5, 0.5, 0.5]
+        return [3, 3, 3] if "SupportsInt" in kind else [0.5, 0.5, 0.5]
     if "Tensor" in kind:
         return None if "None" in kind else torch.zeros(16, dtype=torch.bfloat16)
     if "SupportsFloat" in kind:

@@ -45,9 +45,41 @@ def test_plot_roundtrip(tmp_path):
 
 def test_runtime_config_from_env():
     from ncnet_amd.config import RuntimeConfig
-    c = RuntimeConfig.from_env({"NCNET_TRUNK_GRAPH": "0", "NCNET_BWD_OVERLAP": "0"})
-    assert c.nc_encoding == "ij" and not c.trunk_graph and c.trunk_plan and not c.bwd_overlap
-    assert set(c.as_dict()) >= {"nc_encoding", "trunk_prefetch", "allow_torch_fallback"}
+    c = RuntimeConfig.from_env({"NCNET_TRUNK_GRAPH": "0", "NCNET_BWD_OVERLAP": "0", "NCNET_GP_TPW": "3",
+                                "NCNET_TRUNK_CONV": "native"})
+    assert not c.trunk_graph and c.trunk_plan and not c.bwd_overlap and c.gp_tpw == 3 and c.trunk_conv == "native"
+    assert set(c.as_dict()) >= {"trunk_prefetch", "allow_torch_fallback", "nc_fp8", "stats2d", "nt_store"}
+    assert set(c.tuning()) == set(RuntimeConfig.TUNING)
+
+
+def test_runtime_override_restores():
+    from ncnet_amd import config
+    before = config.RUNTIME
+    with config.override(nc_fp8=True, gp_tpw=2) as c:
+        assert config.RUNTIME is c and c.nc_fp8 and c.gp_tpw == 2
+    assert config.RUNTIME is before
+
+
+def test_no_environment_reads_outside_config():
+    """SURVEY 5.6: the NCNET_* switches are read once, in ncnet_amd/config.py;
+    the package reads no other environment variable but the launcher's
+    (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* / TORCHELASTIC_RUN_ID) and the
+    build script's."""
+    import pathlib
+    import re
+    root = pathlib.Path(__file__).resolve().parents[1] / "ncnet_amd"
+    allowed = {"WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR", "TORCHELASTIC_RUN_ID"}
+    bad = []
+    for f in list(root.rglob("*.py")) + list(root.rglob("*.hip")) + list(root.rglob("*.h")) + list(root.rglob("*.cpp")):
+        if f.name in ("config.py", "build.py"):
+            continue
+        for n, line in enumerate(f.read_text().splitlines(), 1):
+            for m in re.finditer(r'(?:os\.environ(?:\.get|\.setdefault)?\(?\[?|getenv\()\s*"([A-Z_]+)"', line):
+                if m.group(1) not in allowed:
+                    bad.append(f"{f.name}:{n}: {m.group(1)}")
+            if "getenv(" in line and "getenv(\"" not in line:
+                bad.append(f"{f.name}:{n}: getenv")
+    assert not bad, bad
 
 
 def test_segment_timer_cpu():
