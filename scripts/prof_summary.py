@@ -24,7 +24,10 @@ def main():
     marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     per_step = len(marks) // (a.warmup + a.steps)
     first = marks[a.warmup * per_step] if per_step else 0
-    sel = rows[first:]
+    # the window ends at the marker of the first step after the timed ones (when
+    # the traced program runs more after them, e.g. bench_inloc's eager breakdown)
+    end = marks[(a.warmup + a.steps) * per_step] if per_step and len(marks) > (a.warmup + a.steps) * per_step else None
+    sel = rows[first:end]
     t0, t1 = int(sel[0]["Start_Timestamp"]), int(sel[-1]["End_Timestamp"])
     agg = collections.defaultdict(lambda: [0, 0])
     for r in sel:
