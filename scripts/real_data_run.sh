@@ -2,10 +2,10 @@
 # train.py on synthetic JPEG pairs (the real input path: DataLoader workers
 # decode, one packed H2D copy + one resize/normalise launch per batch), one GPU,
 # as a plain process and under torchrun --nproc-per-node 1 (RCCL process
-# group, world 1) -> gpurun_out/r4_real/{plain,torchrun}.jsonl + summary.json
+# group, world 1) -> gpurun_out/$REAL_TAG/{plain,torchrun}.log + summary.json
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT="$ROOT/gpurun_out/r4_real"
+OUT="$ROOT/gpurun_out/${REAL_TAG:-r5_real}"
 mkdir -p "$OUT"
 D=/tmp/ncnet_jpeg_pairs
 python3 "$ROOT/scripts/make_jpeg_pairs.py" --out "$D" --pairs 1200 || exit $?
