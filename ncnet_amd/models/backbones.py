@@ -8,7 +8,7 @@ layer3])`` (lib/model.py:37-44), VGG16 ``features[:pool4]`` (lib/model.py:24-35)
 and DenseNet-201 ``features[:-4]`` (lib/model.py:69-74).
 
 Weights are random-initialised (there is no network to fetch ImageNet weights);
-a local state-dict can be loaded with ``load_state_dict``.
+a local state-dict is loaded strictly with ``load_trunk_state``.
 """
 from __future__ import annotations
 
@@ -180,6 +180,75 @@ def densenet201_trunk() -> nn.Sequential:
     seq = nn.Sequential(*list(full.children())[:-4])
     seq.apply(_kaiming)
     return seq
+
+
+DENSENET_FEATURES = ["conv0", "norm0", "relu0", "pool0", "denseblock1", "transition1", "denseblock2",
+                     "transition2", "denseblock3", "transition3", "denseblock4", "norm5"]
+
+
+def _trunk_key(key: str, cnn: str, n_mods: int) -> str | None:
+    """Maps a full-model key (torchvision names: 'layer1.0.conv1.weight',
+    'features.3.weight', 'features.denseblock1...') or a trunk key
+    ('4.0.conv1.weight') to the trunk's key; None for a key of a layer past the
+    truncation (layer4, fc, classifier, ...)."""
+    for p in ("module.", "model."):
+        if key.startswith(p):
+            key = key[len(p):]
+    head, _, rest = key.partition(".")
+    if head.isdigit():
+        return key if int(head) < n_mods else None
+    if cnn.startswith("resnet"):
+        if head == "fc":
+            return None
+        if head in RESNET_LAYERS:
+            i = RESNET_LAYERS.index(head)
+            return f"{i}.{rest}" if i < n_mods else None
+        return key
+    if head == "classifier":
+        return None
+    if head == "features":
+        sub, _, rest2 = rest.partition(".")
+        if cnn == "densenet201" and sub in DENSENET_FEATURES:
+            i = DENSENET_FEATURES.index(sub)
+        elif sub.isdigit():
+            i = int(sub)
+        else:
+            return key
+        return f"{i}.{rest2}" if i < n_mods else None
+    return key
+
+
+def load_trunk_state(trunk: nn.Sequential, sd: dict, cnn: str = "resnet101") -> None:
+    """Strict load of a local state dict into a truncated trunk.
+
+    The file may hold the trunk's own keys or the whole torchvision model's (the
+    reference starts from ``models.resnet101(pretrained=True)`` and truncates,
+    lib/model.py:37-44): keys of the layers past the truncation are dropped,
+    and any trunk tensor the file does not fill, or any other key, raises an
+    error that names them (never a silently half-initialised trunk)."""
+    mapped, dropped = {}, 0
+    for k, v in sd.items():
+        tk = _trunk_key(k, cnn, len(trunk))
+        if tk is None:
+            dropped += 1
+        else:
+            mapped[tk] = v
+    want = trunk.state_dict()
+    missing = sorted(set(want) - set(mapped))
+    unexpected = sorted(set(mapped) - set(want))
+    bad_shape = sorted(k for k in set(want) & set(mapped) if tuple(want[k].shape) != tuple(mapped[k].shape))
+    if missing or unexpected or bad_shape:
+        def few(xs):
+            return ", ".join(xs[:8]) + (f" ... (+{len(xs) - 8})" if len(xs) > 8 else "")
+        msg = [f"feature_extraction_model_file does not match the {cnn} trunk ({len(want)} tensors):"]
+        if missing:
+            msg.append(f"missing {len(missing)}: {few(missing)}")
+        if unexpected:
+            msg.append(f"unexpected {len(unexpected)}: {few(unexpected)}")
+        if bad_shape:
+            msg.append(f"shape mismatch {len(bad_shape)}: {few(bad_shape)}")
+        raise RuntimeError("; ".join(msg))
+    trunk.load_state_dict(mapped, strict=True)
 
 
 def build_trunk(cnn: str = "resnet101", last_layer: str = "") -> tuple[nn.Sequential, int, int]:

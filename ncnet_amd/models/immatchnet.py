@@ -34,7 +34,7 @@ from ..ops.neigh_consensus import neigh_consensus
 _nc_ops = importlib.import_module("ncnet_amd.ops.neigh_consensus")
 _ext_count = _ext_mod.count
 from ..utils.timing import segment
-from .backbones import FrozenResNetPlan, FrozenResNetPlanX3, build_trunk, fold_frozen_bn
+from .backbones import FrozenResNetPlan, FrozenResNetPlanX3, build_trunk, fold_frozen_bn, load_trunk_state
 
 from .. import config as _config
 
@@ -69,7 +69,7 @@ class FeatureExtraction(nn.Module):
         self.model, self.out_channels, self.stride = build_trunk(feature_extraction_cnn, last_layer)
         if feature_extraction_model_file:
             sd = torch.load(feature_extraction_model_file, map_location="cpu", weights_only=True)
-            self.model.load_state_dict(sd, strict=False)
+            load_trunk_state(self.model, sd, feature_extraction_cnn)
         if not train_fe:
             for p in self.model.parameters():
                 p.requires_grad = False
