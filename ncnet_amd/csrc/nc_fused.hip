@@ -180,7 +180,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 1) void nc_fused_k3_kernel(c
   // plane byte offsets: one multiply per gather, the 9 combos differ by constants
   const int pstride = KLi * 2, rstride = g.J * KLi * 2;
   // every load is issued (branch-free: a combo outside the volume gets the
-  // scalar offset nrec, past the buffer's range -> 0); a conditional load let
+  // scalar offset nrec, past the buffer's range -> 0: on gfx950 the raw-buffer
+  // range check covers voffset + soffset, pinned by
+  // tests/test_gpu_kernels.py::test_nc_fused_k3_last_volume_borders, which
+  // places large non-zero data right after a single volume); a conditional load let
   // the compiler merge the loads of both gather paths behind a VGPR phi of
   // the offset, i.e. a readfirstlane waterfall loop around each load
   const int nrec = (int)((size_t)g.I * g.J * KL * 2);

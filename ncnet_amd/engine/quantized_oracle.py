@@ -85,3 +85,73 @@ def weak_loss_volumes(feats: torch.Tensor, hw, b: int, ws_std, bs, normalize: bo
     corr = ref.mutual_matching(corr)
     corr = neigh_consensus(corr, [w_.to(dtype) for w_ in ws_std], [b_.to(dtype) for b_ in bs])
     return ref.mutual_matching(corr)
+
+
+def _rl2(a, b) -> float:
+    a, b = a.detach().double(), b.detach().double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def training_grad_errors(fe_finetune: int = 0, point_seed: int = 0, batch_seed: int = 7,
+                         device: str = "cuda") -> dict:
+    """Relative L2 errors of the fused training path against this oracle at a
+    non-degenerate operating point (tests/test_gpu_quality.py,
+    scripts/oracle_tolerance.py): a 5,5,5 / 16,16,1 model after three NC Adam
+    steps on known-correspondence pairs (trunk frozen, seeds ``point_seed`` ..
+    +2), then one weak-loss-volume backward with a random cotangent on batch
+    ``batch_seed``.  Keys: 'vols', 'nc0' .. 'nc5' (weight, bias per layer) and,
+    with ``fe_finetune`` (the last layer3 bottleneck unfrozen, train.py:60-63),
+    'd_raw_features' (the gradient w.r.t. the raw trunk features)."""
+    from ..data.datasets import synthetic_correspondence_batch
+    from ..engine.trainer import make_adam, weak_loss
+    from ..models import ImMatchNet
+    from ..ops.correlation import l2norm_pack
+    torch.manual_seed(0)
+    m = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1]).to(device)
+    for p in m.NeighConsensus.parameters():
+        if p.dim() == 1:
+            p.data.uniform_(0.0, 0.05)
+    m.train()
+    opt = make_adam([p for p in m.parameters() if p.requires_grad], 5e-4)
+    for s in range(3):
+        b = synthetic_correspondence_batch(2, 240, device, seed=point_seed + s)
+        opt.zero_grad(set_to_none=True)
+        weak_loss(m, {"source_image": b["source_image"], "target_image": b["target_image"]}).backward()
+        opt.step()
+    if fe_finetune:
+        for p in m.FeatureExtraction.model[-1][-1].parameters():
+            p.requires_grad = True
+    b = synthetic_correspondence_batch(2, 240, device, seed=batch_seed)
+    imgs = torch.cat((b["source_image"], b["target_image"]))
+    opt.zero_grad(set_to_none=True)
+    if fe_finetune:
+        raw = m.FeatureExtraction.trunk_forward(imgs, torch.bfloat16).detach().requires_grad_(True)
+        f, hw = l2norm_pack(raw), tuple(raw.shape[-2:])
+    else:
+        with torch.no_grad():
+            f, hw = m.extract(imgs)
+    vols = m.weak_loss_volumes_from_features(f, hw, 2)
+    gen = torch.Generator(device=vols.device).manual_seed(batch_seed)
+    G = torch.randn(vols.shape, device=vols.device, dtype=vols.dtype, generator=gen)
+    (vols * G).sum().backward()
+    g_hip = [p.grad.detach().double().clone() for p in m.NeighConsensus.parameters()]
+    layers = m.NeighConsensus.conv_layers()
+    ws = [ref.conv4d_weight_to_std(l.weight_ref()).detach().double().requires_grad_(True) for l in layers]
+    bs = [l.bias.detach().double().requires_grad_(True) for l in layers]
+    if fe_finetune:
+        raw64 = raw.detach().double().requires_grad_(True)
+        ovols = weak_loss_volumes(raw64, hw, 2, ws, bs, normalize=True)
+    else:
+        ovols = weak_loss_volumes(f.detach(), hw, 2, ws, bs, normalize=False)
+    (ovols * G.double()).sum().backward()
+    errs = {"vols": _rl2(vols, ovols)}
+    o_grads = []
+    for w, x in zip(ws, bs):
+        o_grads += [w.grad, x.grad]
+    for i, (gh, go) in enumerate(zip(g_hip, o_grads)):
+        if gh.dim() == 6:
+            go = ref.conv4d_weight_from_std(go)
+        errs[f"nc{i}"] = _rl2(gh, go)
+    if fe_finetune:
+        errs["d_raw_features"] = _rl2(raw.grad, raw64.grad)
+    return errs

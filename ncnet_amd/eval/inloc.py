@@ -78,6 +78,9 @@ def _fused_candidates(corr4d, delta4d, k: int, do_softmax: bool):
     b, _, fs1, fs2, fs3, fs4 = corr4d.shape
     if b != 1 or not (_ext.use_hip(corr4d) and corr4d.dtype == torch.float32):
         return None
+    if delta4d is not None and k > 4:
+        # the kernel decodes 2-bit offsets: k_size > 4 stays on the op-by-op path
+        return None
     if delta4d is not None and not torch.is_tensor(delta4d):
         # unpacked (di, dj, dk, dl) offsets -> the packed 2-bit code (same decode as the fused pool's codes)
         if len(delta4d) != 4:

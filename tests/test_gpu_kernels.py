@@ -918,12 +918,14 @@ def test_stats2d_matches_row_and_col_kernels(shape, sum_kind):
             assert torch.allclose(a[i], b[i], rtol=1e-5, atol=1e-5), (i, (a[i] - b[i]).abs().max())
 
 
-@pytest.mark.parametrize("k,packed,softmax", [(2, True, True), (2, True, False), (1, False, True), (2, False, True)])
+@pytest.mark.parametrize("k,packed,softmax", [(2, True, True), (2, True, False), (1, False, True), (2, False, True),
+                                               (3, "tuple", True), (4, "tuple", False)])
 def test_fused_match_candidates_match_op_path(k, packed, softmax, monkeypatch):
     """InLoc pair_matches through stats2d + match_candidates (one launch for
     both directions' candidates, offsets decoded, recentred) against the
     op-by-op corr_to_matches path: identical de-duplicated order and keys,
-    coordinates to 1e-6 (linspace rounding)."""
+    coordinates to 1e-6 (linspace rounding).  ``packed="tuple"`` passes the
+    unpacked (di, dj, dk, dl) offsets that _fused_candidates packs itself."""
     import ncnet_amd.eval.inloc as inl
     torch.manual_seed(33)
     fs = (9, 12, 9, 12)
@@ -932,6 +934,11 @@ def test_fused_match_candidates_match_op_path(k, packed, softmax, monkeypatch):
     if packed:   # 2-bit fields, each an in-cell offset < k (as the fused pool writes them)
         f4 = torch.randint(0, k, (4, 1, 1) + fs, device=DEV)
         code = ((f4[0] << 6) | (f4[1] << 4) | (f4[2] << 2) | f4[3]).to(torch.uint8)
+        if packed == "tuple":
+            code = tuple(f4[i].long() for i in range(4))
+            assert inl._fused_candidates(corr, code, k, softmax) is not None
+            # 2-bit fields cannot hold offsets of a k > 4 pool: op-by-op path
+            assert inl._fused_candidates(corr, code, 5, softmax) is None
     if k > 1 and not packed:
         code = None
     got, n_got = inl.pair_matches(corr, code, k, do_softmax=softmax, static=True)
@@ -963,6 +970,38 @@ def test_nc_fused_k3_one_wide_workgroup():
     assert torch.isfinite(y).all()
     yr = qo.nc_stack(x0.double().unsqueeze(1), [w1.double(), w2.double()], [b1.double(), b2.double()])
     assert relerr(y, yr.squeeze(1)) < 2e-3
+
+
+@pytest.mark.parametrize("tiles", [(8, 4, 8, 8), (10, 4, 15, 20), (24, 4, 15, 20)])
+def test_nc_fused_k3_last_volume_borders(tiles):
+    """The fused NC kernel's out-of-volume gathers issue their load with the
+    scalar offset past the volume's buffer range (csrc/nc_fused.hip gather):
+    a single volume followed by large non-zero data in the same allocation
+    must still see zero padding at every border (the range check covers the
+    scalar offset on gfx950; a read past the tensor would show here as a
+    large error at the I/J borders)."""
+    import importlib
+    from ncnet_amd.engine import quantized_oracle as qo
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    torch.manual_seed(29)
+    I, J, K, L = 7, 9, 11, 13
+    n = I * J * K * L
+    big = torch.full((3 * n,), 50.0, device=DEV, dtype=torch.bfloat16)    # poison after the tensor
+    big[:n] = torch.rand(n, device=DEV).to(torch.bfloat16)
+    x0 = big[:n].view(1, I, J, K, L)
+    w1 = torch.randn(16, 1, 3, 3, 3, 3, device=DEV) * 0.2
+    w2 = torch.randn(1, 16, 3, 3, 3, 3, device=DEV) * 0.1
+    b1, b2 = torch.rand(16, device=DEV) * 0.1 - 0.03, torch.rand(1, device=DEV) * 0.1
+    wts = nc._fused_weights([ref.conv4d_weight_from_std(w1), ref.conv4d_weight_from_std(w2)], [b1, b2])
+    y = torch.full((1, I, J, K, L), float("nan"), device=DEV)
+    _ext.ext().nc_fused_k3(x0, *wts, y, *tiles)          # R, IR, TK, TL (runtime, 3200-px static, 16-wave)
+    torch.cuda.synchronize()
+    yr = qo.nc_stack(x0.double().unsqueeze(1), [w1.double(), w2.double()], [b1.double(), b2.double()])
+    assert torch.isfinite(y).all()
+    assert relerr(y, yr.squeeze(1)) < 2e-3
+    # the border planes alone (where every out-of-volume combo lands)
+    for sl in ((slice(None), 0), (slice(None), I - 1), (slice(None), slice(None), 0), (slice(None), slice(None), J - 1)):
+        assert relerr(y[sl], yr.squeeze(1)[sl]) < 2e-3, sl
 
 
 def test_neigh_consensus_fused_symmetric_wrapper():

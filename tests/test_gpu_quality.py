@@ -75,10 +75,14 @@ def test_training_tracks_fp32_reference():
     assert summary["pck_final_hip"] > summary["pck_final_ref"] - 0.3, summary
 
 
-def _nc_std(m):
-    from ncnet_amd.ops import reference as ref
-    layers = m.NeighConsensus.conv_layers()
-    return [ref.conv4d_weight_to_std(l.weight_ref()).detach() for l in layers], [l.bias.detach() for l in layers]
+# bounds just above the errors measured at these four operating points
+# (scripts/oracle_tolerance.py, profiles/r5/quality/oracle_tolerance.json; one build
+# reproduces them bitwise): frozen trunk max NC 1.4e-2, volumes 2.6e-4;
+# fe_finetune NC 6.5e-3 / 1.4e-2 / 7.5e-3 / 5.1e-2 (point 30: a first-MM
+# near-tie), volumes 4.9e-4, raw-feature gradient 4.6e-2
+ORACLE_POINTS = (0, 10, 20, 30)
+ORACLE_TOL = {0: {"vols": 5e-4, "nc": 2e-2, "nc_any": 2e-2},
+              1: {"vols": 1e-3, "nc": 2e-2, "nc_any": 6e-2, "d_raw": 6e-2}}
 
 
 @pytest.fixture
@@ -99,83 +103,34 @@ def test_training_grads_vs_quantized_oracle(fe_finetune, deterministic_trunk):
     """End-to-end gradients of the fused training path (features reused for the
     rolled negatives, HIP correlation / MutualMatching / ij-encoded NC with the
     side-stream weight gradients) against its own math in float64 with bf16
-    rounding at exactly the stored-bf16 points (engine/quantized_oracle.py), at
-    a non-degenerate operating point (known-correspondence pairs, after three
-    Adam steps).  fe_finetune=1 unfreezes the last layer3 bottleneck
-    (train.py:60-63): the L2-norm, correlation and first-MutualMatching
-    backward and the NC input gradient are then checked too, as the gradient
-    w.r.t. the raw trunk features."""
-    from ncnet_amd.data.datasets import synthetic_correspondence_batch
-    from ncnet_amd.engine import quantized_oracle as qo
-    from ncnet_amd.engine.trainer import make_adam, weak_loss
-    from ncnet_amd.models import ImMatchNet
-    from ncnet_amd.ops.correlation import l2norm_pack
-    torch.manual_seed(0)
-    m = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1]).to(DEV)
-    for p in m.NeighConsensus.parameters():
-        if p.dim() == 1:
-            p.data.uniform_(0.0, 0.05)
-    m.train()
-    opt = make_adam([p for p in m.parameters() if p.requires_grad], 5e-4)
-    # the operating point: three NC Adam steps with the trunk frozen.  (Training
-    # the trunk here too makes the point itself run-dependent -- MIOpen's
-    # backward-weight convolutions are not bitwise deterministic -- and with it
-    # how many MutualMatching argmax near-ties the bf16 path and the oracle
-    # resolve differently: measured 2.6e-3 .. 2.7e-2 NC gradient error over
-    # runs of one build, profiles/r2_sanitizers/README.md.)
-    for s in range(3):
-        b = synthetic_correspondence_batch(2, 240, DEV, seed=s)
-        opt.zero_grad(set_to_none=True)
-        weak_loss(m, {"source_image": b["source_image"], "target_image": b["target_image"]}).backward()
-        opt.step()
-    if fe_finetune:
-        for p in m.FeatureExtraction.model[-1][-1].parameters():
-            p.requires_grad = True
-    b = synthetic_correspondence_batch(2, 240, DEV, seed=7)
-    imgs = torch.cat((b["source_image"], b["target_image"]))
-    opt.zero_grad(set_to_none=True)
-    if fe_finetune:
-        raw = m.FeatureExtraction.trunk_forward(imgs, torch.bfloat16).detach().requires_grad_(True)
-        f, hw = l2norm_pack(raw), tuple(raw.shape[-2:])
-    else:
-        with torch.no_grad():
-            f, hw = m.extract(imgs)
-    vols = m.weak_loss_volumes_from_features(f, hw, 2)
-    G = torch.randn_like(vols)
-    (vols * G).sum().backward()
-    g_hip = [p.grad.detach().double().clone() for p in m.NeighConsensus.parameters()]
-    ws, bs = _nc_std(m)
-    ws = [w.double().requires_grad_(True) for w in ws]
-    bs = [x.double().requires_grad_(True) for x in bs]
-    if fe_finetune:
-        raw64 = raw.detach().double().requires_grad_(True)
-        ovols = qo.weak_loss_volumes(raw64, hw, 2, ws, bs, normalize=True)
-    else:
-        ovols = qo.weak_loss_volumes(f.detach(), hw, 2, ws, bs, normalize=False)
-    (ovols * G.double()).sum().backward()
-    errs = {"vols": rl2(vols, ovols)}
-    o_grads = []
-    for w, x in zip(ws, bs):
-        o_grads += [w.grad, x.grad]
-    # NC parameters are (weight, bias) per layer in module order; the oracle's are std-layout weights
-    from ncnet_amd.ops import reference as ref
-    for i, (gh, go) in enumerate(zip(g_hip, o_grads)):
-        if gh.dim() == 6:
-            go = ref.conv4d_weight_from_std(go)
-        errs[f"nc{i}"] = rl2(gh, go)
-    if fe_finetune:
-        errs["d_raw_features"] = rl2(raw.grad, raw64.grad)
-    print("quantized-oracle errors:", {k: f"{v:.2e}" for k, v in errs.items()})
-    assert errs["vols"] < 2e-3, errs
+    rounding at exactly the stored-bf16 points (engine/quantized_oracle.py
+    training_grad_errors), at four non-degenerate operating points (known-
+    correspondence pairs, after three Adam steps with the trunk frozen).
+    fe_finetune=1 unfreezes the last layer3 bottleneck (train.py:60-63): the
+    L2-norm, correlation and first-MutualMatching backward and the NC input
+    gradient are then checked too, as the gradient w.r.t. the raw trunk
+    features.  One point is run twice: a build must reproduce itself bitwise
+    (measured: it does, profiles/r5/quality/oracle_tolerance.json)."""
+    from ncnet_amd.engine.quantized_oracle import training_grad_errors
+    runs = {s: training_grad_errors(fe_finetune=fe_finetune, point_seed=s) for s in ORACLE_POINTS}
+    again = training_grad_errors(fe_finetune=fe_finetune, point_seed=ORACLE_POINTS[0])
+    for s, e in runs.items():
+        print(f"point {s}: quantized-oracle errors:", {k: f"{v:.2e}" for k, v in e.items()})
+    assert runs[ORACLE_POINTS[0]] == again, (runs[ORACLE_POINTS[0]], again)
+    nc = sorted(max(v for k, v in e.items() if k.startswith("nc")) for e in runs.values())
+    vols = max(e["vols"] for e in runs.values())
+    tol = ORACLE_TOL[fe_finetune]
+    assert vols < tol["vols"], runs
     # continuous data: the NC gradient error is set by ReLU-mask flips and
-    # MutualMatching argmax near-ties (an L2 error ~ sqrt(flip rate)), measured
-    # 2.6e-3 .. 2.7e-2 over runs of one build (above).  The kernel-level check
-    # at 1e-3 runs on exactly representable data, where nothing flips:
-    # tests/test_gpu_kernels.py::test_fast1x_stack_vs_quantized_oracle.
-    assert max(v for k, v in errs.items() if k.startswith("nc")) < 3e-2, errs
-    # the raw-feature gradient crosses the first MutualMatching's argmax: an
-    # argmax near-tie resolved differently by the bf16 path and the oracle
-    # moves it discretely, and which ties exist depends on the operating point
-    # (the three Adam steps above; a different fp32 summation order of the
-    # weight gradients alone moved it 2.2e-2 -> 2.8e-2)
-    assert errs.get("d_raw_features", 0.0) < 6e-2, errs
+    # MutualMatching argmax near-ties (an L2 error ~ sqrt(flip rate)).  Frozen
+    # trunk: every point within tol["nc"].  fe_finetune: the oracle recomputes
+    # the correlation from the raw features in fp64, so a first-MutualMatching
+    # near-tie can flip between the two -- typical points stay within
+    # tol["nc"], one of the four measured ones reached 5.1e-2 (tol["nc_any"]).
+    # The kernel-level check at 1e-3 runs on exactly representable data, where
+    # nothing flips: tests/test_gpu_kernels.py::test_fast1x_stack_vs_quantized_oracle.
+    assert nc[-2] < tol["nc"] and nc[-1] < tol["nc_any"], (nc, runs)
+    if fe_finetune:
+        # the raw-feature gradient crosses the first MutualMatching's argmax
+        d_raw = max(e["d_raw_features"] for e in runs.values())
+        assert d_raw < tol["d_raw"], runs

@@ -209,3 +209,31 @@ def test_trunk_x3_plan_vs_fp64():
     print("x3 trunk vs fp64:", err, "bf16 trunk would be ~1e-2")
     assert torch.equal(got, got2)
     assert err < 1e-4, err
+
+
+def test_trunk_x3_vs_miopen_fp32():
+    """the fp32 trunk modes side by side.  The evaluation default
+    (nc_precision 'bf16' / fp32 eval: ``fp32_trunk == 'miopen'``) runs true fp32
+    MIOpen convs, the reference's numerics; the bf16x3 plan (``'x3'``, the
+    default of nc_precision='fp32' training only) agrees with it to the x3
+    split's ~2^-16 operand accuracy: features within 1e-4 relative L2 and
+    argmax-over-channels decisions almost everywhere identical."""
+    from ncnet_amd import config as _config
+    from ncnet_amd.models import ImMatchNet
+    torch.manual_seed(0)
+    m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1]).cuda().eval()
+    fe = m.FeatureExtraction
+    assert fe.fp32_trunk == "miopen"
+    x = torch.randn(2, 3, 160, 192, device="cuda")
+    with torch.no_grad():
+        ref32 = fe.trunk_forward(x, torch.float32)
+        want = fe._folded_trunk().double()(x.double())
+        fe._folded = None
+        with _config.override(trunk_fp32="x3"):
+            got = fe.trunk_forward(x, torch.float32)
+    e_x3, e_mi, e_pair = rl2(got, want), rl2(ref32, want), rl2(got, ref32)
+    print(f"trunk vs fp64: x3 {e_x3:.2e}, miopen fp32 {e_mi:.2e}; x3 vs miopen {e_pair:.2e}")
+    assert e_mi < 1e-5, e_mi
+    assert e_pair < 1e-4, e_pair
+    same = (got.argmax(1) == ref32.argmax(1)).float().mean().item()
+    assert same > 0.99, same
