@@ -39,6 +39,14 @@ sys.path.insert(0, ROOT)
 
 # Measured reference-algorithm baseline on one MI355X (pairs/s), see BASELINE.md.
 BASELINE_PAIRS_PER_S = None
+# per-GPU batch of the headline step, sized for the 288 GB HBM of one MI355X
+# (BASELINE.json north star and config 3): the throughput-optimal batch of the
+# r5 sweep (profiles/r5/batch: 16 -> 764, 128 -> 801, 256 -> 836 pairs/s at
+# 57.8 GB, 512 -> 567 at 115 GB); the reference train.py's default batch 16 is
+# timed as the train_b16 secondary
+HEADLINE_BATCH = 256
+# the secondary training records (other sizes / recipes / precisions): train.py's batch
+SECONDARY_BATCH = 16
 _BASELINE_FILE = os.path.join(ROOT, "profiles", "baseline_reference.json")
 
 
@@ -270,7 +278,8 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="pairs per GPU (train.py default 16)")
+    ap.add_argument("--batch", type=int, default=HEADLINE_BATCH,
+                    help=f"pairs per GPU (default {HEADLINE_BATCH}: sized for HBM; train.py's default is 16)")
     ap.add_argument("--image-size", type=int, default=400)
     ap.add_argument("--impl", choices=["hip", "reference"], default="hip")
     ap.add_argument("--ref-dtype", choices=["fp32", "bf16"], default="fp32")
@@ -392,11 +401,11 @@ def main(argv=None):
     if args.inloc and ctx.world_size == 1 and dev.type == "cuda" and args.impl == "hip":
         secondary = _inloc_secondary()
         try:
-            secondary["fe_finetune_1"] = _fe_finetune_secondary(args.batch, s)
+            secondary["fe_finetune_1"] = _fe_finetune_secondary(SECONDARY_BATCH, s)
         except Exception as e:  # the headline record must still print
             secondary["fe_finetune_1"] = {"error": repr(e)}
         try:
-            secondary["train_nc_fp32"] = _nc_precision_secondary(args.batch, s, "fp32")
+            secondary["train_nc_fp32"] = _nc_precision_secondary(SECONDARY_BATCH, s, "fp32")
         except Exception as e:  # the headline record must still print
             secondary["train_nc_fp32"] = {"error": repr(e)}
         # the training step at the other --image_size values and the IVD recipe
@@ -404,19 +413,16 @@ def main(argv=None):
                                    ("train_480", 480, (5, 5, 5), (16, 16, 1)),
                                    ("train_ivd_400", 400, (3, 3), (16, 1))):
             try:
-                secondary[name] = _train_secondary(args.batch, size, ks, ch)
+                secondary[name] = _train_secondary(SECONDARY_BATCH, size, ks, ch)
             except Exception as e:  # the headline record must still print
                 secondary[name] = {"error": repr(e)}
-        # BASELINE config 3's per-GPU batch sized for HBM: the r5 sweep
-        # (profiles/r5/batch) rises 764 -> 801 pairs/s from batch 16 to 128 at
-        # 29 GB of 288 GB; the headline keeps the reference's batch 16 so the
-        # per-GPU work matches the baseline measurement and every N
-        try:
-            torch.cuda.reset_peak_memory_stats(dev)
-            secondary["train_b128"] = _train_secondary(128, s, steps=3, warmup=1)
-            secondary["train_b128"]["hbm_peak_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
-        except Exception as e:  # the headline record must still print
-            secondary["train_b128"] = {"error": repr(e)}
+        # the headline step at the reference train.py's batch 16 (the headline
+        # of rounds 1-4), next to the HBM-sized headline batch
+        if args.batch != SECONDARY_BATCH:
+            try:
+                secondary["train_b16"] = _train_secondary(SECONDARY_BATCH, s, steps=10, warmup=3)
+            except Exception as e:  # the headline record must still print
+                secondary["train_b16"] = {"error": repr(e)}
         secondary["headline_useful_tflops"] = round(pairs_per_s / ctx.world_size * train_tflop_per_pair(s), 1)
     if ctx.is_main:
         rec = {

@@ -38,6 +38,8 @@ int ncnet_corr_gemm_pool2(const void*, const void*, float*, uint8_t*, int, int, 
 int ncnet_stats_rows(const float*, float*, int*, float*, long long, int, int, hipStream_t);
 int ncnet_stats_cols(const float*, float*, int*, float*, int, int, int, float*, int, int, hipStream_t);
 int ncnet_gather_bf16(const float*, const int*, void*, long long, long long, hipStream_t);
+int ncnet_reduce_cols(const float* const*, float* const*, const int* const*, const int*, const int*, const long long*,
+                      int, hipStream_t);
 int ncnet_stats2d(const float*, float*, int*, float*, float*, int*, float*, int, int, int, float*, int, hipStream_t);
 int ncnet_match_candidates(const float*, const float*, const int*, const float*, const float*, const int*,
                            const uint8_t*, int, int, int, int, int, float*, float*, long long*, hipStream_t);
@@ -540,6 +542,31 @@ void gather_bf16(Tensor src, Tensor idx, Tensor out) {
      "gather_bf16");
 }
 
+// segments (src fp32 [R, N] contiguous, dst fp32, idx int32 [N] or None): dst[idx[j]] =
+// sum_r src[r, j] (idx None: dst[j]); <= 4 segments, one launch, deterministic order
+void reduce_cols(std::vector<Tensor> src, std::vector<Tensor> dst, std::vector<c10::optional<Tensor>> idx) {
+  const int n = (int)src.size();
+  TORCH_CHECK(n >= 1 && n <= 4 && (int)dst.size() == n && (int)idx.size() == n, "reduce_cols: 1..4 segments");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(src[0].device());
+  const float* s[4]; float* d[4]; const int* ix[4]; int R[4], N[4]; long long nd[4];
+  for (int k = 0; k < n; ++k) {
+    check(src[k], "src", at::kFloat); check(dst[k], "dst", at::kFloat);
+    TORCH_CHECK(src[k].dim() == 2, "reduce_cols: src [R, N]");
+    TORCH_CHECK(src[k].device() == src[0].device() && dst[k].device() == src[0].device(), "reduce_cols: one device");
+    R[k] = (int)src[k].size(0); N[k] = (int)src[k].size(1);
+    s[k] = (const float*)src[k].data_ptr(); d[k] = (float*)dst[k].data_ptr(); nd[k] = dst[k].numel();
+    if (idx[k].has_value()) {
+      check(*idx[k], "idx", at::kInt);
+      TORCH_CHECK(idx[k]->numel() == N[k], "reduce_cols: idx [N]");
+      ix[k] = (const int*)idx[k]->data_ptr();
+    } else {
+      TORCH_CHECK(nd[k] >= N[k], "reduce_cols: dst smaller than N");
+      ix[k] = nullptr;
+    }
+  }
+  ok(ncnet_reduce_cols(s, d, ix, R, N, nd, n, cur_stream(src[0])), "reduce_cols");
+}
+
 // pad (ks, I2, J2): out_x / out_xt are the zero-padded bf16 planes of csrc/conv1x.hip ([V*R, PPL] /
 // [V*C, PPL], halos written too) of a square volume R = C = I2 * J2; else [V,R,C] / [V,C,R] bf16 or f16.
 void mm_apply(Tensor c, Tensor rmax, Tensor cmax, c10::optional<Tensor> out, c10::optional<Tensor> out_x,
@@ -942,6 +969,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stats_cols", &stats_cols);
   m.def("stats2d", &stats2d);
   m.def("gather_bf16", &gather_bf16);
+  m.def("reduce_cols", &reduce_cols);
   m.def("match_candidates", &match_candidates);
   m.def("mm_apply", &mm_apply, py::arg("c"), py::arg("rmax"), py::arg("cmax"), py::arg("out"), py::arg("out_x"),
         py::arg("out_xt"), py::arg("eps"), py::arg("pad") = std::vector<int64_t>{});

@@ -296,3 +296,71 @@ extern "C" int ncnet_gather_bf16(const float* src, const int* idx, void* out, lo
                      nsrc);
   return (int)hipGetLastError();
 }
+
+// reduce_cols: per segment s, for every source column j < N_s
+//   dst_s[map_s(j)] = sum_{r < R_s} src_s[r * N_s + j]
+// map = idx_s[j] (a layout permutation; < 0 drops the column) or j (idx null);
+// the weight-gradient partials of the NeighConsensus layers reduced and laid
+// out in the checkpoint layout in one launch (ops/neigh_consensus.py
+// reduce_partials).  A block owns 64 column quads; its 4 row slices sum rows
+// r = slice (mod 4) and are combined in a fixed order through LDS, so the
+// result is the same on every run.
+struct RedSeg {
+  const float* src;
+  float* dst;
+  const int* idx;
+  int R, N;
+  int blk0;         // first block of this segment
+  long long ndst;   // dst elements: a map entry past them is dropped (never a fault)
+};
+struct RedSegs { RedSeg s[4]; int nseg; };
+
+__global__ __launch_bounds__(256) void reduce_cols_kernel(RedSegs a) {
+  __shared__ f32x4 part[4][64];
+  int si = 0;
+#pragma unroll
+  for (int k = 1; k < 4; ++k)
+    if (k < a.nseg && (int)blockIdx.x >= a.s[k].blk0) si = k;
+  const RedSeg sg = a.s[si];
+  const int cq = ((int)blockIdx.x - sg.blk0) * 64 + (threadIdx.x & 63);
+  const int slice = threadIdx.x >> 6;
+  const int nq = sg.N >> 2;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (cq < nq) {
+    const f32x4* src = (const f32x4*)sg.src + cq;
+    f32x4 acc1 = acc;
+    int r = slice;
+    for (; r + 4 < sg.R; r += 8) {
+      acc += src[(size_t)r * nq];
+      acc1 += src[(size_t)(r + 4) * nq];
+    }
+    if (r < sg.R) acc += src[(size_t)r * nq];
+    acc += acc1;
+  }
+  part[slice][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (slice == 0 && cq < nq) {
+    const f32x4 t = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = cq * 4 + e;
+      const int o = sg.idx ? sg.idx[j] : j;
+      if (o >= 0 && o < sg.ndst) sg.dst[o] = t[e];
+    }
+  }
+}
+
+extern "C" int ncnet_reduce_cols(const float* const* src, float* const* dst, const int* const* idx, const int* R,
+                                 const int* N, const long long* ndst, int nseg, hipStream_t s) {
+  if (nseg < 1 || nseg > 4) return -2;
+  RedSegs a{};
+  a.nseg = nseg;
+  int blk = 0;
+  for (int k = 0; k < nseg; ++k) {
+    if (N[k] % 4 || R[k] < 1) return -3;
+    a.s[k] = RedSeg{src[k], dst[k], idx[k], R[k], N[k], blk, ndst[k]};
+    blk += (N[k] / 4 + 63) / 64;
+  }
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)blk), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}

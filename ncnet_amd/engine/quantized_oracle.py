@@ -99,7 +99,8 @@ def training_grad_errors(fe_finetune: int = 0, point_seed: int = 0, batch_seed: 
     scripts/oracle_tolerance.py): a 5,5,5 / 16,16,1 model after three NC Adam
     steps on known-correspondence pairs (trunk frozen, seeds ``point_seed`` ..
     +2), then one weak-loss-volume backward with a random cotangent on batch
-    ``batch_seed``.  Keys: 'vols', 'nc0' .. 'nc5' (weight, bias per layer) and,
+    ``batch_seed``.  Keys: 'vols', 'nc0' .. 'nc5' (weight, bias per layer),
+    'layer0' .. 'layer2' (each layer's weight and bias gradients as one vector) and,
     with ``fe_finetune`` (the last layer3 bottleneck unfrozen, train.py:60-63),
     'd_raw_features' (the gradient w.r.t. the raw trunk features)."""
     from ..data.datasets import synthetic_correspondence_batch
@@ -148,10 +149,17 @@ def training_grad_errors(fe_finetune: int = 0, point_seed: int = 0, batch_seed: 
     o_grads = []
     for w, x in zip(ws, bs):
         o_grads += [w.grad, x.grad]
+    flat_h, flat_o = [], []
     for i, (gh, go) in enumerate(zip(g_hip, o_grads)):
         if gh.dim() == 6:
             go = ref.conv4d_weight_from_std(go)
         errs[f"nc{i}"] = _rl2(gh, go)
+        flat_h.append(gh.reshape(-1)); flat_o.append(go.reshape(-1))
+    # per layer, weight and bias gradients as one vector: the Cout = 1 layer's
+    # bias gradient is a single sum over all voxels whose relative error alone
+    # is ill-conditioned wherever that sum cancels
+    for li in range(len(layers)):
+        errs[f"layer{li}"] = _rl2(torch.cat(flat_h[2 * li:2 * li + 2]), torch.cat(flat_o[2 * li:2 * li + 2]))
     if fe_finetune:
         errs["d_raw_features"] = _rl2(raw.grad, raw64.grad)
     return errs

@@ -130,13 +130,8 @@ def _nitems(shape) -> int:
     return V * I * J * ((K + 24) // 25) * ((L + 24) // 25)
 
 
-def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, plane_only: bool):
-    """Weight-gradient partials of a 16 -> 16 block and their reduction.
-
-    ``plane_only`` False: all (di, dj) plane offsets (wgrad16v3 when it fits,
-    else wgrad16v2); True: the (P, P) plane only (ij-encoded 1-channel layers,
-    wgrad16v2).  Returns (s, sb): s [dd, tap, ci, co], sb [16] = sum of g16
-    over all voxels (bias gradient, the kernels' ones-MFMA)."""
+def _wgrad16_launch(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, plane_only: bool):
+    """Unreduced partials (part [2 ng, dd, tap, ci, co], partb [2 ng, 16]) of a 16 -> 16 block."""
     shape = x16.shape[:5]
     if plane_only:
         variant, ng = 2, wgrad_plane_groups(_nitems(shape))
@@ -148,7 +143,81 @@ def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, plane_onl
     part = torch.empty((2 * ng, ndd, ks * ks, 16, 16), dtype=torch.float32, device=x16.device)
     partb = torch.empty((2 * ng, 16), dtype=torch.float32, device=x16.device)
     C.wgrad16(x16, g16, part, partb, ks, 2 if plane_only else 0, variant)
+    return part, partb
+
+
+def wgrad16_partials(C, x16: torch.Tensor, g16: torch.Tensor, ks: int, plane_only: bool):
+    """Weight-gradient partials of a 16 -> 16 block and their reduction.
+
+    ``plane_only`` False: all (di, dj) plane offsets (wgrad16v3 when it fits,
+    else wgrad16v2); True: the (P, P) plane only (ij-encoded 1-channel layers,
+    wgrad16v2).  Returns (s, sb): s [dd, tap, ci, co], sb [16] = sum of g16
+    over all voxels (bias gradient, the kernels' ones-MFMA)."""
+    part, partb = _wgrad16_launch(C, x16, g16, ks, plane_only)
     return part.sum(0), partb.sum(0)
+
+
+def wgrad16_ckpt(C, x16: torch.Tensor, g16: torch.Tensor, ks: int):
+    """The 16 -> 16 layer's weight gradient straight in the checkpoint layout
+    [k, 16, 16, k, k, k] and its bias gradient [16]: the partials of every
+    workgroup reduced and permuted by ONE reduce_cols launch (was two torch
+    reductions, the std permute and the checkpoint permute)."""
+    part, partb = _wgrad16_launch(C, x16, g16, ks, False)
+    dw, db = reduce_partials([
+        (part, ("w16", ks), lambda t: ref.conv4d_weight_from_std(_reduce_wgrad16(t, ks, 16, 16))),
+        (partb, None, None)])
+    return dw, db
+
+
+# reduce_partials plans: (key, device) -> (int32 map [N], output shape)
+_RED_PLANS: dict = {}
+
+
+def _col_map(key, part_shape, fn, device):
+    """Scatter map of a layout function: position in fn's output of every
+    source column (-1: dropped by a slice), from fn applied to the column ids."""
+    k = (key, tuple(part_shape), str(device))
+    ent = _RED_PLANS.get(k)
+    if ent is None:
+        n = 1
+        for d in part_shape:
+            n *= d
+        out = fn(torch.arange(n, dtype=torch.int64).reshape(part_shape))
+        m = torch.full((n,), -1, dtype=torch.int64)
+        m[out.reshape(-1)] = torch.arange(out.numel(), dtype=torch.int64)
+        ent = (m.to(torch.int32).to(device), tuple(out.shape))
+        _RED_PLANS[k] = ent
+    return ent
+
+
+def reduce_partials(segs):
+    """segs: [(part [R, ...] fp32, key, fn)] -> [fn(part.sum(0))] (fn None: the
+    plain sum).  ``fn`` is a layout-only function (permute / reshape / flip /
+    slice) and ``key`` names it for the plan cache.  On the GPU every segment
+    is reduced, laid out and written in ONE reduce_cols launch (fixed summation
+    order: the same bits on every run); on the CPU the same by torch ops."""
+    outs, srcs, dsts, idxs = [], [], [], []
+    for part, key, fn in segs:
+        R = part.shape[0]
+        src = part.reshape(R, -1)
+        if fn is None:
+            idx, shape = None, tuple(part.shape[1:])
+        else:
+            idx, shape = _col_map(key, part.shape[1:], fn, part.device)
+        out = torch.empty(shape, dtype=torch.float32, device=part.device)
+        outs.append(out); srcs.append(src); dsts.append(out); idxs.append(idx)
+    if srcs[0].is_cuda and _ext.use_hip(srcs[0]) and hasattr(_ext.ext(), "reduce_cols"):
+        for i in range(0, len(srcs), 4):
+            _ext.ext().reduce_cols(srcs[i:i + 4], dsts[i:i + 4], idxs[i:i + 4])
+    else:
+        for src, out, idx in zip(srcs, dsts, idxs):
+            s = src.sum(0)
+            if idx is None:
+                out.view(-1).copy_(s)
+            else:
+                keep = idx >= 0
+                out.view(-1)[idx[keep].long()] = s[keep]
+    return outs
 
 
 # Plane-only weight gradient of the Cout=1 layer on wgrad16p (double-buffered
@@ -376,13 +445,30 @@ def _pad_1ch(x3: torch.Tensor, I2: int, J2: int, ks: int, trans: int, out: torch
     return out
 
 
-def _wgrad1x(C, d16: torch.Tensor, xp: torch.Tensor, ks: int, bias: bool):
-    """wgrad1x16 partials, reduced: R [ks^2 taps, ks^2 combos, 16] and the bias sum [16] (or None)."""
+def _wgrad1x(C, d16: torch.Tensor, xp: torch.Tensor, ks: int, bias: bool, ch: int, first: bool):
+    """wgrad1x16 partials reduced straight into the checkpoint layout by one
+    reduce_cols launch: R[tap (dk, dl)][combo (di, dj)][c] (the kernel's
+    partial layout, combos padded to 32) becomes
+      first layer (Cin = 1):  dW[co = c, 0, di, dj, dk, dl] = R  -> [k, ch, 1, k, k, k];
+      Cout = 1 last layer:    dW[0, ci = c, t] = R[2P - t] (all four axes
+                              flipped)                          -> [k, 1, ch, k, k, k];
+    and the bias sum [16] (or None) in the same launch."""
     G = _num_cus(d16.device.index)
     part = torch.empty((G, ks * ks, 32, 16), dtype=torch.float32, device=d16.device)
     partb = torch.empty((G, 16), dtype=torch.float32, device=d16.device) if bias else None
+
+    def layout(t):
+        r = t[:, : ks * ks, :ch].reshape((ks,) * 4 + (ch,))          # [dk, dl, di, dj, c]
+        if first:
+            return r.permute(2, 4, 3, 0, 1).unsqueeze(2)
+        return r.flip(0, 1, 2, 3).permute(2, 4, 3, 0, 1).unsqueeze(1)
+
     C.wgrad1x16(d16, xp, part, partb, ks)
-    return part.sum(0)[:, : ks * ks], (partb.sum(0) if bias else None)
+    segs = [(part, ("w1x", ks, ch, first), layout)]
+    if bias:
+        segs.append((partb, None, None))
+    outs = reduce_partials(segs)
+    return outs[0], (outs[1][:ch] if bias else None)
 
 
 def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list, xp=None, shp=None, packs=None):
@@ -542,10 +628,7 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
                 gp = _pad_1ch(g.reshape(g.shape[0], g.shape[1] * g.shape[2], g.shape[3] * g.shape[4]),
                               g.shape[3], g.shape[4], ks, 0)
                 with _OnSide(main if li > 0 else None, side if li > 0 else None, (xin, g, gp)):
-                    R, _ = _wgrad1x(C, xin[0], gp, ks, False)
-                    # dW[0, ci, t] = R[2P - t][ci], straight into the checkpoint layout [k, 1, ci, k, k, k]
-                    Rf = R[:, :, :cin].reshape((ks,) * 4 + (cin,)).flip(0, 1, 2, 3)     # [dk, dl, di, dj, ci]
-                    dw = Rf.permute(2, 4, 3, 0, 1).unsqueeze(1).contiguous()
+                    dw, _ = _wgrad1x(C, xin[0], gp, ks, False, cin, False)
                     db = g.sum(dtype=torch.float32).reshape(1)
                 if li > 0 or need_dx0:
                     gn = torch.empty((1,) + tuple(hin.shape[1:]), dtype=torch.bfloat16, device=g.device)
@@ -553,10 +636,7 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
                                ks, 2)
                     g = gn
             else:                                    # first layer: xin = padded NC-input planes
-                R, sb = _wgrad1x(C, g[0], xin, ks, True)
-                # dW[co, 0, di, dj, dk, dl] = R[(dk, dl)][(di, dj)][co] -> checkpoint layout [k, co, 1, k, k, k]
-                dw = R[:, :, :cout].reshape((ks,) * 4 + (cout,)).permute(2, 4, 3, 0, 1).unsqueeze(2).contiguous()
-                db = sb[:cout]
+                dw, db = _wgrad1x(C, g[0], xin, ks, True, cout, True)
                 if need_dx0:
                     gx0 = conv_layer(g, transpose_for_dgrad(w), cout, 1, relu=False)
             dws[li] = dw
@@ -569,7 +649,12 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
         on_side = li > 0
         with _OnSide(main if on_side else None, side if on_side else None,
                      tuple(t for t in (xin, g, gs) if t is not None)):
-            dw, db = _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout)
+            if kind == "16" and cin == 16 and cout == 16:
+                # one reduce_cols launch: partials -> checkpoint layout + bias
+                dw, db = wgrad16_ckpt(C, xin[0], g[0], ks)
+                ref_layout[li] = True
+            else:
+                dw, db = _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout)
         if li > 0 or need_dx0:
             if kind == "1out":                       # reuses ijpack(g, -1) of the weight gradient
                 # each input block's gradient is written straight into its slot
@@ -1024,18 +1109,16 @@ def _x3_fast1x_layer(C, ctx, li, kind, w, xin, g, dws, dbs, main, side, shp, ks,
         for h in range(2):
             _pad_1ch(g[h].reshape(n, I * J, K * L), K, L, ks, 0, out=gp[h])
         with _OnSide(main, side, (xin, g, gp)):
-            R = sum(_wgrad1x(C, xin[a], gp[b], ks, False)[0] for a, b in ((0, 0), (0, 1), (1, 0)))
-            Rf = R[:, :, :cin].reshape((ks,) * 4 + (cin,)).flip(0, 1, 2, 3)
-            dws[li] = Rf.permute(2, 4, 3, 0, 1).unsqueeze(1).contiguous()
+            # (each product already in the checkpoint layout: the layout is linear)
+            dws[li] = sum(_wgrad1x(C, xin[a], gp[b], ks, False, cin, False)[0] for a, b in ((0, 0), (0, 1), (1, 0)))
             dbs[li] = (g[0].sum(dtype=torch.float32) + g[1].sum(dtype=torch.float32)).reshape(1)
         gn = torch.empty((2,) + tuple(shp) + (16,), dtype=torch.bfloat16, device=g.device)
         C.conv1x16(gp, _pack2(pack_w1x, transpose_for_dgrad(w)), None, xin[0], gn, ks, 2 | 4)
         return gn
     # first layer: xin = padded planes of the NC input [2, N, PPL]; g [2, 2V, ..., 16]
-    parts = [_wgrad1x(C, g[a], xin[b], ks, b == 0) for a, b in ((0, 0), (1, 0), (0, 1))]
-    R = parts[0][0] + parts[1][0] + parts[2][0]
-    dws[li] = R[:, :, :cout].reshape((ks,) * 4 + (cout,)).permute(2, 4, 3, 0, 1).unsqueeze(2).contiguous()
-    dbs[li] = (parts[0][1] + parts[1][1])[:cout]
+    parts = [_wgrad1x(C, g[a], xin[b], ks, b == 0, cout, True) for a, b in ((0, 0), (1, 0), (0, 1))]
+    dws[li] = parts[0][0] + parts[1][0] + parts[2][0]
+    dbs[li] = parts[0][1] + parts[1][1]
     return None
 
 

@@ -38,13 +38,13 @@ def main(argv=None):
     for fe in (0, 1):
         sel = [x for x in rows if x["fe_finetune"] == fe]
         keys = [k for k in sel[0] if k not in ("fe_finetune", "point_seed", "repeat")]
-        nc = [max(v for k, v in x.items() if k.startswith("nc")) for x in sel]
+        nc = [max(v for k, v in x.items() if k.startswith("layer")) for x in sel]
         spread = 0.0
         for s in args.seeds:
             rs = [x for x in sel if x["point_seed"] == s]
             for k in keys:
                 spread = max(spread, max(x[k] for x in rs) - min(x[k] for x in rs))
-        summary[f"fe{fe}"] = {"max_nc": max(nc), "max_vols": max(x["vols"] for x in sel),
+        summary[f"fe{fe}"] = {"max_layer": max(nc), "layer_by_point": nc, "max_vols": max(x["vols"] for x in sel),
                               "max_d_raw": max((x.get("d_raw_features", 0.0) for x in sel)),
                               "max_repeat_spread": spread}
     print(json.dumps({"summary": summary}), flush=True)

@@ -121,3 +121,28 @@ def test_process_correlation_padded_mm_bitwise():
             # partials with LDS float atomics (order not fixed): within fp32 rounding
             err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
             assert err < 1e-5, (name, err)
+
+
+def test_reduce_cols_matches_torch_layouts():
+    """reduce_cols (one launch for up to four segments: column sums of the
+    weight-gradient partials scattered into the checkpoint layout) against the
+    torch path of reduce_partials; the fixed summation order makes two runs
+    bitwise equal."""
+    import importlib
+    from ncnet_amd.ops import reference as ref
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    torch.manual_seed(1)
+    ks = 5
+    p16 = torch.randn(204, ks * ks, ks * ks, 16, 16, device=DEV)
+    pb = torch.randn(204, 16, device=DEV)
+    p1x = torch.randn(256, ks * ks, 32, 16, device=DEV)
+    f16 = lambda t: ref.conv4d_weight_from_std(nc._reduce_wgrad16(t, ks, 16, 16))  # noqa: E731
+    f_last = lambda t: t[:, :25, :16].reshape((ks,) * 4 + (16,)).flip(0, 1, 2, 3).permute(2, 4, 3, 0, 1).unsqueeze(1)  # noqa: E731
+    segs = [(p16, ("g16", ks), f16), (pb, None, None), (p1x, ("gl", ks), f_last)]
+    got = nc.reduce_partials(segs)
+    again = nc.reduce_partials(segs)
+    want = [f16(p16.double().sum(0)), pb.double().sum(0), f_last(p1x.double().sum(0))]
+    for g, a, w in zip(got, again, want):
+        assert g.shape == w.shape
+        assert torch.equal(g, a)
+        assert torch.allclose(g.double(), w, rtol=1e-5, atol=1e-4), (g.double() - w).abs().max()

@@ -75,14 +75,19 @@ def test_training_tracks_fp32_reference():
     assert summary["pck_final_hip"] > summary["pck_final_ref"] - 0.3, summary
 
 
-# bounds just above the errors measured at these four operating points
-# (scripts/oracle_tolerance.py, profiles/r5/quality/oracle_tolerance.json; one build
-# reproduces them bitwise): frozen trunk max NC 1.4e-2, volumes 2.6e-4;
-# fe_finetune NC 6.5e-3 / 1.4e-2 / 7.5e-3 / 5.1e-2 (point 30: a first-MM
-# near-tie), volumes 4.9e-4, raw-feature gradient 4.6e-2
+# bounds just above the errors measured at these four operating points by
+# scripts/oracle_tolerance.py (profiles/r5/quality/; one build reproduces them
+# bitwise; the per-layer metric joins each layer's weight and bias gradients):
+#   frozen trunk:  layer error <= 8.2e-3 (per-tensor NC error <= 1.4e-2 in an
+#                  earlier build whose different wgrad summation order moved
+#                  the operating points), volumes <= 3.4e-4;
+#   fe_finetune:   layer error 4.6e-3 .. 1.9e-2, volumes <= 4.9e-4, raw-feature
+#                  gradient <= 4.6e-2; a first-MutualMatching near-tie point
+#                  reached 3.9e-2 .. 5.1e-2 per NC tensor in the earlier build
+#                  (nc_any: one of the four points may sit at such a tie)
 ORACLE_POINTS = (0, 10, 20, 30)
 ORACLE_TOL = {0: {"vols": 5e-4, "nc": 2e-2, "nc_any": 2e-2},
-              1: {"vols": 1e-3, "nc": 2e-2, "nc_any": 6e-2, "d_raw": 6e-2}}
+              1: {"vols": 1e-3, "nc": 2.5e-2, "nc_any": 6e-2, "d_raw": 6e-2}}
 
 
 @pytest.fixture
@@ -117,7 +122,7 @@ def test_training_grads_vs_quantized_oracle(fe_finetune, deterministic_trunk):
     for s, e in runs.items():
         print(f"point {s}: quantized-oracle errors:", {k: f"{v:.2e}" for k, v in e.items()})
     assert runs[ORACLE_POINTS[0]] == again, (runs[ORACLE_POINTS[0]], again)
-    nc = sorted(max(v for k, v in e.items() if k.startswith("nc")) for e in runs.values())
+    nc = sorted(max(v for k, v in e.items() if k.startswith("layer")) for e in runs.values())
     vols = max(e["vols"] for e in runs.values())
     tol = ORACLE_TOL[fe_finetune]
     assert vols < tol["vols"], runs

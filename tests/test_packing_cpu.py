@@ -49,3 +49,26 @@ def test_packed_weights_plan_matches_packers(ks, shared):
         want = fn(conv4d_weight_to_std(ws[wi]).float())
         assert got.shape == want.shape
         assert torch.equal(got.to(torch.bfloat16), want.to(torch.bfloat16)), fn.__name__
+
+
+def test_reduce_partials_layouts_cpu():
+    """ops/neigh_consensus.reduce_partials (the CPU path of the reduce_cols
+    launch): the scatter map built from the layout function reproduces
+    layout(part.sum(0)) for the three weight-gradient layouts of the training
+    stack, slices included."""
+    from ncnet_amd.ops import reference as ref
+    from ncnet_amd.ops.neigh_consensus import _reduce_wgrad16, reduce_partials
+    torch.manual_seed(0)
+    ks = 5
+    p16 = torch.randn(6, ks * ks, ks * ks, 16, 16)
+    pb = torch.randn(6, 16)
+    p1x = torch.randn(5, ks * ks, 32, 16)
+    f16 = lambda t: ref.conv4d_weight_from_std(_reduce_wgrad16(t, ks, 16, 16))  # noqa: E731
+    f_first = lambda t: t[:, :25, :16].reshape((ks,) * 4 + (16,)).permute(2, 4, 3, 0, 1).unsqueeze(2)  # noqa: E731
+    f_last = lambda t: t[:, :25, :7].reshape((ks,) * 4 + (7,)).flip(0, 1, 2, 3).permute(2, 4, 3, 0, 1).unsqueeze(1)  # noqa: E731
+    got = reduce_partials([(p16, ("t16", ks), f16), (pb, None, None), (p1x, ("tf", ks), f_first),
+                           (p1x, ("tl", ks, 7), f_last)])
+    want = [f16(p16.sum(0)), pb.sum(0), f_first(p1x.sum(0)), f_last(p1x.sum(0))]
+    for g, w in zip(got, want):
+        assert g.shape == w.shape
+        assert torch.allclose(g, w, rtol=1e-6, atol=1e-6)
