@@ -308,6 +308,11 @@ def fold_frozen_bn(trunk: nn.Module) -> nn.Module:
     return t
 
 
+# images per stem conv call of FrozenResNetPlan: the batch of train.py's default
+# (16 pairs = 32 images), whose MIOpen solver choice the rounds' benches pinned
+STEM_CHUNK = 32
+
+
 class FrozenResNetPlan(nn.Module):
     """Inference plan of a frozen (BN-folded) ResNet trunk in one compute dtype.
 
@@ -425,6 +430,27 @@ class FrozenResNetPlan(nn.Module):
         _ext.ext().maxpool_bias_act(y, b.float().contiguous(), out, k, st, pad, 1 if relu else 0)
         return out
 
+    def _stem_chunked(self, x, w, b, stride, pad, relu, pool):
+        """The stem conv + fused bias / ReLU / max-pool over chunks of at most
+        STEM_CHUNK images, into one channels-last output; None where the pool
+        cannot be fused (the caller then runs the unchunked path)."""
+        from ..ops import _ext
+        k, st, pp = self._pool_args(pool)
+        if None in (k, st, pp) or not (x.dtype in (torch.bfloat16, torch.float16) and w.shape[0] % 8 == 0
+                                       and _ext.use_hip(x) and 2 * pp <= k):
+            return None
+        n = x.shape[0]
+        bf = b.float().contiguous()
+        out = None
+        for c0 in range(0, n, STEM_CHUNK):
+            y = F.conv2d(x[c0:c0 + STEM_CHUNK], w, None, stride, pad).contiguous(memory_format=torch.channels_last)
+            if out is None:
+                ho, wo = y.shape[-2:]
+                out = torch.empty((n, y.shape[1], (ho + 2 * pp - k) // st + 1, (wo + 2 * pp - k) // st + 1),
+                                  dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            _ext.ext().maxpool_bias_act(y, bf, out[c0:c0 + STEM_CHUNK], k, st, pp, 1 if relu else 0)
+        return out
+
     @staticmethod
     def _nconv(x: torch.Tensor, p, relu: bool, res: torch.Tensor | None = None) -> torch.Tensor:
         from ..ops import _ext
@@ -522,8 +548,17 @@ class FrozenResNetPlan(nn.Module):
                 bi += 1
             if kind == "conv":
                 w, b, stride, pad, relu = p
-                y = F.conv2d(x, w, None, stride, pad).contiguous(memory_format=torch.channels_last)
                 nxt = self.steps[si + 1] if si + 1 < len(self.steps) else None
+                if nxt is not None and nxt[0] == "maxpool" and x.is_cuda and x.shape[0] > STEM_CHUNK:
+                    # stem on MIOpen in fixed chunks of STEM_CHUNK images: its solver
+                    # search at a large batch can settle on a naive kernel (a whole
+                    # batch-256 step measured 1002 vs 306 ms in one of two runs);
+                    # each chunk's bias + ReLU + max-pool writes its slice of the output
+                    pooled = self._stem_chunked(x, w, b, stride, pad, relu, nxt[1])
+                    if pooled is not None:
+                        x, fused_pool = pooled, True
+                        continue
+                y = F.conv2d(x, w, None, stride, pad).contiguous(memory_format=torch.channels_last)
                 if nxt is not None and nxt[0] == "maxpool" and self._pool_fusable(y, nxt[1]):
                     # stem: bias + ReLU + max-pool in one pass (csrc/epilogue.hip maxpool_bias_act)
                     x = self._maxpool_bias_act(y, b, nxt[1], relu)

@@ -517,6 +517,24 @@ def test_frozen_trunk_plan_gpu():
     assert rel_l2(p.float(), r) < 3e-2
 
 
+def test_frozen_trunk_plan_stem_chunks(monkeypatch):
+    """The stem of a batch larger than STEM_CHUNK runs chunk by chunk (each
+    chunk's fused bias / ReLU / max-pool writes its slice of one output):
+    same features as the unchunked stem, to bf16 rounding."""
+    from ncnet_amd.models import backbones as bb
+    torch.manual_seed(0)
+    t = bb.resnet_trunk("resnet101", "layer3").eval().to(DEV)
+    x = torch.randn(5, 3, 96, 128, device=DEV)
+    plan = bb.FrozenResNetPlan(bb.fold_frozen_bn(t), torch.bfloat16)
+    plan.use_graphs = False
+    with torch.no_grad():
+        whole = plan(x)
+        monkeypatch.setattr(bb, "STEM_CHUNK", 2)
+        chunked = plan(x)
+    assert chunked.shape == whole.shape
+    assert rel_l2(chunked.float(), whole.float()) < 1e-2
+
+
 def test_fp8_l2norm_and_correlation():
     """fp8 (OCP e4m3) operands: pack kernel vs torch's e4m3 cast, MX-fp8 MFMA
     GEMM (plain and fused 2x2x2x2 pool) vs fp64 math on the same fp8 values.
