@@ -521,9 +521,26 @@ def _side_stream(dev: torch.device):
     return st
 
 
+# side-stream inputs kept alive until the backward joins the side stream back
+# (_join_side).  Not record_stream: a block marked in use by the side stream
+# is reusable only once the allocator sees the side stream's event complete --
+# with the host a step ahead of the GPU that is never in time, so every step
+# hipMalloc'ed fresh blocks for its 16-channel volumes (reserved memory grew
+# to the whole 288 GB at a per-GPU batch of 256 and the allocator's
+# release-and-retry stalled whole steps for seconds).  Freed on the host after
+# main.wait_stream(side), the blocks return to main's pool, where every later
+# use is ordered after the side stream's reads.
+_SIDE_KEEP: dict = {}
+
+
+def _join_side(main, side):
+    main.wait_stream(side)
+    _SIDE_KEEP.pop(id(side), None)
+
+
 class _OnSide:
     """Run a block on the side stream after everything queued on ``main``;
-    inputs are marked in use by the side stream, outputs by ``main``."""
+    inputs stay referenced until _join_side, outputs are marked in use by ``main``."""
 
     def __init__(self, main, side, inputs):
         self.main, self.side, self.inputs = main, side, inputs
@@ -533,8 +550,7 @@ class _OnSide:
         if self.side is None:
             return self
         self.side.wait_stream(self.main)
-        for t in self.inputs:
-            t.record_stream(self.side)
+        _SIDE_KEEP.setdefault(id(self.side), []).extend(self.inputs)
         self.ctx = torch.cuda.stream(self.side)
         self.ctx.__enter__()
         return self
@@ -676,7 +692,7 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
         dws[li] = dw
         dbs[li] = db
     if side is not None:
-        main.wait_stream(side)
+        _join_side(main, side)
         for t in dws + dbs:          # produced on the side stream, consumed (and freed) on main
             t.record_stream(main)
     return [d if ref_layout[i] else ref.conv4d_weight_from_std(d) for i, d in enumerate(dws)], dbs, gx0
@@ -1261,7 +1277,7 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
                                 ks, 2)
             g = gn
         if side is not None:
-            main.wait_stream(side)
+            _join_side(main, side)
             for t in dws + dbs:
                 t.record_stream(main)
         if gx is not None:
