@@ -23,7 +23,9 @@ namespace ncnet {
 
 namespace cv {
 constexpr int BK = 64;
-__device__ __forceinline__ uint32_t toff(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ (row & 7)) << 4)); }
+// chunk ^ ((row >> 1) & 7): the 16 rows of a ds_read_b128 lane group land on 16
+// distinct 16-B bank slots (chunk ^ (row & 7) put rows r and r + 8 on one slot)
+__device__ __forceinline__ uint32_t toff(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4)); }
 }  // namespace cv
 
 struct Conv2dArgs {
@@ -360,7 +362,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void conv2d_nhwc_v2_kernel(Conv2dA
 // ===========================================================================
 namespace cv3 {
 constexpr int NS = 3;
-__device__ __forceinline__ uint32_t toff(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ (row & 7)) << 4)); }
+// chunk ^ ((row >> 1) & 7): the 16 rows of a ds_read_b128 lane group land on 16
+// distinct 16-B bank slots (chunk ^ (row & 7) put rows r and r + 8 on one slot)
+__device__ __forceinline__ uint32_t toff(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4)); }
 template <int TM, int TN>
 struct Geo {
   static constexpr int BM = 16 * TM, BN = 64 * TN;
@@ -417,7 +421,7 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
       kind[m] = 0;
       const int row = 8 * j + sub;
       const int pix = m0 + row;
-      coff[m] = (uint32_t)((pos ^ (row & 7)) * 8);
+      coff[m] = (uint32_t)((pos ^ ((row >> 1) & 7)) * 8);
       dst[m] = (uint32_t)(j * 1024);
       if (pix < p.M) {
         const int wo = pix % p.Wo, t = pix / p.Wo, ho = t % p.Ho, n = t / p.Ho;
@@ -428,7 +432,7 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
     } else if (j < G::NI) {
       kind[m] = 1;
       const int row = 8 * (j - G::NIA) + sub;
-      b_src[m] = p.W + (size_t)(n0 + row) * K + (pos ^ (row & 7)) * 8;
+      b_src[m] = p.W + (size_t)(n0 + row) * K + (pos ^ ((row >> 1) & 7)) * 8;
       dst[m] = (uint32_t)(BM * 128 + (j - G::NIA) * 1024);
     } else {
       kind[m] = 2;

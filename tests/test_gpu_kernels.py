@@ -679,8 +679,9 @@ def test_nc_forward_deterministic_and_fully_written():
     (128, 192, 3, 1, 1, True, False, (2, 19, 23)),
     # large enough for the 128-row tiles (>= 512 workgroups)
     (64, 128, 3, 1, 1, True, True, (4, 129, 127)), (64, 64, 1, 1, 0, False, True, (4, 129, 127)),
-    # >= 512 tiles of 256 rows: the 8-wave 256 x 128 variant
-    (64, 128, 3, 1, 1, True, True, (4, 160, 208))])
+    # >= 384 tiles of 256 rows: the 8-wave 256 x 128 variant (3x3 / 1x1 + residual / stride 2)
+    (64, 128, 3, 1, 1, True, True, (4, 160, 208)), (256, 1024, 1, 1, 0, True, True, (8, 60, 60)),
+    (128, 128, 3, 2, 1, False, True, (16, 101, 99))])
 def test_conv2d_nhwc_kernel(cin, cout, k, stride, pad, res, relu, shape):
     """NHWC implicit-GEMM conv (+bias, +residual, ReLU) vs F.conv2d in fp64 on bf16 inputs
     (both the 64- and 128-row tile variants)."""
