@@ -286,7 +286,7 @@ def main(argv=None):
     ap.add_argument("--profile", type=str, default="", help="write a torch.profiler trace to this dir")
     ap.add_argument("--only-secondary", type=str, default="",
                     help="debug: skip the headline and print one secondary record "
-                         "(nc_fp32 | fe_finetune | train | train_ivd, at --image-size)")
+                         "(nc_fp32 | nc_mixed | fe_finetune | train | train_ivd, at --image-size)")
     ap.add_argument("--inloc", type=int, default=1,
                     help="1: after the timed training steps of a 1-GPU run, also time the InLoc inference configs "
                          "(BASELINE configs 3-5: 1600 px bf16, 3200 px bf16, 3200 px fp8) into config.secondary")
@@ -295,6 +295,8 @@ def main(argv=None):
         return _self_launch(args, argv)
     if args.only_secondary:
         fn = {"nc_fp32": lambda: _nc_precision_secondary(args.batch, args.image_size, "fp32", args.steps, args.warmup),
+              "nc_mixed": lambda: _nc_precision_secondary(args.batch, args.image_size, "mixed", args.steps,
+                                                          args.warmup),
               "fe_finetune": lambda: _fe_finetune_secondary(args.batch, args.image_size, args.steps, args.warmup),
               "train": lambda: _train_secondary(args.batch, args.image_size, steps=args.steps, warmup=args.warmup),
               "train_ivd": lambda: _train_secondary(args.batch, args.image_size, (3, 3), (16, 1), args.steps,
@@ -408,6 +410,10 @@ def main(argv=None):
             secondary["train_nc_fp32"] = _nc_precision_secondary(SECONDARY_BATCH, s, "fp32")
         except Exception as e:  # the headline record must still print
             secondary["train_nc_fp32"] = {"error": repr(e)}
+        try:
+            secondary["train_nc_mixed"] = _nc_precision_secondary(SECONDARY_BATCH, s, "mixed")
+        except Exception as e:  # the headline record must still print
+            secondary["train_nc_mixed"] = {"error": repr(e)}
         # the training step at the other --image_size values and the IVD recipe
         for name, size, ks, ch in (("train_320", 320, (5, 5, 5), (16, 16, 1)),
                                    ("train_480", 480, (5, 5, 5), (16, 16, 1)),

@@ -258,10 +258,13 @@ class ImMatchNet(nn.Module):
         self.corr_dtype = corr_dtype
         # nc_precision='fp32': NeighConsensus forward AND backward as bf16x3 splits
         # (fp32-accurate training at 3x the NC cost; ops/neigh_consensus.py NeighConsensusX3Fn)
-        if nc_precision not in ("bf16", "fp32"):
-            raise ValueError("nc_precision must be 'bf16' or 'fp32'")
+        # nc_precision='mixed': the cheapest mix the per-stage ablation found to
+        # train like 'fp32' (profiles/r5/ablation): fp32-accurate (bf16x3) trunk
+        # and NeighConsensus forward, bf16 correlation and NeighConsensus backward
+        if nc_precision not in ("bf16", "fp32", "mixed"):
+            raise ValueError("nc_precision must be 'bf16', 'fp32' or 'mixed'")
         self.nc_precision = nc_precision
-        if nc_precision == "fp32":
+        if nc_precision in ("fp32", "mixed"):
             # fp32-accurate training: fp32 trunk, split (bf16x3) correlation when the
             # trunk is frozen, bf16x3 NeighConsensus forward and backward
             self.compute_dtype = torch.float32
@@ -272,7 +275,7 @@ class ImMatchNet(nn.Module):
         # fp32-accurate training runs its frozen trunk as bf16x3 splits (3x the bf16
         # MFMA work instead of MIOpen's fp32 convs at 1/16 of the bf16 rate); fp32
         # inference (corr_dtype='fp32', parity runs) keeps MIOpen's true fp32
-        self.FeatureExtraction.fp32_trunk = "x3" if nc_precision == "fp32" else "miopen"
+        self.FeatureExtraction.fp32_trunk = "x3" if nc_precision in ("fp32", "mixed") else "miopen"
         self.FeatureCorrelation = FeatureCorrelation(shape="4D", normalization=False)
         self.NeighConsensus = NeighConsensus(use_cuda=self.use_cuda, kernel_sizes=list(ncons_kernel_sizes),
                                              channels=list(ncons_channels))
@@ -320,7 +323,8 @@ class ImMatchNet(nn.Module):
     def process_correlation(self, corr4d: torch.Tensor) -> torch.Tensor:
         """MutualMatching -> NeighConsensus -> MutualMatching (lib/model.py:274-276)."""
         self.NeighConsensus.fp8 = self.corr_dtype == "fp8"
-        self.NeighConsensus.precision = "fp32" if "fp32" in (self.corr_dtype, self.nc_precision) else "bf16"
+        self.NeighConsensus.precision = ("fp32" if "fp32" in (self.corr_dtype, self.nc_precision)
+                                         else "mixed" if self.nc_precision == "mixed" else "bf16")
         nc = self.NeighConsensus
         if (not torch.is_grad_enabled() and nc.symmetric_mode and corr4d.is_cuda
                 and tuple(corr4d.shape[2:4]) == tuple(corr4d.shape[4:6])
@@ -413,6 +417,8 @@ class ImMatchNet(nn.Module):
         one step ahead on a side stream when the trunk is frozen)."""
         h, w = hw
         if isinstance(f, tuple):               # split operands (nc_precision / corr_dtype 'fp32')
+            if _nc_ops.x3_dropped("corr"):     # precision ablation: bf16 correlation operands
+                f = (f[0], torch.zeros_like(f[1]))
             amap, bmap = _pair_maps(b, f[0].device)
             with segment("correlation"):
                 corr = correlation_x3((f[0][:b], f[1][:b]), (f[0][b:], f[1][b:]), amap, bmap)

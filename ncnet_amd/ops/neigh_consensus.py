@@ -33,6 +33,7 @@ kernels (even kernel sizes) raises unless config.RUNTIME.allow_torch_fallback
 """
 from __future__ import annotations
 
+import contextlib
 import functools
 
 import numpy as np
@@ -613,10 +614,13 @@ def _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout):
 
 
 def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool, fast1x: bool = False,
-               packs=None):
+               packs=None, saved_lo=None):
     """g_last: grad w.r.t. the last conv's PRE-activation, bf16: [V,I,J,K,L] for
     a 1-channel output, else blocks [NB, V,I,J,K,L,16].
-    Returns (dW list in checkpoint layout, db list, grad of x0 fp32 or None)."""
+    Returns (dW list in checkpoint layout, db list, grad of x0 fp32 or None).
+    ``saved_lo`` (nc_precision='mixed', fast1x only): per layer the lo part of
+    a bf16x3-split forward input; each weight gradient then adds the
+    (X_lo, G) product to the (X_hi, G) one (G bf16)."""
     C = _ext.ext()
     nl = len(kinds)
     dws, dbs = [None] * nl, [None] * nl
@@ -643,8 +647,12 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
             if kind == "1out":                       # padded planes of the 1-channel output gradient
                 gp = _pad_1ch(g.reshape(g.shape[0], g.shape[1] * g.shape[2], g.shape[3] * g.shape[4]),
                               g.shape[3], g.shape[4], ks, 0)
-                with _OnSide(main if li > 0 else None, side if li > 0 else None, (xin, g, gp)):
+                xlo = saved_lo[li] if saved_lo is not None else None
+                with _OnSide(main if li > 0 else None, side if li > 0 else None,
+                             (xin, g, gp) + ((xlo,) if xlo is not None else ())):
                     dw, _ = _wgrad1x(C, xin[0], gp, ks, False, cin, False)
+                    if xlo is not None:
+                        dw = dw + _wgrad1x(C, xlo[0], gp, ks, False, cin, False)[0]
                     db = g.sum(dtype=torch.float32).reshape(1)
                 if li > 0 or need_dx0:
                     gn = torch.empty((1,) + tuple(hin.shape[1:]), dtype=torch.bfloat16, device=g.device)
@@ -653,6 +661,8 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
                     g = gn
             else:                                    # first layer: xin = padded NC-input planes
                 dw, db = _wgrad1x(C, g[0], xin, ks, True, cout, True)
+                if saved_lo is not None:
+                    dw = dw + _wgrad1x(C, g[0], saved_lo[li], ks, False, cout, True)[0]
                 if need_dx0:
                     gx0 = conv_layer(g, transpose_for_dgrad(w), cout, 1, relu=False)
             dws[li] = dw
@@ -663,11 +673,14 @@ def _stack_bwd(g_last: torch.Tensor, saved, ws, kinds, channels, need_dx0: bool,
             gs = torch.empty((ij_groups(ks),) + tuple(g.shape) + (16,), dtype=torch.bfloat16, device=g.device)
             C.ijpack(g, gs, ks, -1)                  # adjoint of ijsum: shared by wgrad and dgrad
         on_side = li > 0
+        xlo = saved_lo[li] if saved_lo is not None else None
         with _OnSide(main if on_side else None, side if on_side else None,
-                     tuple(t for t in (xin, g, gs) if t is not None)):
+                     tuple(t for t in (xin, g, gs, xlo) if t is not None)):
             if kind == "16" and cin == 16 and cout == 16:
                 # one reduce_cols launch: partials -> checkpoint layout + bias
                 dw, db = wgrad16_ckpt(C, xin[0], g[0], ks)
+                if xlo is not None:
+                    dw = dw + wgrad16_ckpt(C, xlo[0], g[0], ks)[0]
                 ref_layout[li] = True
             else:
                 dw, db = _layer_wgrad(C, kind, xin, g, gs, ks, cin, cout)
@@ -1086,6 +1099,43 @@ class NeighConsensusX3Fn(torch.autograd.Function):
 # 1 -> (16 ->)* 1 stacks with KS 3 / 5 (every NC-Net config); others use
 # NeighConsensusX3Fn's per-conv path.
 
+# bf16x3 precision ablation (scripts/train_quality.py --x3-drop): stages of the
+# fp32-accurate training path that run in plain bf16 instead (their lo parts
+# zeroed: bf16 x bf16 products accumulated in fp32, exactly the bf16 path's
+# arithmetic), to find which stages the weak-loss signal needs:
+#   corr     the correlation operands (the L2-normalised trunk features)
+#   nc_in    the NeighConsensus input (the MutualMatching output)
+#   nc_w     the NeighConsensus weights
+#   nc_act   the hidden NeighConsensus activations
+#   nc_grad  the backward's activation gradients
+#   nc_w_bwd the NeighConsensus weights in the backward only (data gradients)
+X3_STAGES = ("corr", "nc_in", "nc_w", "nc_act", "nc_grad", "nc_w_bwd")
+_X3_DROP: frozenset = frozenset()
+
+
+@contextlib.contextmanager
+def x3_ablation(stages):
+    """Run the bf16x3 training path with ``stages`` (subset of X3_STAGES) in bf16."""
+    global _X3_DROP
+    bad = set(stages) - set(X3_STAGES)
+    if bad:
+        raise ValueError(f"unknown x3 stages {sorted(bad)}; known: {X3_STAGES}")
+    old, _X3_DROP = _X3_DROP, frozenset(stages)
+    try:
+        yield
+    finally:
+        _X3_DROP = old
+
+
+def x3_dropped(stage: str) -> bool:
+    return stage in _X3_DROP
+
+
+def _x3_weights(ws, backward: bool = False):
+    drop = "nc_w" in _X3_DROP or (backward and "nc_w_bwd" in _X3_DROP)
+    return [w.to(torch.bfloat16).float() for w in ws] if drop else ws
+
+
 def _wsplit(w: torch.Tensor):
     hi = w.to(torch.bfloat16).float()
     return hi, w - hi
@@ -1176,6 +1226,9 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
             C.ijpack(xsp[0], xs[0], ks0, 1)
             C.ijpack(xsp[1], xs[1], ks0, 1)
             del xsp
+        if "nc_in" in _X3_DROP:
+            xs[1].zero_()
+        ws = _x3_weights(ws)
         saved = [xs]
         h = None
         for li, kind in enumerate(kinds):
@@ -1195,6 +1248,8 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
                                 _pad_bias(b, 16), None, a[0], a[1], ks, 1)
             else:
                 C.conv16_fwd_x3(h[0], h[1], _pack2(pack_w16, w), _pad_bias(b, 16), None, a[0], a[1], ks, 1)
+            if "nc_act" in _X3_DROP:
+                a[1].zero_()
             saved.append(a)
             h = a
         z = h                                                      # [2V, I, J, K, L] fp32 (ReLU'd)
@@ -1211,7 +1266,7 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
         nl = len(kinds)
         z, *rest = ctx.saved_tensors
         params, saved = rest[:2 * nl], rest[2 * nl:]
-        ws = [_std(w) for w in params[0::2]]
+        ws = _x3_weights([_std(w) for w in params[0::2]], backward=True)
         V, I, J, K, L = ctx.dims
         R, Cc = I * J, K * L
         shp = tuple(z.shape)
@@ -1227,6 +1282,8 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
             main = torch.cuda.current_stream(dev)
             side = _side_stream(dev)
         for li in range(nl - 1, -1, -1):
+            if "nc_grad" in _X3_DROP:
+                g[1].zero_()
             kind, w = kinds[li], ws[li]
             ks = w.shape[-1]
             cout = channels[li]
@@ -1283,6 +1340,54 @@ class NeighConsensusX3FusedFn(torch.autograd.Function):
         if gx is not None:
             gx = gx[:V] + gx[V:].permute(0, 3, 4, 1, 2)
             gx = gx.reshape(V, 1, I, J, K, L)
+        grads = []
+        for dw, db in zip(dws, dbs):
+            grads += [dw, db]
+        return (gx, None, None, *grads)
+
+
+class NeighConsensusMixedFn(torch.autograd.Function):
+    """nc_precision='mixed' training NeighConsensus: the bf16x3 forward of
+    NeighConsensusX3FusedFn (fp32-accurate input, weights and hidden
+    activations) with a bf16 backward -- bf16 gradients, bf16 weights in the
+    data gradients, each weight gradient the (X_hi, G) + (X_lo, G) products --
+    on the bf16 training kernels (the padded-plane 1-channel path).  The
+    per-stage ablation (scripts/precision_ablation.py, profiles/r5/ablation)
+    measured this mix at the PCK of the all-bf16x3 mode (0.533 vs 0.535 over 4
+    seeds) for 2/3 of its NeighConsensus work."""
+
+    @staticmethod
+    def forward(ctx, x, kinds, channels, *params):
+        y = NeighConsensusX3FusedFn.forward(ctx, x, kinds, channels, *params)
+        ctx.nparams = len(params)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        if not ctx.fast1x:
+            return NeighConsensusX3FusedFn.backward(ctx, gy)
+        C = _ext.ext()
+        kinds, channels = ctx.kinds, ctx.channels
+        nl = len(kinds)
+        z, *rest = ctx.saved_tensors
+        params, saved = rest[:2 * nl], rest[2 * nl:]
+        ws = list(params[0::2])
+        V, I, J, K, L = ctx.dims
+        R, Cc = I * J, K * L
+        gz = torch.empty(z.numel(), dtype=torch.bfloat16, device=z.device)
+        C.combine_bwd(gy.reshape(V, R, Cc).float().contiguous(), z, gz, R, Cc)
+        xs, acts = saved[0], saved[1:]
+        hi = [xs[0]] + [a[0:1] for a in acts]
+        lo = [xs[1]] + [a[1:2] for a in acts]
+        need_dx0 = ctx.needs_input_grad[0]
+        dws, dbs, g0 = _stack_bwd(gz.reshape(tuple(z.shape)), hi, ws, kinds, channels, need_dx0, True,
+                                  _stack_packs(ws, kinds), saved_lo=lo)
+        gx = None
+        if need_dx0:
+            g0 = g0.reshape(-1)
+            ga, gbt = g0[:V * R * Cc], g0[V * R * Cc:]
+            gb = _swap_flat(gbt.reshape(V, Cc, R), (K, L, I, J))
+            gx = (ga.reshape(V, R, Cc) + gb).reshape(V, 1, I, J, K, L)
         grads = []
         for dw, db in zip(dws, dbs):
             grads += [dw, db]
@@ -1487,7 +1592,7 @@ def fused_applies(x: torch.Tensor, weights, channels, fp8: bool = False, precisi
     """Would ``neigh_consensus`` run this input on the fused kernel?"""
     kernel_sizes = [w.shape[0] for w in weights]
     kinds = layer_kinds(channels, kernel_sizes)
-    return (x.is_cuda and _ext.use_hip(x) and kinds is not None and precision != "fp32"
+    return (x.is_cuda and _ext.use_hip(x) and kinds is not None and precision not in ("fp32", "mixed")
             and _fused_ok(kinds, kernel_sizes, channels, x) and not (fp8 and _config.RUNTIME.nc_fp8))
 
 
@@ -1546,12 +1651,16 @@ def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool 
         if kinds is None:
             _ext.torch_fallback(f"NeighConsensus kernel sizes {kernel_sizes}")
         else:
-            if precision == "fp32":
+            if precision in ("fp32", "mixed"):
                 _ext.count("nc_x3")
                 if torch.is_grad_enabled() and (x.requires_grad or any(w.requires_grad for w in weights)):
                     params = []
                     for w, b in zip(weights, biases):
                         params += [w, b]
+                    if precision == "mixed" and x3_fused_ok(kinds, channels, kernel_sizes, x, symmetric):
+                        _ext.count("nc_mixed")
+                        return NeighConsensusMixedFn.apply(x.float().contiguous(), tuple(kinds), tuple(channels),
+                                                           *params)
                     if x3_fused_ok(kinds, channels, kernel_sizes, x, symmetric):
                         _ext.count("nc_x3_fused")
                         return NeighConsensusX3FusedFn.apply(x.float().contiguous(), tuple(kinds), tuple(channels),

@@ -86,6 +86,14 @@ def run(args):
     if args.nc_precision == "fp32":      # fp32-accurate HIP training: bf16x3 correlation + NC
         m_h.nc_precision = "fp32"
         m_h.compute_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[args.hip_trunk]
+    elif args.nc_precision == "mixed":   # ImMatchNet(nc_precision='mixed'): bf16x3 trunk + NC forward
+        m_h.nc_precision = "mixed"
+        m_h.compute_dtype = torch.float32
+        m_h.FeatureExtraction.fp32_trunk = "x3"
+    if args.fp32_trunk:                  # 'x3' (bf16x3 plan) or 'miopen' (true fp32) for the fp32 trunk
+        m_h.FeatureExtraction.fp32_trunk = args.fp32_trunk
+    if getattr(args, "no_ref", False):
+        return _run_hip_only(args, m_h, dev)
     rdt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[args.ref_dtype]
     alg = ReferenceAlgorithm(m_r, rdt, conv=ref.conv4d)   # same sums as the reference, k conv3d per layer
     # fp16 autocast needs loss scaling (the weak loss is ~1e-8 in this regime)
@@ -137,6 +145,33 @@ def run(args):
     return res
 
 
+def _run_hip_only(args, m_h, dev):
+    """The HIP run alone (precision ablations: scripts/precision_ablation.py):
+    loss curve and PCK before / after, no reference run."""
+    p_h = [p for p in m_h.parameters() if p.requires_grad]
+    opt_h = make_adam(p_h, args.lr)
+    eval_pairs = [synthetic_correspondence_batch(args.batch, args.image_size, dev, seed=10_000 + i)
+                  for i in range(args.eval_batches)]
+    fwd_h = lambda b: m_h(b)  # noqa: E731
+    m_h.eval()
+    res = {"config": vars(args), "pck_init_hip": pck_of(fwd_h, eval_pairs)}
+    m_h.train()
+    lh = []
+    for step in range(args.steps):
+        batch = synthetic_correspondence_batch(args.batch, args.image_size, dev, seed=step)
+        batch = {"source_image": batch["source_image"], "target_image": batch["target_image"]}
+        opt_h.zero_grad(set_to_none=True)
+        loss = weak_loss(m_h, batch)
+        loss.backward()
+        opt_h.step()
+        lh.append(float(loss.detach()))
+    m_h.eval()
+    res.update({"loss_hip": lh, "pck_final_hip": pck_of(fwd_h, eval_pairs)})
+    w = max(1, args.steps // 10)
+    res["summary"] = {"loss_first_hip": float(np.mean(lh[:w])), "loss_last_hip": float(np.mean(lh[-w:])), "window": w}
+    return res
+
+
 def _heartbeat(period=60):
     """MIOpen compiles its conv3d kernels (the reference run) on first use,
     minutes of silence on a fresh box: keep the log alive."""
@@ -160,15 +195,23 @@ def main(argv=None):
     ap.add_argument("--eval-batches", type=int, default=8)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--last-layer", type=str, default="", help="trunk cut (default layer3, the reference's)")
-    ap.add_argument("--nc-precision", choices=["bf16", "fp32"], default="bf16",
+    ap.add_argument("--nc-precision", choices=["bf16", "fp32", "mixed"], default="bf16",
                     help="HIP run's NeighConsensus precision (fp32: bf16x3 forward+backward)")
     ap.add_argument("--hip-trunk", choices=["bf16", "fp32"], default="fp32",
                     help="trunk dtype of the --nc-precision fp32 HIP run (the trunk is frozen)")
     ap.add_argument("--ref-dtype", choices=["fp32", "bf16", "fp16"], default="fp32",
                     help="the reference run's compute dtype (bf16 / fp16: autocast; fp16 with loss scaling)")
+    ap.add_argument("--x3-drop", type=str, default="",
+                    help="with --nc-precision fp32: comma list of bf16x3 stages run in plain bf16 "
+                         "(ops/neigh_consensus.py X3_STAGES: corr, nc_in, nc_w, nc_act, nc_grad)")
+    ap.add_argument("--no-ref", action="store_true", help="skip the fp32 reference run (ablations)")
+    ap.add_argument("--fp32-trunk", choices=["", "x3", "miopen"], default="",
+                    help="the fp32 trunk's implementation (default: the mode's own)")
     ap.add_argument("--out", type=str, default="")
     a = ap.parse_args(argv)
-    res = run(a)
+    from ncnet_amd.ops.neigh_consensus import x3_ablation
+    with x3_ablation([x for x in a.x3_drop.split(",") if x]):
+        res = run(a)
     print(json.dumps({k: v for k, v in res.items() if k not in ("loss_hip", "loss_ref")}))
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

@@ -237,3 +237,36 @@ def test_trunk_x3_vs_miopen_fp32():
     assert e_pair < 1e-4, e_pair
     same = (got.argmax(1) == ref32.argmax(1)).float().mean().item()
     assert same > 0.99, same
+
+
+@pytest.mark.parametrize("ks,ch,shape", [((5, 5, 5), (16, 16, 1), (1, 1, 25, 25, 25, 25)),
+                                         ((3, 3), (16, 1), (1, 1, 25, 25, 25, 25))])
+def test_mixed_backward_matches_x3_ablation(ks, ch, shape):
+    """precision='mixed' (NeighConsensusMixedFn: the bf16x3 forward, a bf16
+    backward on the padded-plane training kernels with the (X_lo, G) weight-
+    gradient products) against the bf16x3 stack run with the same stages
+    dropped to bf16 (x3_ablation nc_grad + nc_w_bwd: mathematically the same
+    products): identical forward, gradients within the summation-order noise."""
+    from ncnet_amd.ops.neigh_consensus import neigh_consensus, x3_ablation
+    torch.manual_seed(8)
+    x0 = torch.rand(shape, device="cuda")
+    outs = {}
+    for mode in ("mixed", "ablation"):
+        ws, bs = _params(ks, ch, 12)
+        x = x0.clone().requires_grad_(True)
+        if mode == "mixed":
+            n0 = _ext.DISPATCH["nc_mixed"]
+            y = neigh_consensus(x, ws, bs, list(ch), symmetric=True, precision="mixed")
+            assert _ext.DISPATCH["nc_mixed"] == n0 + 1
+        else:
+            with x3_ablation(["nc_grad", "nc_w_bwd"]):
+                y = neigh_consensus(x, ws, bs, list(ch), symmetric=True, precision="fp32")
+        gy = torch.rand(y.shape, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+        with x3_ablation(["nc_grad", "nc_w_bwd"] if mode == "ablation" else []):
+            (y * gy).sum().backward()
+        outs[mode] = [y.detach()] + [x.grad] + [t.grad for pair in zip(ws, bs) for t in pair]
+    errs = [rl2(a, b) for a, b in zip(outs["mixed"], outs["ablation"])]
+    print("mixed vs ablation:", [f"{e:.1e}" for e in errs])
+    assert outs["mixed"][0].abs().max() > 0 and all(t.abs().max() > 0 for t in outs["mixed"][1:])
+    assert errs[0] == 0.0, errs
+    assert max(errs[1:]) < 2e-3, errs

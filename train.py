@@ -9,15 +9,18 @@ Same flags and defaults as the reference, plus:
   --max_steps S        stop after S training steps (smoke / profiling)
   --metrics PATH       JSONL metrics (rank 0)
   --dtype bf16|fp32    backbone compute dtype of the default (bf16) NC mode
-  --nc_precision bf16|fp32
+  --nc_precision bf16|mixed|fp32
                        bf16 (default, the headline benchmark): bf16 MFMA operands,
                        fp32 accumulation.  fp32: fp32-accurate training -- fp32
                        trunk, bf16x3 correlation and a bf16x3 NeighConsensus
                        forward AND backward on the fused kernels (~16 mantissa
-                       bits per operand; 204 pairs/s vs 682 on one MI355X,
-                       profiles/r3/x3/).
+                       bits per operand).  mixed: the stages the per-stage
+                       ablation found necessary (profiles/r5/ablation): the
+                       fp32-accurate trunk and NeighConsensus forward, a bf16
+                       correlation and bf16 NeighConsensus backward -- the PCK
+                       of fp32 mode (0.533 vs 0.535, 4 seeds) at 2/3 of its NC work.
 
-Which precision to train with: use --nc_precision fp32 whenever the weak
+Which precision to train with: use --nc_precision mixed (or fp32) whenever the weak
 loss's signal is below bf16 resolution -- the first steps from a random or
 weakly trained NC, or a trunk whose features are nearly collinear (random-init
 trunks: per-step loss ~1e-8).  There the bf16 mode loses the gradient
@@ -90,10 +93,11 @@ def build_parser():
     p.add_argument("--max_steps", type=int, default=0)
     p.add_argument("--metrics", type=str, default="")
     p.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--nc_precision", type=str, default="bf16", choices=["bf16", "fp32"],
+    p.add_argument("--nc_precision", type=str, default="bf16", choices=["bf16", "mixed", "fp32"],
                    help="fp32: fp32-accurate training (fp32 trunk, bf16x3 correlation + NeighConsensus fwd/bwd on "
-                        "the fused kernels); use it when the weak-loss signal is below bf16 resolution (see --help text "
-                        "at the top of train.py)")
+                        "the fused kernels); mixed: fp32-accurate trunk + NeighConsensus forward, bf16 correlation "
+                        "and backward (trains like fp32, cheaper); use either when the weak-loss signal is below bf16 "
+                        "resolution (see --help text at the top of train.py)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--segment_timing", action="store_true")
     p.add_argument("--profile", type=str, default="")
