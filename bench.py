@@ -69,8 +69,12 @@ def _inloc_secondary():
     kernels)."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import bench_inloc
+    from ncnet_amd.eval.inloc import INLOC_CUDNN_BENCHMARK
     from ncnet_amd.models import ImMatchNet
     out = {}
+    # eval_inloc.py's MIOpen state, not the training headline's solver search
+    old_bench = torch.backends.cudnn.benchmark
+    torch.backends.cudnn.benchmark = INLOC_CUDNN_BENCHMARK
     try:
         torch.manual_seed(0)
         model = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], half_precision=True,
@@ -98,6 +102,7 @@ def _inloc_secondary():
         del model
     except Exception as e:  # the headline record must still print
         out["error"] = repr(e)
+    torch.backends.cudnn.benchmark = old_bench
     torch.cuda.empty_cache()
     return out
 

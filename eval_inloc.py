@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from ncnet_amd.data.transforms import read_image  # noqa: E402
 from ncnet_amd.engine.checkpoint import str_to_bool  # noqa: E402
-from ncnet_amd.eval.inloc import (PairMatcher, load_shortlist, n_matches, output_folder, pair_matches, prepare_image,  # noqa: E402
+from ncnet_amd.eval.inloc import (INLOC_CUDNN_BENCHMARK, PairMatcher, load_shortlist, n_matches, output_folder, pair_matches, prepare_image,  # noqa: E402
                                   save_query)
 from ncnet_amd.models import ImMatchNet  # noqa: E402
 from ncnet_amd.parallel.dist import barrier, destroy, init_distributed  # noqa: E402
@@ -110,6 +110,7 @@ def main(argv=None):
         args.inloc_shortlist, args.query_path, args.pano_path = make_synthetic_inloc(
             tmp, args.synthetic_queries, args.n_panos, *args.synthetic_hw)
         args.n_queries = args.synthetic_queries
+    torch.backends.cudnn.benchmark = INLOC_CUDNN_BENCHMARK   # the state bench.py's InLoc secondaries time
     torch.manual_seed(1)   # checkpoint-less (synthetic) runs: the same random NC weights on every launch
     model = ImMatchNet(use_cuda=ctx.device.type == "cuda", checkpoint=args.checkpoint or None,
                        ncons_kernel_sizes=args.ncons_kernel_sizes, ncons_channels=args.ncons_channels,

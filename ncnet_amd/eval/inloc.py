@@ -26,6 +26,11 @@ from ..ops import _ext
 from .point_tnf import best_both, corr_to_matches
 
 SCALE_FACTOR = 0.0625  # feature stride 1/16 (eval_inloc.py:77)
+# MIOpen solver search (torch.backends.cudnn.benchmark) of the InLoc runs:
+# eval_inloc.py and bench.py's InLoc secondaries both run in this state, so the
+# bench times the trunk kernels the CLI runs (3200 px bf16 measured 10.6-10.8
+# ms/pair with it off or on, profiles/r5/inloc/cudnn_ab.txt)
+INLOC_CUDNN_BENCHMARK = False
 
 
 def output_folder(shortlist: str, image_size: int, k_size: int, both_dirs: bool, flip: bool, softmax: bool,
