@@ -20,25 +20,14 @@ Same flags and defaults as the reference, plus:
                        correlation and bf16 NeighConsensus backward -- the PCK
                        of fp32 mode (0.533 vs 0.535, 4 seeds) at 2/3 of its NC work.
 
-Which precision to train with: use --nc_precision mixed (or fp32) whenever the weak
-loss's signal is below bf16 resolution -- the first steps from a random or
-weakly trained NC, or a trunk whose features are nearly collinear (random-init
-trunks: per-step loss ~1e-8).  There the bf16 mode loses the gradient
-direction and its ReLUs die within ~10 steps (PCK stays ~0), while fp32 mode
-learns like the fp32 reference (PCK 0.64 vs 0.68 after 80 steps,
-profiles/r3/x3/README.md).  Measured NOT to be enough in that regime, so not
-offered: a bf16 trunk under an fp32-accurate NC (PCK 0.003), and fp16 autocast
-with loss scaling (the reference algorithm in fp16: PCK 0.003).  Once the loss
-signal is well above bf16 resolution (a pretrained trunk, |loss| >> 1e-3),
-the default bf16 mode trains 3.3x faster.
-  --segment_timing     HIP-event timers per step segment (backbone, correlation,
-                       mutual_matching, neigh_consensus, forward, backward,
-                       allreduce, optimizer), written to the --metrics records
-  --profile DIR        torch.profiler (ROCm activity) over the --max_steps loop,
-                       kernel table + chrome trace under DIR (rank 0)
-
-Multi-GPU: launch with torchrun (one process per GPU); gradients are averaged
-with one bucketed RCCL all-reduce, every rank trains on its own shard.
+Which precision to train with: bf16 unless you need fp32-class numerics.  A
+per-stage ablation over 24 seeds in the hardest offline regime (random-init
+trunk, per-step loss ~1e-8; profiles/r5/ablation/README.md) found the run
+either takes off (PCK ~0.7) or its ReLUs die, at rates within noise of each
+other for bf16 (10/24), mixed (12/24) and fp32 (13/24): the earlier few-seed
+finding that only fp32 learns there did not hold.  mixed / fp32 keep the
+reference's fp32 forward numerics (parity studies, checkpoints compared
+bit-closely against fp32 training) at 2.2x / 2.9x the bf16 step time.
 """
 from __future__ import annotations
 
