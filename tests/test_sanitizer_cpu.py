@@ -35,6 +35,8 @@ def _variant_module():
 
 def _dummy(kind: str):
     if "Sequence" in kind:
+        if "Tensor" in kind:        # tensor lists (reduce_cols): CPU tensors must be rejected too
+            return [torch.zeros(16, dtype=torch.float32)]
         return [3, 3, 3] if "SupportsInt" in kind else [0.5, 0.5, 0.5]
     if "Tensor" in kind:
         return None if "None" in kind else torch.zeros(16, dtype=torch.bfloat16)
