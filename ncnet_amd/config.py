@@ -32,7 +32,7 @@ class RuntimeConfig:
     trunk_conv: str = "auto"         # NCNET_TRUNK_CONV: auto | native | blas (models/backbones.py)
     trunk_fp32: str = "auto"         # NCNET_TRUNK_FP32: the fp32 frozen trunk -- x3 (bf16x3 splits on the
                                      #   native MFMA convs, ~2^-16 relative) | miopen (true fp32) | auto:
-                                     #   x3 for nc_precision='fp32' training, miopen for corr_dtype='fp32'
+                                     #   x3 for nc_precision 'fp32' / 'mixed' training, miopen for corr_dtype='fp32'
                                      #   inference (the reference's evaluation numerics)
     force_torch: bool = False        # NCNET_FORCE_TORCH (with allow_torch_fallback): PyTorch reference ops
     allow_torch_fallback: bool = False  # NCNET_ALLOW_TORCH_FALLBACK: configs without a HIP kernel may run PyTorch

@@ -35,6 +35,20 @@ def with_env(key, val, fn):
     return run
 
 
+def _nc_fused_case(dev):
+    """The InLoc 3200 px fused NeighConsensus (3,3 / 16,1) on one symmetric
+    volume pair: [2, 75, 100, 75, 100] bf16 -> fp32."""
+    import importlib
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    from ncnet_amd.ops import reference as ref
+    g = torch.Generator(device=dev).manual_seed(5)
+    x2 = torch.rand((2, 75, 100, 75, 100), device=dev, generator=g).to(torch.bfloat16)
+    ws = [ref.conv4d_weight_from_std(torch.randn(16, 1, 3, 3, 3, 3, device=dev, generator=g) * 0.2),
+          ref.conv4d_weight_from_std(torch.randn(1, 16, 3, 3, 3, 3, device=dev, generator=g) * 0.1)]
+    bs = [torch.rand(16, device=dev, generator=g) * 0.1, torch.rand(1, device=dev, generator=g) * 0.1]
+    return lambda: nc.neigh_consensus_fused_x2(x2, ws, bs)
+
+
 def timeit(fn, reps):
     fn()
     torch.cuda.synchronize()
@@ -124,6 +138,7 @@ def main():
         "ijpack": (lambda: C.ijpack(x1, xs, ks, 1), None),
         "pad_planes": (lambda: C.pad_planes(x1.reshape(V, S * S, S * S), xpad, S, S, ks, 0), None),
         "pad_planes_t": (lambda: C.pad_planes(x1.reshape(V, S * S, S * S), xpad, S, S, ks, 1), None),
+        "nc_fused_3200": (_nc_fused_case(dev), 2.0 * 2 * (75 * 100) ** 2 * 2 * 16 * 81),
         "conv1x16_fwd": (lambda: C.conv1x16(xpad, w1x, b16, None, y16, ks, 1), fl1),
         "conv1x16_dgrad": (lambda: C.conv1x16(xpad, w1x, None, x16, y16, ks, 2), fl1),
         "conv1x16_fwd_pd2": (with_env("NCNET_C1X_PD", "2", lambda: C.conv1x16(xpad, w1x, b16, None, y16, ks, 1)), fl1),
