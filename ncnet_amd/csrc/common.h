@@ -143,6 +143,19 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblocks) {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// CUs of the current device (persistent grids, tile picking), cached per device
+static inline int device_num_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 // Debug-build bounds checks (python -m ncnet_amd.build --debug -> _C_debug.so).
 // NCNET_OK(cond) is `cond` in the debug build -- printing the failed condition
 // with file:line and the block / thread, so the guarded access is skipped

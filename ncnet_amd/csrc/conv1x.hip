@@ -628,22 +628,12 @@ extern "C" int ncnet_pad_planes(const void* x, int x_is_bf16, void* y, int V, in
 // 3 output j-planes per item -- 1 in the bf16x3 mode -- to fit LDS), KS 3 at
 // 25 x 25 (the IVD recipe, NC 3,3 / 16,1).  Mirrored in
 // ops/neigh_consensus.py FAST1X_SHAPES.
-static int c1x_num_cus() {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  }
-  return ncu;
-}
-
 template <int KS, int K, int L, int R, bool X3>
 static void c1x_launch(int epi, int V, int I, int J, const bf16* x, const u32x4* w, const float* bias, const bf16* m,
                        bf16* y, int nt_store, long long xlo, long long ylo, hipStream_t s) {
   using C = C1X<KS, K, L>;
   const int nitems = V * I * cdiv(J, R);
-  dim3 grid((unsigned)std::min(nitems, c1x_num_cus())), block(512);   // persistent: one workgroup per CU
+  dim3 grid((unsigned)std::min(nitems, device_num_cus())), block(512);   // persistent: one workgroup per CU
   // X3: both weight sets ahead of the planes
   constexpr size_t lds = (size_t)C::lds(R + KS - 1, 1) + (X3 ? (size_t)C::NT * 1024 : 0);
   static_assert(lds <= 160 * 1024, "LDS");

@@ -588,21 +588,7 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
   }
 }
 
-// number of CUs of the current device (cached per device)
-static int c3_num_cus() {
-  static int cache[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cache[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cache[dev] = n;
-  }
-  return cache[dev];
-}
-
 static int c3_pick_tm(int M, int Cout, int Cin, int TN, int ncu, long long* cost);
-static int c3_num_cus();
 // mode 0: bf16, 1: IEEE half, 2: bf16x3
 template <int TM, int TN>
 static void c3_launch1(int mode, dim3 g, dim3 b, hipStream_t stream, const Conv2dArgs& p) {
@@ -621,7 +607,7 @@ static void c3_launch(int tm, int mode, dim3 g, dim3 b, hipStream_t stream, cons
 // launch v3 with its tile choice; false when it does not apply
 static bool c3_run(Conv2dArgs& p, int mode, hipStream_t stream) {
   const int TNv = (p.Cout % 256 == 0) ? 4 : (p.Cout % 128 == 0) ? 2 : 1;
-  const int tm = c3_pick_tm(p.M, p.Cout, p.Ck, TNv, c3_num_cus(), nullptr);
+  const int tm = c3_pick_tm(p.M, p.Cout, p.Ck, TNv, device_num_cus(), nullptr);
   if (!tm || p.Cx % 64) return false;
   p.tiles_n = p.Cout / (64 * TNv);
   p.tiles_m = cdiv(p.M, 16 * tm);

@@ -313,8 +313,11 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
 // compute shorter than the load latency).  Rows past M / N read a 16-byte zero
 // block.  Tile order: GM consecutive row tiles per column sweep, so the ~32
 // workgroups an XCD runs at once share 4 A and 8 B tiles in its L2 instead of
-// 1 A and 32 B.  Epilogues as v1 (plain fp32 / bf16 store, fused 2x2x2x2
-// max-pool with packed argmax offsets).
+// 1 A and 32 B.  Epilogues: plain fp32 / bf16 store, or the fused 2x2x2x2
+// max-pool with packed argmax offsets, division-free and reduced through DPP
+// quad moves (the v1-style epilogue with per-sub-tile integer divisions and
+// ds_bpermute shuffles was ~1800 VALU per wave, more issue time than the
+// tile's MFMAs at K = 1024: `profiles/r5/kernels/pmc_corr_3200*.md`).
 // ===========================================================================
 __device__ const uint4 g_corr_zero16 = {0u, 0u, 0u, 0u};
 
@@ -353,40 +356,51 @@ __device__ __forceinline__ void corr_v2_epilogue(const f32x4 (&acc)[TM][TN], con
         }
   } else {
     // rows / columns in 2x2-block order: a lane's 4 accumulator rows are one A
-    // block, the 4 columns of a B block sit in lanes fr&~3 .. fr|3 (as v1)
-    const int pa_w = p.wA >> 1, pb_w = p.wB >> 1;
-    const size_t vol = (size_t)(p.hA >> 1) * pa_w * (p.hB >> 1) * pb_w;
+    // block, the 4 columns of a B block sit in the lane quad fr&~3 .. fr|3.
+    // Block index = pooled index (ba = ai * wA/2 + aj), so the pooled offset
+    // is ba * nb + bb with no division.  Max first (quad max through DPP),
+    // then the smallest packed offset code among the lanes / rows holding it:
+    // the code is a bit-spread of r * 4 + (fr & 3), so its order is the
+    // row-major tie order of the unfused pool.  M, N are multiples of 4: a
+    // block is wholly inside or outside the volume.
+    const size_t nb = (size_t)(p.hB >> 1) * (p.wB >> 1);
+    const size_t vol = (size_t)(p.hA >> 1) * (p.wA >> 1) * nb;
+    const int lcode = ((fr & 2) << 1) | (fr & 1);
+    const bool lead = (fr & 3) == 0;
+    size_t aoff[TM];
+    bool aok[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      const int gm = row0 + i * 16 + 4 * fq;
+      aok[i] = gm < p.M;
+      aoff[i] = (size_t)b * vol + (size_t)(gm >> 2) * nb;
+    }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float best = acc[i][j][0];
-        int bidx = 0;
+    for (int j = 0; j < TN; ++j) {
+      const int gn = col0 + j * 16 + (fr & ~3);
+      const bool bok = lead && gn < p.N;
 #pragma unroll
-        for (int r = 1; r < 4; ++r)
-          if (acc[i][j][r] > best) { best = acc[i][j][r]; bidx = r * 4; }
-        bidx += (fr & 3);
-#pragma unroll
-        for (int o = 1; o < 4; o <<= 1) {
-          const float ob = __shfl_xor(best, o, 64);
-          const int oi = __shfl_xor(bidx, o, 64);
-          const bool take = (ob > best) || (ob == best && oi < bidx);
-          best = take ? ob : best;
-          bidx = take ? oi : bidx;
-        }
-        const int gm = row0 + i * 16 + 4 * fq, gn = col0 + j * 16 + (fr & ~3);
-        if ((fr & 3) == 0 && gm < p.M && gn < p.N) {
-          const int ba = gm >> 2, bb = gn >> 2;
-          const int ai = ba / pa_w, aj = ba - ai * pa_w, bi = bb / pb_w, bj = bb - bi * pb_w;
-          const int ra_ = bidx >> 2, rb_ = bidx & 3;
-          const uint8_t code = (uint8_t)(((ra_ >> 1) << 6) | ((ra_ & 1) << 4) | ((rb_ >> 1) << 2) | (rb_ & 1));
-          const size_t o = (size_t)b * vol + (((size_t)ai * pa_w + aj) * (p.hB >> 1) + bi) * pb_w + bj;
+      for (int i = 0; i < TM; ++i) {
+        const f32x4 v = acc[i][j];
+        float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xF, 0xF, false)));   // quad xor 1
+        m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x4E, 0xF, 0xF, false)));   // quad xor 2
+        int c = v[3] == m ? 0x50 : 0xFF;
+        c = v[2] == m ? 0x40 : c;
+        c = v[1] == m ? 0x10 : c;
+        c = v[0] == m ? 0x00 : c;
+        c |= lcode;
+        c = min(c, __builtin_amdgcn_mov_dpp(c, 0xB1, 0xF, 0xF, false));
+        c = min(c, __builtin_amdgcn_mov_dpp(c, 0x4E, 0xF, 0xF, false));
+        if (bok && aok[i]) {
+          const size_t o = aoff[i] + (size_t)(gn >> 2);
           if (NCNET_OK(o < (size_t)(b + 1) * vol)) {
-            p.pool_val[o] = best;
-            p.pool_idx[o] = code;
+            p.pool_val[o] = m;
+            p.pool_idx[o] = (uint8_t)c;
           }
         }
       }
+    }
   }
 }
 
@@ -503,49 +517,69 @@ __device__ __forceinline__ int h(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1
 __device__ __forceinline__ uint32_t roff(int row, int chunk) { return (uint32_t)(row * 128 + ((chunk ^ h(row)) << 4)); }
 }  // namespace cf2
 
+// Persistent: one workgroup per CU walks tiles lid = it * gridDim + r(blockIdx)
+// (r = the XCD remap, so the tiles an XCD holds at once are neighbours), and
+// the DMA ring runs across tile boundaries: the first NS - 1 stages of the
+// next tile are in flight during the last k-steps and the epilogue of the
+// current one.  With K = 1024 a tile is only 8 k-steps, so a per-tile ring
+// fill (one workgroup per CU: nothing else hides it) cost as much as the
+// MFMAs.  Every wave of a workgroup runs the same tile sequence (uniform exit).
+__device__ __forceinline__ void cf2_tile(uint32_t lid, const GemmArgs& p, int& b, int& m0, int& n0) {
+  const int per_b = p.tiles_m * p.tiles_n;
+  b = (int)lid / per_b;
+  int t = (int)lid - b * per_b;
+  const int grp = t / (cf2::GM * p.tiles_n), first = grp * cf2::GM;
+  const int gsz = min(cf2::GM, p.tiles_m - first);
+  t -= grp * cf2::GM * p.tiles_n;
+  m0 = (first + t % gsz) * cf2::BM;
+  n0 = (t / gsz) * cf2::BN;
+}
+
 template <bool OUT_BF16, bool POOL>
-__global__ __launch_bounds__(512, 1) void corr_gemm_f8v2_kernel(GemmArgs p) {
-  constexpr int BM = cf2::BM, BN = cf2::BN, NS = cf2::NS, GM = cf2::GM;
+__global__ __launch_bounds__(512, 1) void corr_gemm_f8v2_kernel(GemmArgs p, int total_tiles) {
+  constexpr int BM = cf2::BM, NS = cf2::NS;
   constexpr int APW = cf2::APW, BPW = cf2::BPW, PER = cf2::PER, STAGE = cf2::STAGE;
   constexpr int TM = 4, TN = 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int per_b = p.tiles_m * p.tiles_n;
-  const int b = bid / per_b;
-  int t = bid - b * per_b;
-  const int grp = t / (GM * p.tiles_n), first = grp * GM;
-  const int gsz = min(GM, p.tiles_m - first);
-  t -= grp * GM * p.tiles_n;
-  const int tm = first + t % gsz, tn = t / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const uint8_t* A = (const uint8_t*)p.A + (size_t)(p.amap ? p.amap[b] : b) * p.sA;
-  const uint8_t* B = (const uint8_t*)p.B + (size_t)(p.bmap ? p.bmap[b] : b) * p.sB;
+  const uint32_t G = gridDim.x, r0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = r0 < (uint32_t)total_tiles ? (int)((total_tiles - 1 - r0) / G) + 1 : 0;
+  const int nk = p.K / 128;
+  const int nsteps = ntiles * nk;
   const uint8_t* zero = (const uint8_t*)&g_corr_zero16;
   const int pos = lane & 7;
 
+  // issue side: the tile whose stages are being fetched
   const uint8_t* a_ptr[APW];
   bool a_ok[APW];
-#pragma unroll
-  for (int m = 0; m < APW; ++m) {
-    const int row = 8 * (wave * APW + m) + (lane >> 3);
-    a_ok[m] = m0 + row < p.M;
-    a_ptr[m] = A + (size_t)(a_ok[m] ? m0 + row : 0) * p.K + (pos ^ cf2::h(row)) * 16;
-  }
   const uint8_t* b_ptr[BPW];
   bool b_ok[BPW];
+  int is_tile = -1, is_ks = 0;
+  auto issue_tile = [&](int it) {
+    int b, m0, n0;
+    cf2_tile(r0 + (uint32_t)it * G, p, b, m0, n0);
+    const uint8_t* A = (const uint8_t*)p.A + (size_t)(p.amap ? p.amap[b] : b) * p.sA;
+    const uint8_t* B = (const uint8_t*)p.B + (size_t)(p.bmap ? p.bmap[b] : b) * p.sB;
 #pragma unroll
-  for (int m = 0; m < BPW; ++m) {
-    const int row = 8 * (wave * BPW + m) + (lane >> 3);
-    b_ok[m] = n0 + row < p.N;
-    b_ptr[m] = B + (size_t)(b_ok[m] ? n0 + row : 0) * p.K + (pos ^ cf2::h(row)) * 16;
-  }
-  const int nk = p.K / 128;
-  auto issue = [&](int ks, int buf) {
+    for (int m = 0; m < APW; ++m) {
+      const int row = 8 * (wave * APW + m) + (lane >> 3);
+      a_ok[m] = m0 + row < p.M;
+      a_ptr[m] = A + (size_t)(a_ok[m] ? m0 + row : 0) * p.K + (pos ^ cf2::h(row)) * 16;
+    }
+#pragma unroll
+    for (int m = 0; m < BPW; ++m) {
+      const int row = 8 * (wave * BPW + m) + (lane >> 3);
+      b_ok[m] = n0 + row < p.N;
+      b_ptr[m] = B + (size_t)(b_ok[m] ? n0 + row : 0) * p.K + (pos ^ cf2::h(row)) * 16;
+    }
+  };
+  // fetch global step g (= the next unissued one) into ring slot buf
+  auto issue = [&](int buf) {
+    if (is_ks == 0) issue_tile(++is_tile);
     char* sb = smem + buf * STAGE;
-    const int kk = ks * 128;
+    const int kk = is_ks * 128;
 #pragma unroll
     for (int m = 0; m < APW; ++m)
       __builtin_amdgcn_global_load_lds((const void*)(a_ok[m] ? a_ptr[m] + kk : zero),
@@ -554,51 +588,58 @@ __global__ __launch_bounds__(512, 1) void corr_gemm_f8v2_kernel(GemmArgs p) {
     for (int m = 0; m < BPW; ++m)
       __builtin_amdgcn_global_load_lds((const void*)(b_ok[m] ? b_ptr[m] + kk : zero),
                                        LDS_PTR(void, sb + BM * 128 + (wave * BPW + m) * 1024), 16, 0, 0);
+    is_ks = (is_ks + 1 == nk) ? 0 : is_ks + 1;
   };
 
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) issue(s, s);
+    if (s < nsteps) issue(s);
   const int fr = lane & 15, fq = lane >> 4;
-  int buf = 0;
-  for (int ks = 0; ks < nk; ++ks) {
-    if (ks + 1 < nk) cg2_wait_barrier<PER>();
-    else cg2_wait_barrier<0>();
-    if (ks + NS - 1 < nk) issue(ks + NS - 1, (buf + NS - 1) % NS);
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + BM * 128;
-    auto frag = [&](const char* base, int r) {
-      const u32x4 lo = *(const u32x4*)(base + cf2::roff(r, 2 * fq)), hi = *(const u32x4*)(base + cf2::roff(r, 2 * fq + 1));
-      return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-    };
-    // column fragments stream one ahead of their MFMAs, so the matrix cores
-    // start after the A fragments and the first B fragment have landed
-    i32x8 af[TM];
+  int buf = 0, g = 0;
+  for (int it = 0; it < ntiles; ++it) {
+    f32x4 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) af[i] = frag(As, wm * 64 + i * 16 + fr);
-    i32x8 bcur = frag(Bs, wn * 64 + fr);
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      i32x8 bnext = bcur;
-      if (j + 1 < TN) bnext = frag(Bs, wn * 64 + (j + 1) * 16 + fr);
-      __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of these MFMAs (counted lgkmcnt)
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < nk; ++ks, ++g) {
+      // stage g landed (the one after it may still be in flight; a previous
+      // tile's epilogue stores, issued later, make this wait conservative)
+      if (g + 1 < nsteps) cg2_wait_barrier<PER>();
+      else cg2_wait_barrier<0>();
+      if (g + NS - 1 < nsteps) issue((buf + NS - 1) % NS);
+      const char* As = smem + buf * STAGE;
+      const char* Bs = As + BM * 128;
+      auto frag = [&](const char* base, int r) {
+        const u32x4 lo = *(const u32x4*)(base + cf2::roff(r, 2 * fq)), hi = *(const u32x4*)(base + cf2::roff(r, 2 * fq + 1));
+        return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      };
+      // column fragments stream one ahead of their MFMAs, so the matrix cores
+      // start after the A fragments and the first B fragment have landed
+      i32x8 af[TM];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) acc[i][j] = mfma_fp8_k128(af[i], bcur, acc[i][j]);
-      __builtin_amdgcn_sched_barrier(0);
-      bcur = bnext;
+      for (int i = 0; i < TM; ++i) af[i] = frag(As, wm * 64 + i * 16 + fr);
+      i32x8 bcur = frag(Bs, wn * 64 + fr);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        i32x8 bnext = bcur;
+        if (j + 1 < TN) bnext = frag(Bs, wn * 64 + (j + 1) * 16 + fr);
+        __builtin_amdgcn_sched_barrier(0);   // keep the read ahead of these MFMAs (counted lgkmcnt)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][j] = mfma_fp8_k128(af[i], bcur, acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+        bcur = bnext;
+      }
+      buf = (buf + 1 == NS) ? 0 : buf + 1;
     }
-    buf = (buf + 1 == NS) ? 0 : buf + 1;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] * p.out_scale;
+    int b, m0, n0;
+    cf2_tile(r0 + (uint32_t)it * G, p, b, m0, n0);
+    corr_v2_epilogue<TM, TN, OUT_BF16, POOL>(acc, p, b, m0 + wm * 64, n0 + wn * 64, lane);
   }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] * p.out_scale;
-  corr_v2_epilogue<TM, TN, OUT_BF16, POOL>(acc, p, b, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
 }  // namespace ncnet
@@ -661,10 +702,11 @@ extern "C" int ncnet_corr_gemm(const void* A, const void* B, void* C, const int*
   p.out_scale = fp8_out_scale;
   if (f8 && use_v2(f8, batch, M, N, K)) {
     p.tiles_m = cdiv(M, cf2::BM); p.tiles_n = cdiv(N, cf2::BN);
-    dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);
+    const int tiles = batch * p.tiles_m * p.tiles_n;
+    dim3 grid((unsigned)std::min(tiles, device_num_cus())), block(512);   // persistent
     const size_t lds = cf2::NS * cf2::STAGE;
-    if (out_bf16) hipLaunchKernelGGL((corr_gemm_f8v2_kernel<true, false>), grid, block, lds, stream, p);
-    else hipLaunchKernelGGL((corr_gemm_f8v2_kernel<false, false>), grid, block, lds, stream, p);
+    if (out_bf16) hipLaunchKernelGGL((corr_gemm_f8v2_kernel<true, false>), grid, block, lds, stream, p, tiles);
+    else hipLaunchKernelGGL((corr_gemm_f8v2_kernel<false, false>), grid, block, lds, stream, p, tiles);
     return (int)hipGetLastError();
   }
   if (use_v2(f8, batch, M, N, K)) {
@@ -713,8 +755,9 @@ extern "C" int ncnet_corr_gemm_pool2(const void* A, const void* B, float* pool_v
   p.hA = hA; p.wA = wA; p.hB = hB; p.wB = wB;
   if (f8 && use_v2(f8, batch, p.M, p.N, K)) {
     p.tiles_m = cdiv(p.M, cf2::BM); p.tiles_n = cdiv(p.N, cf2::BN);
-    dim3 grid((unsigned)(batch * p.tiles_m * p.tiles_n)), block(512);
-    hipLaunchKernelGGL((corr_gemm_f8v2_kernel<false, true>), grid, block, cf2::NS * cf2::STAGE, stream, p);
+    const int tiles = batch * p.tiles_m * p.tiles_n;
+    dim3 grid((unsigned)std::min(tiles, device_num_cus())), block(512);   // persistent
+    hipLaunchKernelGGL((corr_gemm_f8v2_kernel<false, true>), grid, block, cf2::NS * cf2::STAGE, stream, p, tiles);
     return (int)hipGetLastError();
   }
   if (use_v2(f8, batch, p.M, p.N, K)) {
