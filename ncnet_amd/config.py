@@ -41,8 +41,8 @@ class RuntimeConfig:
     trunk_prefetch: bool = True      # NCNET_TRUNK_PREFETCH: next batch's frozen backbone on a side stream
     bwd_overlap: bool = True         # NCNET_BWD_OVERLAP: NC weight gradients on a side stream
     nc_fused: bool = True            # NCNET_NC_FUSED: fused (3,3)/(<=16,1) inference NeighConsensus kernel
-    nc_fp8: bool = False             # NCNET_NC_FP8: fp8 inference NC on the fp8 Conv4d kernels even where
-                                     #   the fused bf16 kernel applies
+    nc_fp8: bool = False             # NCNET_NC_FP8: e4m3 NC in fp8 mode: the fused fp8 kernel for the
+                                     #   (3,3)/(<=16,1) stack, the fp8 Conv4d kernels for other stacks
     stats2d: bool = True             # NCNET_STATS2D: one-pass row + column statistics (csrc/volume.hip)
     pair_graph: bool = True          # NCNET_PAIR_GRAPH: InLoc pair matching replayed as a HIP graph
     fault_step: int = -1             # NCNET_FAULT_STEP: inject a failure at this training step (tests)

@@ -67,6 +67,8 @@ int ncnet_conv1x16(const void*, const void*, const float*, const void*, void*, i
 int ncnet_wgrad1x16(const void*, const void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_nc_fused_k3(const void*, const void*, const float*, const void*, const float*, float*, int, int, int, int,
                       int, int, int, int, int, int, hipStream_t);
+int ncnet_nc_fused_k3_f8(const void*, const void*, const void*, const float*, const void*, const void*, const float*,
+                         float*, int, int, int, int, int, int, int, int, int, float, float, float, float, hipStream_t);
 }
 
 namespace {
@@ -796,6 +798,28 @@ void nc_fused_k3(Tensor X, Tensor W1p, Tensor b1, Tensor W2p, Tensor b2, Tensor 
      "nc_fused_k3");
 }
 
+// Fused NC on e4m3 operands: X bf16 [V,I,J,K,L] -> Y fp32; W1a / W2a [64, 32] and
+// W1b / W2b [64, 8] float8_e4m3fn fragments (taps 0-7 MX, tap 8); b1 [16], b2 [1]
+// fp32; scales (sx, inv1, sh, inv2) as csrc/nc_fused.hip nc_fused_k3_f8_kernel.
+void nc_fused_k3_f8(Tensor X, Tensor W1a, Tensor W1b, Tensor b1, Tensor W2a, Tensor W2b, Tensor b2, Tensor Y,
+                    int64_t R, int64_t IR, int64_t TK, int64_t TL, double sx, double inv1, double sh, double inv2) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16);
+  for (auto* t : {&W1a, &W1b, &W2a, &W2b}) check(*t, "W", at::kFloat8_e4m3fn);
+  check(b1, "b1", at::kFloat); check(b2, "b2", at::kFloat); check(Y, "Y", at::kFloat);
+  TORCH_CHECK(X.dim() == 5, "X must be [V,I,J,K,L]");
+  check_shape(Y, "Y", X.sizes().vec());
+  check_shape(W1a, "W1a", {64, 32}); check_shape(W2a, "W2a", {64, 32});
+  check_shape(W1b, "W1b", {64, 8}); check_shape(W2b, "W2b", {64, 8});
+  check_shape(b1, "b1", {16}); check_shape(b2, "b2", {1});
+  TORCH_CHECK(R >= 1 && IR >= 1 && TK >= 1 && TL >= 1, "nc_fused_k3_f8: bad tiling");
+  ok(ncnet_nc_fused_k3_f8(X.data_ptr(), W1a.data_ptr(), W1b.data_ptr(), (const float*)b1.data_ptr(), W2a.data_ptr(),
+                          W2b.data_ptr(), (const float*)b2.data_ptr(), (float*)Y.data_ptr(), X.size(0), X.size(1),
+                          X.size(2), X.size(3), X.size(4), (int)R, (int)IR, (int)TK, (int)TL, (float)sx, (float)inv1,
+                          (float)sh, (float)inv2, cur_stream(X)),
+     "nc_fused_k3_f8");
+}
+
 // NHWC implicit-GEMM conv with fused bias (+ residual) (+ ReLU).  X [N,Cin,H,W],
 // W [Cout,Cin,KH,KW], R / Y [N,Cout,Ho,Wo]: all bf16 channels-last; bias fp32 [Cout].
 void conv2d_nhwc(Tensor X, Tensor W, Tensor bias, c10::optional<Tensor> R, Tensor Y, int64_t stride, int64_t pad,
@@ -984,6 +1008,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool4d", &maxpool4d);
   m.def("transpose", &transpose);
   m.def("nc_fused_k3", &nc_fused_k3);
+  m.def("nc_fused_k3_f8", &nc_fused_k3_f8);
   m.def("resize_norm_u8", &resize_norm_u8);
   m.def("debug_selftest", &debug_selftest);
   m.def("nonfinite_count", &nonfinite_count);

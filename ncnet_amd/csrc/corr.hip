@@ -142,6 +142,11 @@ struct GemmArgs {
   int hA, wA, hB, wB;    // full-res feature grid (pooling only)
 };
 
+// plain / fused-pool epilogue of a wave's TM x TN 16 x 16 sub-tiles (below)
+template <int TM, int TN, bool OUT_BF16, bool POOL, bool F16 = false>
+__device__ __forceinline__ void corr_v2_epilogue(const f32x4 (&acc)[TM][TN], const GemmArgs& p, int b, int row0,
+                                                 int col0, int lane);
+
 // F16 (with !FP8): IEEE-half operands (f16 MFMA) and, with OUT_BF16, an IEEE-half output.
 template <bool OUT_BF16, bool POOL, bool FP8, bool F16 = false>
 __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
@@ -245,63 +250,7 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
   }
 
   finish();
-  if (!POOL) {
-    // D[row = 4fq + r][col = fr] of sub-tile (i,j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int gm = m0 + wm * 64 + i * 16 + 4 * fq + r, gn = n0 + wn * 64 + j * 16 + fr;
-          if (gm < p.M && gn < p.N) {
-            size_t o = (size_t)b * p.sC + (size_t)gm * p.N + gn;
-            if (OUT_BF16) ((uint16_t*)p.C)[o] = f2s16<F16>(acc[i][j][r]);
-            else ((float*)p.C)[o] = acc[i][j][r];
-          }
-        }
-  } else {
-    // Pooling epilogue for ks = 2: rows are ordered so that the 4 rows of a
-    // 2x2 spatial block are consecutive (row = 4*blk + 2*dy + dx), same for
-    // columns.  A lane's 4 accumulator rows (4fq..4fq+3) are exactly one A
-    // block; the 4 columns of a B block live in lanes fr&~3 .. fr|3.
-    // Reduce over the 4 rows in registers, then over 4 lanes with shuffles.
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float best = acc[i][j][0];
-        int bidx = 0;  // (dyA*2+dxA)*4 + (dyB*2+dxB)
-#pragma unroll
-        for (int r = 1; r < 4; ++r)
-          if (acc[i][j][r] > best) { best = acc[i][j][r]; bidx = r * 4; }
-        bidx += (fr & 3);
-        // butterfly over the 4 lanes of the B block (keep first max on ties)
-#pragma unroll
-        for (int o = 1; o < 4; o <<= 1) {
-          float ob = __shfl_xor(best, o, 64);
-          int oi = __shfl_xor(bidx, o, 64);
-          bool take = (ob > best) || (ob == best && oi < bidx);
-          best = take ? ob : best;
-          bidx = take ? oi : bidx;
-        }
-        int gm = m0 + wm * 64 + i * 16 + 4 * fq;   // first row of the A block
-        int gn = n0 + wn * 64 + j * 16 + (fr & ~3); // first col of the B block
-        if ((fr & 3) == 0 && gm < p.M && gn < p.N) {
-          int ba = gm >> 2, bb = gn >> 2;          // pooled A / B cell (block-major)
-          int pa_w = p.wA >> 1, pb_w = p.wB >> 1;
-          int ai = ba / pa_w, aj = ba - ai * pa_w;
-          int bi = bb / pb_w, bj = bb - bi * pb_w;
-          int ra_ = bidx >> 2, rb_ = bidx & 3;
-          // offsets (di, dj, dk, dl) packed 2 bits each
-          uint8_t code = (uint8_t)(((ra_ >> 1) << 6) | ((ra_ & 1) << 4) | ((rb_ >> 1) << 2) | (rb_ & 1));
-          size_t o = (size_t)b * ((size_t)(p.hA >> 1) * pa_w * (p.hB >> 1) * pb_w) +
-                     (((size_t)ai * pa_w + aj) * (p.hB >> 1) + bi) * pb_w + bj;
-          p.pool_val[o] = best;
-          p.pool_idx[o] = code;
-        }
-      }
-  }
+  corr_v2_epilogue<4, 4, OUT_BF16, POOL, F16>(acc, p, b, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
 // ===========================================================================
@@ -315,9 +264,9 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(GemmArgs p) {
 // workgroups an XCD runs at once share 4 A and 8 B tiles in its L2 instead of
 // 1 A and 32 B.  Epilogues: plain fp32 / bf16 store, or the fused 2x2x2x2
 // max-pool with packed argmax offsets, division-free and reduced through DPP
-// quad moves (the v1-style epilogue with per-sub-tile integer divisions and
-// ds_bpermute shuffles was ~1800 VALU per wave, more issue time than the
-// tile's MFMAs at K = 1024: `profiles/r5/kernels/pmc_corr_3200*.md`).
+// quad moves, shared with v1 (the earlier epilogue with per-sub-tile integer
+// divisions and ds_bpermute shuffles was ~1800 VALU per wave, more issue time
+// than the tile's MFMAs at K = 1024: `profiles/r5/kernels/pmc_corr_3200*.md`).
 // ===========================================================================
 __device__ const uint4 g_corr_zero16 = {0u, 0u, 0u, 0u};
 
@@ -336,7 +285,7 @@ __device__ __forceinline__ void cg2_wait_barrier() {
 
 // Epilogue of the v2 kernels for one wave's TM x TN 16 x 16 sub-tiles at
 // (row0, col0): plain fp32 / bf16 store, or the fused 2x2x2x2 max-pool.
-template <int TM, int TN, bool OUT_BF16, bool POOL, bool F16 = false>
+template <int TM, int TN, bool OUT_BF16, bool POOL, bool F16>
 __device__ __forceinline__ void corr_v2_epilogue(const f32x4 (&acc)[TM][TN], const GemmArgs& p, int b, int row0,
                                                  int col0, int lane) {
   const int fr = lane & 15, fq = lane >> 4;

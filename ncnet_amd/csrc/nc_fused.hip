@@ -373,6 +373,268 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 1) void nc_fused_k3_kernel(c
   for (int io = max(i0, ih_hi - 1); io < i1; ++io) flush(io);
 }
 
+// ===========================================================================
+// nc_fused_k3_f8: the same fused stack on OCP e4m3 operands (BASELINE config
+// 5, the all-fp8 InLoc pipeline).  Differences from nc_fused_k3:
+//  * S and h voxels are 16 bytes (16 fp8 channels): half the LDS tiles;
+//  * layer 1 / layer 2 per 16-voxel tile = ONE v_mfma_scale_f32_16x16x128_f8f6f4
+//    (taps 0..7 x 16 channels: a lane's 32 operand bytes are taps 2fq, 2fq+1,
+//    two ds_read_b128 at per-lane tap offsets) + one v_mfma_f32_16x16x32_fp8_fp8
+//    for tap 8 (lane groups fq = 0, 1: channels 0-7 / 8-15; fq = 2, 3 carry
+//    zero weights) instead of 5 bf16 MFMAs: 48 instead of 80 matrix cycles and
+//    3 instead of 5 LDS reads per tile and layer;
+//  * the weight fragments (20 VGPRs) stay in registers for the whole kernel;
+//  * power-of-two scales: x0 * sx (x0 in [0, 1] after MutualMatching),
+//    weights * sw (amax -> 240), h * sh (sh from the layer-1 output bound, host
+//    side), undone in fp32 in the epilogues (inv1 = 1 / (sw1 sx), inv2 =
+//    1 / (sw2 sh)).
+// Row strides: a 16-voxel tile that wraps a row jumps 1 mod 16 voxels (one
+// 256-B bank period + 1): SRS = TL + 18, HRS = TL + 16.
+// ===========================================================================
+struct NCF8Scales {
+  float sx, inv1, sh, inv2;
+};
+
+// two floats -> e4m3 bytes 0-1 (HI = false) or 2-3 (HI = true) of `old`
+template <bool HI>
+__device__ __forceinline__ uint32_t f8x2(float a, float b, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, (int)old, HI);
+}
+
+template <int CTK = 0, int CTL = 0, int CR = 0>
+__global__ __launch_bounds__(512, 4) void nc_fused_k3_f8_kernel(const bf16* __restrict__ X, const i32x8* __restrict__ W1a,
+                                                                const long* __restrict__ W1b, const float* __restrict__ b1,
+                                                                const i32x8* __restrict__ W2a, const long* __restrict__ W2b,
+                                                                const float* __restrict__ b2, float* __restrict__ Y,
+                                                                NCFGeom g, NCF8Scales sc) {
+  constexpr int NW = 8, MT1 = 4, MT2 = 3;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int TK = CTK ? CTK : g.TK, TL = CTL ? CTL : g.TL;
+  const int GR = CR ? CR : g.R;
+  const int SRS = CTL ? CTL + 18 : g.SRS, HRS = CTL ? CTL + 16 : g.HRS;
+  const int SR = TK + 4, SW = TL + 4;
+  const int HR = TK + 2, HW = TL + 2;
+  char* S = smem;
+  char* H = S + SR * SRS * 16;
+  float* ring = (float*)(H + HR * HRS * 16);
+  const int nvox = TK * TL;
+
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __builtin_assume(wave >= 0 && wave < NW);
+  uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int lt = bid % g.nlt; bid /= g.nlt;
+  const int kt = bid % g.nkt; bid /= g.nkt;
+  const int jb = bid % g.njb; bid /= g.njb;
+  const int ib = bid % g.nib;
+  const int v = bid / g.nib;
+  const int k0 = kt * TK, l0 = lt * TL, j0 = jb * GR, i0 = ib * g.IR;
+  const int i1 = min(g.I, i0 + g.IR);
+  const int R = min(GR, g.J - j0);
+  const size_t KL = (size_t)g.K * g.L;
+  const int KLi = g.K * g.L;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(X + (size_t)v * g.I * g.J * KL), (short)0, (int)((size_t)g.I * g.J * KL * 2), 0x00020000);
+
+  // ---- static maps (as nc_fused_k3, 16-byte voxels) -------------------------
+  int s_lds, s_goff;
+  {
+    const int e = threadIdx.x;
+    const int r = e / SW, c = e - r * SW;
+    const int kg = k0 - 2 + r, lg = l0 - 2 + c;
+    const bool in = e < SR * SW && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
+    s_lds = (e < SR * SW) ? (r * SRS + c) * 16 : SW * 16;
+    s_goff = in ? (kg * g.L + lg) * 2 : 0x7ffffff0;
+  }
+  const int fr = lane & 15, fq = lane >> 4;
+  // per-lane tap offsets (voxels) of the MX fragment (taps 2fq, 2fq + 1) and of tap 8
+  auto tapoff = [](int t, int rs) { return (t / 3) * rs + t % 3; };
+  const int st0 = tapoff(2 * fq, SRS) * 16, st1 = tapoff(2 * fq + 1, SRS) * 16, st8 = tapoff(8, SRS) * 16 + 8 * (fq & 1);
+  const int ht0 = tapoff(2 * fq, HRS) * 16, ht1 = tapoff(2 * fq + 1, HRS) * 16, ht8 = tapoff(8, HRS) * 16 + 8 * (fq & 1);
+  const int nt1 = (HR * HW + 15) >> 4;
+  uint32_t s1b[MT1], h_wr[MT1];
+  bool h_in[MT1];
+#pragma unroll
+  for (int t = 0; t < MT1; ++t) {
+    int e = (wave + NW * t) * 16 + fr;
+    const bool ok = e < HR * HW;
+    if (!ok) e = 0;
+    const int r = e / HW, c = e - r * HW;
+    s1b[t] = (uint32_t)((r * SRS + c) * 16);
+    h_wr[t] = (uint32_t)((ok ? r * HRS + c : HW) * 16 + 4 * fq);
+    const int kg = k0 - 1 + r, lg = l0 - 1 + c;
+    h_in[t] = ok && kg >= 0 && kg < g.K && lg >= 0 && lg < g.L;
+  }
+  const int nt2 = (nvox + 15) >> 4;
+  uint32_t h2b[MT2];
+  int vo[MT2];
+#pragma unroll
+  for (int t = 0; t < MT2; ++t) {
+    int vi = (wave + NW * t) * 16 + fr;
+    vo[t] = vi < nvox ? vi : -1;
+    if (vi >= nvox) vi = 0;
+    const int kk = vi / TL, ll = vi - kk * TL;
+    h2b[t] = (uint32_t)((kk * HRS + ll) * 16);
+  }
+  // weights: register-resident fragments (rows = output channels / layer-2 combos)
+  const i32x8 w1a = W1a[lane], w2a = W2a[lane];
+  const long w1b = W1b[lane], w2b = W2b[lane];
+  const int co0 = 4 * fq;
+  const int dj2 = fq;
+  float bias1[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bias1[r] = b1[co0 + r];
+  const float bias2 = b2[0];
+
+  for (int o = threadIdx.x; o < 3 * GR * nvox; o += NW * 64) ring[o] = 0.f;
+
+  const int ih_lo = max(0, i0 - 1), ih_hi = min(g.I, i1 + 1);
+  const int jh_lo = max(0, j0 - 1), jh_hi = min(g.J, j0 + R + 1);
+  const int nplane = jh_hi - jh_lo;
+  const int nsteps = (ih_hi - ih_lo) * nplane;
+
+  const int pstride = KLi * 2, rstride = g.J * KLi * 2;
+  const int nrec = (int)((size_t)g.I * g.J * KL * 2);
+  auto gather = [&](int ih, int jh, uint32_t (&raw)[9]) {
+    const int base = (ih * g.J + jh) * pstride;
+    const bool iok[3] = {ih >= 1, true, ih + 1 < g.I}, jok[3] = {jh >= 1, true, jh + 1 < g.J};
+#pragma unroll
+    for (int c = 0; c < 9; ++c) {
+      const int di = c / 3, dj = c % 3;
+      const int so = (iok[di] && jok[dj]) ? base + (di - 1) * rstride + (dj - 1) * pstride : nrec;
+      raw[c] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(xr, s_goff, __builtin_amdgcn_readfirstlane(so), 0);
+    }
+  };
+  auto gather_slide = [&](int ih, int jh, uint32_t (&raw)[9], const uint32_t (&prev)[9]) {
+    const int base = (ih * g.J + jh) * pstride;
+    const bool iok[3] = {ih >= 1, true, ih + 1 < g.I};
+    const bool jok = jh + 1 < g.J;
+#pragma unroll
+    for (int di = 0; di < 3; ++di) {
+      const int so = (iok[di] && jok) ? base + (di - 1) * rstride + pstride : nrec;
+      raw[di * 3 + 2] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(xr, s_goff, __builtin_amdgcn_readfirstlane(so), 0);
+    }
+#pragma unroll
+    for (int di = 0; di < 3; ++di) {
+      raw[di * 3 + 0] = prev[di * 3 + 1];
+      raw[di * 3 + 1] = prev[di * 3 + 2];
+    }
+  };
+  // S voxel: the 9 combos as e4m3 (x0 * sx, clamped), channels 9..15 zero
+  auto write_s = [&](const uint32_t (&raw)[9]) {
+    float f[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) f[c] = fminf(fmaxf(__uint_as_float(raw[c] << 16) * sc.sx, -448.f), 448.f);
+    uint32_t w0 = f8x2<false>(f[0], f[1], 0u);
+    w0 = f8x2<true>(f[2], f[3], w0);
+    uint32_t w1 = f8x2<false>(f[4], f[5], 0u);
+    w1 = f8x2<true>(f[6], f[7], w1);
+    const uint32_t w2 = f8x2<false>(f[8], 0.f, 0u);
+    *(u32x4*)(S + s_lds) = u32x4{w0, w1, w2, 0u};
+  };
+  auto frag = [&](const char* buf, uint32_t a0, uint32_t a1) -> i32x8 {
+    const u32x4 lo = *(const u32x4*)(buf + a0), hi = *(const u32x4*)(buf + a1);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+
+  int yvox[MT2];
+#pragma unroll
+  for (int t = 0; t < MT2; ++t) {
+    const int vv = vo[t] < 0 ? 0 : vo[t];
+    const int kk = vv / TL, ll = vv - kk * TL;
+    const int kg = k0 + kk, lg = l0 + ll;
+    yvox[t] = (vo[t] >= 0 && kg < g.K && lg < g.L) ? kg * g.L + lg : -1;
+  }
+  auto flush = [&](int io) {
+    const int slot = io % 3;
+    float* yrow = Y + (((size_t)v * g.I + io) * g.J + j0) * KL;
+    const int pg = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < MT2; ++t) {
+      if (wave + NW * t >= nt2) continue;
+      if (vo[t] < 0) continue;
+      for (int p = pg; p < R; p += 4) {
+        float* rp = ring + (slot * GR + p) * nvox + vo[t];
+        const float val = fmaxf(*rp + bias2, 0.f);
+        if (yvox[t] >= 0) yrow[(size_t)p * KL + yvox[t]] = val;
+        *rp = 0.f;
+      }
+    }
+  };
+
+  int ih = ih_lo, pj = 0, gih = ih_lo, gpj = 0;
+  int slot0 = (ih_lo + 1) % 3;
+  auto advance = [&](int& a, int& b) {
+    if (++b == nplane) { b = 0; ++a; }
+  };
+  auto step = [&](uint32_t (&raw)[9], const uint32_t (&other)[9]) {
+    const int jh = jh_lo + pj;
+    write_s(raw);
+    if (gih < ih_hi) {
+      if (gpj >= 1) gather_slide(gih, jh_lo + gpj, raw, other);
+      else gather(gih, jh_lo + gpj, raw);
+    }
+    advance(gih, gpj);
+    __syncthreads();                   // S complete
+    // ---- layer 1 -> h (e4m3 h * sh, zero outside the volume) ----
+#pragma unroll
+    for (int u = 0; u < MT1; ++u) {
+      if (wave + NW * u >= nt1) continue;
+      const i32x8 bx = frag(S, s1b[u] + st0, s1b[u] + st1);
+      const long b8 = *(const long*)(S + s1b[u] + st8);
+      // two independent accumulators, summed by VALU: a 16x16x32 fp8 MFMA
+      // reading the scaled MFMA's result as srcC read stale rows (no wait
+      // states are inserted between the two MFMA kinds for that chain;
+      // tests/test_gpu_kernels.py test_nc_fused_k3_f8_vs_quantized_oracle).
+      // One tile at a time: all tiles' accumulators live at once spill at
+      // the 128-VGPR budget of two workgroups per CU.
+      const f32x4 a8 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(w1b, b8, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const f32x4 acc = mfma_fp8_k128(w1a, bx, f32x4{0.f, 0.f, 0.f, 0.f}) + a8;
+      float hv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hv[r] = fminf(fmaxf(acc[r] * sc.inv1 + bias1[r], 0.f) * sc.sh, 448.f);
+      uint32_t pk = f8x2<false>(hv[0], hv[1], 0u);
+      pk = f8x2<true>(hv[2], hv[3], pk);
+      *(uint32_t*)(H + h_wr[u]) = h_in[u] ? pk : 0u;
+    }
+    __syncthreads();                   // h complete
+    // ---- layer 2 combos -> ring ----
+    const int p2 = jh - dj2 + 1 - j0;
+    const bool p_ok = dj2 < 3 && p2 >= 0 && p2 < R;
+#pragma unroll
+    for (int u = 0; u < MT2; ++u) {
+      if (wave + NW * u >= nt2) continue;
+      const i32x8 bh = frag(H, h2b[u] + ht0, h2b[u] + ht1);
+      const long b8 = *(const long*)(H + h2b[u] + ht8);
+      const f32x4 a8 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(w2b, b8, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const f32x4 acc = mfma_fp8_k128(w2a, bh, f32x4{0.f, 0.f, 0.f, 0.f}) + a8;
+      const bool lok = vo[u] >= 0 && p_ok;
+      const int roff = p2 * nvox + vo[u];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int io = ih - r + 1;
+        if (io < i0 || io >= i1) continue;
+        const int slot = r == 0 ? slot0 : r == 1 ? (slot0 == 0 ? 2 : slot0 - 1) : (slot0 == 2 ? 0 : slot0 + 1);
+        float* rp = ring + (lok ? slot * GR * nvox + roff : 3 * GR * nvox + lane);
+        *rp += lok ? acc[r] * sc.inv2 : 0.f;
+      }
+    }
+    if (pj + 1 == nplane && ih - 1 >= i0 && ih - 1 < i1) flush(ih - 1);
+    if (++pj == nplane) { pj = 0; ++ih; slot0 = slot0 == 2 ? 0 : slot0 + 1; }
+  };
+
+  __syncthreads();
+  uint32_t rawA[9], rawB[9];
+  gather(gih, jh_lo + gpj, rawA);
+  advance(gih, gpj);
+  if (gih < ih_hi) gather(gih, jh_lo + gpj, rawB);
+  advance(gih, gpj);
+  for (int t = 0; t < nsteps; t += 2) {
+    step(rawA, rawB);
+    if (t + 1 < nsteps) step(rawB, rawA);
+  }
+  for (int io = max(i0, ih_hi - 1); io < i1; ++io) flush(io);
+}
+
 }  // namespace ncnet
 
 using namespace ncnet;
@@ -414,5 +676,36 @@ extern "C" int ncnet_nc_fused_k3(const void* X, const void* W1p, const float* b1
     else if (t3200) NCF(false, 15, 20, 10, 8); else if (t1600) NCF(false, 19, 17, 8, 8); else NCF(false, 0, 0, 0, 8);
   }
 #undef NCF
+  return (int)hipGetLastError();
+}
+
+// fp8 fused stack: x0 bf16 [V,I,J,K,L]; W1a / W2a [64] x 32 B MX fragments of
+// taps 0..7, W1b / W2b [64] x 8 B fragments of tap 8 (e4m3, weights * sw);
+// b1 fp32 [16], b2 fp32 [1]; y fp32.  Scales: sx (x0), inv1 = 1 / (sw1 sx),
+// sh (hidden), inv2 = 1 / (sw2 sh).
+extern "C" int ncnet_nc_fused_k3_f8(const void* X, const void* W1a, const void* W1b, const float* b1, const void* W2a,
+                                    const void* W2b, const float* b2, float* Y, int V, int I, int J, int K, int L, int R,
+                                    int IR, int TK, int TL, float sx, float inv1, float sh, float inv2,
+                                    hipStream_t stream) {
+  NCFGeom g{};
+  g.V = V; g.I = I; g.J = J; g.K = K; g.L = L;
+  g.TK = TK; g.TL = TL; g.R = R; g.IR = IR;
+  g.nkt = cdiv(K, TK); g.nlt = cdiv(L, TL); g.njb = cdiv(J, R); g.nib = cdiv(I, IR);
+  g.SRS = TL + 18;
+  g.HRS = TL + 16;
+  if ((long long)I * J * K * L * 2 >= (1ll << 31)) return -4;
+  const size_t lds = (size_t)(TK + 4) * g.SRS * 16 + (size_t)(TK + 2) * g.HRS * 16 + (size_t)(3 * R * TK * TL + 64) * 4;
+  if ((TK + 2) * (TL + 2) > 512 || TK * TL > 8 * 3 * 16 || (TK + 4) * (TL + 4) > 512 || R < 1 || IR < 1) return -2;
+  if (lds > 80 * 1024) return -3;
+  NCF8Scales sc{sx, inv1, sh, inv2};
+  dim3 grid((unsigned)((size_t)V * g.nib * g.njb * g.nkt * g.nlt)), block(512);
+#define NCF8(A, B, C) hipLaunchKernelGGL((nc_fused_k3_f8_kernel<A, B, C>), grid, block, lds, stream, (const bf16*)X, \
+                                         (const i32x8*)W1a, (const long*)W1b, b1, (const i32x8*)W2a, (const long*)W2b, b2, Y, g, sc)
+  // ops/neigh_consensus.py runs the bf16 kernel's tiling (fused_tiles): the
+  // 3200 px and 1600 px tiles get compile-time geometry
+  if (TK == 15 && TL == 20 && R == 10) NCF8(15, 20, 10);
+  else if (TK == 19 && TL == 17 && R == 8) NCF8(19, 17, 8);
+  else NCF8(0, 0, 0);
+#undef NCF8
   return (int)hipGetLastError();
 }

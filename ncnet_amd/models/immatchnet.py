@@ -326,20 +326,23 @@ class ImMatchNet(nn.Module):
         self.NeighConsensus.precision = ("fp32" if "fp32" in (self.corr_dtype, self.nc_precision)
                                          else "mixed" if self.nc_precision == "mixed" else "bf16")
         nc = self.NeighConsensus
-        if (not torch.is_grad_enabled() and nc.symmetric_mode and corr4d.is_cuda
-                and tuple(corr4d.shape[2:4]) == tuple(corr4d.shape[4:6])
-                and _nc_ops.fused_applies(corr4d, [m.weight_ref() for m in nc.conv_layers()], nc.channels,
-                                          nc.fp8, nc.precision)):
-            # inference on the fused NC stack: MutualMatching writes the bf16
-            # input of both symmetric branches directly
+        square = tuple(corr4d.shape[2:4]) == tuple(corr4d.shape[4:6])
+        wrefs = [m.weight_ref() for m in nc.conv_layers()] if corr4d.is_cuda else []
+        f8 = (not torch.is_grad_enabled() and nc.symmetric_mode and corr4d.is_cuda and square
+              and _nc_ops.fused_f8_applies(corr4d, wrefs, nc.channels, nc.fp8))
+        if f8 or (not torch.is_grad_enabled() and nc.symmetric_mode and corr4d.is_cuda and square
+                  and _nc_ops.fused_applies(corr4d, wrefs, nc.channels, nc.fp8, nc.precision)):
+            # inference on the fused NC stack (bf16 / half, or e4m3 with
+            # NCNET_NC_FP8 in fp8 mode): MutualMatching writes the 16-bit input
+            # of both symmetric branches directly
             layers = nc.conv_layers()
             with segment("mutual_matching"):
                 x2 = _mm_nc_input(corr4d, torch.float16 if self.corr_dtype == "fp16" else torch.bfloat16)
-            _ext_count("nc_fused_k3")
+            biases = [m.bias if m.bias is not None else torch.zeros(m.out_channels, device=x2.device) for m in layers]
+            _ext_count("nc_fused_k3_f8" if f8 else "nc_fused_k3")
             with segment("neigh_consensus"):
-                corr4d = _nc_ops.neigh_consensus_fused_x2(
-                    x2, [m.weight_ref() for m in layers],
-                    [m.bias if m.bias is not None else torch.zeros(m.out_channels, device=x2.device) for m in layers])
+                fused = _nc_ops.neigh_consensus_fused_x2_fp8 if f8 else _nc_ops.neigh_consensus_fused_x2
+                corr4d = fused(x2, wrefs, biases)
             with segment("mutual_matching"):
                 return MutualMatching(corr4d)
         pks = nc.padded_input_ks(corr4d) if _ext_mod.use_hip(corr4d) else 0

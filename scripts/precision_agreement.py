@@ -10,7 +10,10 @@ similarity warps) the same random-init model is evaluated by
   correlation and NC on the f16 MFMA (the reference's half_precision; for
   PF-Pascal the 5,5,5 NC stays on the bf16 Conv4d kernels);
 * ``fp32`` -- ``corr_dtype='fp32'``: fp32 trunk, bf16x3 correlation and NC;
-* ``fp8``  -- ``corr_dtype='fp8'`` (InLoc config only): e4m3 correlation + NC.
+* ``fp8``  -- ``corr_dtype='fp8'`` (InLoc config only): e4m3 correlation, bf16
+  fused NC (the fp8 default);
+* ``fp8_nc`` -- ``corr_dtype='fp8'`` with config ``nc_fp8``: e4m3 correlation
+  and the e4m3 fused NC (BASELINE config 5 as specified).
 Reported per precision: relative L2 of the output volume vs ``ref``, the
 fraction of B cells (and A cells) whose best match (argmax over the other
 image) equals the reference's, and PCK@0.1 of keypoint transfer.  Two
@@ -28,6 +31,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from ncnet_amd import config as _config  # noqa: E402
 from ncnet_amd.data.datasets import synthetic_correspondence_batch  # noqa: E402
 from ncnet_amd.engine.reference_impl import ReferenceAlgorithm, reference_inloc_forward  # noqa: E402
 from ncnet_amd.eval.pck import pck  # noqa: E402
@@ -74,9 +78,10 @@ def run_cfg(name, size, ks, ch, k_reloc, nbatch, batch, precisions, dev):
                 r, rdelta = alg(b), None
             out["ref"]["pck"] += pck_batch(r, b, rdelta, max(1, k_reloc))
             for p in precisions:
-                model.corr_dtype = p
+                model.corr_dtype = "fp8" if p == "fp8_nc" else p
                 model.compute_dtype = torch.float32 if p == "fp32" else torch.bfloat16
-                res = model(b)
+                with _config.override(nc_fp8=p == "fp8_nc"):
+                    res = model(b)
                 c, delta = (res if k_reloc > 1 else (res, None))
                 a = agreement(c, r)
                 for kk, vv in a.items():
@@ -100,7 +105,7 @@ def main(argv=None):
     res = [run_cfg("pf_pascal_400", 400, [5, 5, 5], [16, 16, 1], 0, a.pf_batches, 4, ["bf16", "fp16", "fp32"], dev)]
     for size in a.inloc_sizes:
         res.append(run_cfg(f"inloc_{size}_k2", size, [3, 3], [16, 1], 2, a.inloc_batches, 1,
-                           ["bf16", "fp16", "fp32", "fp8"], dev))
+                           ["bf16", "fp16", "fp32", "fp8", "fp8_nc"], dev))
     for r in res:
         print(json.dumps(r), flush=True)
     if a.out:

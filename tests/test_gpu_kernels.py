@@ -615,10 +615,13 @@ def test_conv16_fp8_kernel(ks, shape):
 
 
 def test_immatchnet_fp8_nc_path(runtime):
-    """corr_dtype='fp8' (fp8 correlation + fp8 Conv4d NC kernels, forced with
-    config nc_fp8 (NCNET_NC_FP8=1): by default this (3,3)/(16,1) stack takes the faster fused
-    bf16 NC kernel) vs the bf16 path; the dispatch counters prove which NC
-    implementation ran."""
+    """corr_dtype='fp8' with config nc_fp8 (NCNET_NC_FP8=1): fp8 correlation and
+    the e4m3 fused NC kernel (nc_fused_k3_f8) for this symmetric (3,3)/(16,1)
+    stack, vs the bf16 path; the fp8 Conv4d NC kernels (the nc_fp8 path of
+    the other stacks) on the same NC input; without nc_fp8 the fused bf16
+    kernel.  The dispatch counters prove which NC implementation ran."""
+    import importlib
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
     runtime(nc_fp8=True)
     from ncnet_amd.models import ImMatchNet
     torch.manual_seed(0)
@@ -630,12 +633,23 @@ def test_immatchnet_fp8_nc_path(runtime):
     batch = {"source_image": torch.randn(1, 3, 256, 320, device=DEV),
              "target_image": torch.randn(1, 3, 256, 320, device=DEV)}
     with torch.inference_mode():
-        n_fused, n_fp8 = _ext.DISPATCH["nc_fused_k3"], _ext.DISPATCH["nc_fp8"]
+        n_fused, n_f8 = _ext.DISPATCH["nc_fused_k3"], _ext.DISPATCH["nc_fused_k3_f8"]
         c16, _ = m(batch)
         assert _ext.DISPATCH["nc_fused_k3"] == n_fused + 1          # bf16: the fused InLoc kernel
         m.corr_dtype = "fp8"
         c8, _ = m(batch)
-        assert _ext.DISPATCH["nc_fp8"] == n_fp8 + 1                # fp8: the fp8 MFMA Conv4d path
+        assert _ext.DISPATCH["nc_fused_k3_f8"] == n_f8 + 1          # fp8: the e4m3 fused kernel
+        # the fp8 Conv4d stack on a MutualMatching-like input vs the fused fp8 kernel and fp32
+        layers = m.NeighConsensus.conv_layers()
+        ws, bs = [l.weight_ref() for l in layers], [l.bias for l in layers]
+        x = torch.rand(1, 1, 8, 10, 8, 10, device=DEV) ** 3
+        n_fp8 = _ext.DISPATCH["nc_fp8"]
+        y_conv = nc.neigh_consensus(x, ws, bs, m.NeighConsensus.channels, symmetric=False, fp8=True)
+        assert _ext.DISPATCH["nc_fp8"] == n_fp8 + 1
+        y_fused = nc.neigh_consensus(x, ws, bs, m.NeighConsensus.channels, symmetric=True, fp8=True)
+        y32 = ref.neigh_consensus(x.double(), [w.double() for w in ws], [b.double() for b in bs], symmetric=True)
+        y32n = ref.neigh_consensus(x.double(), [w.double() for w in ws], [b.double() for b in bs], symmetric=False)
+    assert rel_l2(y_conv, y32n) < 0.15 and rel_l2(y_fused, y32) < 0.05
     assert c8.shape == c16.shape
     assert rel_l2(c8, c16) < 0.15
     runtime(nc_fp8=False)
@@ -1040,6 +1054,50 @@ def test_neigh_consensus_fused_symmetric_wrapper():
                                      [b1, b2], symmetric=True)
     yr = qo.neigh_consensus(x.double(), [w1.double(), w2.double()], [b1.double(), b2.double()], symmetric=True)
     assert relerr(y, yr) < 2e-3
+
+
+def _f8q(t, s):
+    """OCP e4m3 rounding at the power-of-two scale s (values returned unscaled, fp64)."""
+    return (t.double() * s).float().clamp(-448, 448).to(torch.float8_e4m3fn).double() / s
+
+
+@pytest.mark.parametrize("cfg", [None, (3, 4, 6, 7), (10, 4, 15, 20), (8, 3, 19, 17), (5, 2, 9, 11)])
+def test_nc_fused_k3_f8_vs_quantized_oracle(cfg):
+    """The e4m3 fused NC kernel (csrc/nc_fused.hip nc_fused_k3_f8: one MX
+    16x16x128 MFMA for taps 0-7 + one 16x16x32 fp8 MFMA for tap 8 per tile and
+    layer, register-resident weight fragments) against fp64 math with the same
+    e4m3 roundings (x0 * sx, weights * sw, hidden * sh): a wrong lane -> tap /
+    channel map shows as an O(1) error, the fp8 quantisation itself cancels.
+    cfg = (R, IR, TK, TL); the 3200 px (15 x 20, R 10) and 1600 px (19 x 17,
+    R 8) tiles are the compile-time instantiations."""
+    import importlib
+    nc = importlib.import_module("ncnet_amd.ops.neigh_consensus")
+    torch.manual_seed(41)
+    V, I, J, K, L = 2, 9, 13, 11, 14
+    w1 = torch.randn(16, 1, 3, 3, 3, 3, device=DEV) * 0.2
+    w2 = torch.randn(1, 16, 3, 3, 3, 3, device=DEV) * 0.1
+    b1, b2 = torch.rand(16, device=DEV) * 0.1 - 0.03, torch.rand(1, device=DEV) * 0.1
+    ws = [ref.conv4d_weight_from_std(w1), ref.conv4d_weight_from_std(w2)]
+    # MutualMatching-like input: [0, 1], most entries small
+    x0 = (torch.rand(V, I, J, K, L, device=DEV) ** 3).to(torch.bfloat16)
+    tens, (sx, inv1, sh, inv2) = nc._fused_weights_f8_build(ws, [b1, b2])
+    sw1, sw2 = 1.0 / (inv1 * sx), 1.0 / (inv2 * sh)
+    y = torch.full((V, I, J, K, L), float("nan"), device=DEV)
+    tk, tl, R, IR = nc.fused_tiles(V, I, J, K, L) if cfg is None else (cfg[2], cfg[3], cfg[0], cfg[1])
+    _ext.ext().nc_fused_k3_f8(x0, *tens, y, R, IR, tk, tl, sx, inv1, sh, inv2)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    xq = _f8q(x0, sx).unsqueeze(1)
+    h = torch.relu(ref.conv4d(xq, ref.conv4d_weight_from_std(_f8q(w1, sw1))) + b1.double().view(1, -1, 1, 1, 1, 1))
+    h = _f8q(h, sh)
+    yr = torch.relu(ref.conv4d(h, ref.conv4d_weight_from_std(_f8q(w2, sw2))) + b2.double().view(1, -1, 1, 1, 1, 1))
+    # (a hidden value on the other side of an e4m3 rounding boundary in fp32
+    # vs fp64 moves by one e4m3 ulp, 6 %: a few such flips, not O(1) errors)
+    assert relerr(y, yr.squeeze(1)) < 2e-2 and rel_l2(y, yr.squeeze(1)) < 2e-3
+    # and the unquantised fp64 stack: the e4m3 error of the whole NC
+    yf = ref.neigh_consensus(x0.double().unsqueeze(1), [w.double() for w in ws], [b1.double(), b2.double()],
+                             symmetric=False)
+    assert rel_l2(y, yf.squeeze(1)) < 0.05
 
 
 def _pad_1ch(x5, ks, trans=False):
