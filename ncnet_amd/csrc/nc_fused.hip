@@ -45,6 +45,13 @@ struct NCFGeom {
 };
 
 constexpr int NCF_NW = 8;          // waves per workgroup
+
+// Output-ring plane stride (words): nvox rounded up to 16 mod 32.  The ring
+// read-add-writes of one wave touch two planes at once (lane groups fq = 0, 1
+// hold combo columns dj2 = 0, 1 of the same voxels): with the planes 16 banks
+// apart the two 16-lane halves of a ds_read_b32 / ds_write_b32 never share a
+// bank (a 300-voxel plane put 4 of them on the same banks).
+__host__ __device__ constexpr int ncf_ring_stride(int nvox) { return nvox + ((16 - nvox % 32) + 32) % 32; }
 constexpr int NCF_MAXT1 = 4;       // layer-1 tiles per wave: (TK+2)(TL+2) <= 512 voxels
 constexpr int NCF_MAXT2 = 3;       // layer-2 tiles per wave: TK*TL <= 384 voxels
 
@@ -77,8 +84,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 1) void nc_fused_k3_kernel(c
   char* H = S + SR * SRS * 32;
   float* ring = (float*)(H + HR * HRS * 32);
   // ring + 64 trash words (one per lane), rounded to 16 B; then the weight fragments [2 layers][5 tap pairs][64 lanes]
-  u32x4* wl = (u32x4*)(ring + ((3 * GR * TK * TL + 64 + 3) & ~3));
   const int nvox = TK * TL;
+  const int rps = ncf_ring_stride(nvox);
+  u32x4* wl = (u32x4*)(ring + ((3 * GR * rps + 64 + 3) & ~3));
 
   // wave index made wave-uniform (an SGPR): the per-wave tile-count checks are
   // then scalar branches, not exec-mask save / restore sequences
@@ -166,7 +174,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 1) void nc_fused_k3_kernel(c
   const float bias2 = b2[0];
 
   // zero the output ring (3 row slots x R planes x TK*TL)
-  for (int o = threadIdx.x; o < 3 * GR * nvox; o += NW * 64) ring[o] = 0.f;
+  for (int o = threadIdx.x; o < 3 * GR * rps; o += NW * 64) ring[o] = 0.f;
 
   const int ih_lo = max(0, i0 - 1), ih_hi = min(g.I, i1 + 1);   // hidden rows [lo, hi)
   const int jh_lo = max(0, j0 - 1), jh_hi = min(g.J, j0 + R + 1); // hidden planes [lo, hi)
@@ -251,7 +259,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 1) void nc_fused_k3_kernel(c
       if (wave + NW * t >= nt2) continue;
       if (vo[t] < 0) continue;     // padding lanes of the last tile own no ring entry
       for (int p = pg; p < R; p += 4) {
-        float* rp = ring + (slot * GR + p) * nvox + vo[t];
+        float* rp = ring + (slot * GR + p) * rps + vo[t];
         const float val = fmaxf(*rp + bias2, 0.f);
         if (yvox[t] >= 0) yrow[(size_t)p * KL + yvox[t]] = val;
         *rp = 0.f;
@@ -342,13 +350,13 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 1) void nc_fused_k3_kernel(c
       // (never an entry another lane owns: the RMW would race): no exec-mask
       // branch around the update
       const bool lok = vo[u] >= 0 && p_ok;
-      const int roff = p2 * nvox + vo[u];
+      const int roff = p2 * rps + vo[u];
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int io = ih - r + 1;
         if (io < i0 || io >= i1) continue;
         const int slot = r == 0 ? slot0 : r == 1 ? (slot0 == 0 ? 2 : slot0 - 1) : (slot0 == 2 ? 0 : slot0 + 1);   // io % 3
-        float* rp = ring + (lok ? slot * GR * nvox + roff : 3 * GR * nvox + lane);   // trash: one word per lane
+        float* rp = ring + (lok ? slot * GR * rps + roff : 3 * GR * rps + lane);   // trash: one word per lane
         // read-add-write (lane-private entries); the LDS float atomic
         // (ds_add_f32) measured 3.2x slower for the whole kernel
         *rp += lok ? acc[r] : 0.f;
@@ -418,6 +426,7 @@ __global__ __launch_bounds__(512, 4) void nc_fused_k3_f8_kernel(const bf16* __re
   char* H = S + SR * SRS * 16;
   float* ring = (float*)(H + HR * HRS * 16);
   const int nvox = TK * TL;
+  const int rps = ncf_ring_stride(nvox);
 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   __builtin_assume(wave >= 0 && wave < NW);
@@ -485,7 +494,7 @@ __global__ __launch_bounds__(512, 4) void nc_fused_k3_f8_kernel(const bf16* __re
   for (int r = 0; r < 4; ++r) bias1[r] = b1[co0 + r];
   const float bias2 = b2[0];
 
-  for (int o = threadIdx.x; o < 3 * GR * nvox; o += NW * 64) ring[o] = 0.f;
+  for (int o = threadIdx.x; o < 3 * GR * rps; o += NW * 64) ring[o] = 0.f;
 
   const int ih_lo = max(0, i0 - 1), ih_hi = min(g.I, i1 + 1);
   const int jh_lo = max(0, j0 - 1), jh_hi = min(g.J, j0 + R + 1);
@@ -553,7 +562,7 @@ __global__ __launch_bounds__(512, 4) void nc_fused_k3_f8_kernel(const bf16* __re
       if (wave + NW * t >= nt2) continue;
       if (vo[t] < 0) continue;
       for (int p = pg; p < R; p += 4) {
-        float* rp = ring + (slot * GR + p) * nvox + vo[t];
+        float* rp = ring + (slot * GR + p) * rps + vo[t];
         const float val = fmaxf(*rp + bias2, 0.f);
         if (yvox[t] >= 0) yrow[(size_t)p * KL + yvox[t]] = val;
         *rp = 0.f;
@@ -608,13 +617,13 @@ __global__ __launch_bounds__(512, 4) void nc_fused_k3_f8_kernel(const bf16* __re
       const f32x4 a8 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(w2b, b8, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       const f32x4 acc = mfma_fp8_k128(w2a, bh, f32x4{0.f, 0.f, 0.f, 0.f}) + a8;
       const bool lok = vo[u] >= 0 && p_ok;
-      const int roff = p2 * nvox + vo[u];
+      const int roff = p2 * rps + vo[u];
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int io = ih - r + 1;
         if (io < i0 || io >= i1) continue;
         const int slot = r == 0 ? slot0 : r == 1 ? (slot0 == 0 ? 2 : slot0 - 1) : (slot0 == 2 ? 0 : slot0 + 1);
-        float* rp = ring + (lok ? slot * GR * nvox + roff : 3 * GR * nvox + lane);
+        float* rp = ring + (lok ? slot * GR * rps + roff : 3 * GR * rps + lane);
         *rp += lok ? acc[r] * sc.inv2 : 0.f;
       }
     }
@@ -652,8 +661,8 @@ extern "C" int ncnet_nc_fused_k3(const void* X, const void* W1p, const float* b1
   g.SRS = TL + 10;   // S rows: a layer-1 tile wrapping from column TL+1 to 0 jumps 9 voxels (one 256-B bank period + 1)
   g.HRS = TL + 8;    // h rows: a layer-2 tile wrapping from column TL-1 to 0 jumps 9 voxels
   if ((long long)I * J * K * L * 2 >= (1ll << 31)) return -4;   // buffer-resource byte offsets
-  size_t lds = (size_t)(TK + 4) * g.SRS * 32 + (size_t)(TK + 2) * g.HRS * 32 + (size_t)((3 * R * TK * TL + 64 + 3) & ~3) * 4 +
-               2 * 5 * 64 * 16;
+  size_t lds = (size_t)(TK + 4) * g.SRS * 32 + (size_t)(TK + 2) * g.HRS * 32 +
+               (size_t)((3 * R * ncf_ring_stride(TK * TL) + 64 + 3) & ~3) * 4 + 2 * 5 * 64 * 16;
   // > 80 KB: one 16-wave workgroup per CU (NW = 16) instead of two 8-wave ones
   const bool big = lds > 80 * 1024;
   const int nw = big ? 16 : 8;
@@ -694,7 +703,8 @@ extern "C" int ncnet_nc_fused_k3_f8(const void* X, const void* W1a, const void* 
   g.SRS = TL + 18;
   g.HRS = TL + 16;
   if ((long long)I * J * K * L * 2 >= (1ll << 31)) return -4;
-  const size_t lds = (size_t)(TK + 4) * g.SRS * 16 + (size_t)(TK + 2) * g.HRS * 16 + (size_t)(3 * R * TK * TL + 64) * 4;
+  const size_t lds = (size_t)(TK + 4) * g.SRS * 16 + (size_t)(TK + 2) * g.HRS * 16 +
+                     (size_t)(3 * R * ncf_ring_stride(TK * TL) + 64) * 4;
   if ((TK + 2) * (TL + 2) > 512 || TK * TL > 8 * 3 * 16 || (TK + 4) * (TL + 4) > 512 || R < 1 || IR < 1) return -2;
   if (lds > 80 * 1024) return -3;
   NCF8Scales sc{sx, inv1, sh, inv2};

@@ -1535,7 +1535,8 @@ def fused_tiles(V: int, I: int, J: int, K: int, L: int):
                 best = (cost, tk, tl)
     _, tk, tl = best
     fixed = (tk + 4) * (tl + 10) * 32 + (tk + 2) * (tl + 8) * 32 + 2 * 5 * 64 * 16 + 268   # + ring trash / alignment
-    r_max = max(1, (_FUSED_LDS - fixed) // (12 * tk * tl))
+    rps = tk * tl + (16 - (tk * tl) % 32) % 32        # ring plane stride (csrc/nc_fused.hip ncf_ring_stride)
+    r_max = max(1, (_FUSED_LDS - fixed) // (12 * rps))
     base = V * _cdiv(K, tk) * _cdiv(L, tl)
 
     def nwg(r, ir):
