@@ -45,6 +45,10 @@ struct Conv2dArgs {
 template <int BM, int BN, int TM, int TN, int NT, bool F16>
 __device__ __forceinline__ void conv2d_epilogue(const f32x4 (&acc)[TM][TN], const Conv2dArgs& p, char* smem, int m0,
                                                 int n0, int wm, int wn, int fr, int fq) {
+  constexpr int CPR = BN / 8;                     // 16-B chunks per tile row
+  constexpr int NIT = (BM * CPR + NT - 1) / NT;   // chunks per thread
+  const uint16_t* R = (const uint16_t*)p.R;
+  uint16_t* Y = (uint16_t*)p.Y;
   uint16_t* Ts = (uint16_t*)smem;                 // BM * BN * 2 bytes (fits the operand buffers)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -56,32 +60,48 @@ __device__ __forceinline__ void conv2d_epilogue(const f32x4 (&acc)[TM][TN], cons
       for (int r = 0; r < 4; ++r) Ts[(wm * TM * 16 + i * 16 + 4 * fq + r) * BN + col] = f2s16<F16>(acc[i][j][r] + b);
   }
   __syncthreads();
-  constexpr int CPR = BN / 8;                     // 16-B chunks per tile row
-  const uint16_t* R = (const uint16_t*)p.R;
-  uint16_t* Y = (uint16_t*)p.Y;
+  // Residual: the chunks of the thread are loaded RB at a time ahead of their
+  // stores.  Loaded inside the store loop, each load waited vmcnt(0) -- stores
+  // count in vmcnt -- behind the previous chunk's store: NIT serialised memory
+  // round trips per tile, which made the short-K residual 1x1 convs (K = 64 ...
+  // 256) epilogue-bound.  (All NIT ahead: the scheduler hoists them over the
+  // staging and the kernel doubles its VGPRs, halving the occupancy.)
+  constexpr int RB = NIT < 4 ? NIT : 4;
 #pragma unroll
-  for (int c = threadIdx.x; c < BM * CPR; c += NT) {
-    const int row = c / CPR, cc = c - row * CPR;
-    const int pix = m0 + row;
-    if (pix < p.M) {
-      const u32x4 tv = *(const u32x4*)(Ts + row * BN + cc * 8);
-      const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
-      u32x4 rv = {0u, 0u, 0u, 0u};
-      if (R) rv = *(const u32x4*)(R + o);
-      u32x4 out;
+  for (int i0 = 0; i0 < NIT; i0 += RB) {
+    u32x4 rv[RB];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        uint32_t w = 0;
+    for (int q = 0; q < RB; ++q) {
+      rv[q] = u32x4{0u, 0u, 0u, 0u};
+      const int c = (int)threadIdx.x + (i0 + q) * NT;
+      const int row = c / CPR, cc = c - row * CPR;
+      if (R && i0 + q < NIT && c < BM * CPR && m0 + row < p.M)
+        rv[q] = *(const u32x4*)(R + (size_t)(m0 + row) * p.Cout + n0 + cc * 8);
+    }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float v = s162f<F16>((uint16_t)(tv[e] >> (16 * h)));
-          if (R) v = s162f<F16>(f2s16<F16>(v + s162f<F16>((uint16_t)(rv[e] >> (16 * h)))));
-          if (p.relu) v = fmaxf(v, 0.f);
-          w |= (uint32_t)f2s16<F16>(v) << (16 * h);
+    for (int q = 0; q < RB; ++q) {
+      const int c = (int)threadIdx.x + (i0 + q) * NT;
+      const int row = c / CPR, cc = c - row * CPR;
+      const int pix = m0 + row;
+      if (i0 + q < NIT && c < BM * CPR && pix < p.M) {
+        const u32x4 tv = *(const u32x4*)(Ts + row * BN + cc * 8);
+        const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
+        const u32x4 rvi = rv[q];
+        u32x4 out;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint32_t w = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float v = s162f<F16>((uint16_t)(tv[e] >> (16 * h)));
+            if (R) v = s162f<F16>(f2s16<F16>(v + s162f<F16>((uint16_t)(rvi[e] >> (16 * h)))));
+            if (p.relu) v = fmaxf(v, 0.f);
+            w |= (uint32_t)f2s16<F16>(v) << (16 * h);
+          }
+          out[e] = w;
         }
-        out[e] = w;
+        *(u32x4*)(Y + o) = out;
       }
-      *(u32x4*)(Y + o) = out;
     }
   }
 }
@@ -532,10 +552,29 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
   constexpr int CPR = BN / 8;
   const uint16_t* R = (const uint16_t*)p.R;
   uint16_t* Y = (uint16_t*)p.Y;
-  for (int c = threadIdx.x; c < BM * CPR; c += 512) {
+  // residual loads RB at a time ahead of their stores (conv2d_epilogue)
+  constexpr int NIT = (BM * CPR + 511) / 512;
+  constexpr int RB = NIT < (X3 ? 2 : 4) ? NIT : (X3 ? 2 : 4);
+#pragma unroll
+  for (int i0 = 0; i0 < NIT; i0 += RB) {
+    u32x4 rh[RB], rl[RB];
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+      rh[q] = rl[q] = u32x4{0u, 0u, 0u, 0u};
+      const int c = (int)threadIdx.x + (i0 + q) * 512;
+      const int row = c / CPR, cc = c - row * CPR;
+      if (R && i0 + q < NIT && c < BM * CPR && m0 + row < p.M) {
+        const size_t o = (size_t)(m0 + row) * (X3 ? 2 * p.Cout : p.Cout) + n0 + cc * 8;
+        rh[q] = *(const u32x4*)(R + o);
+        if constexpr (X3) rl[q] = *(const u32x4*)(R + o + p.Cout);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RB; ++q) {
+    const int c = (int)threadIdx.x + (i0 + q) * 512;
     const int row = c / CPR, cc = c - row * CPR;
     const int pix = m0 + row;
-    if (pix >= p.M) continue;
+    if (i0 + q >= NIT || c >= BM * CPR || pix >= p.M) continue;
     if constexpr (X3) {
       // 8 channels: fp32 sum (+ residual hi + lo), ReLU, split into hi / lo
       const f32x4 v0 = *(const f32x4*)(P + row * G::PSTR + cc * 8);
@@ -543,11 +582,10 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
       float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       const size_t o = (size_t)pix * (2 * p.Cout) + n0 + cc * 8;
       if (R) {
-        const u32x4 rh = *(const u32x4*)(R + o), rl = *(const u32x4*)(R + o + p.Cout);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          v[e] += s162f<false>((uint16_t)(rh[e >> 1] >> (16 * (e & 1)))) +
-                  s162f<false>((uint16_t)(rl[e >> 1] >> (16 * (e & 1))));
+          v[e] += s162f<false>((uint16_t)(rh[q][e >> 1] >> (16 * (e & 1)))) +
+                  s162f<false>((uint16_t)(rl[q][e >> 1] >> (16 * (e & 1))));
       }
       u32x4 oh, ol;
 #pragma unroll
@@ -568,8 +606,7 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
     } else {
       const u32x4 tv = *(const u32x4*)(S + row * BN + cc * 8);
       const size_t o = (size_t)pix * p.Cout + n0 + cc * 8;
-      u32x4 rv = {0u, 0u, 0u, 0u};
-      if (R) rv = *(const u32x4*)(R + o);
+      const u32x4 rv = rh[q];
       u32x4 out;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -584,6 +621,7 @@ __global__ __launch_bounds__(512, 1) void conv2d_nhwc_v3_kernel(Conv2dArgs p) {
         out[e] = w;
       }
       *(u32x4*)(Y + o) = out;
+    }
     }
   }
 }

@@ -33,6 +33,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--res", type=int, default=3200)
     ap.add_argument("--n", type=int, default=0, help="images (default: 2 at 3200 px, 32 at 400 px)")
+    ap.add_argument("--residual", action="store_true",
+                    help="the n3 layers with their bottleneck residual (as the trunk runs them); auto variant only")
     a = ap.parse_args()
     C = _ext.ext()
     dev = torch.device("cuda")
@@ -58,7 +60,19 @@ def main():
         y = torch.empty(n, cout, Ho, Wo, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
         M, K = n * Ho * Wo, cin * k * k
         fl = 2.0 * M * cout * K
-        run = lambda: C.conv2d_nhwc(x, w, b, None, y, s, k // 2, 1)   # noqa: E731
+        res = None
+        if a.residual and name.endswith(".n3"):
+            res = torch.randn_like(y)
+        run = lambda: C.conv2d_nhwc(x, w, b, res, y, s, k // 2, 1)   # noqa: E731
+        if a.residual:
+            if res is None:
+                continue
+            C.set_tuning("conv2d_variant", 0)
+            t_a = timeit(run)
+            gb = (x.numel() + 2 * y.numel()) * 2 / 1e9
+            print(f"{name:8s}+res M={M} N={cout} K={K}: {t_a * 1e3:7.1f} us {fl / t_a / 1e9:5.0f} TF "
+                  f"{gb / t_a * 1e3:5.2f} TB/s", flush=True)
+            continue
         C.set_tuning("conv2d_variant", 1)
         t_1 = timeit(run)
         C.set_tuning("conv2d_variant", 2)
