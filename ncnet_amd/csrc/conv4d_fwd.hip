@@ -163,11 +163,22 @@ __device__ __forceinline__ void store16(const f32x4& acc, bf16* __restrict__ Y, 
 // Requires RW = TL + KS - 1 <= 32.  KS = 7 keeps its 25 weight fragments in
 // registers at one workgroup per CU (256 VGPRs) instead of two.
 // ===========================================================================
-template <int KS, int EPI, bool MT>
+// CT > 0: the (k, l) planes are CT x CT and the tile is the whole plane, fixed
+// at compile time (the Cout = 1 block layer at the 400 px training volume):
+// plane geometry, tile decode and the per-tap LDS offsets fold into constants
+// and instruction offsets instead of per-MFMA address VALU.
+template <int KS, int EPI, bool MT, int CT = 0>
 __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(const bf16* __restrict__ X, const u32x4* __restrict__ Wp,
                                                               const float* __restrict__ bias,
                                                               const bf16* __restrict__ M, bf16* __restrict__ Y,
-                                                              ConvGeom g) {
+                                                              ConvGeom g_in) {
+  ConvGeom g = g_in;
+  if constexpr (CT > 0) {
+    g.K = g.L = g.TK = g.TL = CT;
+    g.nkt = g.nlt = 1;
+    g.PR = g.RW = CT + KS - 1;
+    g.RS = CT + ((KS - 1 + 7) / 8) * 8;
+  }
   constexpr int P = KS / 2;
   constexpr int NT = KS * KS;
   constexpr int NQ = (NT + 1) / 2;
@@ -223,6 +234,19 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
     if (tap >= NT) tap = NT - 1;
     int dk = tap / KS, dl = tap - dk * KS;
     toff[q] = (uint32_t)((dk * g.RS + dl) * 32);
+  }
+  // CT: per-lane bases of the two lane halves (taps 2q and 2q + 1: the next
+  // voxel, or one row down with dl wrapped when 2q + 1 is a multiple of KS;
+  // the padded last pair reads voxel + 1 of its row against zero weights), so
+  // each tap's offset (2q's) is a compile-time ds_read immediate
+  uint32_t c1[CT > 0 ? MAXT : 1], c2[CT > 0 ? MAXT : 1];
+  if constexpr (CT > 0) {
+    const uint32_t hh = (uint32_t)(lane >> 5);
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      c1[tt] = vbase[tt] + hh * 32u;
+      c2[tt] = vbase[tt] + hh * (uint32_t)((g.RS - KS + 1) * 32);
+    }
   }
   f32x4 acc[MAXT];
 #pragma unroll
@@ -371,7 +395,14 @@ __global__ __launch_bounds__(512, KS >= 7 ? 1 : 2) void conv16v2_fwd_kernel(cons
       if (wave + NW * tt < ntile) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          bf16x8 xf = lds_read16(cur, vbase[tt] + toff[q]);
+          uint32_t a;
+          if constexpr (CT > 0) {
+            const uint32_t t0 = (uint32_t)((((2 * q) / KS) * g.RS + (2 * q) % KS) * 32);
+            a = (((2 * q + 1) % KS == 0 && 2 * q + 1 < NT) ? c2[tt] : c1[tt]) + t0;
+          } else {
+            a = vbase[tt] + toff[q];
+          }
+          bf16x8 xf = lds_read16(cur, a);
           acc[tt] = mfma16(wf[q], xf, acc[tt]);
         }
       }
@@ -1231,6 +1262,11 @@ extern "C" int ncnet_conv16_blk_fwd(const void* X, const void* Wp, const float* 
   size_t lds2 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
   dim3 grid((unsigned)(V * g.nib * g.njb * g.nkt * g.nlt)), block(512);
   const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp;
+  if (!x3 && KS == 5 && K == 25 && L == 25 && tk == 25 && tl == 25) {
+    hipLaunchKernelGGL((conv16v2_fwd_kernel<5, EPI_BLK1, false, 25>), grid, block, lds2, stream, x, w, bias, nullptr,
+                       (bf16*)Y, g);
+    return (int)hipGetLastError();
+  }
 #define LBLK(KSV, _) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPI_BLK1, false>), grid, block, lds2, stream, x, w, bias, nullptr, (bf16*)Y, g)
 #define LBLKX(KSV) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPI_BLK1 | EPI_X3, false>), grid, block, lds2, stream, x, w, bias, nullptr, (bf16*)Y, g)
   if (x3) {
