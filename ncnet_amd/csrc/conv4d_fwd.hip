@@ -1262,9 +1262,13 @@ extern "C" int ncnet_conv16_blk_fwd(const void* X, const void* Wp, const float* 
   size_t lds2 = 2 * (size_t)g.PR * g.RS * 32 + (size_t)nq * 1024;
   dim3 grid((unsigned)(V * g.nib * g.njb * g.nkt * g.nlt)), block(512);
   const bf16* x = (const bf16*)X; const u32x4* w = (const u32x4*)Wp;
-  if (!x3 && KS == 5 && K == 25 && L == 25 && tk == 25 && tl == 25) {
-    hipLaunchKernelGGL((conv16v2_fwd_kernel<5, EPI_BLK1, false, 25>), grid, block, lds2, stream, x, w, bias, nullptr,
-                       (bf16*)Y, g);
+  if (KS == 5 && K == 25 && L == 25 && tk == 25 && tl == 25) {   // the 400 px training planes
+    if (x3)
+      hipLaunchKernelGGL((conv16v2_fwd_kernel<5, EPI_BLK1 | EPI_X3, false, 25>), grid, block, lds2, stream, x, w, bias,
+                         nullptr, (bf16*)Y, g);
+    else
+      hipLaunchKernelGGL((conv16v2_fwd_kernel<5, EPI_BLK1, false, 25>), grid, block, lds2, stream, x, w, bias, nullptr,
+                         (bf16*)Y, g);
     return (int)hipGetLastError();
   }
 #define LBLK(KSV, _) hipLaunchKernelGGL((conv16v2_fwd_kernel<KSV, EPI_BLK1, false>), grid, block, lds2, stream, x, w, bias, nullptr, (bf16*)Y, g)
