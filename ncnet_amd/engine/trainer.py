@@ -3,7 +3,10 @@
 Differences from the reference, all semantics-preserving:
 * the negative pass reuses the positive-pass backbone features rolled by one
   (exact: the backbone is in eval mode and per-sample; SURVEY.md section 7.5);
-* the loss is read back to the host only every ``log_interval`` steps;
+* the loss is read back to the host asynchronously (``AsyncLossLog``: pinned
+  copies behind events, printed once complete; no per-step host sync), every
+  ``log_interval`` steps; ``sync_log`` restores the reference's synchronous
+  per-step ``float(loss)`` (train.py:175-180);
 * evaluation (``mode='test'``) runs under ``torch.inference_mode`` (the
   reference builds graphs it never uses, train.py:170-174);
 * gradients are averaged over ranks with one bucketed RCCL all-reduce;
@@ -27,6 +30,52 @@ from .. import config as _config
 from ..ops.loss import weak_loss_from_corr
 from ..parallel.dist import DistContext, GradBucket, all_reduce_mean
 from ..utils.timing import active as active_timer, segment
+
+
+class AsyncLossLog:
+    """Loss readback without host syncs.  ``push`` queues a device scalar:
+    a non-blocking copy into pinned host memory and an event behind it on the
+    current stream; ``poll`` returns the records whose events have completed
+    (``Event.query``, never a wait), in push order, each with the GPU time since
+    the log was created (``elapsed_s``, from timing events, so it does not
+    drift with the host running ahead).  ``drain`` waits for the rest (epoch
+    end).  Without CUDA, or with ``sync=True`` (the reference's synchronous
+    ``float(loss)`` per logged step), ``push`` reads the value immediately."""
+
+    def __init__(self, device, sync: bool = False):
+        self.cuda = torch.device(device).type == "cuda" and torch.cuda.is_available()
+        self.sync = sync or not self.cuda
+        self.pending = []
+        self.t0 = time.perf_counter()
+        self.ev0 = None
+        if self.cuda:
+            self.ev0 = torch.cuda.Event(enable_timing=True)
+            self.ev0.record()
+
+    def push(self, value: torch.Tensor, meta: dict) -> list:
+        if self.sync:
+            rec = dict(meta, loss=float(value))
+            if self.cuda:
+                torch.cuda.synchronize()
+            rec["elapsed_s"] = time.perf_counter() - self.t0
+            return [rec]
+        host = torch.empty((), dtype=torch.float32, pin_memory=True)
+        host.copy_(value.detach().float().reshape(()), non_blocking=True)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.pending.append((host, ev, meta))
+        return self.poll()
+
+    def poll(self, block: bool = False) -> list:
+        out = []
+        while self.pending and (block or self.pending[0][1].query()):
+            host, ev, meta = self.pending.pop(0)
+            ev.synchronize()
+            out.append(dict(meta, loss=float(host), elapsed_s=self.ev0.elapsed_time(ev) / 1e3))
+        return out
+
+    def drain(self) -> list:
+        return self.poll(block=True)
 
 
 def make_adam(params, lr: float) -> torch.optim.Optimizer:
@@ -228,18 +277,31 @@ class Trainer:
             with open(self.metrics_path, "a") as f:
                 f.write(json.dumps(rec) + "\n")
 
-    def process_epoch(self, mode: str, epoch: int, loader, log_interval: int = 1) -> float:
-        """Returns the epoch's mean loss (averaged over ranks)."""
+    def process_epoch(self, mode: str, epoch: int, loader, log_interval: int = 1, sync_log: bool = False) -> float:
+        """Returns the epoch's mean loss (averaged over ranks).  Every
+        ``log_interval``-th step's loss is printed and logged as in the
+        reference (train.py:175-180), read back through ``AsyncLossLog`` (no
+        per-step host sync; ``sync_log=True``: synchronous, as the reference)."""
         is_train = mode == "train"
         self.model.train(is_train)
         total = torch.zeros((), device=self.ctx.device)
         n = 0
-        t0 = time.perf_counter()
         nb = len(loader)
         it = iter(loader)
         nxt = next(it, None)
         nxt = self.to_device(nxt) if nxt is not None else None
         batch_idx = -1
+        log = AsyncLossLog(self.ctx.device, sync=sync_log)
+
+        def emit(recs):
+            for rec in recs:
+                if self.ctx.is_main:
+                    bi = rec["step"]
+                    print(f"{mode.capitalize()} Epoch: {epoch} [{bi}/{nb} ({100.0 * bi / max(nb, 1):.0f}%)]"
+                          f"\t\tLoss: {rec['loss']:.6f}", flush=True)
+                rec["pairs_per_s"] = rec["pairs"] / max(rec["elapsed_s"], 1e-9)
+                self._log(rec)
+
         while nxt is not None:
             batch_idx += 1
             batch = nxt
@@ -249,20 +311,17 @@ class Trainer:
             total += loss.float()
             n += 1
             if log_interval and batch_idx % log_interval == 0:
-                lv = float(all_reduce_mean(loss, self.ctx))
-                dt = time.perf_counter() - t0
-                if self.ctx.is_main:
-                    print(f"{mode.capitalize()} Epoch: {epoch} [{batch_idx}/{nb} ({100.0 * batch_idx / max(nb, 1):.0f}%)]"
-                          f"\t\tLoss: {lv:.6f}", flush=True)
                 pairs = n * batch["source_image"].shape[0] * self.ctx.world_size
-                rec = {"mode": mode, "epoch": epoch, "step": batch_idx, "loss": lv, "elapsed_s": dt,
-                       "pairs": pairs, "pairs_per_s": pairs / max(dt, 1e-9)}
+                meta = {"mode": mode, "epoch": epoch, "step": batch_idx, "pairs": pairs}
                 if self.ctx.device.type == "cuda":
-                    rec["hbm_peak_gb"] = torch.cuda.max_memory_allocated(self.ctx.device) / 2 ** 30
+                    meta["hbm_peak_gb"] = torch.cuda.max_memory_allocated(self.ctx.device) / 2 ** 30
                 timer = active_timer()
                 if timer is not None and timer.enabled:
-                    rec["segments_ms"] = timer.collect()
-                self._log(rec)
+                    meta["segments_ms"] = timer.collect()
+                emit(log.push(all_reduce_mean(loss, self.ctx), meta))
+            else:
+                emit(log.poll())
+        emit(log.drain())
         mean = float(all_reduce_mean(total / max(n, 1), self.ctx))
         if self.ctx.is_main:
             print(f"{mode.capitalize()} set: Average loss: {mean:.4f}", flush=True)

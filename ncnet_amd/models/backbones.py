@@ -226,14 +226,26 @@ def load_trunk_state(trunk: nn.Sequential, sd: dict, cnn: str = "resnet101") -> 
     lib/model.py:37-44): keys of the layers past the truncation are dropped,
     and any trunk tensor the file does not fill, or any other key, raises an
     error that names them (never a silently half-initialised trunk)."""
+    import re
+    # torchvision's legacy densenet keys ('denselayer1.norm.1.weight' ->
+    # 'denselayer1.norm1.weight'), as its densenet loader remaps them
+    legacy = re.compile(r"^(.*denselayer\d+\.(?:norm|relu|conv))\.((?:[12])\.(?:weight|bias|running_mean|running_var))$")
     mapped, dropped = {}, 0
     for k, v in sd.items():
+        m = legacy.match(k)
+        if m:
+            k = m.group(1) + m.group(2)
         tk = _trunk_key(k, cnn, len(trunk))
         if tk is None:
             dropped += 1
         else:
             mapped[tk] = v
     want = trunk.state_dict()
+    # files older than BatchNorm's counter (the ImageNet checkpoints the
+    # reference starts from) have no num_batches_tracked: 0, as BN's own loader
+    for k in want:
+        if k.endswith("num_batches_tracked") and k not in mapped:
+            mapped[k] = torch.zeros_like(want[k])
     missing = sorted(set(want) - set(mapped))
     unexpected = sorted(set(mapped) - set(want))
     bad_shape = sorted(k for k in set(want) & set(mapped) if tuple(want[k].shape) != tuple(mapped[k].shape))

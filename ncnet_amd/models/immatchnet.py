@@ -9,8 +9,11 @@ Compute policy (MI355X):
   (MIOpen); frozen BN is optionally folded into the convs;
 * L2-norm + operand packing, correlation GEMM, MutualMatching, the Conv4d
   stack and the loss reductions run on the hand-written HIP kernels;
-* ``half_precision`` is kept for API parity: the NC path always runs bf16
-  operands with fp32 accumulation on GPU.
+* ``half_precision`` (the reference's InLoc setting) runs the correlation and
+  the NeighConsensus on IEEE-half operands (f16 MFMA, fp32 accumulation);
+  otherwise the NC path runs bf16 operands, or, by ``nc_precision``, the
+  fp32-accurate bf16x3 split ('fp32') or its fp32-forward / bf16-backward mix
+  ('mixed'), and ``corr_dtype='fp8'`` selects the e4m3 inference path.
 """
 from __future__ import annotations
 
@@ -289,6 +292,15 @@ class ImMatchNet(nn.Module):
             for name, t in self.NeighConsensus.state_dict().items():
                 t.copy_(sd["NeighConsensus." + name])
         self.FeatureExtraction.eval()
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """nn.Module.load_state_dict, then drop the cross-call weight-pack cache
+        (ops/packing.py): a load with ``assign=True`` rebinds the parameters and a
+        later ``p.data`` edit would not bump their versions."""
+        from ..ops.packing import clear_pack_cache
+        out = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        clear_pack_cache()
+        return out
 
     # -- training-mode control: the backbone stays in eval (BN frozen), as in
     #    lib/model.py:251 and train.py:188.

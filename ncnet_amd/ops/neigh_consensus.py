@@ -1351,10 +1351,12 @@ class NeighConsensusMixedFn(torch.autograd.Function):
     NeighConsensusX3FusedFn (fp32-accurate input, weights and hidden
     activations) with a bf16 backward -- bf16 gradients, bf16 weights in the
     data gradients, each weight gradient the (X_hi, G) + (X_lo, G) products --
-    on the bf16 training kernels (the padded-plane 1-channel path).  The
-    per-stage ablation (scripts/precision_ablation.py, profiles/r5/ablation)
-    measured this mix at the PCK of the all-bf16x3 mode (0.533 vs 0.535 over 4
-    seeds) for 2/3 of its NeighConsensus work."""
+    on the bf16 training kernels (the padded-plane 1-channel path).  It keeps
+    the fp32-accurate forward for ~2/3 of the fp32 mode's NeighConsensus work.
+    Over 24 seeds (scripts/precision_ablation.py, profiles/r5/ablation) bf16,
+    this mix and fp32 took off at the same rate within noise (the earlier
+    4-seed 0.533 vs 0.535 PCK comparison is withdrawn): there is no evidence
+    that it learns where bf16 does not."""
 
     @staticmethod
     def forward(ctx, x, kinds, channels, *params):

@@ -15,8 +15,10 @@ Packing is a single gather with cached index tensors, done once per forward
 from __future__ import annotations
 
 import functools
+import weakref
 
 import torch
+import torch.utils.weak as _weak
 
 
 def transpose_for_dgrad(w_std: torch.Tensor) -> torch.Tensor:
@@ -199,7 +201,18 @@ def gather_pack(fn, w_std: torch.Tensor) -> torch.Tensor:
 
 
 _PLAN_CACHE: dict = {}
-_PACK_CACHE: dict = {}
+# cross-call pack cache, keyed by the first weight OBJECT (weakly: a freed model
+# drops its packs, and a new model whose weights land at the same addresses
+# can never hit them); each entry also holds weak references to the other
+# weights, checked by identity, and their (storage, offset, version) triples.
+# In-place writes through ``p.data`` do not bump ``p._version``: call
+# ``clear_pack_cache()`` after such an edit (ImMatchNet.load_state_dict does).
+_PACK_CACHE = _weak.WeakIdKeyDictionary()
+
+
+def clear_pack_cache() -> None:
+    """Forget every cached weight pack (the next call re-packs)."""
+    _PACK_CACHE.clear()
 
 
 def _source(ws):
@@ -238,19 +251,23 @@ def _plan(shapes, offsets, nsrc, specs, device):
 
 def packed_weights(ws, specs):
     """The packs ``[fn(std(ws[i])) for i, fn in specs]`` (bf16) with one gather
-    launch on the GPU (the weights in checkpoint layout, fp32)."""
+    launch on the GPU (the weights in checkpoint layout, fp32).  Reused across
+    calls while the same weight objects are unchanged (see ``_PACK_CACHE``)."""
     from . import _ext
     specs = tuple(specs)
-    ws = [w.detach() for w in ws]
+    orig = list(ws)
+    ws = [w.detach() for w in orig]
     if not (ws[0].is_cuda and _ext.use_hip(ws[0]) and all(fn in _F64 for _, fn in specs)):
         from .reference import conv4d_weight_to_std
         return [gather_pack(fn, conv4d_weight_to_std(ws[i]).float()) for i, fn in specs]
     src = _source(ws)
-    ver = tuple((w.untyped_storage().data_ptr(), w.storage_offset(), w._version) for w in ws)
-    ckey = (ver, specs)
-    hit = _PACK_CACHE.get(specs)
-    if hit is not None and hit[0] == ckey and not torch.cuda.is_current_stream_capturing():
-        return hit[1]
+    ckey = tuple((w.untyped_storage().data_ptr(), w.storage_offset(), w._version, tuple(w.shape)) for w in ws)
+    capturing = torch.cuda.is_current_stream_capturing()
+    per = _PACK_CACHE.get(orig[0])
+    hit = per.get(specs) if per is not None else None
+    if (hit is not None and not capturing and hit[0] == ckey and len(hit[1]) == len(orig) - 1
+            and all(r() is o for r, o in zip(hit[1], orig[1:]))):
+        return hit[2]
     if src is None:
         flat = torch.cat([w.float().reshape(-1) for w in ws])
         offs, o = [], 0
@@ -269,8 +286,10 @@ def packed_weights(ws, specs):
             n *= d
         res.append(out[o:o + n].view(sh))
         o += n
-    if not torch.cuda.is_current_stream_capturing():
-        _PACK_CACHE[specs] = (ckey, res)
+    if not capturing:
+        if per is None:
+            per = _PACK_CACHE[orig[0]] = {}
+        per[specs] = (ckey, [weakref.ref(w) for w in orig[1:]], res)
     return res
 
 

@@ -126,6 +126,10 @@ def main():
     cases = {
         "conv16_fwd": (lambda: C.conv16_fwd(x16, w16, b16, None, y16, ks, 1), fl16),
         "conv16_dgrad_mask": (lambda: C.conv16_fwd(g16, w16, None, x16, y16, ks, 2), fl16),
+        # same kernels with the other operand distribution (DVFS: the clock the
+        # chip holds depends on the data, so fwd vs dgrad is compared both ways)
+        "conv16_fwd_dense": (lambda: C.conv16_fwd(g16, w16, b16, None, y16, ks, 1), fl16),
+        "conv16_dgrad_sparse": (lambda: C.conv16_fwd(x16, w16, None, x16, y16, ks, 2), fl16),
         "conv16_fwd_v3": (with_env("NCNET_CONV_V3", "1", lambda: C.conv16_fwd(x16, w16, b16, None, y16, ks, 1)), fl16),
         "conv16_dgrad_v3": (with_env("NCNET_CONV_V3", "1", lambda: C.conv16_fwd(g16, w16, None, x16, y16, ks, 2)), fl16),
         "conv16_f32": (lambda: C.conv16_fwd(x16, w16, None, None, torch.empty((16,) + shp, device=dev), ks, 4), fl16),

@@ -67,6 +67,34 @@ def test_packed_weights_gpu_equal_packers(ks):
     assert torch.equal(b[0], P.pack_w1x(conv4d_weight_to_std(ws[0]).float()).to(torch.bfloat16))
 
 
+def test_pack_cache_keyed_on_weight_objects():
+    """A model freed and a new one of the same shape (whose weights the
+    caching allocator may place at the old addresses, with equal version
+    counters) must never get the old model's packs; a ``p.data`` edit (no
+    version bump) re-packs after clear_pack_cache (ImMatchNet.load_state_dict)."""
+    ks = 5
+    shapes = [(ks, 16, 1, ks, ks, ks), (ks, 16, 16, ks, ks, ks), (ks, 1, 16, ks, ks, ks)]
+    specs = [(0, P.pack_w1x), (1, P.pack_w16), (2, P._blk_packed)]
+
+    def model(seed):
+        g = torch.Generator(device=DEV).manual_seed(seed)
+        return [torch.nn.Parameter(torch.randn(sh, device=DEV, generator=g)) for sh in shapes]
+
+    for seed in range(4):
+        ws = model(seed)
+        got = [g.clone() for g in P.packed_weights(ws, specs)]
+        for (wi, fn), g in zip(specs, got):
+            assert torch.equal(g, fn(conv4d_weight_to_std(ws[wi]).float()).to(torch.bfloat16)), seed
+        del ws
+    ws = model(7)
+    a = P.packed_weights(ws, specs)
+    ws[1].data.mul_(3.0)                     # no version bump
+    P.clear_pack_cache()
+    b = P.packed_weights(ws, specs)
+    assert torch.equal(b[1], P.pack_w16(conv4d_weight_to_std(ws[1]).float()).to(torch.bfloat16))
+    assert not torch.equal(a[1], b[1])
+
+
 @pytest.mark.parametrize("norm", [0, 1, 2])
 def test_score_sum_and_gscale(norm):
     from ncnet_amd.ops import loss as L

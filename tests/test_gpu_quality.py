@@ -83,11 +83,12 @@ def test_training_tracks_fp32_reference():
 #                  the operating points), volumes <= 3.4e-4;
 #   fe_finetune:   layer error 4.6e-3 .. 1.9e-2, volumes <= 4.9e-4, raw-feature
 #                  gradient <= 4.6e-2; a first-MutualMatching near-tie point
-#                  reached 3.9e-2 .. 5.1e-2 per NC tensor in the earlier build
-#                  (nc_any: one of the four points may sit at such a tie)
+#                  reached 3.9e-2 .. 5.1e-2 per NC tensor in the earlier build;
+#                  nc_any (the worst of the four points) sits just above what
+#                  this build measures, so a regression at one point fails
 ORACLE_POINTS = (0, 10, 20, 30)
 ORACLE_TOL = {0: {"vols": 5e-4, "nc": 2e-2, "nc_any": 2e-2},
-              1: {"vols": 1e-3, "nc": 2.5e-2, "nc_any": 6e-2, "d_raw": 6e-2}}
+              1: {"vols": 1e-3, "nc": 2.5e-2, "nc_any": 3e-2, "d_raw": 6e-2}}
 
 
 @pytest.fixture

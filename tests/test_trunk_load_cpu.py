@@ -65,3 +65,34 @@ def test_vgg_features_keys():
     trunk, _, _ = build_trunk("vgg")
     load_trunk_state(trunk, sd, "vgg")
     assert torch.equal(trunk.state_dict()["21.weight"], full.state_dict()["21.weight"])
+
+
+def test_file_without_num_batches_tracked_loads():
+    """ImageNet checkpoints older than BatchNorm's counter have no
+    num_batches_tracked keys; BN's own loader fills them with 0, and so must
+    the strict trunk load."""
+    sd = {k: v for k, v in _full_resnet_sd().items() if not k.endswith("num_batches_tracked")}
+    trunk, _, _ = build_trunk("resnet50")
+    load_trunk_state(trunk, sd, "resnet50")
+    got = trunk.state_dict()
+    assert torch.equal(got["6.5.conv3.weight"], sd["layer3.5.conv3.weight"])
+    assert int(got["1.num_batches_tracked"]) == 0
+
+
+def test_densenet_legacy_keys_load():
+    """The legacy torchvision densenet file names 'denselayerN.norm.1.weight';
+    the load remaps it to 'norm1' as torchvision's densenet loader does."""
+    import re
+    src, _, _ = build_trunk("densenet201")
+    pat = re.compile(r"^(.*denselayer\d+\.(?:norm|relu|conv))((?:[12])\.(?:weight|bias|running_mean|running_var))$")
+    sd = {}
+    for k, v in src.state_dict().items():
+        if k.endswith("num_batches_tracked"):
+            continue
+        m = pat.match(k)
+        sd[(m.group(1) + "." + m.group(2)) if m else k] = v.clone() + 1
+    assert any(".norm.1." in k for k in sd)
+    trunk, _, _ = build_trunk("densenet201")
+    load_trunk_state(trunk, sd, "densenet201")
+    k = next(k for k in trunk.state_dict() if "denselayer" in k and k.endswith("norm1.weight"))
+    assert torch.equal(trunk.state_dict()[k], src.state_dict()[k] + 1)

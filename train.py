@@ -4,7 +4,9 @@
 Same flags and defaults as the reference, plus:
   --synthetic N        train on N random pairs instead of a CSV dataset
   --num_workers W      data-loader workers per rank (reference: 0 train / 4 test)
-  --log_interval L     loss readback interval (reference: 1)
+  --log_interval L     loss print interval (reference: 1); the values are read
+                       back asynchronously (no per-step host sync)
+  --sync_log           synchronous per-step loss readback, as the reference
   --resume PATH        real resume: weights + optimizer + epoch + RNG state
   --max_steps S        stop after S training steps (smoke / profiling)
   --metrics PATH       JSONL metrics (rank 0)
@@ -17,8 +19,8 @@ Same flags and defaults as the reference, plus:
                        bits per operand).  mixed: the stages the per-stage
                        ablation found necessary (profiles/r5/ablation): the
                        fp32-accurate trunk and NeighConsensus forward, a bf16
-                       correlation and bf16 NeighConsensus backward -- the PCK
-                       of fp32 mode (0.533 vs 0.535, 4 seeds) at 2/3 of its NC work.
+                       correlation and bf16 NeighConsensus backward (fp32-class
+                       forward numerics at 2/3 of the fp32 mode's NC work).
 
 Which precision to train with: bf16 unless you need fp32-class numerics.  A
 per-stage ablation over 24 seeds in the hardest offline regime (random-init
@@ -50,7 +52,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from ncnet_amd.data import ImagePairDataset, NormalizeImageDict, SyntheticPairDataset  # noqa: E402
 from ncnet_amd.data.datasets import collate_uint8_pairs, gpu_pair_batch  # noqa: E402
 from ncnet_amd.engine.checkpoint import capture_rng, load_checkpoint, restore_rng, save_checkpoint  # noqa: E402
-from ncnet_amd.engine.trainer import Trainer, make_adam  # noqa: E402
+from ncnet_amd.engine.trainer import AsyncLossLog, Trainer, make_adam  # noqa: E402
 from ncnet_amd.models import ImMatchNet  # noqa: E402
 from ncnet_amd.parallel.dist import barrier, broadcast_module, destroy, init_distributed, shard_indices  # noqa: E402
 from ncnet_amd.utils.timing import SegmentTimer, set_active  # noqa: E402
@@ -78,6 +80,9 @@ def build_parser():
     p.add_argument("--cpu_resize", action="store_true",
                    help="resize/normalise in the workers (reference behaviour) instead of on the GPU")
     p.add_argument("--log_interval", type=int, default=1)
+    p.add_argument("--sync_log", action="store_true",
+                   help="read every logged loss back synchronously (the reference's float(loss) per step); "
+                        "default: asynchronous pinned-memory readback, printed when ready")
     p.add_argument("--resume", type=str, default="")
     p.add_argument("--max_steps", type=int, default=0)
     p.add_argument("--metrics", type=str, default="")
@@ -85,8 +90,9 @@ def build_parser():
     p.add_argument("--nc_precision", type=str, default="bf16", choices=["bf16", "mixed", "fp32"],
                    help="fp32: fp32-accurate training (fp32 trunk, bf16x3 correlation + NeighConsensus fwd/bwd on "
                         "the fused kernels); mixed: fp32-accurate trunk + NeighConsensus forward, bf16 correlation "
-                        "and backward (trains like fp32, cheaper); use either when the weak-loss signal is below bf16 "
-                        "resolution (see --help text at the top of train.py)")
+                        "and backward (fp32-class forward numerics at ~1/3 less NC cost than fp32). Over 24 seeds "
+                        "bf16, mixed and fp32 took off at the same rate (profiles/r5/ablation): there is no evidence "
+                        "that either learns where bf16 does not; pick them for forward numerics, not for learning")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--segment_timing", action="store_true")
     p.add_argument("--profile", type=str, default="")
@@ -211,6 +217,14 @@ def main(argv=None):
                 for b in train_loader:
                     yield b
         it = batches()
+        steplog = AsyncLossLog(ctx.device, sync=args.sync_log)
+
+        def show(recs):
+            for r in recs:
+                msg = f"step {r['step']} loss {r['loss']:.6f}"
+                if "segments_ms" in r:
+                    msg += " " + " ".join(f"{k}={v:.2f}ms" for k, v in r["segments_ms"].items())
+                print(msg, flush=True)
         nxt = trainer.to_device(next(it))
         while steps < args.max_steps:
             batch = nxt
@@ -223,10 +237,14 @@ def main(argv=None):
                     torch.cuda.synchronize()
                 t_warm = time.perf_counter()
             if ctx.is_main and (steps % max(1, args.log_interval) == 0):
-                msg = f"step {steps} loss {float(loss):.6f}"
+                meta = {"step": steps}
                 if timer is not None:
-                    msg += " " + " ".join(f"{k}={v:.2f}ms" for k, v in timer.collect().items())
-                print(msg, flush=True)
+                    meta["segments_ms"] = timer.collect()
+                show(steplog.push(loss, meta))
+            elif ctx.is_main:
+                show(steplog.poll())
+        if ctx.is_main:
+            show(steplog.drain())
         if ctx.device.type == "cuda":
             torch.cuda.synchronize()
         if prof is not None:
@@ -253,8 +271,8 @@ def main(argv=None):
         print("Starting training...")
     for epoch in range(start_epoch, args.num_epochs + 1):
         tr_sampler.set_epoch(epoch)
-        train_loss[epoch - 1] = trainer.process_epoch("train", epoch, train_loader, args.log_interval)
-        test_loss[epoch - 1] = trainer.process_epoch("test", epoch, test_loader, args.log_interval)
+        train_loss[epoch - 1] = trainer.process_epoch("train", epoch, train_loader, args.log_interval, args.sync_log)
+        test_loss[epoch - 1] = trainer.process_epoch("test", epoch, test_loader, args.log_interval, args.sync_log)
         is_best = test_loss[epoch - 1] < best_test_loss
         best_test_loss = min(test_loss[epoch - 1], best_test_loss)
         if ctx.is_main:
