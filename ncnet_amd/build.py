@@ -134,7 +134,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, v
     if force or steps or not target.exists() or any(o.stat().st_mtime > target.stat().st_mtime for o in objs):
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(target) + ".tmp",
                 "-L", libdir, "-Wl,-rpath," + libdir, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
-                "-ltorch_hip", "-ltorch_python", "-L", os.path.join(ROCM, "lib"), "-lamdhip64"]
+                "-ltorch_hip", "-ltorch_python", "-L", os.path.join(ROCM, "lib"), "-lamdhip64", "-lhipblaslt",
+                "-Wl,-rpath," + os.path.join(ROCM, "lib")]
         if variant == "asan":
             link += ["-shared-libasan", "-fsanitize=address"]
         _run(link)

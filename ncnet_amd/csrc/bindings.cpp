@@ -29,6 +29,7 @@ int ncnet_stem_im2col_x3(const float*, void*, int, int, int, int, int, int, int,
 int ncnet_maxpool_x3(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_x3_to_f32(const void*, float*, long long, int, hipStream_t);
 int ncnet_conv2d_nhwc(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_gemm_lt(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, hipStream_t);
 int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, void*, int, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
 int ncnet_corr_gemm(const void*, const void*, void*, const int*, const int*, int, int, int, int, long long, long long,
@@ -850,6 +851,38 @@ void conv2d_nhwc(Tensor X, Tensor W, Tensor bias, c10::optional<Tensor> R, Tenso
      "conv2d_nhwc");
 }
 
+// 1x1 conv as a hipBLASLt GEMM with the fused bias (+ residual) (+ ReLU)
+// epilogue (csrc/gemm_lt.hip).  X [N,Cin,H,W], W [Cout,Cin,1,1], R / Y
+// [N,Cout,H,W]: bf16 / fp16 channels-last (or 2-D row-major [M, C]); bias fp32.
+void gemm_lt(Tensor X, Tensor W, Tensor bias, c10::optional<Tensor> R, Tensor Y, int64_t relu, int64_t tune) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  const bool h = X.scalar_type() == at::kHalf;
+  const auto dt = h ? at::kHalf : at::kBFloat16;
+  auto rows = [&](const Tensor& t, const char* name, int64_t c) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == dt, "gemm_lt: ", name, " must be a GPU tensor of X's dtype");
+    if (t.dim() == 4) {
+      TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast) && t.size(1) == c,
+                  "gemm_lt: ", name, " must be channels-last with ", c, " channels");
+      return t.size(0) * t.size(2) * t.size(3);
+    }
+    TORCH_CHECK(t.dim() == 2 && t.is_contiguous() && t.size(1) == c, "gemm_lt: ", name, " must be [M, ", c, "]");
+    return t.size(0);
+  };
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 || h, "gemm_lt: X must be bf16 or fp16");
+  const int64_t Cout = W.size(0), Cin = W.size(1);
+  TORCH_CHECK(W.is_cuda() && W.scalar_type() == dt && W.numel() == Cout * Cin &&
+              (W.dim() == 2 ? W.is_contiguous() : W.is_contiguous(at::MemoryFormat::ChannelsLast)),
+              "gemm_lt: W must be [Cout, Cin(, 1, 1)] of X's dtype");
+  const int64_t M = rows(X, "X", Cin);
+  TORCH_CHECK(rows(Y, "Y", Cout) == M, "gemm_lt: Y rows mismatch");
+  if (R.has_value()) TORCH_CHECK(rows(*R, "R", Cout) == M, "gemm_lt: R rows mismatch");
+  check(bias, "bias", at::kFloat); check_shape(bias, "bias", {Cout});
+  TORCH_CHECK(M < (1LL << 31), "gemm_lt: M exceeds int32");
+  ok(ncnet_gemm_lt(X.data_ptr(), W.data_ptr(), (const float*)bias.data_ptr(), R.has_value() ? R->data_ptr() : nullptr,
+                   Y.data_ptr(), (int)M, (int)Cin, (int)Cout, relu ? 1 : 0, h ? 1 : 0, tune ? 1 : 0, cur_stream(X)),
+     "gemm_lt");
+}
+
 // bf16x3 (fp32-accurate) trunk, csrc/conv2d.hip conv2d_nhwc_v3 X3 + csrc/epilogue.hip:
 // activations are contiguous [N, H, W, 2C] bf16 = [hi | lo] channel pairs.
 // W3 [Cout, KH, KW, 3 Cin] = [W_hi | W_hi | W_lo]; bias fp32 [Cout].
@@ -985,6 +1018,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_", &bias_act_);
   m.def("maxpool_bias_act", &maxpool_bias_act);
   m.def("conv2d_nhwc", &conv2d_nhwc);
+  m.def("gemm_lt", &gemm_lt, py::arg("X"), py::arg("W"), py::arg("bias"), py::arg("R"), py::arg("Y"),
+        py::arg("relu"), py::arg("tune") = 0);
   m.def("l2norm_rows", &l2norm_rows);
   m.def("l2norm_rows_bwd", &l2norm_rows_bwd);
   m.def("corr_gemm", &corr_gemm);

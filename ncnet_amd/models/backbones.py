@@ -401,10 +401,11 @@ class FrozenResNetPlan(nn.Module):
         self.use_graphs = _config.RUNTIME.trunk_graph
         # "native": NHWC implicit-GEMM HIP kernels with fused bias/residual/ReLU
         # (csrc/conv2d.hip); "blas": hipBLASLt 1x1 GEMMs + MIOpen 3x3 + bias_act;
-        # "auto" (default): native, except each bottleneck's first 1x1 conv
-        # (bias + ReLU, no residual) goes to hipBLASLt's fused-epilogue GEMM
-        # where that measured faster for this input shape (timed once per shape
-        # in the eager warm-up before the graph capture)
+        # "auto" (default): native 3x3 / strided convs; every 1x1 stride-1 conv
+        # (n1, the residual n3, the layer-1 downsample) on the native kernel or
+        # on hipBLASLt with the same fused bias + residual + ReLU epilogue
+        # (csrc/gemm_lt.hip), whichever measured faster for this input shape
+        # (timed once per shape in the eager warm-up before the graph capture)
         self.conv_mode = _config.RUNTIME.trunk_conv
         self._graphs = {}
         self._tuned = {}
@@ -518,15 +519,27 @@ class FrozenResNetPlan(nn.Module):
         graph.replay()
         return static_out.clone(memory_format=torch.channels_last)
 
-    def _n1_blas(self, x: torch.Tensor, p) -> torch.Tensor:
-        n, _, h, w = x.shape
-        return self._nchw(torch._addmm_activation(p["b1"], self._rows(x), p["w1t"]), n, h, w)
+    @staticmethod
+    def _lt(x: torch.Tensor, p, relu: bool, res: torch.Tensor | None = None, tune: bool = False) -> torch.Tensor:
+        """1x1 stride-1 conv as a hipBLASLt GEMM with the fused bias (+ residual)
+        (+ ReLU) epilogue (csrc/gemm_lt.hip)."""
+        from ..ops import _ext
+        w, b = p[0], p[1]
+        n, _, h, wd = x.shape
+        y = torch.empty((n, w.shape[0], h, wd), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        _ext.ext().gemm_lt(x, w, b, res, y, 1 if relu else 0, 1 if tune else 0)
+        return y
 
-    def _n1(self, x: torch.Tensor, p, bi: int) -> torch.Tensor:
-        """First 1x1 conv of bottleneck ``bi`` (bias + ReLU): the native kernel or
-        hipBLASLt, whichever measured faster at this shape (tuned outside graph
-        capture; until tuned, and on any tie, native)."""
-        key = (tuple(x.shape), bi)
+    def _c1(self, x: torch.Tensor, p, relu: bool, res: torch.Tensor | None, name) -> torch.Tensor:
+        """A bottleneck conv (``name`` = (block, 'n1' | 'n3' | 'nd')): the native
+        implicit-GEMM kernel or, for 1x1 stride-1 convs, hipBLASLt with the same
+        fused epilogue, whichever measured faster at this input shape (timed in
+        the eager warm-up before the graph capture; until then, and on a tie,
+        native)."""
+        w, _, stride, pad = p
+        if not (w.shape[-1] == 1 and w.shape[-2] == 1 and stride == 1 and pad == 0):
+            return self._nconv(x, p, relu, res)
+        key = (tuple(x.shape), name)
         choice = self._tuned.get(key)
         if choice is None:
             if torch.cuda.is_current_stream_capturing():
@@ -541,11 +554,12 @@ class FrozenResNetPlan(nn.Module):
                     e1.record()
                     e1.synchronize()
                     return e0.elapsed_time(e1)
-                tn = t(lambda: self._nconv(x, p["n1"], True))
-                tb = t(lambda: self._n1_blas(x, p))
-                choice = "blas" if tb < 0.95 * tn else "native"
+                self._lt(x, p, relu, res, tune=True)          # hipBLASLt's candidates timed once per shape
+                tn = t(lambda: self._nconv(x, p, relu, res))
+                tb = t(lambda: self._lt(x, p, relu, res))
+                choice = "blas" if tb < 0.97 * tn else "native"
                 self._tuned[key] = choice
-        return self._n1_blas(x, p) if choice == "blas" else self._nconv(x, p["n1"], True)
+        return self._lt(x, p, relu, res) if choice == "blas" else self._nconv(x, p, relu, res)
 
     def tuned_choices(self) -> dict:
         """{(input shape, bottleneck index): 'native' | 'blas'} picked so far."""
@@ -583,10 +597,16 @@ class FrozenResNetPlan(nn.Module):
                 else:
                     x = F.max_pool2d(x, *p).contiguous(memory_format=torch.channels_last)
             elif self.conv_mode in ("native", "auto") and x.is_cuda and self.dtype in (torch.bfloat16, torch.float16):
-                y1 = self._n1(x, p, bi) if self.conv_mode == "auto" else self._nconv(x, p["n1"], True)
-                y2 = self._nconv(y1, p["n2"], True)
-                idt = x if p["nd"] is None else self._nconv(x, p["nd"], False)
-                x = self._nconv(y2, p["n3"], True, idt)
+                if self.conv_mode == "auto":
+                    y1 = self._c1(x, p["n1"], True, None, (bi, "n1"))
+                    y2 = self._nconv(y1, p["n2"], True)
+                    idt = x if p["nd"] is None else self._c1(x, p["nd"], False, None, (bi, "nd"))
+                    x = self._c1(y2, p["n3"], True, idt, (bi, "n3"))
+                else:
+                    y1 = self._nconv(x, p["n1"], True)
+                    y2 = self._nconv(y1, p["n2"], True)
+                    idt = x if p["nd"] is None else self._nconv(x, p["nd"], False)
+                    x = self._nconv(y2, p["n3"], True, idt)
             else:
                 n, _, h, w = x.shape
                 x2d = self._rows(x)

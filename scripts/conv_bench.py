@@ -45,7 +45,7 @@ def main():
         n, hw = 32, {1: (100, 100), 2: (50, 50), 3: (25, 25)}
     n = a.n or n
     # (name, layer, cin, cout, k, stride, input hw layer)
-    shapes = [("l1.n1", 1, 256, 64, 1, 1, 1), ("l1.n2", 1, 64, 64, 3, 1, 1), ("l1.n3", 1, 64, 256, 1, 1, 1),
+    shapes = [("l1.nd", 1, 64, 256, 1, 1, 1), ("l1.n1", 1, 256, 64, 1, 1, 1), ("l1.n2", 1, 64, 64, 3, 1, 1), ("l1.n3", 1, 64, 256, 1, 1, 1),
               ("l2.n1", 2, 512, 128, 1, 1, 2), ("l2.n2", 2, 128, 128, 3, 1, 2), ("l2.n3", 2, 128, 512, 1, 1, 2),
               ("l3.n1", 3, 1024, 256, 1, 1, 3), ("l3.n2", 3, 256, 256, 3, 1, 3), ("l3.n3", 3, 256, 1024, 1, 1, 3),
               ("l3.nd", 3, 512, 1024, 1, 2, 2), ("l3.n2s", 3, 256, 256, 3, 2, 2)]
@@ -65,13 +65,21 @@ def main():
             res = torch.randn_like(y)
         run = lambda: C.conv2d_nhwc(x, w, b, res, y, s, k // 2, 1)   # noqa: E731
         if a.residual:
-            if res is None:
+            # every 1x1 stride-1 conv as the trunk runs it (n3 with its residual):
+            # the native kernel vs hipBLASLt with the same fused epilogue
+            # (csrc/gemm_lt.hip, candidates timed once) -- models/backbones.py
+            # 'auto' takes the faster per shape
+            if not (k == 1 and s == 1):
                 continue
             C.set_tuning("conv2d_variant", 0)
             t_a = timeit(run)
-            gb = (x.numel() + 2 * y.numel()) * 2 / 1e9
-            print(f"{name:8s}+res M={M} N={cout} K={K}: {t_a * 1e3:7.1f} us {fl / t_a / 1e9:5.0f} TF "
-                  f"{gb / t_a * 1e3:5.2f} TB/s", flush=True)
+            C.gemm_lt(x, w, b, res, y, 1, 1)
+            t_l = timeit(lambda: C.gemm_lt(x, w, b, res, y, 1, 0))
+            gb = (x.numel() + (2 if res is not None else 1) * y.numel()) * 2 / 1e9
+            tag = "+res" if res is not None else "    "
+            print(f"{name:8s}{tag} M={M} N={cout} K={K}: native {t_a * 1e3:7.1f} us {fl / t_a / 1e9:5.0f} TF "
+                  f"{gb / t_a * 1e3:5.2f} TB/s | hipBLASLt {t_l * 1e3:7.1f} us {fl / t_l / 1e9:5.0f} TF "
+                  f"{gb / t_l * 1e3:5.2f} TB/s | auto {min(t_a, t_l) * 1e3:7.1f} us", flush=True)
             continue
         C.set_tuning("conv2d_variant", 1)
         t_1 = timeit(run)
