@@ -292,6 +292,10 @@ def main(argv=None):
     ap.add_argument("--only-secondary", type=str, default="",
                     help="debug: skip the headline and print one secondary record "
                          "(nc_fp32 | nc_mixed | fe_finetune | train | train_ivd, at --image-size)")
+    ap.add_argument("--lr", type=float, default=5e-4,
+                    help="Adam learning rate (train.py's 5e-4).  Diagnostics only: the kernels' clocks depend on the "
+                         "data, which drifts with the weights, so same-box kernel A/Bs whose numerics differ in the "
+                         "last bits compare at --lr 0 (identical weights every step, the optimizer still runs)")
     ap.add_argument("--inloc", type=int, default=1,
                     help="1: after the timed training steps of a 1-GPU run, also time the InLoc inference configs "
                          "(BASELINE configs 3-5: 1600 px bf16, 3200 px bf16, 3200 px fp8) into config.secondary")
@@ -329,7 +333,7 @@ def main(argv=None):
     broadcast_module(model, ctx)
     # the reference baseline keeps the reference's optimizer (train.py:71:
     # torch.optim.Adam); the HIP path uses FlatAdam (engine/optim.py)
-    opt = make_adam(params, 5e-4) if args.impl == "hip" else torch.optim.Adam(params, lr=5e-4)
+    opt = make_adam(params, args.lr) if args.impl == "hip" else torch.optim.Adam(params, lr=args.lr)
 
     # a small pool of synthetic batches (random normalised images), generated on device
     gen = torch.Generator(device=dev).manual_seed(1234 + ctx.rank)   # (CPU: gloo smoke runs only)
@@ -456,7 +460,7 @@ def main(argv=None):
                        "comm": comm_info(ctx),
                        "launcher": ("self-launched torchrun" if os.environ.get("NCNET_BENCH_SELF_LAUNCHED")
                                     else "torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else "python"),
-                       "optimizer": type(opt).__name__,
+                       "optimizer": type(opt).__name__, "lr": args.lr,
                        "hbm_peak_gb": (round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
                                        if dev.type == "cuda" else None),
                        "runtime": _config.RUNTIME.as_dict(),

@@ -41,6 +41,7 @@ class RuntimeConfig:
     trunk_prefetch: bool = True      # NCNET_TRUNK_PREFETCH: next batch's frozen backbone on a side stream
     bwd_overlap: bool = True         # NCNET_BWD_OVERLAP: NC weight gradients on a side stream
     nc_fused: bool = True            # NCNET_NC_FUSED: fused (3,3)/(<=16,1) inference NeighConsensus kernel
+    cout1_taps: bool = True          # NCNET_COUT1_TAPS: tap-row Cout=1 forward (csrc/cout1.hip) at 25x25 planes, k 5
     nc_fp8: bool = False             # NCNET_NC_FP8: e4m3 NC in fp8 mode: the fused fp8 kernel for the
                                      #   (3,3)/(<=16,1) stack, the fp8 Conv4d kernels for other stacks
     stats2d: bool = True             # NCNET_STATS2D: one-pass row + column statistics (csrc/volume.hip)

@@ -29,6 +29,7 @@ int ncnet_stem_im2col_x3(const float*, void*, int, int, int, int, int, int, int,
 int ncnet_maxpool_x3(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_x3_to_f32(const void*, float*, long long, int, hipStream_t);
 int ncnet_conv2d_nhwc(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ncnet_cout1_taps_fwd(const void*, const void*, const float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ncnet_gemm_lt(const void*, const void*, const float*, const void*, void*, int, int, int, int, int, int, hipStream_t);
 int ncnet_l2norm_rows(const void*, int, void*, float*, int, int, float, void*, int, hipStream_t);
 int ncnet_l2norm_rows_bwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
@@ -269,6 +270,26 @@ void conv16_blk_fwd(Tensor X, Tensor Wp, c10::optional<Tensor> bias, Tensor Y, i
   ok(ncnet_conv16_blk_fwd(X.data_ptr(), Wp.data_ptr(), opt_ptr<float>(bias), Y.data_ptr<float>(), vs[0], vs[1], vs[2],
                           vs[3], vs[4], ks, (int)relu, 0, 0, cur_stream(X)),
      "conv16_blk_fwd");
+}
+
+// Cout = 1 layer with the in-plane taps as the MFMA rows (csrc/cout1.hip):
+// Wt [ks*ks, 64, 8] (ops/packing.py cout1_taps_weights).  Returns false for a
+// shape without an instantiation (nothing launched).
+bool cout1_taps_fwd(Tensor X, Tensor Wt, c10::optional<Tensor> bias, Tensor Y, int64_t ks, int64_t relu) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  check(X, "X", at::kBFloat16); check(Wt, "Wt", at::kBFloat16); check(Y, "Y", at::kFloat);
+  check_ks(ks);
+  TORCH_CHECK(X.dim() == 6 && X.size(-1) == 16, "X must be [V,I,J,K,L,16]");
+  std::vector<int64_t> vs(X.sizes().begin(), X.sizes().end() - 1);
+  check_shape(Y, "Y", vs);
+  check_shape(Wt, "Wt", {ks * ks, 64, 8});
+  if (bias.has_value()) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == 1, "bias must have 1 element"); }
+  TORCH_CHECK(vs[0] * vs[1] * vs[2] * vs[3] * vs[4] < (1LL << 40), "cout1_taps_fwd: volume too large");
+  const int rc = ncnet_cout1_taps_fwd(X.data_ptr(), Wt.data_ptr(), opt_ptr<float>(bias), Y.data_ptr<float>(), vs[0],
+                                      vs[1], vs[2], vs[3], vs[4], ks, (int)relu, cur_stream(X));
+  if (rc == -1) return false;
+  ok(rc, "cout1_taps_fwd");
+  return true;
 }
 
 // bf16x3 Cout = 1 layer in output-plane-block mode: X / Xl hi / lo input blocks,
@@ -1007,6 +1028,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("x3_to_f32", &x3_to_f32);
   m.def("wgrad1x16", &wgrad1x16);
   m.def("conv16_blk_fwd", &conv16_blk_fwd);
+  m.def("cout1_taps_fwd", &cout1_taps_fwd);
   m.def("conv16_fwd_x3", &conv16_fwd_x3);
   m.def("set_tuning", &set_tuning, py::arg("name"), py::arg("value") = py::none());
   m.def("conv16_blk_fwd_x3", &conv16_blk_fwd_x3);

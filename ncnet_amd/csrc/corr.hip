@@ -334,13 +334,14 @@ __device__ __forceinline__ void corr_v2_epilogue(const f32x4 (&acc)[TM][TN], con
         float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
         m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0xB1, 0xF, 0xF, false)));   // quad xor 1
         m = fmaxf(m, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m), 0x4E, 0xF, 0xF, false)));   // quad xor 2
-        int c = v[3] == m ? 0x50 : 0x00;   // no match (an all-NaN quad): offset 0, never an out-of-range code
+        int c = v[3] == m ? 0x50 : 0xFF;   // 0xFF: no element of this lane holds the quad max
         c = v[2] == m ? 0x40 : c;
         c = v[1] == m ? 0x10 : c;
         c = v[0] == m ? 0x00 : c;
         c |= lcode;
         c = min(c, __builtin_amdgcn_mov_dpp(c, 0xB1, 0xF, 0xF, false));
         c = min(c, __builtin_amdgcn_mov_dpp(c, 0x4E, 0xF, 0xF, false));
+        if (c == 0xFF) c = 0;                // an all-NaN quad: offset 0, never an out-of-range code
         if (bok && aok[i]) {
           const size_t o = aoff[i] + (size_t)(gn >> 2);
           if (NCNET_OK(o < (size_t)(b + 1) * vol)) {

@@ -325,6 +325,10 @@ def fold_frozen_bn(trunk: nn.Module) -> nn.Module:
 STEM_CHUNK = 32
 
 
+# process-wide native / hipBLASLt choice per 1x1 conv shape (FrozenResNetPlan._c1)
+_C1_CHOICE: dict = {}
+
+
 class FrozenResNetPlan(nn.Module):
     """Inference plan of a frozen (BN-folded) ResNet trunk in one compute dtype.
 
@@ -539,8 +543,11 @@ class FrozenResNetPlan(nn.Module):
         w, _, stride, pad = p
         if not (w.shape[-1] == 1 and w.shape[-2] == 1 and stride == 1 and pad == 0):
             return self._nconv(x, p, relu, res)
-        key = (tuple(x.shape), name)
-        choice = self._tuned.get(key)
+        # one choice per (input shape, conv shape, epilogue) for the whole process:
+        # every plan built in it (a fresh model, the volume-parallel slices) then
+        # runs the same kernels on the same shapes, bit for bit
+        key = (tuple(x.shape), x.dtype, tuple(w.shape), relu, res is not None)
+        choice = _C1_CHOICE.get(key)
         if choice is None:
             if torch.cuda.is_current_stream_capturing():
                 choice = "native"
@@ -558,7 +565,8 @@ class FrozenResNetPlan(nn.Module):
                 tn = t(lambda: self._nconv(x, p, relu, res))
                 tb = t(lambda: self._lt(x, p, relu, res))
                 choice = "blas" if tb < 0.97 * tn else "native"
-                self._tuned[key] = choice
+                _C1_CHOICE[key] = choice
+        self._tuned[(tuple(x.shape), name)] = choice
         return self._lt(x, p, relu, res) if choice == "blas" else self._nconv(x, p, relu, res)
 
     def tuned_choices(self) -> dict:

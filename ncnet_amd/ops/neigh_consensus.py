@@ -43,7 +43,7 @@ import torch.utils.weak as _weak
 from .. import config as _config
 from . import _ext
 from . import reference as ref
-from .packing import (_blk_packed, _w16_dgrad, _w1x_dgrad, blk_out_weights, gather_pack, ij_groups, ij_in_grad,
+from .packing import (_blk_packed, _cout1_packed, _w16_dgrad, _w1x_dgrad, blk_out_weights, gather_pack, ij_groups, ij_in_grad,
                       ij_in_weights, ij_out_grad, ij_out_weights, pack_w16, pack_w1x, pack_w16_planes, packed_weights,
                       plane_dgrad_weights, transpose_for_dgrad)
 
@@ -300,8 +300,14 @@ def _ij_out_planes(w_std: torch.Tensor, nbi: int) -> torch.Tensor:
     return torch.stack(per, 1).contiguous()
 
 
+def cout1_taps_ok(shp, ks: int) -> bool:
+    """Does the tap-row Cout=1 kernel (csrc/cout1.hip) cover this layer?
+    (k, l) planes of 25 x 25 (the 400 px training volume), kernel size 5."""
+    return _config.RUNTIME.cout1_taps and ks == 5 and tuple(shp[3:5]) == (25, 25)
+
+
 def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=None, relu: bool = True,
-               mask=None, f32: bool = False, xs=None, wp=None) -> torch.Tensor:
+               mask=None, f32: bool = False, xs=None, wp=None, wt=None) -> torch.Tensor:
     """One "same" Conv4d on the HIP kernels, any channel counts.
 
     h: the 1-channel input [V,I,J,K,L] (bf16/fp32) when cin == 1, else bf16
@@ -312,7 +318,8 @@ def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=N
     ``mask`` (bf16 blocks like the output, cout > 1, f32=False only) replaces
     bias/ReLU by the data-gradient epilogue y = acc * (mask > 0).  ``wp``: the
     layer's packed operand from ``packed_weights`` (single-block 16 -> 16 and
-    output-plane-block Cout=1 layers), else packed here."""
+    output-plane-block Cout=1 layers), else packed here; ``wt``: the tap-row
+    Cout=1 operand (cout1_taps_weights) where cout1_taps_ok."""
     C = _ext.ext()
     ks = w_std.shape[-1]
     shp = tuple(h.shape[:5]) if cin == 1 else tuple(h.shape[1:6])
@@ -334,6 +341,13 @@ def conv_layer(h: torch.Tensor, w_std: torch.Tensor, cin: int, cout: int, bias=N
             wb = _ij_in_planes(w_std[_blk(w_std, b, cout)])
             outs.append(_epilogue_call(C, xs, wb, bias, b, cout, relu, mask, f32, shp, ks))
         return _gather(outs, f32, cout)
+    if cout == 1 and nbi == 1 and cout1_taps_ok(shp, ks) and mask is None:
+        # tap rows: the 25 in-plane taps on the MFMA rows, 76 % useful work
+        # (csrc/cout1.hip), the in-plane shift applied once per output plane
+        y = torch.empty(shp, dtype=torch.float32, device=dev)
+        if C.cout1_taps_fwd(h[0], wt if wt is not None else gather_pack(_cout1_packed, w_std),
+                            None if bias is None else bias.float().reshape(1).contiguous(), y, ks, 1 if relu else 0):
+            return y
     if cout == 1 and nbi == 1 and BLK_1OUT:
         # output-plane blocks: the 16 MFMA rows are 4x4 output planes, no
         # combo-planar partials (2.5 GB at the training shape) and no ijsum
@@ -499,7 +513,7 @@ def _stack_fwd(x0: torch.Tensor, ws, bs, kinds, save: list, xp=None, shp=None, p
         else:
             save.append(h)
         y = conv_layer(h, w, cin, cout, bias=b, relu=True, f32=last and cout > 1, xs=xs,
-                       wp=packs.get(("f", li)) if packs else None)
+                       wp=packs.get(("f", li)) if packs else None, wt=packs.get(("t", li)) if packs else None)
         if cout == 1 and not last:
             y = y.to(torch.bfloat16)
         h = y
@@ -723,7 +737,8 @@ def _stack_packs(ws, kinds):
         if li == 0:
             specs.append((0, pack_w1x)); keys.append(("f", 0))
         elif li == nl - 1:
-            specs += [(li, _blk_packed), (li, _w1x_dgrad)]; keys += [("f", li), ("b", li)]
+            specs += [(li, _blk_packed), (li, _cout1_packed), (li, _w1x_dgrad)]
+            keys += [("f", li), ("t", li), ("b", li)]
         else:
             specs += [(li, pack_w16), (li, _w16_dgrad)]; keys += [("f", li), ("b", li)]
     return dict(zip(keys, packed_weights(list(ws), specs)))

@@ -121,6 +121,19 @@ def blk_out_weights(w_std: torch.Tensor) -> torch.Tensor:
     return planes[_blk_index(ks, str(w_std.device))].reshape(sp * sp, 16, 16, ks, ks)
 
 
+def cout1_taps_weights(w_std: torch.Tensor) -> torch.Tensor:
+    """[1, ci<=16, k^4] -> [k*k (di, dj), 64 lanes, 8]: the A fragments of the
+    tap-row Cout=1 kernel (csrc/cout1.hip, v_mfma_f32_32x32x16_bf16): lane
+    l = r + 32 h holds row r = the in-plane tap dk*k + dl (zero for r >= k*k),
+    input channels 8h .. 8h + 7."""
+    ci, ks = w_std.shape[1], w_std.shape[-1]
+    nt = ks * ks
+    w = w_std[0].reshape(ci, nt, nt).permute(1, 2, 0)                      # [pd, tap, ci]
+    out = w_std.new_zeros((nt, 32, 16))
+    out[:, :nt, :ci] = w
+    return out.reshape(nt, 32, 2, 8).permute(0, 2, 1, 3).reshape(nt, 64, 8).contiguous()
+
+
 @functools.lru_cache(maxsize=None)
 def _blk_index(ks: int, device: str) -> torch.Tensor:
     """[(ks+3)^2 * 16] plane index of blk_out_weights: (pi, qj, row 4a+b) ->
@@ -297,6 +310,10 @@ def _blk_packed(w, out_dtype=torch.bfloat16):
     return pack_w16_planes(blk_out_weights(w), out_dtype)
 
 
+def _cout1_packed(w, out_dtype=torch.bfloat16):
+    return cout1_taps_weights(w).to(out_dtype)
+
+
 def _w16_dgrad(w, out_dtype=torch.bfloat16):
     return pack_w16(transpose_for_dgrad(w), out_dtype)
 
@@ -307,5 +324,6 @@ def _w1x_dgrad(w, out_dtype=torch.bfloat16):
 
 # the index builders: the same packs with fp64 output (indices stay exact)
 _F64 = {pack_w16: lambda w: pack_w16(w, torch.float64), pack_w1x: lambda w: pack_w1x(w, torch.float64),
-        _blk_packed: lambda w: _blk_packed(w, torch.float64), _w16_dgrad: lambda w: _w16_dgrad(w, torch.float64),
+        _blk_packed: lambda w: _blk_packed(w, torch.float64), _cout1_packed: lambda w: _cout1_packed(w, torch.float64),
+        _w16_dgrad: lambda w: _w16_dgrad(w, torch.float64),
         _w1x_dgrad: lambda w: _w1x_dgrad(w, torch.float64)}

@@ -101,6 +101,8 @@ def main():
     wz = pack_w16_planes(ij_out_weights(torch.randn(1, 16, ks, ks, ks, ks, device=dev) * 0.05))
     from ncnet_amd.ops.packing import blk_out_weights
     wblk = pack_w16_planes(blk_out_weights(torch.randn(1, 16, ks, ks, ks, ks, device=dev) * 0.05))
+    from ncnet_amd.ops.packing import cout1_taps_weights
+    wct = cout1_taps_weights(torch.randn(1, 16, ks, ks, ks, ks, device=dev) * 0.05).to(torch.bfloat16)
     pq = torch.empty((1024, G, ks * ks, 16, 16), device=dev)
     pqb = torch.empty((1024, G, 16), device=dev)
     nq = ks * ks
@@ -159,6 +161,7 @@ def main():
         "ij_out_fwd_total": (ij_out_fwd, fl1),
         "ijsum": (lambda: C.ijsum(zq, b1, y1, ks, 1, 1), None),
         "blk_out_fwd": (lambda: C.conv16_blk_fwd(x16, wblk, b1, y1, ks, 1), fl1),
+        "cout1_taps_fwd": (lambda: C.cout1_taps_fwd(x16, wct, b1, y1, ks, 1), fl1),
         "wgrad16v2_plane": (lambda: C.wgrad16(xs[0], g16, pp, ppb, ks, 2, 2), fl1 / G),
         "wgrad16p_1out": (lambda: C.wgrad16p(x16.unsqueeze(0), xs, pq, pqb, ks), fl1),
         "wgrad16p_1in": (lambda: C.wgrad16p(xs, g16.unsqueeze(0), pq, pqb, ks), fl1),

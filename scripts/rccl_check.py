@@ -50,7 +50,9 @@ def main(argv=None):
     # at other shapes than the single-device forward it is compared with, so a
     # timing-dependent choice could differ between the two (bf16-level feature
     # differences, seen once as a 3e-3 mismatch)
-    os.environ["NCNET_TRUNK_CONV"] = "native"
+    import dataclasses
+    from ncnet_amd import config as _config
+    _config.set_runtime(dataclasses.replace(_config.RUNTIME, trunk_conv="native"))
     m = ImMatchNet(ncons_kernel_sizes=[3, 3], ncons_channels=[16, 1], feature_extraction_cnn="resnet101").to(dev)
     broadcast_module(m, ctx)
     torch.manual_seed(10)

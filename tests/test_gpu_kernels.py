@@ -171,6 +171,45 @@ def test_conv16_blk_fwd(ks, shape, cin, relu):
     assert relerr(y, yr) < 1e-4
 
 
+@pytest.mark.parametrize("shape,cin,relu", [((3, 25, 25, 25, 25), 16, 1), ((2, 25, 25, 25, 25), 16, 0),
+                                          ((1, 7, 10, 25, 25), 16, 1), ((1, 1, 1, 25, 25), 16, 0),
+                                          ((2, 4, 3, 25, 25), 10, 1)])
+def test_cout1_taps_fwd(shape, cin, relu):
+    """Cout=1 conv with the 25 in-plane taps on the MFMA rows (csrc/cout1.hip:
+    2 x 2 output-plane items, odd I / J edges, the in-plane shift-sum through
+    LDS) vs the fp64 Conv4d oracle on the same bf16 operands, and bit for bit
+    across two launches; a one-tap weight perturbation must be detected."""
+    from ncnet_amd.ops.packing import cout1_taps_weights
+    torch.manual_seed(3)
+    ks = 5
+    V, I, J, K, L = shape
+    x = torch.rand(V, cin, I, J, K, L, device=DEV)
+    w = torch.randn(1, cin, ks, ks, ks, ks, device=DEV) * 0.05
+    b = torch.randn(1, device=DEV) * 0.1 - (0.3 if relu else 0.0)
+    xcl = torch.zeros(V, I, J, K, L, 16, device=DEV, dtype=torch.bfloat16)
+    xcl[..., :cin] = x.permute(0, 2, 3, 4, 5, 1).to(torch.bfloat16)
+    wt = cout1_taps_weights(w).to(torch.bfloat16)
+    y = torch.full((V, I, J, K, L), float("nan"), device=DEV)
+    assert _ext.ext().cout1_taps_fwd(xcl, wt, b, y, ks, relu)
+    yr = ref.conv4d(bf(x), ref.conv4d_weight_from_std(bf(w)), b.double())[:, 0]
+    if relu:
+        yr = torch.relu(yr)
+    assert torch.isfinite(y).all()
+    assert relerr(y, yr) < 1e-4, relerr(y, yr)
+    y2 = torch.full_like(y, float("nan"))
+    _ext.ext().cout1_taps_fwd(xcl, wt, b, y2, ks, relu)
+    assert torch.equal(y, y2)
+    # mutation: one tap of the centre (di, dj) plane (used by every output) off by a visible amount
+    wm = w.clone()
+    wm[0, 3, 2, 2, 4, 0] += 0.5
+    ym = torch.empty_like(y)
+    _ext.ext().cout1_taps_fwd(xcl, cout1_taps_weights(wm).to(torch.bfloat16), b, ym, ks, relu)
+    assert relerr(ym, yr) > 1e-3
+    # other planes: the launcher declines (the caller keeps the block kernel)
+    xs = torch.zeros(1, 3, 3, 20, 20, 16, device=DEV, dtype=torch.bfloat16)
+    assert not _ext.ext().cout1_taps_fwd(xs, wt, b, torch.empty(1, 3, 3, 20, 20, device=DEV), ks, relu)
+
+
 @pytest.mark.parametrize("ks,shape,nx,ng", [(5, (2, 25, 25, 25, 25), 1, 2), (5, (2, 25, 25, 25, 25), 2, 1),
                                             (3, (2, 7, 9, 11, 13), 1, 1), (7, (1, 9, 8, 25, 25), 1, 2),
                                             (1, (2, 5, 6, 20, 25), 2, 1)])
