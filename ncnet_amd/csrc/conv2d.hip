@@ -245,13 +245,15 @@ __device__ __forceinline__ void c2_wait_barrier() {
 }
 
 // NW waves (4: 2x2 / 4x1 of 64x64 / 32x64; 8: 4x2 of 64x64 for the 256x128
-// tile, 85 FLOP per L2 byte instead of 64), NSTG ring stages.
+// tile, 85 FLOP per L2 byte instead of 64; 8: 4x2 of 64x128 for the 256x256
+// tile of the Cout = 256 layers, 128 FLOP per L2 byte: the im2col A rows are
+// read once per pixel tile instead of once per 128-channel half), NSTG ring stages.
 template <int BM, int BN, int NW, int NSTG, bool F16 = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void conv2d_nhwc_v2_kernel(Conv2dArgs p) {
   using namespace cv2;
   constexpr int NS = NSTG;
   constexpr int NT = NW * 64;
-  constexpr int WN = BN == 128 ? 2 : 1;
+  constexpr int WN = BN >= 128 ? 2 : 1;
   constexpr int WMW = NW / WN;
   constexpr int TM = BM / WMW / 16;
   constexpr int TN = BN / WN / 16;
@@ -712,6 +714,22 @@ extern "C" int ncnet_conv2d_nhwc(const void* X, const void* W, const float* bias
   // layer 3, 467 us v2 vs 707 us v3)
   const bool v3_auto = variant == 0 && tuning().conv2d_v3 && !big && Cout <= 256 && KH * KW * Cin >= 1024;
   if ((variant == 3 || v3_auto) && c3_run(p, f16 ? 1 : 0, stream)) return (int)hipGetLastError();
+  // 256 x 256 tiles for Cout % 256 == 0 with a deep K (the layer-3 3x3 convs,
+  // K = 2304: 447 -> 417 us, the stride-2 one 495 -> 447 us at the batch-256
+  // training trunk, profiles/r6/kernels/conv_bench_400_n512_256tile.txt); the
+  // short-K 1x1s (K <= 512) measured slower than the 256 x 128 tile.  Auto where
+  // the grid still gives >= 3 workgroups per CU; forced by variant 4.
+  const int t2562 = cdiv(p.M, 256) * (Cout / 256);
+  const bool big2 = Cout % 256 == 0 && !f16 &&
+                    ((variant == 0 && tuning().conv2d_256 && t2562 >= 768 && KH * KW * Cin >= 1024) || variant == 4);
+  if (big2) {
+    p.tiles_n = Cout / 256;
+    p.tiles_m = cdiv(p.M, 256);
+    dim3 g2((unsigned)(p.tiles_m * p.tiles_n)), b2(512);
+    const size_t lds = (size_t)4 * (256 + 256) * 64;   // = the 256 x 256 16-bit epilogue tile
+    hipLaunchKernelGGL((conv2d_nhwc_v2_kernel<256, 256, 8, 4>), g2, b2, lds, stream, p);
+    return (int)hipGetLastError();
+  }
   if (big && variant != 1) {
     p.tiles_m = cdiv(p.M, 256);
     dim3 g2((unsigned)(p.tiles_m * p.tiles_n)), b2(512);

@@ -756,6 +756,34 @@ def test_conv2d_nhwc_kernel(cin, cout, k, stride, pad, res, relu, shape):
     assert relerr(y, yr) < 1e-2
 
 
+@pytest.mark.parametrize("cin,cout,k,stride,pad,res,relu,shape", [
+    (256, 256, 3, 1, 1, False, True, (5, 25, 25)),     # layer-3 3x3 (M = 3125: a partial last 256-row tile)
+    (1024, 256, 1, 1, 0, True, True, (3, 25, 25)),     # 1x1 with a residual
+    (256, 512, 3, 2, 1, False, False, (2, 30, 31)),    # two 256-column tiles, stride 2, no ReLU
+    (64, 256, 1, 1, 0, False, True, (2, 20, 20))])     # Cin 64: two k-steps per tap
+def test_conv2d_nhwc_256x256_tile(cin, cout, k, stride, pad, res, relu, shape, tune):
+    """The 256 x 256 DMA-ring tile of the Cout = 256 trunk convs (conv2d_nhwc_v2
+    <256, 256>, forced by conv2d_variant 4) vs F.conv2d in fp64 on bf16 inputs."""
+    tune("conv2d_variant", 4)
+    C = _ext.ext()
+    torch.manual_seed(23)
+    cl = torch.channels_last
+    x = torch.randn(shape[0], cin, shape[1], shape[2], device=DEV).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(cout, cin, k, k, device=DEV) * 0.05).to(torch.bfloat16).contiguous(memory_format=cl)
+    b = torch.randn(cout, device=DEV)
+    yr = torch.nn.functional.conv2d(x.double(), w.double(), b.double(), stride, pad)
+    r = None
+    if res:
+        r = torch.randn(yr.shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=cl)
+        yr = yr + r.double()
+    if relu:
+        yr = torch.relu(yr)
+    y = torch.full(yr.shape, float("nan"), dtype=torch.bfloat16, device=DEV).contiguous(memory_format=cl)
+    C.conv2d_nhwc(x, w, b, r, y, stride, pad, 1 if relu else 0)
+    assert torch.isfinite(y).all()
+    assert relerr(y, yr) < 1e-2
+
+
 @pytest.mark.parametrize("cin,cout,k,stride,pad,res,relu,shape,dt", [
     (256, 256, 3, 1, 1, False, True, (4, 25, 25), torch.bfloat16),     # layer-3 3x3 at the training size
     (1024, 256, 1, 1, 0, False, True, (3, 25, 25), torch.bfloat16),    # layer-3 reduce 1x1
