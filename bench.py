@@ -50,14 +50,22 @@ SECONDARY_BATCH = 16
 _BASELINE_FILE = os.path.join(ROOT, "profiles", "baseline_reference.json")
 
 
-def _baseline():
+def _baseline(batch: int = SECONDARY_BATCH):
+    """(reference-algorithm pairs/s per GPU, the per-GPU batch it was measured
+    at): the same-batch number when profiles/baseline_reference.json holds one
+    ("bf16_pairs_per_s_b<batch>"), else the batch-16 one -- recorded next to
+    vs_baseline as baseline_batch, so a cross-batch ratio is never unlabelled."""
     if BASELINE_PAIRS_PER_S is not None:
-        return BASELINE_PAIRS_PER_S
+        return BASELINE_PAIRS_PER_S, SECONDARY_BATCH
     try:
         with open(_BASELINE_FILE) as f:
-            return float(json.load(f)["pairs_per_s_per_gpu"])
+            rec = json.load(f)
     except Exception:
-        return None
+        return None, None
+    key = f"bf16_pairs_per_s_b{batch}"
+    if key in rec:
+        return float(rec[key]), batch
+    return float(rec["pairs_per_s_per_gpu"]), int(rec.get("batch", SECONDARY_BATCH))
 
 
 def _inloc_secondary():
@@ -399,9 +407,10 @@ def main(argv=None):
 
     ms_per_step = 1000.0 * elapsed / args.steps
     pairs_per_s = args.batch * ctx.world_size * args.steps / elapsed
-    base = _baseline()
+    base, base_batch = _baseline(args.batch)
     # vs_baseline = value / the BASELINE.md number (the reference algorithm
-    # measured on ONE MI355X); per-GPU ratio = vs_baseline / n_gpus.
+    # measured on ONE MI355X, at this per-GPU batch when measured there, else
+    # at batch 16: see baseline_batch); per-GPU ratio = vs_baseline / n_gpus.
     vs = None
     if base:
         vs = pairs_per_s / base
@@ -456,7 +465,8 @@ def main(argv=None):
             "config": {"model": "ResNet-101(layer3)+NC-Net ncons 5,5,5/16,16,1", "global_batch": args.batch * ctx.world_size,
                        "per_gpu_batch": args.batch, "seq_len": None, "image_size": s,
                        "parallelism": f"dp{ctx.world_size}", "impl": args.impl,
-                       "baseline_pairs_per_s_1gpu": base, "final_loss": float(loss.detach()),
+                       "baseline_pairs_per_s_1gpu": base, "baseline_batch": base_batch,
+                       "final_loss": float(loss.detach()),
                        "comm": comm_info(ctx),
                        "launcher": ("self-launched torchrun" if os.environ.get("NCNET_BENCH_SELF_LAUNCHED")
                                     else "torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else "python"),
