@@ -289,50 +289,36 @@ __global__ __launch_bounds__(512, 1) void conv1x16_kernel(const bf16* __restrict
 #pragma unroll
       for (int dj = 0; dj < KS; ++dj) A[dj] = lds_read16(smem, C::WOFF + (wset + di * KS + dj) * 1024 + lane * 16);
       const uint32_t sb = (uint32_t)((n & 1) * S * C::SLOTB);
-      // B fragments of the step's S planes x MAXT tiles as ONE sequence g =
-      // s MAXT + tt, read PD fragments ahead ACROSS plane boundaries (per plane
-      // the first PD reads used to wait in front of its MFMAs: with 1-5 MFMAs per
-      // fragment, that latency was a third of the step).  Reads are
-      // unconditional (a plane outside the volume is a zero slot); the MFMAs of
-      // such a plane are skipped.
-      constexpr int NG = S * MAXT;
-      constexpr int PDG = PD < NG ? PD : NG;
-      u32x4 B[PD + 1];
-      auto load_b = [&](auto gc) {
-        constexpr int g = decltype(gc)::value;
-        constexpr int s = g / MAXT, tt = g % MAXT;
-        const uint32_t a0 = rowoff[0] + sb + s * C::SLOTB, a1 = rowoff[1] + sb + s * C::SLOTB;
-        B[g % (PD + 1)] = cat4u(lds_read_tr16u(smem, a0 + tt * NW * 32), lds_read_tr16u(smem, a1 + tt * NW * 32));
-      };
-      xstatic_for<0, PDG>([&](auto gc) { load_b(gc); });
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 * PDG, 0);
       xstatic_for<0, S>([&](auto sc) {
         constexpr int s = decltype(sc)::value;   // plane j' = j0 - P + s
         const int jp = j0 - P + s;
-        constexpr int dlo = (s - R + 1) > 0 ? (s - R + 1) : 0;
-        constexpr int dhi = s < KS - 1 ? s : KS - 1;   // inclusive
-        constexpr int NDJ = dhi - dlo + 1;
-        // one branch per plane (a plane outside the volume only issues its
-        // reads); per-tile branches split every read from its MFMAs
-        auto plane = [&](auto livec) {
-          constexpr bool LIVE = decltype(livec)::value;
+        if (jp >= 0 && jp < J) {
+          constexpr int dlo = (s - R + 1) > 0 ? (s - R + 1) : 0;
+          constexpr int dhi = s < KS - 1 ? s : KS - 1;   // inclusive
+          constexpr int NDJ = dhi - dlo + 1;
+          const uint32_t a0 = rowoff[0] + sb + s * C::SLOTB, a1 = rowoff[1] + sb + s * C::SLOTB;
+          // B fragments read PD tiles ahead of their MFMAs (PD = 1: the round-4
+          // schedule; 2: a deeper lookahead for the planes that feed only one or
+          // two output planes, A/B via the c1x_pd tuning switch)
+          u32x4 B[PD + 1];
+          auto load_b = [&](auto tc) {
+            constexpr int tt = decltype(tc)::value;
+            B[tt % (PD + 1)] = cat4u(lds_read_tr16u(smem, a0 + tt * NW * 32), lds_read_tr16u(smem, a1 + tt * NW * 32));
+          };
+          xstatic_for<0, (PD < MAXT ? PD : MAXT)>([&](auto tc) { load_b(tc); });
+          __builtin_amdgcn_sched_group_barrier(0x100, 2 * (PD < MAXT ? PD : MAXT), 0);
           xstatic_for<0, MAXT>([&](auto tc) {
             constexpr int tt = decltype(tc)::value;
-            constexpr int g = s * MAXT + tt;
-            if constexpr (g + PD < NG) load_b(std::integral_constant<int, g + PD>{});
-            if constexpr (LIVE) {
-              xstatic_for<dlo, dhi + 1>([&](auto dc) {
-                constexpr int dj = decltype(dc)::value;
-                acc[s - dj][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                    A[dj], __builtin_bit_cast(bf16x8, B[g % (PD + 1)]), acc[s - dj][tt], 0, 0, 0);
-              });
-              if constexpr (g + PD < NG) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-              __builtin_amdgcn_sched_group_barrier(0x008, NDJ, 0);
-            }
+            if constexpr (tt + PD < MAXT) load_b(std::integral_constant<int, tt + PD>{});
+            xstatic_for<dlo, dhi + 1>([&](auto dc) {
+              constexpr int dj = decltype(dc)::value;
+              acc[s - dj][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  A[dj], __builtin_bit_cast(bf16x8, B[tt % (PD + 1)]), acc[s - dj][tt], 0, 0, 0);
+            });
+            if constexpr (tt + PD < MAXT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, NDJ, 0);
           });
-        };
-        if (jp >= 0 && jp < J) plane(std::true_type{});
-        else plane(std::false_type{});
+        }
       });
     }
     if (last) {

@@ -64,7 +64,8 @@ struct CT1 {
   static constexpr int ZCOLS = NW * WV;                  // staging row length (>= NV)
   static constexpr int ZPAD = 64;                        // floats before the staging rows (>= P K + P)
   static constexpr int LDS_RING = NW * NSLOT * SLOT;
-  static constexpr int ZBYTES = (ZPAD + NT * ZCOLS) * 4;
+  static constexpr int ZBUF = ZPAD + NT * ZCOLS;          // floats of one staging buffer (two)
+  static constexpr int ZBYTES = 2 * ZBUF * 4;
   static constexpr int LDS = ROFF + (LDS_RING > ZBYTES ? LDS_RING : ZBYTES);
   static constexpr int WI = RI + KS - 1, WJ = RJ + KS - 1;   // input window (planes along i, j)
   static constexpr int NO = RI * RJ;                     // output planes per item
@@ -219,47 +220,60 @@ __global__ __launch_bounds__(256, 1) void cout1_taps_fwd_kernel(const bf16* __re
       }
       zb[m] = (uint32_t)(C::ROFF + (C::ZPAD + oc - (P * L + P)) * 4);
     }
+    // two staging buffers: output plane o + 1 is written while o is gathered
+    // (one barrier per plane instead of two, the writes beside the reads)
+    auto write_z = [&](auto oc) {
+      constexpr int o = decltype(oc)::value, a = o / RJ, b = o % RJ;
+      float* z = zs + (o & 1) * C::ZBUF;
+      // D row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5), col = lane & 31
 #pragma unroll
-    for (int a = 0; a < RI; ++a) {
+      for (int t = 0; t < MT; ++t) {
+        const int col = wave * C::WV + t * 32 + (lane & 31);
 #pragma unroll
-      for (int b = 0; b < RJ; ++b) {
-        if (a < na && b < nb && !(DBG & 1)) {
-          // D row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5), col = lane & 31
-#pragma unroll
-          for (int t = 0; t < MT; ++t) {
-            const int col = wave * C::WV + t * 32 + (lane & 31);
-#pragma unroll
-            for (int r = 0; r < 13; ++r) {
-              const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-              if (row < C::NT) zs[row * C::ZCOLS + col] = acc[a][b][t][r];
-            }
-          }
-          __syncthreads();
-          float* yo = Y + (((size_t)v * I + i0 + a) * J + j0 + b) * NV;
-#pragma unroll
-          for (int m = 0; m < NPT; ++m) {
-            const int o = threadIdx.x + NW * 64 * m;
-            float z[KS][KS];
-            // all 25 reads first (immediate offsets on one base), then the sums
-#pragma unroll
-            for (int dk = 0; dk < KS; ++dk)
-#pragma unroll
-              for (int dl = 0; dl < KS; ++dl)
-                z[dk][dl] = *(const float*)(smem + zb[m] + (uint32_t)(((dk * KS + dl) * C::ZCOLS + dk * L + dl) * 4));
-            float s = b0;
-#pragma unroll
-            for (int dk = 0; dk < KS; ++dk) {
-              float r = 0.f;
-#pragma unroll
-              for (int dl = 0; dl < KS; ++dl) r = fmaf(z[dk][dl], ml[m][dl], r);
-              s = fmaf(r, mk[m][dk], s);
-            }
-            if (relu) s = fmaxf(s, 0.f);
-            if (o < NV) __builtin_nontemporal_store(s, yo + o);
-          }
-          __syncthreads();
+        for (int r = 0; r < 13; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < C::NT) z[row * C::ZCOLS + col] = acc[a][b][t][r];
         }
       }
+    };
+    auto gather = [&](auto oc) {
+      constexpr int o = decltype(oc)::value, a = o / RJ, b = o % RJ;
+      float* yo = Y + (((size_t)v * I + i0 + a) * J + j0 + b) * NV;
+      const uint32_t zo = (uint32_t)((o & 1) * C::ZBUF * 4);
+#pragma unroll
+      for (int m = 0; m < NPT; ++m) {
+        const int oo = threadIdx.x + NW * 64 * m;
+        float z[KS][KS];
+        // all 25 reads first (immediate offsets on one base), then the sums
+#pragma unroll
+        for (int dk = 0; dk < KS; ++dk)
+#pragma unroll
+          for (int dl = 0; dl < KS; ++dl)
+            z[dk][dl] = *(const float*)(smem + zb[m] + zo + (uint32_t)(((dk * KS + dl) * C::ZCOLS + dk * L + dl) * 4));
+        float sum = b0;
+#pragma unroll
+        for (int dk = 0; dk < KS; ++dk) {
+          float r = 0.f;
+#pragma unroll
+          for (int dl = 0; dl < KS; ++dl) r = fmaf(z[dk][dl], ml[m][dl], r);
+          sum = fmaf(r, mk[m][dk], sum);
+        }
+        if (relu) sum = fmaxf(sum, 0.f);
+        if (oo < NV) __builtin_nontemporal_store(sum, yo + oo);
+      }
+    };
+    if constexpr (!(DBG & 1)) {
+      write_z(std::integral_constant<int, 0>{});
+      __syncthreads();
+      c1_static_for<0, NO>([&](auto oc) {
+        constexpr int o = decltype(oc)::value;
+        const bool ok = o / RJ < na && o % RJ < nb;
+        if constexpr (o + 1 < NO) {
+          if ((o + 1) / RJ < na && (o + 1) % RJ < nb) write_z(std::integral_constant<int, o + 1>{});
+        }
+        if (ok) gather(oc);
+        __syncthreads();
+      });
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends

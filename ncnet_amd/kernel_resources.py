@@ -75,8 +75,11 @@ def analyse(src: Path, extra_flags=()) -> list[dict]:
 
 def analyse_all(srcs=None, jobs: int = 4) -> list[dict]:
     srcs = [Path(s) for s in srcs] if srcs else sorted(CSRC.glob("*.hip"))
+    # largest (slowest) sources first so the long compiles overlap the short ones
+    order = sorted(range(len(srcs)), key=lambda i: -srcs[i].stat().st_size)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        return [rec for recs in ex.map(analyse, srcs) for rec in recs]
+        futs = {i: ex.submit(analyse, srcs[i]) for i in order}
+        return [rec for i in range(len(srcs)) for rec in futs[i].result()]
 
 
 def short(name: str) -> str:

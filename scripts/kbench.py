@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--size", type=int, default=25)
     ap.add_argument("--ks", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=1, help="repeat the selected cases (interleaved A/B)")
     ap.add_argument("--only", type=str, default="")
     ap.add_argument("--json", type=str, default="")
     a = ap.parse_args()
@@ -168,7 +169,7 @@ def main():
     }
     only = set(a.only.split(",")) if a.only else None
     res = {}
-    for name, (fn, fl) in cases.items():
+    for name, (fn, fl) in [kv for _ in range(a.rounds) for kv in cases.items()]:
         if only and name not in only:
             continue
         ms = timeit(fn, a.reps)

@@ -36,8 +36,13 @@ HOT = [
     ("stats_cols_kernel", None),
 ]
 
-pytestmark = pytest.mark.skipif(shutil.which(kr.HIPCC) is None and not __import__("os").path.exists(kr.HIPCC),
-                                reason="hipcc not available")
+pytestmark = [
+    pytest.mark.skipif(shutil.which(kr.HIPCC) is None and not __import__("os").path.exists(kr.HIPCC),
+                       reason="hipcc not available"),
+    # device-only compiles of every source; conv4d_fwd.hip alone takes ~11 min on
+    # this 8-CPU container (dozens of fully unrolled instantiations)
+    pytest.mark.timeout(2400),
+]
 
 
 @pytest.fixture(scope="module")
