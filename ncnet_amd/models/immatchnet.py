@@ -340,10 +340,11 @@ class ImMatchNet(nn.Module):
         nc = self.NeighConsensus
         square = tuple(corr4d.shape[2:4]) == tuple(corr4d.shape[4:6])
         wrefs = [m.weight_ref() for m in nc.conv_layers()] if corr4d.is_cuda else []
-        f8 = (not torch.is_grad_enabled() and nc.symmetric_mode and corr4d.is_cuda and square
-              and _nc_ops.fused_f8_applies(corr4d, wrefs, nc.channels, nc.fp8))
-        if f8 or (not torch.is_grad_enabled() and nc.symmetric_mode and corr4d.is_cuda and square
-                  and _nc_ops.fused_applies(corr4d, wrefs, nc.channels, nc.fp8, nc.precision)):
+        # the NC op's own path choice (ops/neigh_consensus.py select_path)
+        path = (_nc_ops.select_path(corr4d, wrefs, nc.channels, nc.symmetric_mode, nc.fp8, nc.precision)
+                if corr4d.is_cuda else "reference")
+        f8 = path == "fused_fp8"
+        if path in ("fused", "fused_fp8") and nc.symmetric_mode and square:
             # inference on the fused NC stack (bf16 / half, or e4m3 with
             # NCNET_NC_FP8 in fp8 mode): MutualMatching writes the 16-bit input
             # of both symmetric branches directly

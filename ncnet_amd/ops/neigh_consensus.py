@@ -30,6 +30,22 @@ MI355X design:
 There is no silent PyTorch fallback on the GPU: a configuration without HIP
 kernels (even kernel sizes) raises unless config.RUNTIME.allow_torch_fallback
 (NCNET_ALLOW_TORCH_FALLBACK=1).
+
+Execution paths: ``select_path`` is the ONE place that picks them (the model's
+``process_correlation`` asks it too); ``neigh_consensus`` dispatches on its
+answer and ``_ext.DISPATCH`` counts what ran.
+
+| path | when | implementation | tests |
+|---|---|---|---|
+| ``reference`` | CPU tensors | ``ops/reference.py`` (fp32 oracle) | ``test_nc_general_cpu.py`` |
+| ``torch_fallback`` | GPU, no HIP kernels (even kernel size) | the oracle, only with allow_torch_fallback | ``test_gpu_kernels.py`` |
+| ``x3_inference`` | precision fp32 / mixed, no autograd | ``neigh_consensus_x3`` (bf16x3 splits) | ``test_gpu_x3.py`` |
+| ``mixed`` | precision mixed, autograd, fast-path shapes | ``NeighConsensusMixedFn`` (x3 forward, bf16 backward) | ``test_gpu_x3.py`` |
+| ``x3_fused`` / ``x3`` | precision fp32 (or mixed off the fast shapes), autograd | ``NeighConsensusX3FusedFn`` / ``NeighConsensusX3Fn`` | ``test_gpu_x3.py`` |
+| ``fused_fp8`` | inference, fp8 mode with nc_fp8, symmetric square (3,3)/(<=16,1) | ``nc_fused_k3_f8`` (csrc/nc_fused.hip) | ``test_gpu_kernels.py`` |
+| ``fused`` | inference, (3,3)/(<=16,1), not all-fp8 | ``nc_fused_k3`` (hidden layer in LDS) | ``test_gpu_kernels.py``, ``test_gpu_fusion.py`` |
+| ``fp8`` | inference, fp8 mode, other 1 -> 16 -> 1 stacks | ``neigh_consensus_fp8`` (e4m3 Conv4d) | ``test_gpu_kernels.py`` |
+| ``bf16_padded`` / ``bf16`` | everything else (training) | ``NeighConsensusPaddedFn`` / ``NeighConsensusFn`` | ``test_gpu_kernels.py``, ``test_gpu_nc_stages.py`` |
 """
 from __future__ import annotations
 
@@ -1686,18 +1702,12 @@ def neigh_consensus_fused_x2_fp8(x2: torch.Tensor, weights, biases) -> torch.Ten
 
 def fused_f8_applies(x: torch.Tensor, weights, channels, fp8: bool) -> bool:
     """Would the fp8 fused kernel run this (symmetric, square) input?"""
-    kernel_sizes = [w.shape[0] for w in weights]
-    kinds = layer_kinds(channels, kernel_sizes)
-    return (fp8 and _config.RUNTIME.nc_fp8 and x.is_cuda and _ext.use_hip(x) and kinds is not None
-            and _fused_ok(kinds, kernel_sizes, channels, x))
+    return x.is_cuda and select_path(x, weights, channels, True, fp8) == "fused_fp8"
 
 
 def fused_applies(x: torch.Tensor, weights, channels, fp8: bool = False, precision: str = "bf16") -> bool:
-    """Would ``neigh_consensus`` run this input on the fused kernel?"""
-    kernel_sizes = [w.shape[0] for w in weights]
-    kinds = layer_kinds(channels, kernel_sizes)
-    return (x.is_cuda and _ext.use_hip(x) and kinds is not None and precision not in ("fp32", "mixed")
-            and _fused_ok(kinds, kernel_sizes, channels, x) and not (fp8 and _config.RUNTIME.nc_fp8))
+    """Would ``neigh_consensus`` run this input on the fused (bf16 / half) kernel?"""
+    return x.is_cuda and select_path(x, weights, channels, True, fp8, precision) == "fused"
 
 
 def neigh_consensus_fused(x: torch.Tensor, weights, biases, symmetric: bool = True) -> torch.Tensor:
@@ -1736,66 +1746,88 @@ def fp8_ok(kinds, channels) -> bool:
             and max(channels) <= 16)
 
 
+def select_path(x: torch.Tensor, weights, channels, symmetric: bool = True, fp8: bool = False,
+                precision: str = "bf16", padded: torch.Tensor | None = None) -> str:
+    """The execution path ``neigh_consensus`` takes for these arguments (the
+    table in the module docstring).  Raises like the ops do on a GPU machine
+    without the extension."""
+    kernel_sizes = [w.shape[0] for w in weights]
+    kinds = layer_kinds(channels, kernel_sizes)
+    if not _ext.use_hip(x):
+        return "reference"
+    if kinds is None:
+        return "torch_fallback"
+    if precision in ("fp32", "mixed"):
+        if not (torch.is_grad_enabled() and (x.requires_grad or any(w.requires_grad for w in weights))):
+            return "x3_inference"
+        fused = x3_fused_ok(kinds, channels, kernel_sizes, x, symmetric)
+        if precision == "mixed" and fused:
+            return "mixed"
+        return "x3_fused" if fused else "x3"
+    # fp8 mode: the fused bf16 stack where it applies (it never writes the
+    # hidden volume), unless NCNET_NC_FP8=1 asks for the all-fp8 pipeline: then
+    # the fused e4m3 kernel for the symmetric (3,3)/(<=16,1) stack and the fp8
+    # Conv4d kernels for the others
+    all_fp8 = fp8 and _config.RUNTIME.nc_fp8
+    fused = _fused_ok(kinds, kernel_sizes, channels, x)
+    if all_fp8 and fused and symmetric and tuple(x.shape[2:4]) == tuple(x.shape[4:6]):
+        return "fused_fp8"
+    if fused and not all_fp8:
+        return "fused"
+    if fp8 and not torch.is_grad_enabled() and fp8_ok(kinds, channels):
+        return "fp8"
+    return "bf16_padded" if padded is not None else "bf16"
+
+
 def neigh_consensus(x: torch.Tensor, weights, biases, channels, symmetric: bool = True, fp8: bool = False,
                     precision: str = "bf16", padded: torch.Tensor | None = None) -> torch.Tensor:
     """x: [V,1,I,J,K,L] fp32; weights in checkpoint layout [k, out, in, k, k, k].
     Returns [V, C_last, I, J, K, L] fp32.
 
-    On the GPU: the (3,3)/(<=16,1) inference stack runs on the fused kernel
-    (hidden layer in LDS; also in fp8 mode unless config.RUNTIME.nc_fp8); ``fp8``
-    (inference, other ``fp8_ok`` stacks) on the fp8 MFMA Conv4d kernels; ``precision='fp32'`` (inference) on the bf16x3
-    kernels (fp32-accurate); everything else with odd kernel sizes <= 7 and
-    any channel counts on the bf16 autograd stack.  ``_ext.DISPATCH`` records
-    which path ran.  ``padded``: x's padded bf16 planes for both symmetric
-    branches from ``mutual.mutual_matching_padded`` (the bf16 training stack
-    uses them instead of padding x itself)."""
+    Dispatches on ``select_path`` (module docstring table): the (3,3)/(<=16,1)
+    inference stack on the fused kernel, ``fp8`` inference on the e4m3 kernels,
+    ``precision='fp32'`` / ``'mixed'`` on the bf16x3 kernels, everything else
+    with odd kernel sizes <= 7 and any channel counts on the bf16 autograd
+    stack.  ``padded``: x's padded bf16 planes for both symmetric branches from
+    ``mutual.mutual_matching_padded`` (the bf16 training stack uses them
+    instead of padding x itself)."""
+    path = select_path(x, weights, channels, symmetric, fp8, precision, padded)
     kernel_sizes = [w.shape[0] for w in weights]
     kinds = layer_kinds(channels, kernel_sizes)
-    if _ext.use_hip(x):
-        if kinds is None:
-            _ext.torch_fallback(f"NeighConsensus kernel sizes {kernel_sizes}")
-        else:
-            if precision in ("fp32", "mixed"):
-                _ext.count("nc_x3")
-                if torch.is_grad_enabled() and (x.requires_grad or any(w.requires_grad for w in weights)):
-                    params = []
-                    for w, b in zip(weights, biases):
-                        params += [w, b]
-                    if precision == "mixed" and x3_fused_ok(kinds, channels, kernel_sizes, x, symmetric):
-                        _ext.count("nc_mixed")
-                        return NeighConsensusMixedFn.apply(x.float().contiguous(), tuple(kinds), tuple(channels),
-                                                           *params)
-                    if x3_fused_ok(kinds, channels, kernel_sizes, x, symmetric):
-                        _ext.count("nc_x3_fused")
-                        return NeighConsensusX3FusedFn.apply(x.float().contiguous(), tuple(kinds), tuple(channels),
-                                                             *params)
-                    return NeighConsensusX3Fn.apply(x.float().contiguous(), symmetric, tuple(kinds),
-                                                    tuple(channels), *params)
-                return neigh_consensus_x3(x, weights, biases, channels, symmetric)
-            # fp8 mode: the fused bf16 stack where it applies (it never writes the
-            # hidden volume), unless NCNET_NC_FP8=1 asks for the all-fp8
-            # pipeline: then the fused e4m3 kernel for the symmetric (3,3)/(<=16,1)
-            # stack and the fp8 Conv4d kernels for the others
-            V, _, I, J, K, L = x.shape
-            if (fp8 and _config.RUNTIME.nc_fp8 and symmetric and (I, J) == (K, L)
-                    and _fused_ok(kinds, kernel_sizes, channels, x)):
-                _ext.count("nc_fused_k3_f8")
-                x2 = torch.empty((2 * V, I, J, K, L), dtype=torch.bfloat16, device=x.device)
-                x2[:V].copy_(x.reshape(V, I, J, K, L))
-                _ext.ext().transpose(x2[:V].reshape(V, I * J, K * L), x2[V:].reshape(V, K * L, I * J))
-                return neigh_consensus_fused_x2_fp8(x2, weights, biases)
-            if _fused_ok(kinds, kernel_sizes, channels, x) and not (fp8 and _config.RUNTIME.nc_fp8):
-                _ext.count("nc_fused_k3")
-                return neigh_consensus_fused(x.float().contiguous(), weights, biases, symmetric)
-            if fp8 and not torch.is_grad_enabled() and fp8_ok(kinds, channels):
-                _ext.count("nc_fp8")
-                return neigh_consensus_fp8(x.float().contiguous(), weights, biases, kinds, symmetric)
-            _ext.count("nc_bf16")
-            params = []
-            for w, b in zip(weights, biases):
-                params += [w, b]
-            if padded is not None:
-                return NeighConsensusPaddedFn.apply(x.float().contiguous(), padded, symmetric, tuple(kinds),
-                                                    tuple(channels), *params)
-            return NeighConsensusFn.apply(x.float().contiguous(), symmetric, tuple(kinds), tuple(channels), *params)
+    params = []
+    for w, b in zip(weights, biases):
+        params += [w, b]
+    xf = x.float().contiguous()
+    if path in ("x3_inference", "mixed", "x3_fused", "x3"):
+        _ext.count("nc_x3")
+    if path == "x3_inference":
+        return neigh_consensus_x3(x, weights, biases, channels, symmetric)
+    if path == "mixed":
+        _ext.count("nc_mixed")
+        return NeighConsensusMixedFn.apply(xf, tuple(kinds), tuple(channels), *params)
+    if path == "x3_fused":
+        _ext.count("nc_x3_fused")
+        return NeighConsensusX3FusedFn.apply(xf, tuple(kinds), tuple(channels), *params)
+    if path == "x3":
+        return NeighConsensusX3Fn.apply(xf, symmetric, tuple(kinds), tuple(channels), *params)
+    if path == "fused_fp8":
+        _ext.count("nc_fused_k3_f8")
+        V, _, I, J, K, L = x.shape
+        x2 = torch.empty((2 * V, I, J, K, L), dtype=torch.bfloat16, device=x.device)
+        x2[:V].copy_(x.reshape(V, I, J, K, L))
+        _ext.ext().transpose(x2[:V].reshape(V, I * J, K * L), x2[V:].reshape(V, K * L, I * J))
+        return neigh_consensus_fused_x2_fp8(x2, weights, biases)
+    if path == "fused":
+        _ext.count("nc_fused_k3")
+        return neigh_consensus_fused(xf, weights, biases, symmetric)
+    if path == "fp8":
+        _ext.count("nc_fp8")
+        return neigh_consensus_fp8(xf, weights, biases, kinds, symmetric)
+    if path in ("bf16", "bf16_padded"):
+        _ext.count("nc_bf16")
+        if path == "bf16_padded":
+            return NeighConsensusPaddedFn.apply(xf, padded, symmetric, tuple(kinds), tuple(channels), *params)
+        return NeighConsensusFn.apply(xf, symmetric, tuple(kinds), tuple(channels), *params)
+    if path == "torch_fallback":
+        _ext.torch_fallback(f"NeighConsensus kernel sizes {kernel_sizes}")
     return ref.neigh_consensus(x.float(), [w.float() for w in weights], [b.float() for b in biases], symmetric)
