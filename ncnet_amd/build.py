@@ -42,6 +42,26 @@ HIP_FLAGS = [
     "-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-mcode-object-version=5",
     "-ffp-contract=fast", "-Wno-unused-result", "-Wno-unused-variable",
 ]
+# release compiles also emit the compiler's per-kernel resource remarks, kept
+# next to the objects (``<stem>.resources.txt``, keyed by resource_key) so
+# ncnet_amd.kernel_resources / tests/test_kernel_resources.py read them instead
+# of compiling every source a second time
+RES_FLAG = "-Rpass-analysis=kernel-resource-usage"
+
+
+def resource_key(src: Path) -> str:
+    """Hash of what a source's device code depends on: its text, every csrc
+    header and the compile flags."""
+    import hashlib
+    h = hashlib.sha256(" ".join(HIP_FLAGS).encode())
+    for f in [src, *sorted(CSRC.glob("*.h"))]:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def resource_cache(src: Path) -> Path:
+    return BUILD / (src.stem + ".resources.txt")
 
 
 def _torch_paths():
@@ -106,11 +126,16 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, v
 
     steps = []
     objs = []
+    remarks = {}                                       # step index -> (cache file, key)
     for src in hip_srcs:
         obj = bdir / (src.stem + ".o")
         objs.append(obj)
-        if force or _newer(src, obj, headers):
-            steps.append([HIPCC, *hip_flags, "-I", str(CSRC), "-c", str(src), "-o", str(obj)])
+        if force or _newer(src, obj, headers) or (variant == "release" and not resource_cache(src).exists()):
+            cmd = [HIPCC, *hip_flags, "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
+            if variant == "release":
+                remarks[len(steps)] = (resource_cache(src), resource_key(src))
+                cmd.append(RES_FLAG)
+            steps.append(cmd)
     bsrc = CSRC / "bindings.cpp"
     bobj = bdir / "bindings.o"
     objs.append(bobj)
@@ -128,7 +153,12 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, v
     if steps:
         jobs = jobs or min(len(steps), max(1, (os.cpu_count() or 4) // 2), 16)
         with cf.ThreadPoolExecutor(jobs) as ex:
-            for out in ex.map(_run, steps):
+            for i, out in enumerate(ex.map(_run, steps)):
+                if i in remarks:
+                    path, key = remarks[i]
+                    lines = [ln for ln in out.splitlines() if RES_FLAG in ln]
+                    path.write_text(f"# key {key}\n" + "\n".join(lines) + "\n")
+                    out = "\n".join(ln for ln in out.splitlines() if RES_FLAG not in ln)
                 if verbose and out.strip():
                     print(out)
     if force or steps or not target.exists() or any(o.stat().st_mtime > target.stat().st_mtime for o in objs):

@@ -18,7 +18,7 @@ import subprocess
 import sys
 from pathlib import Path
 
-from .build import CSRC, HIP_FLAGS, HIPCC
+from .build import CSRC, HIP_FLAGS, HIPCC, resource_cache, resource_key
 
 _FIELDS = {
     "VGPRs": "vgpr", "AGPRs": "agpr", "TotalSGPRs": "sgpr", "ScratchSize [bytes/lane]": "scratch",
@@ -46,16 +46,32 @@ def demangle(name: str) -> str:
     return ident
 
 
-def analyse(src: Path, extra_flags=()) -> list[dict]:
-    """Resource records of every kernel compiled from ``src``."""
-    flags = [f for f in HIP_FLAGS if f != "-fPIC"]
-    cmd = [HIPCC, *flags, *extra_flags, "-I", str(CSRC), "--offload-device-only", "-c", str(src), "-o", "/dev/null",
-           "-Rpass-analysis=kernel-resource-usage"]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr[-4000:]}")
+def _cached_remarks(src: Path) -> str | None:
+    """The remarks the release build wrote for ``src`` (ncnet_amd/build.py), if
+    they were produced from this exact source, headers and flags."""
+    path = resource_cache(src)
+    if not path.exists():
+        return None
+    text = path.read_text()
+    first, _, rest = text.partition("\n")
+    return rest if first == f"# key {resource_key(src)}" else None
+
+
+def analyse(src: Path, extra_flags=(), use_cache: bool = True) -> list[dict]:
+    """Resource records of every kernel compiled from ``src`` (from the build's
+    remarks when they match the source, else a device-only compile)."""
+    src = Path(src)
+    text = _cached_remarks(src) if use_cache and not extra_flags else None
+    if text is None:
+        flags = [f for f in HIP_FLAGS if f != "-fPIC"]
+        cmd = [HIPCC, *flags, *extra_flags, "-I", str(CSRC), "--offload-device-only", "-c", str(src), "-o",
+               "/dev/null", "-Rpass-analysis=kernel-resource-usage"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr[-4000:]}")
+        text = r.stderr
     recs, cur = [], None
-    for line in r.stderr.splitlines():
+    for line in text.splitlines():
         m = _REMARK.search(line)
         if not m:
             continue

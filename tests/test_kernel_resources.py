@@ -64,3 +64,23 @@ def test_hot_kernels_do_not_spill(records, prefix, args):
     bad = [(kr.short(r["name"]), r.get("scratch"), r.get("vgpr_spill")) for r in hits
            if r.get("scratch", 0) or r.get("vgpr_spill", 0)]
     assert not bad, f"scratch / VGPR spills in hot kernels: {bad}"
+
+
+def test_build_remark_cache_is_keyed_on_the_source(tmp_path):
+    """kernel_resources reads the release build's remarks only when they were
+    produced from the same source, headers and flags (ncnet_amd/build.py
+    resource_key); a stale file means a fresh compile."""
+    from ncnet_amd import build as b
+    src = tmp_path / "zz_cache_probe.hip"
+    src.write_text("// probe\n")
+    cache = b.resource_cache(src)
+    cache.parent.mkdir(exist_ok=True)
+    try:
+        cache.write_text("# key stale\nremark line\n")
+        assert kr._cached_remarks(src) is None
+        cache.write_text(f"# key {b.resource_key(src)}\nremark line\n")
+        assert kr._cached_remarks(src) == "remark line\n"
+        src.write_text("// edited\n")
+        assert kr._cached_remarks(src) is None
+    finally:
+        cache.unlink(missing_ok=True)
