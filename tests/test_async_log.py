@@ -36,3 +36,43 @@ def test_gpu_log_async_in_order_and_complete():
     assert [r["loss"] for r in recs] == want
     el = [r["elapsed_s"] for r in recs]
     assert el == sorted(el) and el[0] > 0
+
+
+@pytest.mark.gpu
+def test_training_steps_do_not_sync_the_host():
+    """The default training loop (Trainer.train_step + AsyncLossLog.push /
+    poll, as process_epoch runs it with --log_interval 1) issues no
+    synchronizing CUDA call per step: after a warm-up (HIP graph capture,
+    hipBLASLt candidate timing, pack caches) every step runs under
+    torch.cuda.set_sync_debug_mode('error'), which raises on any torch-level
+    device -> host synchronisation (.item(), float(tensor), blocking copies,
+    nonzero, ...)."""
+    from ncnet_amd.engine.trainer import Trainer, make_adam
+    from ncnet_amd.models import ImMatchNet
+    from ncnet_amd.parallel.dist import init_distributed
+
+    ctx = init_distributed()
+    torch.manual_seed(0)
+    model = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1]).cuda().train()
+    opt = make_adam([p for p in model.parameters() if p.requires_grad], 5e-4)
+    tr = Trainer(model, opt, ctx)
+    batches = [{"source_image": torch.randn(2, 3, 400, 400, device="cuda"),
+                "target_image": torch.randn(2, 3, 400, 400, device="cuda")} for _ in range(2)]
+    log = AsyncLossLog(ctx.device)
+    for i in range(3):                                   # warm-up (captures, tuning)
+        log.push(tr.train_step(batches[i % 2], batches[(i + 1) % 2]), {"step": i})
+    log.drain()
+    torch.cuda.synchronize()
+    recs = []
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        for i in range(4):
+            loss = tr.train_step(batches[i % 2], batches[(i + 1) % 2])
+            recs += log.push(loss, {"step": i}) if i % 2 == 0 else log.poll()
+        with pytest.raises(RuntimeError):             # the mode does catch a host readback here
+            loss.item()
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    recs += log.drain()
+    assert [r["step"] for r in recs] == [0, 2]
+    assert all(r["loss"] == r["loss"] for r in recs)     # finite readback
