@@ -20,17 +20,19 @@
 //
 // through an fp32 staging copy of Z_o in LDS.
 //
-// Work: an item = a 2 x 2 block of output planes (v, i0..i0+1, j0..j0+1), whose
-// 6 x 6 window of input planes streams through LDS; a persistent workgroup (one
-// per CU, 4 waves = one per SIMD) walks items bid, bid + G, ...  The 640 columns
+// Work: an item = an RI x RJ block of output planes (1 x 3 at the training
+// plane: a 2 x 2 block needs 320 accumulator registers, past the 256 a wave
+// can hold without AGPR <-> VGPR copies), whose (RI+KS-1) x (RJ+KS-1) window of
+// input planes streams through LDS; a persistent workgroup (one per CU, 4
+// waves = one per SIMD) walks items bid, bid + G, ...  The 640 columns
 // are split over the waves (5 tiles of 32 each), and each wave DMAs only ITS
 // 160 voxels of every plane into its own 6-slot ring (5 planes ahead), so the
 // main loop has no workgroup barrier at all: a wave waits only for its own
 // LDS-DMAs (counted vmcnt; a fixed count of DMA instructions per step, past the
 // item's last plane they read zeros into the slot the step after next will
-// overwrite anyway).  Accumulators: 4 output planes x 5 tiles x 16 = 320 VGPRs
-// (one wave per SIMD: 512).  The epilogue reuses the ring space as the Z_o
-// staging area (25 taps x 640 fp32).
+// overwrite anyway).  Accumulators: RI x RJ output planes x 5 tiles x 16
+// (240 at 1 x 3).  The epilogue stages Z_o in LDS (two buffers, one barrier
+// per output plane) and sums the shifted tap rows.
 // Layouts: X bf16 [V,I,J,K,L,16]; Wt bf16 [KS*KS (di,dj)][64 lanes][8] =
 // the A fragments (lane l: tap row l & 31, ci 8 (l >> 5) + e); Y fp32 [V,I,J,K,L].
 #include "common.h"
