@@ -62,10 +62,11 @@ class RuntimeConfig:
     corr_ns: int = 3                 # NCNET_CORR_NS: ring stages (3 or 4) of corr_gemm_v2
     c1x_pd: int = 2                  # NCNET_C1X_PD: conv1x16 transposed-read lookahead (tiles), 1, 2 or 3
     conv2d_256: int = 1              # NCNET_CONV2D_256: 256 x 256 trunk conv tiles for Cout = 256 (big grids)
+    s2d_rt: int = 2                  # NCNET_S2D_RT: stats2d 64-row sub-tiles per block, volumes >= 1024 rows (1/2/4)
 
     # the launcher tuning fields, in the order of csrc/common.h tuning_slot()
     TUNING = ("nt_store", "gp_tpw", "conv_v3", "wgrad_v3", "wgrad_flags", "conv2d_variant", "conv2d_v3",
-              "corr_v2", "corr_ns", "c1x_pd", "conv2d_256")
+              "corr_v2", "corr_ns", "c1x_pd", "conv2d_256", "s2d_rt")
 
     @classmethod
     def from_env(cls, env=None) -> "RuntimeConfig":

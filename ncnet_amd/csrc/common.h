@@ -191,9 +191,10 @@ struct NcnetTuning {
   int conv2d_v3;       // chip-round v3 tiles where the auto rule picks them (1)
   int c1x_pd;          // conv1x16 transposed-read lookahead in tiles, 1, 2 or 3 (2)
   int conv2d_256;      // 256 x 256 trunk conv tiles for Cout = 256 where the grid is big enough (1)
+  int s2d_rt;          // stats2d: 64-row sub-tiles per block for volumes of >= 1024 rows, 1, 2 or 4 (2)
 };
 __host__ inline NcnetTuning& tuning() {
-  static NcnetTuning t = {1, 5, 0, 0, 0, 0, -1, 3, 1, 2, 1};
+  static NcnetTuning t = {1, 5, 0, 0, 0, 0, -1, 3, 1, 2, 1, 2};
   return t;
 }
 __host__ inline int* tuning_slot(const char* name) {
@@ -209,5 +210,6 @@ __host__ inline int* tuning_slot(const char* name) {
   if (!strcmp(name, "conv2d_v3")) return &t.conv2d_v3;
   if (!strcmp(name, "c1x_pd")) return &t.c1x_pd;
   if (!strcmp(name, "conv2d_256")) return &t.conv2d_256;
+  if (!strcmp(name, "s2d_rt")) return &t.s2d_rt;
   return nullptr;
 }

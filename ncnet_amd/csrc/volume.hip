@@ -138,7 +138,10 @@ __global__ __launch_bounds__(256) void stats_cols_merge_kernel(const float* __re
 // Partials [V][tiles][n] are merged in tile order by stats2d_merge (ties keep
 // the smallest index either way).  C % 4 != 0: four scalar loads per lane and row.
 // ---------------------------------------------------------------------------
-template <int WS, bool VEC>
+// RT: 64-row sub-tiles per block (the column stats run on in registers over
+// all of them), so a tall volume leaves RT x fewer column partials for the
+// merge (InLoc 3200 px: 118 -> 30 per column, the merge was 40 % of stats2d).
+template <int WS, bool VEC, int RT>
 __global__ __launch_bounds__(256) void stats2d_tile_kernel(const float* __restrict__ x, int R, int C, int nrt, int nct,
                                                            float* __restrict__ rpm, int* __restrict__ rpi,
                                                            float* __restrict__ rps, float* __restrict__ cpm,
@@ -153,50 +156,53 @@ __global__ __launch_bounds__(256) void stats2d_tile_kernel(const float* __restri
   const int c0 = ct * 256 + lane * 4;
   const bool cok = c0 < C;
   const int nk = min(4, C - c0);                         // valid columns of this lane (C % 4 != 0: scalar loads)
-  const int rbase = rt * 64 + wave * 16;
   const float* xv = x + (size_t)v * R * C;
-  float4 val[16];
-#pragma unroll
-  for (int rr = 0; rr < 16; ++rr) {
-    const int r = rbase + rr;
-    if constexpr (VEC) {
-      val[rr] = (cok && r < R) ? *(const float4*)(xv + (size_t)r * C + c0) : float4{0.f, 0.f, 0.f, 0.f};
-    } else {
-      const float* xr = xv + (size_t)(r < R ? r : 0) * C;
-      val[rr] = float4{cok && r < R ? xr[c0] : 0.f, nk > 1 && r < R ? xr[c0 + 1] : 0.f,
-                       nk > 2 && r < R ? xr[c0 + 2] : 0.f, nk > 3 && r < R ? xr[c0 + 3] : 0.f};
-    }
-  }
   Stat col[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) col[k] = Stat{-INFINITY, 0.f, 0x7fffffff};
+  for (int st = 0; st < RT; ++st) {
+    const int rbase = (rt * RT + st) * 64 + wave * 16;
+    if (rbase >= R) break;                                 // wave-uniform
+    float4 val[16];
 #pragma unroll
-  for (int rr = 0; rr < 16; ++rr) {
-    const int r = rbase + rr;
-    if (r >= R) break;                                   // wave-uniform
-    const float e[4] = {val[rr].x, val[rr].y, val[rr].z, val[rr].w};
-    Stat rs{-INFINITY, 0.f, 0x7fffffff};
-    if (cok) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (VEC || k < nk) {
-          col[k] = stat_push(col[k], e[k], r, WS);
-          rs = stat_push(rs, e[k], c0 + k, WS);
-        }
+    for (int rr = 0; rr < 16; ++rr) {
+      const int r = rbase + rr;
+      if constexpr (VEC) {
+        val[rr] = (cok && r < R) ? *(const float4*)(xv + (size_t)r * C + c0) : float4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        const float* xr = xv + (size_t)(r < R ? r : 0) * C;
+        val[rr] = float4{cok && r < R ? xr[c0] : 0.f, nk > 1 && r < R ? xr[c0 + 1] : 0.f,
+                         nk > 2 && r < R ? xr[c0 + 2] : 0.f, nk > 3 && r < R ? xr[c0 + 3] : 0.f};
       }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      Stat ot;
-      ot.m = __shfl_xor(rs.m, o, 64);
-      ot.s = __shfl_xor(rs.s, o, 64);
-      ot.idx = __shfl_xor(rs.idx, o, 64);
-      rs = stat_merge(rs, ot, WS);
-    }
-    if (lane == 0) {
-      const size_t o = ((size_t)v * nct + ct) * R + r;
-      rpm[o] = rs.m; rpi[o] = rs.idx;
-      if (WS) rps[o] = rs.s;
+    for (int rr = 0; rr < 16; ++rr) {
+      const int r = rbase + rr;
+      if (r >= R) break;                                   // wave-uniform
+      const float e[4] = {val[rr].x, val[rr].y, val[rr].z, val[rr].w};
+      Stat rs{-INFINITY, 0.f, 0x7fffffff};
+      if (cok) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (VEC || k < nk) {
+            col[k] = stat_push(col[k], e[k], r, WS);
+            rs = stat_push(rs, e[k], c0 + k, WS);
+          }
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        Stat ot;
+        ot.m = __shfl_xor(rs.m, o, 64);
+        ot.s = __shfl_xor(rs.s, o, 64);
+        ot.idx = __shfl_xor(rs.idx, o, 64);
+        rs = stat_merge(rs, ot, WS);
+      }
+      if (lane == 0) {
+        const size_t o = ((size_t)v * nct + ct) * R + r;
+        rpm[o] = rs.m; rpi[o] = rs.idx;
+        if (WS) rps[o] = rs.s;
+      }
     }
   }
 #pragma unroll
@@ -214,20 +220,33 @@ __global__ __launch_bounds__(256) void stats2d_tile_kernel(const float* __restri
   }
 }
 
-// merge [V][nt][n] partials -> [V][n]
+// merge [V][nt][n] partials -> [V][n]: 4 lanes per output (tiles t = q, q + 4,
+// ...), then a 2-step lane shuffle (max / first argmax exact in any order)
 template <int WS>
 __global__ __launch_bounds__(256) void stats2d_merge_kernel(const float* __restrict__ pm, const int* __restrict__ pi,
                                                             const float* __restrict__ ps, float* __restrict__ mx,
                                                             int* __restrict__ arg, float* __restrict__ se, int V,
                                                             int n, int nt) {
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (long long)V * n) return;
-  const int v = (int)(e / n), i = (int)(e - (long long)v * n);
+  const long long e = ((long long)blockIdx.x * 256 + threadIdx.x) >> 2;
+  const int q = threadIdx.x & 3;
+  const bool live = e < (long long)V * n;                // whole quads share `live` (4 | 256)
+  const int v = live ? (int)(e / n) : 0, i = live ? (int)(e - (long long)v * n) : 0;
   Stat a{-INFINITY, 0.f, 0x7fffffff};
-  for (int t = 0; t < nt; ++t) {
-    const size_t o = ((size_t)v * nt + t) * n + i;
-    a = stat_merge(a, Stat{pm[o], WS ? ps[o] : 0.f, pi[o]}, WS);
+  if (live) {
+    for (int t = q; t < nt; t += 4) {
+      const size_t o = ((size_t)v * nt + t) * n + i;
+      a = stat_merge(a, Stat{pm[o], WS ? ps[o] : 0.f, pi[o]}, WS);
+    }
   }
+#pragma unroll
+  for (int o = 1; o < 4; o <<= 1) {
+    Stat b;
+    b.m = __shfl_xor(a.m, o, 64);
+    b.s = __shfl_xor(a.s, o, 64);
+    b.idx = __shfl_xor(a.idx, o, 64);
+    a = stat_merge(a, b, WS);
+  }
+  if (!live || q != 0) return;
   mx[e] = a.m;
   if (arg) arg[e] = a.idx;
   if (WS && se) se[e] = a.s;
@@ -739,19 +758,28 @@ extern "C" int ncnet_stats_cols(const float* x, float* mx, int* arg, float* se, 
 extern "C" int ncnet_stats2d(const float* x, float* rmx, int* rarg, float* rse, float* cmx, int* carg, float* cse,
                              int V, int R, int C, float* work, int sum_kind, hipStream_t s) {
   const bool vec = C % 4 == 0;   // 16-byte rows: one float4 per lane and row; else four scalar loads
-  const int nrt = cdiv(R, 64), nct = cdiv(C, 256);
+  // tall volumes: 64 rt-row blocks (rt x fewer column partials to merge;
+  // tuning s2d_rt); the work buffer is sized for 64-row blocks (the bound)
+  const int rt = R >= 1024 ? (tuning().s2d_rt >= 4 ? 4 : tuning().s2d_rt == 2 ? 2 : 1) : 1;
+  const int nrt = cdiv(R, 64 * rt), nct = cdiv(C, 256);
   const size_t nr = (size_t)V * nct * R, nc = (size_t)V * nrt * C;
   float* rpm = work; int* rpi = (int*)(work + nr); float* rps = work + 2 * nr;
   float* cpm = work + 3 * nr; int* cpi = (int*)(cpm + nc); float* cps = cpm + 2 * nc;
   const dim3 grid((unsigned)((size_t)V * nrt * nct)), blk(256);
+#define S2D_TILE(WSV, VECV) do { \
+    if (rt == 4) hipLaunchKernelGGL((stats2d_tile_kernel<WSV, VECV, 4>), grid, blk, 0, s, x, R, C, nrt, nct, rpm, rpi, rps, cpm, cpi, cps); \
+    else if (rt == 2) hipLaunchKernelGGL((stats2d_tile_kernel<WSV, VECV, 2>), grid, blk, 0, s, x, R, C, nrt, nct, rpm, rpi, rps, cpm, cpi, cps); \
+    else hipLaunchKernelGGL((stats2d_tile_kernel<WSV, VECV, 1>), grid, blk, 0, s, x, R, C, nrt, nct, rpm, rpi, rps, cpm, cpi, cps); \
+  } while (0)
 #define S2D(WSV) do { \
-    if (vec) hipLaunchKernelGGL((stats2d_tile_kernel<WSV, true>), grid, blk, 0, s, x, R, C, nrt, nct, rpm, rpi, rps, cpm, cpi, cps); \
-    else hipLaunchKernelGGL((stats2d_tile_kernel<WSV, false>), grid, blk, 0, s, x, R, C, nrt, nct, rpm, rpi, rps, cpm, cpi, cps); \
-    hipLaunchKernelGGL(stats2d_merge_kernel<WSV>, dim3((unsigned)cdiv(V * R, 256)), blk, 0, s, rpm, rpi, rps, rmx, rarg, rse, V, R, nct); \
-    hipLaunchKernelGGL(stats2d_merge_kernel<WSV>, dim3((unsigned)cdiv(V * C, 256)), blk, 0, s, cpm, cpi, cps, cmx, carg, cse, V, C, nrt); \
+    if (vec) S2D_TILE(WSV, true); \
+    else S2D_TILE(WSV, false); \
+    hipLaunchKernelGGL(stats2d_merge_kernel<WSV>, dim3((unsigned)cdiv(4 * V * R, 256)), blk, 0, s, rpm, rpi, rps, rmx, rarg, rse, V, R, nct); \
+    hipLaunchKernelGGL(stats2d_merge_kernel<WSV>, dim3((unsigned)cdiv(4 * V * C, 256)), blk, 0, s, cpm, cpi, cps, cmx, carg, cse, V, C, nrt); \
   } while (0)
   if (sum_kind == 1) S2D(1); else if (sum_kind == 2) S2D(2); else S2D(0);
 #undef S2D
+#undef S2D_TILE
   return (int)hipGetLastError();
 }
 extern "C" int ncnet_match_candidates(const float* cmx, const float* cse, const int* carg, const float* rmx,
