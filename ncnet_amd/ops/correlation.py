@@ -208,9 +208,25 @@ def correlation(fa: torch.Tensor, fb: torch.Tensor, amap: torch.Tensor | None = 
     return torch.bmm(fa.float()[amap.long()], fb.float()[bmap.long()].transpose(1, 2))
 
 
+_BLOCK_ORDER: dict = {}
+
+
 def block_order_index(h: int, w: int, k: int, device) -> torch.Tensor:
     """Permutation putting each k x k spatial block's rows next to each other
-    (row = (k*k)*blk + (k*dy + dx), blk row-major over the pooled grid)."""
+    (row = (k*k)*blk + (k*dy + dx), blk row-major over the pooled grid).
+    Cached per (h, w, k, device): a pure function of the shape, built once
+    instead of ~10 small launches per InLoc pair (treat it as read-only)."""
+    key = (h, w, k, str(device))
+    perm = _BLOCK_ORDER.get(key)
+    if perm is None:
+        if torch.cuda.is_available() and torch.device(device).type == "cuda" and torch.cuda.is_current_stream_capturing():
+            return _block_order_index(h, w, k, device)      # not cached from inside a graph capture
+        with torch.inference_mode(False):                   # a normal tensor: usable with autograd later
+            perm = _BLOCK_ORDER[key] = _block_order_index(h, w, k, device)
+    return perm
+
+
+def _block_order_index(h: int, w: int, k: int, device) -> torch.Tensor:
     ii = torch.arange(h, device=device).view(h, 1)
     jj = torch.arange(w, device=device).view(1, w)
     blk = (ii // k) * (w // k) + (jj // k)
