@@ -506,7 +506,11 @@ class FrozenResNetPlan(nn.Module):
         key = (tuple(x.shape), x.dtype, x.device)
         ent = self._graphs.get(key)
         if ent is None:
-            static_in = x.clone()
+            # the graph input is already the plan's operand layout (16-bit,
+            # channels-last): the per-call copy converts the images in one pass
+            # instead of an fp32 copy followed by the conversion inside the graph
+            static_in = torch.empty_like(x, dtype=self.dtype, memory_format=torch.channels_last)
+            static_in.copy_(x)
             side = torch.cuda.Stream(device=x.device)
             side.wait_stream(torch.cuda.current_stream(x.device))
             with torch.cuda.stream(side):

@@ -41,6 +41,8 @@ def _worker(rank, world, port, out_dir, steps):
     import dataclasses
     from ncnet_amd import config
     config.set_runtime(dataclasses.replace(config.RuntimeConfig.from_env(), trunk_conv="native"))
+    # the MIOpen stem with a fixed solver in every process (as the reference below)
+    torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = False, True
     from ncnet_amd.engine.trainer import Trainer, make_adam
     from ncnet_amd.models import ImMatchNet
     from ncnet_amd.parallel.dist import broadcast_module, destroy, init_distributed
@@ -65,40 +67,50 @@ def _worker(rank, world, port, out_dir, steps):
     destroy(ctx)
 
 
+def _reference_worker(_, world, out_dir, steps):
+    """ONE process doing FlatAdam on the summed shard gradients (g0 + g1, the
+    in-place summed bucket, 1/world folded into the step as GradBucket sets
+    it) -- in a fresh process like the ranks, so no state left by earlier
+    tests in the pytest process (MIOpen solver caches, runtime knobs) enters
+    the comparison."""
+    import dataclasses
+    from ncnet_amd import config
+    config.set_runtime(dataclasses.replace(config.RuntimeConfig.from_env(), trunk_conv="native"))
+    torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = False, True
+    from ncnet_amd.engine.trainer import make_adam, weak_loss
+    from ncnet_amd.models import ImMatchNet
+    init = torch.load(os.path.join(out_dir, "r0.pt"), weights_only=True)["init"]
+    torch.manual_seed(300)
+    m = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1], dtype="bf16").cuda()
+    m.train()
+    params = [p for p in m.parameters() if p.requires_grad]
+    with torch.no_grad():
+        for p, v in zip(params, init):
+            p.copy_(v.cuda())
+    opt = make_adam(params, 5e-4)
+    opt.grad_scale = 1.0 / world
+    for step in range(steps):
+        opt.zero_grad()
+        for r in range(world):             # shard gradients accumulate into the flat buffer: g0 + g1
+            b = {k: v.cuda() for k, v in _batch(1000 * step + r).items()}
+            weak_loss(m, b).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    torch.save([p.detach().clone().cpu() for p in params], os.path.join(out_dir, "ref.pt"))
+
+
 def test_dp2_gloo_on_one_gpu_equals_single_process(tmp_path):
     world, steps = 2, 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), steps), nprocs=world, join=True)
     res = [torch.load(str(tmp_path / f"r{r}.pt"), weights_only=True) for r in range(world)]
     for a, b in zip(res[0]["params"], res[1]["params"]):
         assert torch.equal(a, b)
-    import dataclasses
-    from ncnet_amd import config
-    from ncnet_amd.engine.trainer import make_adam, weak_loss
-    from ncnet_amd.models import ImMatchNet
-    old = config.RUNTIME
-    config.set_runtime(dataclasses.replace(old, trunk_conv="native"))
-    try:
-        torch.manual_seed(300)
-        m = ImMatchNet(ncons_kernel_sizes=[5, 5, 5], ncons_channels=[16, 16, 1], dtype="bf16").cuda()
-        m.train()
-        params = [p for p in m.parameters() if p.requires_grad]
-        with torch.no_grad():
-            for p, v in zip(params, res[0]["init"]):
-                p.copy_(v.cuda())
-        opt = make_adam(params, 5e-4)
-        opt.grad_scale = 1.0 / world       # as GradBucket sets it for the in-place summed bucket
-        for step in range(steps):
-            opt.zero_grad()
-            for r in range(world):         # shard gradients accumulate into the flat buffer: g0 + g1
-                b = {k: v.cuda() for k, v in _batch(1000 * step + r).items()}
-                weak_loss(m, b).backward()
-            opt.step()
-    finally:
-        config.set_runtime(old)
+    mp.spawn(_reference_worker, args=(world, str(tmp_path), steps), nprocs=1, join=True)
+    ref = torch.load(str(tmp_path / "ref.pt"), weights_only=True)
     # same kernels and shapes per shard; the all-reduce sums two fp32 values
     # (exact either way round), FlatAdam scales by 1/world in-kernel
-    for a, p in zip(res[0]["params"], params):
-        assert torch.allclose(a, p.detach().cpu(), rtol=1e-5, atol=1e-6), float((a - p.detach().cpu()).abs().max())
+    for a, p in zip(res[0]["params"], ref):
+        assert torch.allclose(a, p, rtol=1e-5, atol=1e-6), float((a - p).abs().max())
     mem = [r["mem"] for r in res]
     out = os.path.join(ROOT, "gpurun_out", "dp_rehearsal_mem.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
